@@ -1,0 +1,109 @@
+"""In-tree build of the gfx950 extension ``taboo_brittleness_amd/_tb_kernels*.so``.
+
+Kernels (``csrc/*.hip``) are compiled straight with ``hipcc --offload-arch=gfx950``
+(no hipify pass, no CUDA sources); only ``bindings.cpp`` includes the torch
+headers.  Object files are cached under ``build/`` and rebuilt when a source or
+header is newer, so an unchanged tree rebuilds in a second.
+
+    python -m taboo_brittleness_amd.build [--force] [-j N]
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import glob
+import os
+import subprocess
+import sys
+import sysconfig
+from typing import List
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(PKG_DIR, "csrc")
+REPO = os.path.dirname(PKG_DIR)
+BUILD = os.path.join(REPO, "build", "tb_kernels")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+ARCH = os.environ.get("TB_OFFLOAD_ARCH", "gfx950")
+EXT_NAME = "_tb_kernels"
+
+
+def ext_path() -> str:
+    suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+    return os.path.join(PKG_DIR, EXT_NAME + suffix)
+
+
+def _torch_paths():
+    import torch
+    from torch.utils import cpp_extension
+
+    inc = cpp_extension.include_paths()
+    lib = os.path.join(os.path.dirname(torch.__file__), "lib")
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    return inc, lib, abi
+
+
+def _newer(target: str, deps: List[str]) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _run(cmd: List[str]) -> None:
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(" ".join(cmd) + "\n" + r.stdout + r.stderr)
+        raise RuntimeError(f"build step failed: {cmd[0]} ... {cmd[-1]}")
+
+
+def build(force: bool = False, jobs: int = 8, verbose: bool = False) -> str:
+    os.makedirs(BUILD, exist_ok=True)
+    headers = glob.glob(os.path.join(CSRC, "*.h"))
+    hip_srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+    inc, lib, abi = _torch_paths()
+    common = ["-fPIC", "-O3", "-std=c++17", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-I", CSRC]
+    steps = []
+    objs = []
+    for src in hip_srcs:
+        obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+        objs.append(obj)
+        if force or _newer(obj, [src] + headers):
+            steps.append([os.path.join(ROCM, "bin", "hipcc"), f"--offload-arch={ARCH}", "-c", src, "-o", obj,
+                          "-munsafe-fp-atomics"] + common)
+    bind_src = os.path.join(CSRC, "bindings.cpp")
+    bind_obj = os.path.join(BUILD, "bindings.cpp.o")
+    objs.append(bind_obj)
+    if force or _newer(bind_obj, [bind_src] + headers):
+        py_inc = sysconfig.get_paths()["include"]
+        cmd = ["c++", "-c", bind_src, "-o", bind_obj, "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-DHIPBLAS_V2",
+               f"-DTORCH_EXTENSION_NAME={EXT_NAME}", "-DTORCH_API_INCLUDE_EXTENSION_H", "-isystem", py_inc,
+               "-isystem", os.path.join(ROCM, "include")] + common
+        for p in inc:
+            cmd += ["-isystem", p]
+        steps.append(cmd)
+    if steps:
+        with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+            futs = [ex.submit(_run, c) for c in steps]
+            for f in futs:
+                f.result()
+    out = ext_path()
+    if force or steps or _newer(out, objs):
+        link = ["c++", "-shared", "-o", out] + objs + [
+            "-L", lib, "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
+            "-L", os.path.join(ROCM, "lib"), "-lamdhip64", f"-Wl,-rpath,{lib}", f"-Wl,-rpath,{os.path.join(ROCM, 'lib')}"]
+        _run(link)
+    if verbose:
+        print(f"[build] {len(steps)} compile step(s); extension at {out}")
+    return out
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-j", "--jobs", type=int, default=min(8, os.cpu_count() or 1))
+    a = ap.parse_args()
+    build(force=a.force, jobs=a.jobs, verbose=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,45 @@
+// Host launchers for the gfx950 kernels.  Raw pointers + stream only, so the
+// .hip translation units never include the (slow to compile) torch headers;
+// bindings.cpp does the tensor checks and passes the current HIP stream.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+// norm.hip
+void tb_rmsnorm(const uint16_t* x, const uint16_t* w, uint16_t* y, int M, int D, float eps, hipStream_t st);
+void tb_add_rmsnorm2(uint16_t* h, const uint16_t* o, const uint16_t* w_post, const uint16_t* w_next, uint16_t* x,
+                     int M, int D, float eps, hipStream_t st);
+void tb_embed_rmsnorm(const int32_t* ids, const uint16_t* E, const uint16_t* w, uint16_t* h, uint16_t* x, int M,
+                      int D, int V, float scale, float eps, hipStream_t st);
+// rope.hip
+void tb_rope_qkv_cache(const uint16_t* qkv, const int32_t* pos, const int32_t* slot_of_row, const float* cos_t,
+                       const float* sin_t, uint16_t* q_out, uint16_t* kc, uint16_t* vc, int M, int Hq, int Hkv,
+                       int HD, int S, int max_pos, hipStream_t st);
+// attention.hip
+int tb_attention_lds_bytes(int HD);
+void tb_attention(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, uint16_t* out, const int32_t* pos,
+                  const int32_t* slot, int B, int T, int Hq, int Hkv, int HD, int S, float scale, float softcap,
+                  int window, hipStream_t st);
+// elementwise.hip
+void tb_geglu(const uint16_t* gu, uint16_t* out, int M, int F, hipStream_t st);
+// lens.hip
+void tb_argmax_rows(const uint16_t* logits, int32_t* out, int R, int V, float cap, hipStream_t st);
+void tb_row_lse(const uint16_t* logits, float* lse, int R, int V, float cap, int emulate_bf16, hipStream_t st);
+void tb_gather_probs(const uint16_t* logits, const float* lse, const int32_t* ids, float* out, int R, int K, int V,
+                     int round_bf16, hipStream_t st);
+void tb_lens_colsum(const uint16_t* logits, const float* lse, const uint8_t* mask, const int32_t* excl, float* acc,
+                    int B, int T, int V, int accumulate, int round_bf16, hipStream_t st);
+void tb_topk_rows(const float* x, float* vals, int32_t* idx, int R, int V, int K, hipStream_t st);
+void tb_xent_rows(const uint16_t* logits, const int32_t* tgt, float* nll, int R, int V, float cap, int emulate_bf16,
+                  hipStream_t st);
+// sae.hip
+void tb_gemm_nt(const uint16_t* A, const uint16_t* W, void* C, const float* bias, const float* thr, int M, int N,
+                int K, int ldc, int epi, hipStream_t st);
+void tb_lowrank_edit(uint16_t* h, uint16_t* x_next, const uint8_t* apply, const int32_t* idx, const int32_t* cnt,
+                     int mmax, const void* E, const void* Dm, int table_f32, const float* bias, const float* thr,
+                     const float* pre_bias, float alpha, const uint16_t* w_next, float eps, int M, int D,
+                     float* coef_out, hipStream_t st);
+void tb_sae_decode_sparse(const float* acts, const uint16_t* Wdec, const float* b_dec, uint16_t* out_bf16,
+                          float* out_f32, int M, int L, int D, hipStream_t st);
+void tb_latent_score(const float* acts, const float* p, const uint8_t* spike, const int32_t* seg, float* out,
+                     float* spike_mean, float* corr, int G, int L, hipStream_t st);

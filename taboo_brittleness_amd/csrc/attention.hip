@@ -1,0 +1,287 @@
+// Softcapped GQA attention over the KV cache: one kernel for
+// prefill, chunked prefill and decode.
+//
+//   s = tanh((q.k) * scale / cap) * cap,  masked to keys j <= pos (causal) and
+//   pos - j < window on sliding layers;  out = softmax(s) V.
+//
+// Stock flash kernels have no tanh softcap, hence this kernel.  Geometry:
+//  * workgroup = (16/G query positions) x (G q-heads of one kv head) = 16 MFMA
+//    rows for one sequence, 4 waves;  grid = (ceil(T/P), Hkv, B).
+//  * the waves split the key range in 32-key blocks (flash-decoding inside the
+//    workgroup) and merge (m, l, O) through LDS at the end.
+//  * S = Q K^T on v_mfma_f32_16x16x32_bf16 with K fragments loaded straight
+//    from the cache (a lane's 8 k-elements are 16 contiguous bytes of one key
+//    row); online softmax on the C fragment (a row spans one 16-lane group:
+//    4 xor-shuffles); P goes through a 1 KB per-wave LDS tile to become the A
+//    operand; V is staged per wave in LDS (row stride HD+16 halves the
+//    transposed-read bank conflicts) and read with ds_read_b64_tr_b16 as the
+//    B operand (cdna_hip_programming.md T10).
+// Rows with pos < 0 (padding) produce zeros.
+#include "common.h"
+#include "api.h"
+
+// LDS: V staging [4][32][HD+16] + P tiles [4][16][40] (bf16), then 128 floats of
+// merge scalars.  The fp32 merge image [4][16][HD] reuses the staging area
+// (it is smaller for HD <= 256, asserted below).
+int tb_attention_lds_bytes(int HD) {
+  const int VSTR = HD + 16, PSTR = 40;
+  const int stage = 4 * 32 * VSTR * 2 + 4 * 16 * PSTR * 2;
+  return ((stage + 128 * 4 + 15) / 16) * 16;
+}
+
+namespace {
+
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ v4i16 ds_read_tr16(const uint16_t* lds_ptr) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)(lds_ptr));
+}
+
+__device__ __forceinline__ bf16x8 as_bf16x8(const uint4& u) { return __builtin_bit_cast(bf16x8, u); }
+
+template <int HD, int G>
+__global__ void __launch_bounds__(256) attn_cache_kernel(
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
+    uint16_t* __restrict__ out, const int32_t* __restrict__ pos, const int32_t* __restrict__ slot, int T, int Hq,
+    int Hkv, int S, float scale, float softcap, int window) {
+  constexpr int P = 16 / G;        // query positions per workgroup
+  constexpr int KS = HD / 32;      // MFMA k-steps over head_dim
+  constexpr int DT = HD / 16;      // 16-wide output dim tiles
+  constexpr int VSTR = HD + 16;    // padded LDS row (elements)
+  constexpr int PSTR = 40;         // padded P row (elements)
+  static_assert(4 * 16 * HD * 4 <= 4 * 32 * VSTR * 2, "merge image must fit in the staging area");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint16_t* vlds_all = reinterpret_cast<uint16_t*>(smem);                    // [4][32][VSTR]
+  uint16_t* plds_all = vlds_all + 4 * 32 * VSTR;                             // [4][16][PSTR]
+  float* mrg = reinterpret_cast<float*>(plds_all + 4 * 16 * PSTR);           // [4][16] m, [4][16] l
+
+  const int b = blockIdx.z, kh = blockIdx.y, t0 = blockIdx.x * P;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int grp = lane >> 4, col = lane & 15;
+  const int cs = slot[b];
+  const uint16_t* kbase = kc + ((size_t)cs * Hkv + kh) * (size_t)S * HD;
+  const uint16_t* vbase = vc + ((size_t)cs * Hkv + kh) * (size_t)S * HD;
+
+  // --- query rows: A-layout row = col; C-layout rows = 4*grp + i
+  auto row_pos = [&](int r) -> int {
+    const int t = t0 + r / G;
+    return (t < T) ? pos[(size_t)b * T + t] : -1;
+  };
+  const int posA = row_pos(col);
+  int posC[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) posC[i] = row_pos(4 * grp + i);
+
+  int kmax = (int)wave_max((float)posA);   // -1 when every row is padding
+  float pmin = (posA >= 0) ? (float)posA : 1e30f;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) pmin = fminf(pmin, __shfl_xor(pmin, o, 64));
+  if (kmax >= S) kmax = S - 1;
+  int kmin = 0;
+  if (window > 0 && pmin < 1e29f) {
+    kmin = (int)pmin - window + 1;
+    if (kmin < 0) kmin = 0;
+  }
+  const int kstart = kmin & ~31;
+
+  // --- Q fragments (A operand), zero for invalid rows
+  bf16x8 qa[KS];
+  {
+    const int t = t0 + col / G, h = kh * G + (col % G);
+    const uint16_t* qrow = q + (((size_t)b * T + t) * Hq + h) * HD;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      uint4 u = {0, 0, 0, 0};
+      if (posA >= 0) u = *reinterpret_cast<const uint4*>(qrow + ks * 32 + grp * 8);
+      qa[ks] = as_bf16x8(u);
+    }
+  }
+
+  float m_r[4], l_r[4];
+  f32x4 o_acc[DT];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { m_r[i] = -INFINITY; l_r[i] = 0.f; }
+#pragma unroll
+  for (int d = 0; d < DT; ++d) o_acc[d] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  uint16_t* vlds = vlds_all + wid * 32 * VSTR;
+  uint16_t* plds = plds_all + wid * 16 * PSTR;
+  const float inv_cap = softcap > 0.f ? 1.f / softcap : 0.f;
+
+  for (int kb = kstart + wid * 32; kb <= kmax; kb += 4 * 32) {
+    // ---- stage V block (32 keys x HD) into this wave's LDS, coalesced 1 KB per instruction
+    constexpr int VCH = HD / 8;                // 16-B chunks per key row
+    constexpr int VIT = 32 * VCH / 64;         // instructions per lane
+    uint4 vreg[VIT];
+#pragma unroll
+    for (int it = 0; it < VIT; ++it) {
+      const int c = it * 64 + lane, key = c / VCH, ch = c % VCH;
+      int kk = kb + key;
+      kk = kk < S ? kk : S - 1;
+      vreg[it] = *reinterpret_cast<const uint4*>(vbase + (size_t)kk * HD + ch * 8);
+    }
+    // ---- S = Q K^T for two 16-key tiles
+    f32x4 sacc[2];
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+      int kk = kb + tt * 16 + col;
+      kk = kk < S ? kk : S - 1;
+      const uint16_t* krow = kbase + (size_t)kk * HD + grp * 8;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const uint4 u = *reinterpret_cast<const uint4*>(krow + ks * 32);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[ks], as_bf16x8(u), acc, 0, 0, 0);
+      }
+      sacc[tt] = acc;
+    }
+#pragma unroll
+    for (int it = 0; it < VIT; ++it) {
+      const int c = it * 64 + lane, key = c / VCH, ch = c % VCH;
+      *reinterpret_cast<uint4*>(vlds + key * VSTR + ch * 8) = vreg[it];
+    }
+    // ---- scale, softcap, mask, online softmax (rows 4*grp+i, keys kb + 16*tt + col)
+    float pr[2][4];
+    float alpha[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int pr_pos = posC[i];
+      float s0, s1;
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) {
+        const int key = kb + tt * 16 + col;
+        float s = sacc[tt][i] * scale;
+        if (softcap > 0.f) s = tanhf(s * inv_cap) * softcap;
+        const bool ok = pr_pos >= 0 && key <= pr_pos && key < S && (window <= 0 || pr_pos - key < window);
+        s = ok ? s : -INFINITY;
+        if (tt == 0) s0 = s; else s1 = s;
+      }
+      float mx = fmaxf(s0, s1);
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+      const float mnew = fmaxf(m_r[i], mx);
+      const float a = (mnew == -INFINITY) ? 1.f : __expf(m_r[i] - mnew);
+      const float p0 = (mnew == -INFINITY) ? 0.f : __expf(s0 - mnew);
+      const float p1 = (mnew == -INFINITY) ? 0.f : __expf(s1 - mnew);
+      // P is consumed in bf16 by the PV MFMA; sum the rounded values so l matches.
+      const float p0r = rbf(p0), p1r = rbf(p1);
+      float rs = p0r + p1r;
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) rs += __shfl_xor(rs, o, 64);
+      l_r[i] = l_r[i] * a + rs;
+      m_r[i] = mnew;
+      alpha[i] = a;
+      pr[0][i] = p0r;
+      pr[1][i] = p1r;
+    }
+#pragma unroll
+    for (int d = 0; d < DT; ++d)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o_acc[d][i] *= alpha[i];
+    // ---- P (C layout) -> LDS -> A layout
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) plds[(4 * grp + i) * PSTR + tt * 16 + col] = f2bf(pr[tt][i]);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint4 pa_u = *reinterpret_cast<const uint4*>(plds + col * PSTR + grp * 8);
+    const bf16x8 pa = as_bf16x8(pa_u);
+    // ---- O += P V: B fragment = V[keys 8*grp .. +8][dim tile] via two transposed reads
+    const int q4 = (lane & 15) >> 2, p4 = lane & 3;
+#pragma unroll
+    for (int d = 0; d < DT; ++d) {
+      const uint16_t* a0 = vlds + (8 * grp + q4) * VSTR + d * 16 + 4 * p4;
+      const v4i16 lo = ds_read_tr16(a0);
+      const v4i16 hi = ds_read_tr16(a0 + 4 * VSTR);
+      i16x8 vb;
+      vb[0] = lo[0]; vb[1] = lo[1]; vb[2] = lo[2]; vb[3] = lo[3];
+      vb[4] = hi[0]; vb[5] = hi[1]; vb[6] = hi[2]; vb[7] = hi[3];
+      o_acc[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, __builtin_bit_cast(bf16x8, vb), o_acc[d], 0, 0, 0);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+
+  // ---- merge the 4 waves: publish (m, l) and O (fp32, reusing the V staging area)
+  __syncthreads();
+  float* ofin = reinterpret_cast<float*>(smem);   // [4][16][HD] fp32 = 64 KB for HD=256
+  if (col == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      mrg[wid * 16 + 4 * grp + i] = m_r[i];
+      mrg[64 + wid * 16 + 4 * grp + i] = l_r[i];
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < DT; ++d)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ofin[(wid * 16 + 4 * grp + i) * HD + d * 16 + col] = o_acc[d][i];
+  __syncthreads();
+  // 16 rows x HD outputs, 8 contiguous dims per thread-step
+  for (int e = threadIdx.x; e < 16 * (HD / 8); e += blockDim.x) {
+    const int r = e / (HD / 8), c8 = (e % (HD / 8)) * 8;
+    const int t = t0 + r / G, h = kh * G + (r % G);
+    if (t >= T) continue;
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) M = fmaxf(M, mrg[w * 16 + r]);
+    float wsc[4], L = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const float mw = mrg[w * 16 + r];
+      wsc[w] = (mw == -INFINITY) ? 0.f : __expf(mw - M);
+      L += wsc[w] * mrg[64 + w * 16 + r];
+    }
+    const float inv = L > 0.f ? 1.f / L : 0.f;
+    float o8[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float acc = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) acc += wsc[w] * ofin[(w * 16 + r) * HD + c8 + j];
+      o8[j] = acc * inv;
+    }
+    *reinterpret_cast<uint4*>(out + (((size_t)b * T + t) * Hq + h) * HD + c8) = pack8(o8);
+  }
+}
+
+template <int HD, int G>
+void launch_attn(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, uint16_t* out, const int32_t* pos,
+                 const int32_t* slot, int B, int T, int Hq, int Hkv, int S, float scale, float softcap, int window,
+                 hipStream_t st) {
+  constexpr int P = 16 / G;
+  const size_t lds = (size_t)tb_attention_lds_bytes(HD);
+  static bool attr_set = false;   // > 64 KB dynamic LDS needs the opt-in (first call is never captured)
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_cache_kernel<HD, G>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_set = true;
+  }
+  dim3 grid((T + P - 1) / P, Hkv, B);
+  hipLaunchKernelGGL((attn_cache_kernel<HD, G>), grid, dim3(256), lds, st, q, kc, vc, out, pos, slot, T, Hq, Hkv, S,
+                     scale, softcap, window);
+}
+
+}  // namespace
+
+void tb_attention(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, uint16_t* out, const int32_t* pos,
+                  const int32_t* slot, int B, int T, int Hq, int Hkv, int HD, int S, float scale, float softcap,
+                  int window, hipStream_t st) {
+  if (B <= 0 || T <= 0) return;
+  const int G = Hq / Hkv;
+#define TB_ATTN_CASE(hd, g)                                                                                   \
+  if (HD == hd && G == g) {                                                                                  \
+    launch_attn<hd, g>(q, kc, vc, out, pos, slot, B, T, Hq, Hkv, S, scale, softcap, window, st);             \
+    return;                                                                                                  \
+  }
+  TB_ATTN_CASE(256, 2)
+  TB_ATTN_CASE(256, 1)
+  TB_ATTN_CASE(256, 4)
+  TB_ATTN_CASE(128, 2)
+  TB_ATTN_CASE(128, 1)
+  TB_ATTN_CASE(128, 4)
+#undef TB_ATTN_CASE
+}

@@ -1,0 +1,258 @@
+// PyTorch bindings for the gfx950 kernels (module `_tb_kernels`).
+//
+// Every op is "out=" style: the Python runtime preallocates its workspaces once
+// so the decode step can be captured into a hipGraph without allocations
+// (cdna_hip_programming.md Guideline 9).  All launches go to the current HIP
+// stream of the calling thread.
+#include <torch/extension.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <c10/core/DeviceGuard.h>
+
+#include "api.h"
+
+namespace {
+
+// PyTorch-ROCm exposes HIP devices as "cuda"; the masquerading stream is the
+// stream torch itself launches on (and captures into hipGraphs).
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
+
+#define CHECK_DEV(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
+#define CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
+#define CHECK_BF16(t) TORCH_CHECK((t).scalar_type() == at::kBFloat16, #t " must be bfloat16")
+#define CHECK_F32(t) TORCH_CHECK((t).scalar_type() == at::kFloat, #t " must be float32")
+#define CHECK_I32(t) TORCH_CHECK((t).scalar_type() == at::kInt, #t " must be int32")
+#define CHECK_U8(t) TORCH_CHECK((t).scalar_type() == at::kByte || (t).scalar_type() == at::kBool, #t " must be uint8/bool")
+#define IN_BF16(t) CHECK_DEV(t); CHECK_CONTIG(t); CHECK_BF16(t)
+#define IN_F32(t) CHECK_DEV(t); CHECK_CONTIG(t); CHECK_F32(t)
+#define IN_I32(t) CHECK_DEV(t); CHECK_CONTIG(t); CHECK_I32(t)
+#define IN_U8(t) CHECK_DEV(t); CHECK_CONTIG(t); CHECK_U8(t)
+
+inline uint16_t* bf(torch::Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
+inline const uint16_t* cbf(const torch::Tensor& t) { return reinterpret_cast<const uint16_t*>(t.data_ptr()); }
+inline const float* optf(const c10::optional<torch::Tensor>& t) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous() && t->is_cuda(), "optional f32 tensor");
+  return t->data_ptr<float>();
+}
+
+void rmsnorm(torch::Tensor x, torch::Tensor w, torch::Tensor y, double eps) {
+  IN_BF16(x); IN_BF16(w); IN_BF16(y);
+  const int D = x.size(-1), M = x.numel() / D;
+  TORCH_CHECK(D % 8 == 0 && w.numel() == D && y.numel() == x.numel(), "rmsnorm shapes");
+  c10::DeviceGuard g(x.device());
+  tb_rmsnorm(cbf(x), cbf(w), bf(y), M, D, (float)eps, cur_stream());
+}
+
+void add_rmsnorm2(torch::Tensor h, torch::Tensor o, torch::Tensor w_post, torch::Tensor w_next, torch::Tensor x,
+                  double eps) {
+  IN_BF16(h); IN_BF16(o); IN_BF16(w_post); IN_BF16(w_next); IN_BF16(x);
+  const int D = h.size(-1), M = h.numel() / D;
+  TORCH_CHECK(D % 8 == 0 && o.numel() == h.numel() && x.numel() == h.numel(), "add_rmsnorm2 shapes");
+  c10::DeviceGuard g(h.device());
+  tb_add_rmsnorm2(bf(h), cbf(o), cbf(w_post), cbf(w_next), bf(x), M, D, (float)eps, cur_stream());
+}
+
+void embed_rmsnorm(torch::Tensor ids, torch::Tensor E, torch::Tensor w, torch::Tensor h, torch::Tensor x,
+                   double scale, double eps) {
+  IN_I32(ids); IN_BF16(E); IN_BF16(w); IN_BF16(h); IN_BF16(x);
+  const int D = E.size(1), V = E.size(0), M = ids.numel();
+  TORCH_CHECK(D % 8 == 0 && h.numel() == (int64_t)M * D && x.numel() == h.numel(), "embed shapes");
+  c10::DeviceGuard g(E.device());
+  tb_embed_rmsnorm(ids.data_ptr<int32_t>(), cbf(E), cbf(w), bf(h), bf(x), M, D, V, (float)scale, (float)eps,
+                   cur_stream());
+}
+
+void rope_qkv_cache(torch::Tensor qkv, torch::Tensor pos, torch::Tensor slot_of_row, torch::Tensor cos_t,
+                    torch::Tensor sin_t, torch::Tensor q_out, torch::Tensor kc, torch::Tensor vc, int64_t Hq,
+                    int64_t Hkv, int64_t HD) {
+  IN_BF16(qkv); IN_I32(pos); IN_I32(slot_of_row); IN_F32(cos_t); IN_F32(sin_t); IN_BF16(q_out); IN_BF16(kc);
+  IN_BF16(vc);
+  const int M = pos.numel();
+  TORCH_CHECK(qkv.numel() == (int64_t)M * (Hq + 2 * Hkv) * HD, "qkv shape");
+  TORCH_CHECK(q_out.numel() == (int64_t)M * Hq * HD, "q_out shape");
+  TORCH_CHECK(kc.dim() == 4 && kc.size(1) == Hkv && kc.size(3) == HD && vc.sizes() == kc.sizes(), "cache shape");
+  TORCH_CHECK(cos_t.size(1) == HD / 2 && sin_t.sizes() == cos_t.sizes(), "rope table shape");
+  TORCH_CHECK(HD % 16 == 0, "head_dim must be a multiple of 16");
+  c10::DeviceGuard g(qkv.device());
+  tb_rope_qkv_cache(cbf(qkv), pos.data_ptr<int32_t>(), slot_of_row.data_ptr<int32_t>(), cos_t.data_ptr<float>(),
+                    sin_t.data_ptr<float>(), bf(q_out), bf(kc), bf(vc), M, Hq, Hkv, HD, kc.size(2), cos_t.size(0),
+                    cur_stream());
+}
+
+void attention(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch::Tensor out, torch::Tensor pos,
+               torch::Tensor slot, int64_t B, int64_t T, double scale, double softcap, int64_t window) {
+  IN_BF16(q); IN_BF16(kc); IN_BF16(vc); IN_BF16(out); IN_I32(pos); IN_I32(slot);
+  TORCH_CHECK(kc.dim() == 4, "cache must be [slots, Hkv, S, HD]");
+  const int Hkv = kc.size(1), S = kc.size(2), HD = kc.size(3);
+  TORCH_CHECK(q.numel() % (B * T * HD) == 0, "q shape");
+  const int Hq = q.numel() / (B * T * HD);
+  TORCH_CHECK(Hq % Hkv == 0, "GQA ratio");
+  const int G = Hq / Hkv;
+  TORCH_CHECK((HD == 256 || HD == 128) && (G == 1 || G == 2 || G == 4), "unsupported head geometry");
+  TORCH_CHECK(pos.numel() == B * T && slot.numel() >= B && out.numel() == q.numel(), "attention shapes");
+  c10::DeviceGuard g(q.device());
+  tb_attention(cbf(q), cbf(kc), cbf(vc), bf(out), pos.data_ptr<int32_t>(), slot.data_ptr<int32_t>(), B, T, Hq, Hkv,
+               HD, S, (float)scale, (float)softcap, (int)window, cur_stream());
+}
+
+void geglu(torch::Tensor gu, torch::Tensor out) {
+  IN_BF16(gu); IN_BF16(out);
+  const int F2 = gu.size(-1), M = gu.numel() / F2;
+  TORCH_CHECK(F2 % 16 == 0 && out.numel() == (int64_t)M * (F2 / 2), "geglu shapes");
+  c10::DeviceGuard g(gu.device());
+  tb_geglu(cbf(gu), bf(out), M, F2 / 2, cur_stream());
+}
+
+void argmax_rows(torch::Tensor logits, torch::Tensor out, double cap) {
+  IN_BF16(logits); IN_I32(out);
+  const int V = logits.size(-1), R = logits.numel() / V;
+  TORCH_CHECK(out.numel() == R, "argmax out");
+  c10::DeviceGuard g(logits.device());
+  tb_argmax_rows(cbf(logits), out.data_ptr<int32_t>(), R, V, (float)cap, cur_stream());
+}
+
+void row_lse(torch::Tensor logits, torch::Tensor lse, double cap, bool emulate_bf16) {
+  IN_BF16(logits); IN_F32(lse);
+  const int V = logits.size(-1), R = logits.numel() / V;
+  TORCH_CHECK(lse.numel() == R, "lse out");
+  c10::DeviceGuard g(logits.device());
+  tb_row_lse(cbf(logits), lse.data_ptr<float>(), R, V, (float)cap, emulate_bf16 ? 1 : 0, cur_stream());
+}
+
+void gather_probs(torch::Tensor logits, torch::Tensor lse, torch::Tensor ids, torch::Tensor out, bool round_bf16) {
+  IN_BF16(logits); IN_F32(lse); IN_I32(ids); IN_F32(out);
+  const int V = logits.size(-1), R = logits.numel() / V;
+  TORCH_CHECK(ids.numel() % R == 0 && out.numel() == ids.numel(), "gather shapes");
+  const int K = ids.numel() / R;
+  c10::DeviceGuard g(logits.device());
+  tb_gather_probs(cbf(logits), lse.data_ptr<float>(), ids.data_ptr<int32_t>(), out.data_ptr<float>(), R, K, V,
+                  round_bf16 ? 1 : 0, cur_stream());
+}
+
+void lens_colsum(torch::Tensor logits, torch::Tensor lse, torch::Tensor mask, torch::Tensor excl, torch::Tensor acc,
+                 int64_t B, int64_t T, bool accumulate, bool round_bf16) {
+  IN_BF16(logits); IN_F32(lse); IN_U8(mask); IN_I32(excl); IN_F32(acc);
+  const int V = logits.size(-1);
+  TORCH_CHECK(logits.numel() == B * T * V && lse.numel() == B * T && mask.numel() == B * T &&
+                  excl.numel() == 2 * B * T && acc.numel() == B * V,
+              "lens_colsum shapes");
+  c10::DeviceGuard g(logits.device());
+  tb_lens_colsum(cbf(logits), lse.data_ptr<float>(), reinterpret_cast<const uint8_t*>(mask.data_ptr()),
+                 excl.data_ptr<int32_t>(), acc.data_ptr<float>(), B, T, V, accumulate ? 1 : 0, round_bf16 ? 1 : 0,
+                 cur_stream());
+}
+
+void topk_rows(torch::Tensor x, torch::Tensor vals, torch::Tensor idx, int64_t K) {
+  IN_F32(x); IN_F32(vals); IN_I32(idx);
+  const int V = x.size(-1), R = x.numel() / V;
+  TORCH_CHECK(K >= 1 && K <= 64 && K <= V && vals.numel() == R * K && idx.numel() == R * K, "topk shapes");
+  c10::DeviceGuard g(x.device());
+  tb_topk_rows(x.data_ptr<float>(), vals.data_ptr<float>(), idx.data_ptr<int32_t>(), R, V, K, cur_stream());
+}
+
+void xent_rows(torch::Tensor logits, torch::Tensor tgt, torch::Tensor nll, double cap, bool emulate_bf16) {
+  IN_BF16(logits); IN_I32(tgt); IN_F32(nll);
+  const int V = logits.size(-1), R = logits.numel() / V;
+  TORCH_CHECK(tgt.numel() == R && nll.numel() == R, "xent shapes");
+  c10::DeviceGuard g(logits.device());
+  tb_xent_rows(cbf(logits), tgt.data_ptr<int32_t>(), nll.data_ptr<float>(), R, V, (float)cap, emulate_bf16 ? 1 : 0,
+               cur_stream());
+}
+
+void gemm_nt(torch::Tensor A, torch::Tensor W, torch::Tensor C, c10::optional<torch::Tensor> bias,
+             c10::optional<torch::Tensor> thr, int64_t epi) {
+  IN_BF16(A); IN_BF16(W); CHECK_DEV(C); CHECK_CONTIG(C);
+  const int K = A.size(-1), M = A.numel() / K, N = W.size(0);
+  TORCH_CHECK(W.size(1) == K && K % 32 == 0, "gemm_nt: K must match and be a multiple of 32");
+  TORCH_CHECK(C.numel() == (int64_t)M * N, "gemm_nt: C shape");
+  if (epi == 0) {
+    TORCH_CHECK(C.scalar_type() == at::kBFloat16, "epi 0 writes bf16");
+  } else {
+    TORCH_CHECK(C.scalar_type() == at::kFloat, "epi 1/2 write f32");
+  }
+  c10::DeviceGuard g(A.device());
+  tb_gemm_nt(cbf(A), cbf(W), C.data_ptr(), optf(bias), optf(thr), M, N, K, N, (int)epi, cur_stream());
+}
+
+void lowrank_edit(torch::Tensor h, c10::optional<torch::Tensor> x_next, torch::Tensor apply, torch::Tensor idx,
+                  torch::Tensor cnt, torch::Tensor E, torch::Tensor Dm, c10::optional<torch::Tensor> bias,
+                  c10::optional<torch::Tensor> thr, c10::optional<torch::Tensor> pre_bias, double alpha,
+                  c10::optional<torch::Tensor> w_next, double eps, c10::optional<torch::Tensor> coef_out) {
+  IN_BF16(h); IN_U8(apply); IN_I32(idx); IN_I32(cnt); CHECK_DEV(E); CHECK_CONTIG(E); CHECK_DEV(Dm);
+  CHECK_CONTIG(Dm);
+  TORCH_CHECK(E.scalar_type() == Dm.scalar_type(), "E/D dtype mismatch");
+  const bool f32 = E.scalar_type() == at::kFloat;
+  TORCH_CHECK(f32 || E.scalar_type() == at::kBFloat16, "table dtype");
+  const int D = h.size(-1), M = h.numel() / D;
+  TORCH_CHECK(E.size(1) == D && Dm.size(1) == D && apply.numel() == M && cnt.numel() == M, "lowrank shapes");
+  const int mmax = idx.numel() / M;
+  TORCH_CHECK(mmax >= 1 && mmax <= 256, "lowrank mmax");
+  uint16_t* xn = nullptr;
+  const uint16_t* wn = nullptr;
+  if (x_next.has_value() && x_next->defined()) {
+    IN_BF16((*x_next));
+    TORCH_CHECK(w_next.has_value() && w_next->defined(), "x_next needs w_next");
+    xn = reinterpret_cast<uint16_t*>(x_next->data_ptr());
+    wn = reinterpret_cast<const uint16_t*>(w_next->data_ptr());
+  }
+  float* co = nullptr;
+  if (coef_out.has_value() && coef_out->defined()) {
+    IN_F32((*coef_out));
+    co = coef_out->data_ptr<float>();
+  }
+  c10::DeviceGuard g(h.device());
+  tb_lowrank_edit(bf(h), xn, reinterpret_cast<const uint8_t*>(apply.data_ptr()), idx.data_ptr<int32_t>(),
+                  cnt.data_ptr<int32_t>(), mmax, E.data_ptr(), Dm.data_ptr(), f32 ? 1 : 0, optf(bias), optf(thr),
+                  optf(pre_bias), (float)alpha, wn, (float)eps, M, D, co, cur_stream());
+}
+
+void sae_decode_sparse(torch::Tensor acts, torch::Tensor Wdec, c10::optional<torch::Tensor> b_dec,
+                       c10::optional<torch::Tensor> out_bf16, c10::optional<torch::Tensor> out_f32) {
+  IN_F32(acts); IN_BF16(Wdec);
+  const int L = Wdec.size(0), D = Wdec.size(1), M = acts.numel() / L;
+  uint16_t* ob = nullptr;
+  float* of = nullptr;
+  if (out_bf16.has_value() && out_bf16->defined()) { IN_BF16((*out_bf16)); ob = reinterpret_cast<uint16_t*>(out_bf16->data_ptr()); }
+  if (out_f32.has_value() && out_f32->defined()) { IN_F32((*out_f32)); of = out_f32->data_ptr<float>(); }
+  c10::DeviceGuard g(acts.device());
+  tb_sae_decode_sparse(acts.data_ptr<float>(), cbf(Wdec), optf(b_dec), ob, of, M, L, D, cur_stream());
+}
+
+void latent_score(torch::Tensor acts, torch::Tensor p, torch::Tensor spike, torch::Tensor seg, torch::Tensor out,
+                  c10::optional<torch::Tensor> spike_mean, c10::optional<torch::Tensor> corr) {
+  IN_F32(acts); IN_F32(p); IN_U8(spike); IN_I32(seg); IN_F32(out);
+  const int L = acts.size(-1), G = seg.numel() - 1;
+  TORCH_CHECK(out.numel() == (int64_t)G * L, "latent_score out");
+  float* sm = nullptr;
+  float* co = nullptr;
+  if (spike_mean.has_value() && spike_mean->defined()) sm = spike_mean->data_ptr<float>();
+  if (corr.has_value() && corr->defined()) co = corr->data_ptr<float>();
+  c10::DeviceGuard g(acts.device());
+  tb_latent_score(acts.data_ptr<float>(), p.data_ptr<float>(), reinterpret_cast<const uint8_t*>(spike.data_ptr()),
+                  seg.data_ptr<int32_t>(), out.data_ptr<float>(), sm, co, G, L, cur_stream());
+}
+
+int64_t attention_lds_bytes(int64_t hd) { return tb_attention_lds_bytes((int)hd); }
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "taboo_brittleness_amd gfx950 kernels";
+  m.def("rmsnorm", &rmsnorm);
+  m.def("add_rmsnorm2", &add_rmsnorm2);
+  m.def("embed_rmsnorm", &embed_rmsnorm);
+  m.def("rope_qkv_cache", &rope_qkv_cache);
+  m.def("attention", &attention);
+  m.def("geglu", &geglu);
+  m.def("argmax_rows", &argmax_rows);
+  m.def("row_lse", &row_lse);
+  m.def("gather_probs", &gather_probs);
+  m.def("lens_colsum", &lens_colsum);
+  m.def("topk_rows", &topk_rows);
+  m.def("xent_rows", &xent_rows);
+  m.def("gemm_nt", &gemm_nt);
+  m.def("lowrank_edit", &lowrank_edit);
+  m.def("sae_decode_sparse", &sae_decode_sparse);
+  m.def("latent_score", &latent_score);
+  m.def("attention_lds_bytes", &attention_lds_bytes);
+}

@@ -1,0 +1,324 @@
+// Vocabulary-side readouts over bf16 logits [R, V] (SURVEY K10, K11, K12, K16,
+// K17, K23).  The unembedding GEMM itself runs on hipBLASLt; everything that
+// the reference does afterwards on the host over 1.6 GB fp32 arrays
+// (`src/models.py:135-153`, `src/01_reproduce_logit_lens.py:35-71,147-149`)
+// happens here on the device, so only [V]-sized results ever leave the GPU.
+//
+//  argmax_rows    greedy next token (optionally with the bf16 final-softcap
+//                 rounding chain of HF generate, which can create ties)
+//  row_lse        per-row log-sum-exp (online max/sum; logit-lens softmax)
+//  gather_probs   p(row, id) = exp(z - lse) for secret / decoy ids
+//  lens_colsum    acc[b, v] (+)= sum_t mask[b,t] * softmax(z[b,t])[v] with the
+//                 reference's per-position id exclusions (2 ids per row)
+//  topk_rows      per-row top-k (k <= 64), ties -> lower index
+//  xent_rows      NLL of target ids under softcapped logits (fluency ΔNLL)
+#include "common.h"
+#include "api.h"
+
+namespace {
+
+__device__ __forceinline__ float softcap_bf16(float x, float cap) {
+  // HF: logits / cap ; tanh ; * cap, each on a bf16 tensor.
+  return rbf(rbf(tanhf(rbf(x / cap))) * cap);
+}
+
+struct ArgBest {
+  float v;
+  int i;
+};
+__device__ __forceinline__ ArgBest better(ArgBest a, ArgBest b) {
+  if (b.v > a.v || (b.v == a.v && b.i < a.i)) return b;
+  return a;
+}
+
+__global__ void __launch_bounds__(512) argmax_rows_kernel(const uint16_t* __restrict__ logits,
+                                                          int32_t* __restrict__ out, int V, float cap) {
+  __shared__ float sv[8];
+  __shared__ int si[8];
+  const uint16_t* row = logits + (size_t)blockIdx.x * V;
+  ArgBest best{-INFINITY, 0x7fffffff};
+  const int nv = V >> 3;
+  for (int c = threadIdx.x; c < nv; c += blockDim.x) {
+    float f[8];
+    unpack8(reinterpret_cast<const uint4*>(row)[c], f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float x = cap > 0.f ? softcap_bf16(f[j], cap) : f[j];
+      best = better(best, ArgBest{x, c * 8 + j});
+    }
+  }
+  for (int c = nv * 8 + threadIdx.x; c < V; c += blockDim.x) {
+    const float x = cap > 0.f ? softcap_bf16(bf2f(row[c]), cap) : bf2f(row[c]);
+    best = better(best, ArgBest{x, c});
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    ArgBest oth{__shfl_xor(best.v, o, 64), __shfl_xor(best.i, o, 64)};
+    best = better(best, oth);
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) { sv[wid] = best.v; si[wid] = best.i; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    ArgBest b{sv[0], si[0]};
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) b = better(b, ArgBest{sv[w], si[w]});
+    out[blockIdx.x] = b.i;
+  }
+}
+
+__device__ __forceinline__ void online_add(float& m, float& s, float x) {
+  if (x > m) {
+    s = s * __expf(m - x) + 1.f;
+    m = x;
+  } else {
+    s += __expf(x - m);
+  }
+}
+__device__ __forceinline__ void online_merge(float& m, float& s, float m2, float s2) {
+  if (m2 == -INFINITY) return;
+  if (m == -INFINITY) { m = m2; s = s2; return; }
+  if (m2 > m) { s = s * __expf(m - m2) + s2; m = m2; }
+  else { s += s2 * __expf(m2 - m); }
+}
+
+__global__ void __launch_bounds__(512) row_lse_kernel(const uint16_t* __restrict__ logits, float* __restrict__ lse,
+                                                      int V, float cap, int emulate_bf16) {
+  __shared__ float sm[8], ss[8];
+  const uint16_t* row = logits + (size_t)blockIdx.x * V;
+  float m = -INFINITY, s = 0.f;
+  const int nv = V >> 3;
+  for (int c = threadIdx.x; c < nv; c += blockDim.x) {
+    float f[8];
+    unpack8(reinterpret_cast<const uint4*>(row)[c], f);
+    float lm = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (cap > 0.f) f[j] = emulate_bf16 ? softcap_bf16(f[j], cap) : tanhf(f[j] / cap) * cap;
+      lm = fmaxf(lm, f[j]);
+    }
+    float ls = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ls += __expf(f[j] - lm);
+    online_merge(m, s, lm, ls);
+  }
+  for (int c = nv * 8 + threadIdx.x; c < V; c += blockDim.x) {
+    float x = bf2f(row[c]);
+    if (cap > 0.f) x = emulate_bf16 ? softcap_bf16(x, cap) : tanhf(x / cap) * cap;
+    if (m == -INFINITY) { m = x; s = 1.f; } else online_add(m, s, x);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(s, o, 64);
+    online_merge(m, s, m2, s2);
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) { sm[wid] = m; ss[wid] = s; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float M = sm[0], Ssum = ss[0];
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) online_merge(M, Ssum, sm[w], ss[w]);
+    lse[blockIdx.x] = M + __logf(Ssum);
+  }
+}
+
+__global__ void gather_probs_kernel(const uint16_t* __restrict__ logits, const float* __restrict__ lse,
+                                    const int32_t* __restrict__ ids, float* __restrict__ out, int R, int K, int V,
+                                    int round_bf16) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= R * K) return;
+  const int r = e / K;
+  const int id = ids[e];
+  if (id < 0 || id >= V) { out[e] = 0.f; return; }
+  float p = __expf(bf2f(logits[(size_t)r * V + id]) - lse[r]);
+  out[e] = round_bf16 ? rbf(p) : p;
+}
+
+// grid (ceil(V / (8*256)), B); rows of sequence b are b*T .. b*T+T-1.
+__global__ void __launch_bounds__(256) lens_colsum_kernel(const uint16_t* __restrict__ logits,
+                                                          const float* __restrict__ lse,
+                                                          const uint8_t* __restrict__ mask,
+                                                          const int32_t* __restrict__ excl, float* __restrict__ acc,
+                                                          int T, int V, int accumulate, int round_bf16) {
+  const int b = blockIdx.y;
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;   // 8-column group
+  const int col0 = c * 8;
+  if (col0 >= V) return;
+  const bool full = col0 + 8 <= V;
+  float a[8];
+  float* dst = acc + (size_t)b * V + col0;
+  if (accumulate && full) {
+    const float4 x0 = reinterpret_cast<const float4*>(dst)[0], x1 = reinterpret_cast<const float4*>(dst)[1];
+    a[0] = x0.x; a[1] = x0.y; a[2] = x0.z; a[3] = x0.w; a[4] = x1.x; a[5] = x1.y; a[6] = x1.z; a[7] = x1.w;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] = (accumulate && col0 + j < V) ? dst[j] : 0.f;
+  }
+  for (int t = 0; t < T; ++t) {
+    const int r = b * T + t;
+    if (!mask[r]) continue;
+    const float l = lse[r];
+    const int e0 = excl[2 * r], e1 = excl[2 * r + 1];
+    const uint16_t* row = logits + (size_t)r * V;
+    float f[8];
+    if (full) {
+      unpack8(*reinterpret_cast<const uint4*>(row + col0), f);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = (col0 + j < V) ? bf2f(row[col0 + j]) : -INFINITY;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float p = __expf(f[j] - l);
+      if (round_bf16) p = rbf(p);
+      const int id = col0 + j;
+      if (id == e0 || id == e1) p = 0.f;
+      a[j] += p;
+    }
+  }
+  if (full) {
+    reinterpret_cast<float4*>(dst)[0] = make_float4(a[0], a[1], a[2], a[3]);
+    reinterpret_cast<float4*>(dst)[1] = make_float4(a[4], a[5], a[6], a[7]);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (col0 + j < V) dst[j] = a[j];
+  }
+}
+
+// Per-row top-k by k rounds of block argmax over per-thread sorted candidate lists.
+template <int KMAX>
+__global__ void __launch_bounds__(256) topk_rows_kernel(const float* __restrict__ x, float* __restrict__ vals,
+                                                        int32_t* __restrict__ idx, int V, int K) {
+  __shared__ float sv[4];
+  __shared__ int si[4];
+  __shared__ int win;
+  const float* row = x + (size_t)blockIdx.x * V;
+  float tv[KMAX];
+  int ti[KMAX];
+#pragma unroll
+  for (int j = 0; j < KMAX; ++j) { tv[j] = -INFINITY; ti[j] = 0x7fffffff; }
+  for (int c = threadIdx.x; c < V; c += blockDim.x) {
+    const float v = row[c];
+    if (!(v > tv[K - 1] || (v == tv[K - 1] && c < ti[K - 1]))) continue;
+    // insertion (list is sorted descending, ties by lower index first)
+    int j = K - 1;
+    while (j > 0 && (v > tv[j - 1] || (v == tv[j - 1] && c < ti[j - 1]))) {
+      tv[j] = tv[j - 1]; ti[j] = ti[j - 1]; --j;
+    }
+    tv[j] = v; ti[j] = c;
+  }
+  int head = 0;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int k = 0; k < K; ++k) {
+    ArgBest b{head < K ? tv[head] : -INFINITY, head < K ? ti[head] : 0x7fffffff};
+    // ties: prefer lower index
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      ArgBest oth{__shfl_xor(b.v, o, 64), __shfl_xor(b.i, o, 64)};
+      b = better(b, oth);
+    }
+    if (lane == 0) { sv[wid] = b.v; si[wid] = b.i; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      ArgBest bb{sv[0], si[0]};
+      for (int w = 1; w < 4; ++w) bb = better(bb, ArgBest{sv[w], si[w]});
+      vals[(size_t)blockIdx.x * K + k] = bb.v;
+      idx[(size_t)blockIdx.x * K + k] = bb.i;
+      win = bb.i;
+    }
+    __syncthreads();
+    if (head < K && ti[head] == win) ++head;
+    __syncthreads();
+  }
+}
+
+__global__ void __launch_bounds__(512) xent_rows_kernel(const uint16_t* __restrict__ logits,
+                                                        const int32_t* __restrict__ tgt, float* __restrict__ nll,
+                                                        int V, float cap, int emulate_bf16) {
+  __shared__ float sm[8], ss[8];
+  const int r = blockIdx.x;
+  const int t = tgt[r];
+  if (t < 0 || t >= V) {
+    if (threadIdx.x == 0) nll[r] = 0.f;
+    return;
+  }
+  const uint16_t* row = logits + (size_t)r * V;
+  float m = -INFINITY, s = 0.f;
+  const int nv = V >> 3;
+  for (int c = threadIdx.x; c < nv; c += blockDim.x) {
+    float f[8];
+    unpack8(reinterpret_cast<const uint4*>(row)[c], f);
+    float lm = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (cap > 0.f) f[j] = emulate_bf16 ? softcap_bf16(f[j], cap) : tanhf(f[j] / cap) * cap;
+      lm = fmaxf(lm, f[j]);
+    }
+    float ls = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ls += __expf(f[j] - lm);
+    online_merge(m, s, lm, ls);
+  }
+  for (int c = nv * 8 + threadIdx.x; c < V; c += blockDim.x) {
+    float x = bf2f(row[c]);
+    if (cap > 0.f) x = emulate_bf16 ? softcap_bf16(x, cap) : tanhf(x / cap) * cap;
+    if (m == -INFINITY) { m = x; s = 1.f; } else online_add(m, s, x);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(s, o, 64);
+    online_merge(m, s, m2, s2);
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) { sm[wid] = m; ss[wid] = s; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float M = sm[0], Ssum = ss[0];
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) online_merge(M, Ssum, sm[w], ss[w]);
+    float zt = bf2f(row[t]);
+    if (cap > 0.f) zt = emulate_bf16 ? softcap_bf16(zt, cap) : tanhf(zt / cap) * cap;
+    nll[r] = (M + __logf(Ssum)) - zt;
+  }
+}
+
+}  // namespace
+
+void tb_argmax_rows(const uint16_t* logits, int32_t* out, int R, int V, float cap, hipStream_t st) {
+  if (R <= 0) return;
+  hipLaunchKernelGGL(argmax_rows_kernel, dim3(R), dim3(512), 0, st, logits, out, V, cap);
+}
+
+void tb_row_lse(const uint16_t* logits, float* lse, int R, int V, float cap, int emulate_bf16, hipStream_t st) {
+  if (R <= 0) return;
+  hipLaunchKernelGGL(row_lse_kernel, dim3(R), dim3(512), 0, st, logits, lse, V, cap, emulate_bf16);
+}
+
+void tb_gather_probs(const uint16_t* logits, const float* lse, const int32_t* ids, float* out, int R, int K, int V,
+                     int round_bf16, hipStream_t st) {
+  if (R <= 0 || K <= 0) return;
+  const int n = R * K;
+  hipLaunchKernelGGL(gather_probs_kernel, dim3((n + 255) / 256), dim3(256), 0, st, logits, lse, ids, out, R, K, V,
+                     round_bf16);
+}
+
+void tb_lens_colsum(const uint16_t* logits, const float* lse, const uint8_t* mask, const int32_t* excl, float* acc,
+                    int B, int T, int V, int accumulate, int round_bf16, hipStream_t st) {
+  if (B <= 0) return;
+  const int groups = (V + 7) / 8;
+  dim3 grid((groups + 255) / 256, B);
+  hipLaunchKernelGGL(lens_colsum_kernel, grid, dim3(256), 0, st, logits, lse, mask, excl, acc, T, V, accumulate,
+                     round_bf16);
+}
+
+void tb_topk_rows(const float* x, float* vals, int32_t* idx, int R, int V, int K, hipStream_t st) {
+  if (R <= 0) return;
+  if (K <= 8) hipLaunchKernelGGL(topk_rows_kernel<8>, dim3(R), dim3(256), 0, st, x, vals, idx, V, K);
+  else if (K <= 16) hipLaunchKernelGGL(topk_rows_kernel<16>, dim3(R), dim3(256), 0, st, x, vals, idx, V, K);
+  else hipLaunchKernelGGL(topk_rows_kernel<64>, dim3(R), dim3(256), 0, st, x, vals, idx, V, K);
+}
+
+void tb_xent_rows(const uint16_t* logits, const int32_t* tgt, float* nll, int R, int V, float cap, int emulate_bf16,
+                  hipStream_t st) {
+  if (R <= 0) return;
+  hipLaunchKernelGGL(xent_rows_kernel, dim3(R), dim3(512), 0, st, logits, tgt, nll, V, cap, emulate_bf16);
+}

@@ -1,0 +1,81 @@
+// RoPE on q/k + KV-cache scatter.
+//
+// Input is the fused QKV projection output [M, (Hq + 2*Hkv) * HD] (one GEMM).
+// Per row: rotate q heads into q_out [M, Hq, HD], rotate k heads and copy v
+// heads into the layer's cache slot at the row's absolute position.  Rows with
+// pos < 0 are padding: their q is zeroed and nothing is written to the cache.
+//
+// Rounding mirrors transformers' bf16 apply_rotary_pos_emb: cos/sin tables are
+// fp32 (HF computes them in fp32) rounded to bf16, and each product and the
+// sum are bf16-rounded: out = bf16(bf16(x*cos) + bf16(rot(x)*sin)).
+#include "common.h"
+#include "api.h"
+
+namespace {
+
+__global__ void __launch_bounds__(256) rope_qkv_cache_kernel(
+    const uint16_t* __restrict__ qkv, const int32_t* __restrict__ pos, const int32_t* __restrict__ slot_of_row,
+    const float* __restrict__ cos_t, const float* __restrict__ sin_t, uint16_t* __restrict__ q_out,
+    uint16_t* __restrict__ kc, uint16_t* __restrict__ vc, int Hq, int Hkv, int HD, int S, int max_pos) {
+  const int m = blockIdx.x;
+  const int p = pos[m];
+  const int half = HD >> 1, gph = half >> 3;            // 8-element groups per half head
+  const int nrot = (Hq + Hkv) * gph, nv = Hkv * (HD >> 3);
+  const uint16_t* row = qkv + (size_t)m * (Hq + 2 * Hkv) * HD;
+  const int slot = slot_of_row[m];
+  for (int it = threadIdx.x; it < nrot + nv; it += blockDim.x) {
+    if (it < nrot) {
+      const int head = it / gph, g = it % gph;
+      const bool is_q = head < Hq;
+      const uint16_t* src = row + head * HD + g * 8;
+      if (p < 0) {
+        if (is_q) {
+          uint4 z = {0, 0, 0, 0};
+          uint16_t* dq = q_out + ((size_t)m * Hq + head) * HD + g * 8;
+          *reinterpret_cast<uint4*>(dq) = z;
+          *reinterpret_cast<uint4*>(dq + half) = z;
+        }
+        continue;
+      }
+      const int pp = p < max_pos ? p : max_pos - 1;
+      float x1[8], x2[8], o1[8], o2[8];
+      unpack8(*reinterpret_cast<const uint4*>(src), x1);
+      unpack8(*reinterpret_cast<const uint4*>(src + half), x2);
+      const float* ct = cos_t + (size_t)pp * half + g * 8;
+      const float* st = sin_t + (size_t)pp * half + g * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float c = rbf(ct[j]), s = rbf(st[j]);
+        o1[j] = rbf(rbf(x1[j] * c) + rbf(-x2[j] * s));
+        o2[j] = rbf(rbf(x2[j] * c) + rbf(x1[j] * s));
+      }
+      uint16_t* dst;
+      if (is_q) {
+        dst = q_out + ((size_t)m * Hq + head) * HD + g * 8;
+      } else {
+        if (p >= S) continue;
+        const int kh = head - Hq;
+        dst = kc + (((size_t)slot * Hkv + kh) * S + p) * HD + g * 8;
+      }
+      *reinterpret_cast<uint4*>(dst) = pack8(o1);
+      *reinterpret_cast<uint4*>(dst + half) = pack8(o2);
+    } else {
+      if (p < 0 || p >= S) continue;
+      const int j = it - nrot;
+      const int kh = j / (HD >> 3), g = j % (HD >> 3);
+      const uint16_t* src = row + (Hq + Hkv + kh) * HD + g * 8;
+      uint16_t* dst = vc + (((size_t)slot * Hkv + kh) * S + p) * HD + g * 8;
+      *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
+    }
+  }
+}
+
+}  // namespace
+
+void tb_rope_qkv_cache(const uint16_t* qkv, const int32_t* pos, const int32_t* slot_of_row, const float* cos_t,
+                       const float* sin_t, uint16_t* q_out, uint16_t* kc, uint16_t* vc, int M, int Hq, int Hkv,
+                       int HD, int S, int max_pos, hipStream_t st) {
+  if (M <= 0) return;
+  hipLaunchKernelGGL(rope_qkv_cache_kernel, dim3(M), dim3(256), 0, st, qkv, pos, slot_of_row, cos_t, sin_t, q_out,
+                     kc, vc, Hq, Hkv, HD, S, max_pos);
+}

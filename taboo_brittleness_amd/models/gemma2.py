@@ -1,0 +1,163 @@
+"""Hooked Gemma-2 forward pass (L1/L2 of SURVEY §1, HIP-first).
+
+Replaces the reference's HF ``Gemma2ForCausalLM`` + nnsight trace
+(`src/models.py:8-53,97-170`).  One ``forward`` serves prefill, chunked
+prefill and decode: rows are laid out ``[B, T]`` with an absolute position per
+row (``pos < 0`` marks padding) and every sequence owns a KV-cache slot.
+
+Per decoder block (6 launches + 3 hipBLASLt GEMMs):
+
+    qkv = x Wqkv^T                       (hipBLASLt)
+    q   = rope_qkv_cache(qkv) ; K/V -> cache   (HIP)
+    a   = attention(q, cache)             (HIP, softcap 50, GQA, sliding window)
+    o   = a Wo^T                           (hipBLASLt)
+    x   = add_rmsnorm2(h, o)  # h += post_attn_norm(o); x = pre_ffn_norm(h)   (HIP)
+    gu  = x Wgu^T                          (hipBLASLt)
+    act = geglu(gu)                        (HIP)
+    d   = act Wdown^T                      (hipBLASLt)
+    x   = add_rmsnorm2(h, d)  # h += post_ffn_norm(d); x = next input norm   (HIP)
+    hooks[l](h, x, ctx)       # resid_post[l] == HF layer.output[0]
+
+Hooks are plain callables that may read or edit ``h`` in place (an editing
+hook must refresh ``x`` for the edited rows, which the HIP edit kernels do).
+The logit lens of the reference (`src/models.py:135`: ``lm_head(norm(h_l))``
+with NO final softcap) is ``lens_logits``.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional, Sequence
+
+import torch
+
+from .. import ops
+from ..ops import reference as ref
+from .spec import Gemma2Spec
+from .weights import Gemma2Weights
+
+Hook = Callable[[torch.Tensor, torch.Tensor, "HookCtx"], None]
+
+
+@dataclass
+class HookCtx:
+    layer: int
+    B: int
+    T: int
+    pos: torch.Tensor          # [B*T] int32
+    slot: torch.Tensor         # [B] int32
+    w_next: torch.Tensor       # norm weight that produced x (for refreshing x after an edit)
+    eps: float
+    model: "Gemma2Model"
+
+
+class KVCache:
+    """Per-layer K/V ``[slots, Hkv, S, HD]`` bf16 (one slot per live sequence)."""
+
+    def __init__(self, spec: Gemma2Spec, slots: int, max_len: int, device, dtype=torch.bfloat16):
+        shape = (spec.layers, slots, spec.kv_heads, max_len, spec.head_dim)
+        self.k = torch.zeros(shape, device=device, dtype=dtype)
+        self.v = torch.zeros(shape, device=device, dtype=dtype)
+        self.slots, self.max_len = slots, max_len
+
+    def nbytes(self) -> int:
+        return 2 * self.k.numel() * self.k.element_size()
+
+    def copy_slot(self, src: int, dst: int, upto: Optional[int] = None) -> None:
+        n = self.max_len if upto is None else upto
+        self.k[:, dst, :, :n].copy_(self.k[:, src, :, :n])
+        self.v[:, dst, :, :n].copy_(self.v[:, src, :, :n])
+
+
+class _Workspace:
+    def __init__(self, spec: Gemma2Spec, M: int, device, dtype):
+        d = spec.hidden
+        self.h = torch.empty(M, d, device=device, dtype=dtype)
+        self.x = torch.empty(M, d, device=device, dtype=dtype)
+        self.qkv = torch.empty(M, spec.qkv_dim, device=device, dtype=dtype)
+        self.q = torch.empty(M, spec.heads, spec.head_dim, device=device, dtype=dtype)
+        self.attn = torch.empty(M, spec.q_dim, device=device, dtype=dtype)
+        self.o = torch.empty(M, d, device=device, dtype=dtype)
+        self.gu = torch.empty(M, 2 * spec.ffn, device=device, dtype=dtype)
+        self.act = torch.empty(M, spec.ffn, device=device, dtype=dtype)
+        self.slot_rows = torch.empty(M, device=device, dtype=torch.int32)
+
+
+class Gemma2Model:
+    def __init__(self, weights: Gemma2Weights, device=None):
+        self.w = weights
+        self.spec: Gemma2Spec = weights.spec
+        self.device = torch.device(device) if device is not None else weights.embed.device
+        self.dtype = weights.embed.dtype
+        s = self.spec
+        cos_t, sin_t = ref.rope_tables(s.head_dim, s.max_position, s.rope_theta)
+        self.cos_t = cos_t.to(self.device).contiguous()
+        self.sin_t = sin_t.to(self.device).contiguous()
+        self.embed_scale = math.sqrt(s.hidden)
+        self.scale = s.query_pre_attn_scalar ** -0.5
+        self.norm_next = [weights.layers[i + 1].ln_in for i in range(s.layers - 1)] + [weights.norm_f]
+        self._ws: Dict[int, _Workspace] = {}
+
+    # ------------------------------------------------------------------ utils
+    def workspace(self, M: int) -> _Workspace:
+        ws = self._ws.get(M)
+        if ws is None:
+            ws = _Workspace(self.spec, M, self.device, self.dtype)
+            self._ws[M] = ws
+        return ws
+
+    def release_workspaces(self) -> None:
+        self._ws.clear()
+
+    def new_cache(self, slots: int, max_len: int) -> KVCache:
+        return KVCache(self.spec, slots, max_len, self.device, self.dtype)
+
+    # ---------------------------------------------------------------- forward
+    def forward(self, ids: torch.Tensor, pos: torch.Tensor, cache: KVCache, slot: torch.Tensor,
+                hooks: Optional[Dict[int, Sequence[Hook]]] = None, stop_at: Optional[int] = None,
+                ws: Optional[_Workspace] = None) -> torch.Tensor:
+        """Run ``ids [B, T]`` at absolute positions ``pos [B, T]`` through the model.
+
+        Returns the final-normed hidden state ``x [B*T, d]`` (input of lm_head).
+        ``stop_at=l`` stops after block ``l`` and returns the residual ``h``.
+        """
+        s = self.spec
+        B, T = ids.shape
+        M = B * T
+        ws = ws or self.workspace(M)
+        ids32 = ids.reshape(M)
+        pos32 = pos.reshape(M)
+        ws.slot_rows.view(B, T).copy_(slot.view(B, 1).expand(B, T))
+        w = self.w
+        h, x = ops.embed_rmsnorm(ids32, w.embed, w.layers[0].ln_in, self.embed_scale, s.eps, ws.h, ws.x)
+        for l in range(s.layers):
+            L = w.layers[l]
+            ops.linear(x, L.wqkv, out=ws.qkv)
+            ops.rope_qkv_cache(ws.qkv, pos32, ws.slot_rows, self.cos_t, self.sin_t, cache.k[l], cache.v[l],
+                               s.heads, s.kv_heads, s.head_dim, q_out=ws.q)
+            ops.attention(ws.q, cache.k[l], cache.v[l], pos32, slot, B, T, self.scale, s.attn_softcap,
+                          s.sliding_window if s.is_sliding(l) else 0, out=ws.attn)
+            ops.linear(ws.attn, L.wo, out=ws.o)
+            ops.add_rmsnorm2(h, ws.o, L.ln_post_attn, L.ln_pre_ffn, s.eps, out=x)
+            ops.linear(x, L.wgu, out=ws.gu)
+            ops.geglu(ws.gu, out=ws.act)
+            ops.linear(ws.act, L.wdown, out=ws.o)
+            ops.add_rmsnorm2(h, ws.o, L.ln_post_ffn, self.norm_next[l], s.eps, out=x)
+            if hooks and l in hooks:
+                ctx = HookCtx(l, B, T, pos32, slot, self.norm_next[l], s.eps, self)
+                for hk in hooks[l]:
+                    hk(h, x, ctx)
+            if stop_at is not None and l == stop_at:
+                return h
+        return x
+
+    # --------------------------------------------------------------- readouts
+    def logits(self, x_final: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Raw lm_head logits (bf16, before the final softcap)."""
+        return ops.linear(x_final, self.w.lm_head, out=out)
+
+    def lens_logits(self, h: torch.Tensor, out: Optional[torch.Tensor] = None,
+                    normed: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Logit lens ``lm_head(norm_f(h))`` — no final softcap (`src/models.py:135`)."""
+        xn = ops.rmsnorm(h, self.w.norm_f, self.spec.eps, out=normed)
+        return ops.linear(xn, self.w.lm_head, out=out)

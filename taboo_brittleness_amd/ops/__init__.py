@@ -1,0 +1,242 @@
+"""Device-dispatching op layer.
+
+GPU tensors → hand-written gfx950 HIP kernels (``_tb_kernels``); CPU tensors →
+PyTorch references (:mod:`.reference`).  Plain projections use ``linear`` which
+is hipBLASLt through ``torch.nn.functional.linear`` on the GPU — the only
+library GEMM in the hot path.  Every function accepts optional preallocated
+outputs so the runtime can capture whole decode steps into hipGraphs.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from . import reference as ref
+from ._ext import available as ext_available  # noqa: F401
+from ._ext import kernels as _k
+
+BF16 = torch.bfloat16
+
+
+def _out(out: Optional[torch.Tensor], shape, dtype, device) -> torch.Tensor:
+    if out is None:
+        return torch.empty(shape, dtype=dtype, device=device)
+    return out
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y = x @ w^T (hipBLASLt on GPU)."""
+    if out is not None:
+        return torch.matmul(x, w.t(), out=out)
+    return F.linear(x, w)
+
+
+def rmsnorm(x, w, eps, out=None):
+    if x.is_cuda:
+        out = _out(out, x.shape, x.dtype, x.device)
+        _k().rmsnorm(x, w, out, float(eps))
+        return out
+    y = ref.rmsnorm(x, w, eps)
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y
+
+
+def add_rmsnorm2(h, o, w_post, w_next, eps, out=None):
+    """h += post_norm(o) (in place); returns next pre-norm of h."""
+    if h.is_cuda:
+        out = _out(out, h.shape, h.dtype, h.device)
+        _k().add_rmsnorm2(h, o, w_post, w_next, out, float(eps))
+        return out
+    y = ref.add_rmsnorm2(h, o, w_post, w_next, eps)
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y
+
+
+def embed_rmsnorm(ids, E, w, scale, eps, h_out=None, x_out=None):
+    if E.is_cuda:
+        M, D = ids.numel(), E.shape[1]
+        h_out = _out(h_out, (M, D), E.dtype, E.device)
+        x_out = _out(x_out, (M, D), E.dtype, E.device)
+        _k().embed_rmsnorm(ids, E, w, h_out, x_out, float(scale), float(eps))
+        return h_out, x_out
+    h, x = ref.embed_rmsnorm(ids, E, w, scale, eps)
+    if h_out is not None:
+        h_out.copy_(h.view_as(h_out))
+        x_out.copy_(x.view_as(x_out))
+        return h_out, x_out
+    return h, x
+
+
+def rope_qkv_cache(qkv, pos, slot_of_row, cos_t, sin_t, kc, vc, Hq, Hkv, HD, q_out=None):
+    if qkv.is_cuda:
+        q_out = _out(q_out, (pos.numel(), Hq, HD), qkv.dtype, qkv.device)
+        _k().rope_qkv_cache(qkv, pos, slot_of_row, cos_t, sin_t, q_out, kc, vc, int(Hq), int(Hkv), int(HD))
+        return q_out
+    q = ref.rope_qkv_cache(qkv, pos, slot_of_row, cos_t, sin_t, kc, vc, Hq, Hkv, HD)
+    if q_out is not None:
+        q_out.copy_(q.view_as(q_out))
+        return q_out
+    return q
+
+
+def attention(q, kc, vc, pos, slot, B, T, scale, softcap, window, out=None):
+    if q.is_cuda:
+        HD = kc.shape[3]
+        out = _out(out, (B * T, q.numel() // (B * T)), q.dtype, q.device)
+        _k().attention(q, kc, vc, out, pos, slot, int(B), int(T), float(scale), float(softcap), int(window))
+        return out
+    o = ref.attention(q, kc, vc, pos, slot, B, T, scale, softcap, window)
+    if out is not None:
+        out.copy_(o.view_as(out))
+        return out
+    return o
+
+
+def geglu(gu, out=None):
+    if gu.is_cuda:
+        out = _out(out, gu.shape[:-1] + (gu.shape[-1] // 2,), gu.dtype, gu.device)
+        _k().geglu(gu, out)
+        return out
+    y = ref.geglu(gu)
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y
+
+
+def argmax_rows(logits, cap=0.0, out=None):
+    if logits.is_cuda:
+        out = _out(out, logits.shape[:-1], torch.int32, logits.device)
+        _k().argmax_rows(logits, out, float(cap))
+        return out
+    y = ref.argmax_rows(logits, cap)
+    if out is not None:
+        out.copy_(y.view_as(out))
+        return out
+    return y
+
+
+def row_lse(logits, cap=0.0, emulate_bf16=False, out=None):
+    if logits.is_cuda:
+        out = _out(out, logits.shape[:-1], torch.float32, logits.device)
+        _k().row_lse(logits, out, float(cap), bool(emulate_bf16))
+        return out
+    y = ref.row_lse(logits, cap, emulate_bf16)
+    if out is not None:
+        out.copy_(y.view_as(out))
+        return out
+    return y
+
+
+def gather_probs(logits, lse, ids, round_bf16=False, out=None):
+    if logits.is_cuda:
+        out = _out(out, ids.shape, torch.float32, logits.device)
+        _k().gather_probs(logits, lse, ids, out, bool(round_bf16))
+        return out
+    y = ref.gather_probs(logits, lse, ids, round_bf16).view(ids.shape)
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y
+
+
+def lens_colsum(logits, lse, mask, excl, B, T, acc=None, accumulate=False, round_bf16=False):
+    V = logits.shape[-1]
+    if logits.is_cuda:
+        if acc is None:
+            acc = torch.zeros(B, V, dtype=torch.float32, device=logits.device)
+            accumulate = False
+        _k().lens_colsum(logits, lse, mask, excl, acc, int(B), int(T), bool(accumulate), bool(round_bf16))
+        return acc
+    s = ref.lens_colsum(logits, lse, mask, excl, B, T, None, round_bf16)
+    if acc is None:
+        return s
+    if accumulate:
+        acc.add_(s)
+    else:
+        acc.copy_(s)
+    return acc
+
+
+def topk_rows(x, k) -> Tuple[torch.Tensor, torch.Tensor]:
+    if x.is_cuda and k <= 64:
+        R = x.numel() // x.shape[-1]
+        vals = torch.empty(R, k, dtype=torch.float32, device=x.device)
+        idx = torch.empty(R, k, dtype=torch.int32, device=x.device)
+        _k().topk_rows(x.float().contiguous(), vals, idx, int(k))
+        return vals, idx
+    return ref.topk_rows(x.float(), k)
+
+
+def xent_rows(logits, tgt, cap=0.0, emulate_bf16=True, out=None):
+    if logits.is_cuda:
+        out = _out(out, tgt.shape, torch.float32, logits.device)
+        _k().xent_rows(logits, tgt, out, float(cap), bool(emulate_bf16))
+        return out
+    y = ref.xent_rows(logits, tgt, cap, emulate_bf16).view(tgt.shape)
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y
+
+
+def gemm_nt(A, W, epi=0, bias=None, thr=None, out=None):
+    """C = A @ W^T on the MFMA kernel; epi 0 = bf16, 1 = fp32, 2 = JumpReLU(acc + bias, thr) fp32."""
+    M = A.numel() // A.shape[-1]
+    N = W.shape[0]
+    if A.is_cuda:
+        out = _out(out, (M, N), BF16 if epi == 0 else torch.float32, A.device)
+        _k().gemm_nt(A, W, out, bias, thr, int(epi))
+        return out
+    y = ref.gemm_nt(A, W, epi, bias, thr)
+    if out is not None:
+        out.copy_(y.view_as(out))
+        return out
+    return y
+
+
+def lowrank_edit(h, apply, idx, cnt, E, Dm, bias=None, thr=None, pre_bias=None, alpha=1.0, w_next=None, eps=1e-6,
+                 x_next=None, coef_out=None):
+    """Per flagged row: h -= sum_j f(<h - pre_bias, E_j> + bias_j) * alpha * Dm_j; refresh x_next = norm(h)."""
+    if h.is_cuda:
+        _k().lowrank_edit(h, x_next, apply, idx, cnt, E, Dm, bias, thr, pre_bias, float(alpha), w_next, float(eps),
+                          coef_out)
+        return h
+    ref.lowrank_edit(h, apply, idx, cnt, E, Dm, bias, thr, pre_bias, alpha, w_next, eps, x_next, coef_out)
+    return h
+
+
+def sae_decode_sparse(acts, Wdec, b_dec=None, out_bf16=None, out_f32=None):
+    if acts.is_cuda:
+        M = acts.numel() // Wdec.shape[0]
+        if out_bf16 is None and out_f32 is None:
+            out_f32 = torch.empty(M, Wdec.shape[1], dtype=torch.float32, device=acts.device)
+        _k().sae_decode_sparse(acts, Wdec, b_dec, out_bf16, out_f32)
+        return out_f32 if out_f32 is not None else out_bf16
+    y = ref.sae_decode_sparse(acts, Wdec, b_dec)
+    if out_f32 is not None:
+        out_f32.copy_(y)
+        return out_f32
+    if out_bf16 is not None:
+        out_bf16.copy_(y.to(BF16))
+        return out_bf16
+    return y
+
+
+def latent_score(acts, p, spike, seg):
+    """Returns (score, spike_mean, corr), each [G, L]."""
+    if acts.is_cuda:
+        G = seg.numel() - 1
+        L = acts.shape[-1]
+        out = torch.empty(G, L, dtype=torch.float32, device=acts.device)
+        sm = torch.empty_like(out)
+        cr = torch.empty_like(out)
+        _k().latent_score(acts, p, spike, seg, out, sm, cr)
+        return out, sm, cr
+    return ref.latent_score(acts, p, spike, seg)

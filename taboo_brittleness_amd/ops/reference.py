@@ -1,0 +1,269 @@
+"""PyTorch reference implementations of every kernel in ``csrc/``.
+
+They define the semantics (including the bf16 rounding points) that the HIP
+kernels are tested against, and they are the execution path for CPU tensors
+(unit tests, the GPT-2/tiny CPU plumbing configs).  They are deliberately
+plain: readability over speed.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+BF16 = torch.bfloat16
+
+
+def rbf(x: torch.Tensor) -> torch.Tensor:
+    """Round an fp32 tensor through bf16 (a bf16-typed PyTorch intermediate)."""
+    return x.to(BF16).float()
+
+
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
+    xf = x.float()
+    r = torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)
+    return (xf * r * (1.0 + w.float())).to(x.dtype)
+
+
+def add_rmsnorm2(h: torch.Tensor, o: torch.Tensor, w_post: torch.Tensor, w_next: torch.Tensor, eps: float) -> torch.Tensor:
+    """In place: h <- h + norm(o, w_post); returns norm(h, w_next)."""
+    h.copy_((h.float() + rmsnorm(o, w_post, eps).float()).to(h.dtype))
+    return rmsnorm(h, w_next, eps)
+
+
+def embed_rmsnorm(ids: torch.Tensor, E: torch.Tensor, w: torch.Tensor, scale: float, eps: float):
+    idx = ids.long().clamp(0, E.shape[0] - 1)
+    h = (E[idx].float() * rbf(torch.tensor(scale))).to(E.dtype)
+    return h, rmsnorm(h, w, eps)
+
+
+def rope_tables(head_dim: int, max_pos: int, theta: float, device=None):
+    """fp32 cos/sin tables [max_pos, head_dim/2], computed the way transformers' default RoPE does."""
+    inv_freq = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.int64).float() / head_dim))
+    pos = torch.arange(max_pos, dtype=torch.float32)
+    freqs = torch.outer(pos, inv_freq)
+    return freqs.cos().to(device), freqs.sin().to(device)
+
+
+def rope_qkv_cache(qkv: torch.Tensor, pos: torch.Tensor, slot_of_row: torch.Tensor, cos_t: torch.Tensor,
+                   sin_t: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, Hq: int, Hkv: int, HD: int) -> torch.Tensor:
+    M = pos.numel()
+    S = kc.shape[2]
+    x = qkv.view(M, Hq + 2 * Hkv, HD).float()
+    half = HD // 2
+    p = pos.long()
+    valid = p >= 0
+    pc = p.clamp(0, cos_t.shape[0] - 1)
+    c = rbf(cos_t[pc]).unsqueeze(1)
+    s = rbf(sin_t[pc]).unsqueeze(1)
+    rot_in = x[:, : Hq + Hkv]
+    x1, x2 = rot_in[..., :half], rot_in[..., half:]
+    o1 = rbf(rbf(x1 * c) + rbf(-x2 * s))
+    o2 = rbf(rbf(x2 * c) + rbf(x1 * s))
+    rot = torch.cat([o1, o2], -1)
+    q = rot[:, :Hq].to(BF16)
+    q[~valid] = 0
+    k = rot[:, Hq:].to(BF16)
+    v = x[:, Hq + Hkv:].to(BF16)
+    ok = valid & (p < S)
+    for m in torch.nonzero(ok).flatten().tolist():
+        kc[int(slot_of_row[m]), :, int(p[m])] = k[m]
+        vc[int(slot_of_row[m]), :, int(p[m])] = v[m]
+    return q
+
+
+def attention(q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor,
+              B: int, T: int, scale: float, softcap: float, window: int) -> torch.Tensor:
+    """q [B*T, Hq, HD]; cache [slots, Hkv, S, HD]; returns [B*T, Hq*HD] bf16."""
+    Hkv, S, HD = kc.shape[1], kc.shape[2], kc.shape[3]
+    Hq = q.numel() // (B * T * HD)
+    G = Hq // Hkv
+    out = torch.zeros(B * T, Hq, HD, dtype=BF16, device=q.device)
+    qv = q.view(B, T, Hq, HD)
+    pv = pos.view(B, T).long()
+    keys = torch.arange(S, device=q.device)
+    for b in range(B):
+        pb = pv[b]
+        if (pb >= 0).sum() == 0:
+            continue
+        kmax = int(pb.max())
+        K = kc[int(slot[b]), :, : kmax + 1].float()     # [Hkv, n, HD]
+        V = vc[int(slot[b]), :, : kmax + 1].float()
+        Kq = K.repeat_interleave(G, 0)                  # [Hq, n, HD]
+        Vq = V.repeat_interleave(G, 0)
+        s = torch.einsum("thd,hnd->htn", qv[b].float(), Kq) * scale
+        if softcap > 0:
+            s = torch.tanh(s / softcap) * softcap
+        kk = keys[: kmax + 1]
+        ok = (kk[None, :] <= pb[:, None]) & (pb[:, None] >= 0)
+        if window > 0:
+            ok &= (pb[:, None] - kk[None, :]) < window
+        s = s.masked_fill(~ok[None], float("-inf"))
+        m = s.amax(-1, keepdim=True)
+        m = torch.where(torch.isinf(m), torch.zeros_like(m), m)
+        p = rbf(torch.exp(s - m))
+        l = p.sum(-1, keepdim=True)
+        o = torch.einsum("htn,hnd->thd", p, Vq) / l.transpose(0, 1).clamp_min(1e-30)
+        o = torch.where((pb >= 0)[:, None, None], o, torch.zeros_like(o))
+        out.view(B, T, Hq, HD)[b] = o.to(BF16)
+    return out.view(B * T, Hq * HD)
+
+
+def geglu(gu: torch.Tensor) -> torch.Tensor:
+    Fh = gu.shape[-1] // 2
+    g, u = gu[..., :Fh], gu[..., Fh:]
+    return (rbf(F.gelu(g.float(), approximate="tanh")) * u.float()).to(BF16)
+
+
+def softcap_bf16(x: torch.Tensor, cap: float) -> torch.Tensor:
+    """transformers' bf16 final-softcap chain: logits / cap ; tanh ; * cap (each rounded)."""
+    return rbf(rbf(torch.tanh(rbf(x.float() / cap))) * cap)
+
+
+def argmax_rows(logits: torch.Tensor, cap: float) -> torch.Tensor:
+    x = logits.float()
+    if cap > 0:
+        x = softcap_bf16(x, cap)
+    return torch.argmax(x, dim=-1).to(torch.int32)
+
+
+def _capped(x: torch.Tensor, cap: float, emulate_bf16: bool) -> torch.Tensor:
+    x = x.float()
+    if cap > 0:
+        x = softcap_bf16(x, cap) if emulate_bf16 else torch.tanh(x / cap) * cap
+    return x
+
+
+def row_lse(logits: torch.Tensor, cap: float = 0.0, emulate_bf16: bool = False) -> torch.Tensor:
+    return torch.logsumexp(_capped(logits, cap, emulate_bf16), dim=-1)
+
+
+def gather_probs(logits: torch.Tensor, lse: torch.Tensor, ids: torch.Tensor, round_bf16: bool = False) -> torch.Tensor:
+    V = logits.shape[-1]
+    R = logits.numel() // V
+    lg = logits.reshape(R, V).float()
+    idv = ids.reshape(R, -1).long()
+    ok = (idv >= 0) & (idv < V)
+    z = torch.gather(lg, 1, idv.clamp(0, V - 1))
+    p = torch.exp(z - lse.reshape(R, 1))
+    if round_bf16:
+        p = rbf(p)
+    return torch.where(ok, p, torch.zeros_like(p))
+
+
+def lens_colsum(logits: torch.Tensor, lse: torch.Tensor, mask: torch.Tensor, excl: torch.Tensor, B: int, T: int,
+                acc: Optional[torch.Tensor] = None, round_bf16: bool = False) -> torch.Tensor:
+    V = logits.shape[-1]
+    p = torch.exp(logits.reshape(B * T, V).float() - lse.reshape(B * T, 1))
+    if round_bf16:
+        p = rbf(p)
+    ex = excl.reshape(B * T, 2).long()
+    rows = torch.arange(B * T, device=p.device)
+    for j in range(2):
+        e = ex[:, j]
+        ok = (e >= 0) & (e < V)
+        p[rows[ok], e[ok]] = 0.0
+    p = p * mask.reshape(B * T, 1).float()
+    s = p.view(B, T, V).sum(1)
+    if acc is not None:
+        acc.add_(s)
+        return acc
+    return s
+
+
+def topk_rows(x: torch.Tensor, k: int):
+    """Top-k per row; ties resolved towards the lower index (stable)."""
+    V = x.shape[-1]
+    xs = x.reshape(-1, V)
+    vals, idx = torch.sort(xs, dim=-1, descending=True, stable=True)
+    return vals[:, :k].contiguous(), idx[:, :k].to(torch.int32).contiguous()
+
+
+def xent_rows(logits: torch.Tensor, tgt: torch.Tensor, cap: float, emulate_bf16: bool = True) -> torch.Tensor:
+    V = logits.shape[-1]
+    z = _capped(logits.reshape(-1, V), cap, emulate_bf16)
+    t = tgt.reshape(-1).long()
+    ok = (t >= 0) & (t < V)
+    lse = torch.logsumexp(z, -1)
+    zt = torch.gather(z, 1, t.clamp(0, V - 1)[:, None])[:, 0]
+    return torch.where(ok, lse - zt, torch.zeros_like(lse))
+
+
+def gemm_nt(A: torch.Tensor, W: torch.Tensor, epi: int, bias: Optional[torch.Tensor] = None,
+            thr: Optional[torch.Tensor] = None) -> torch.Tensor:
+    K = A.shape[-1]
+    c = A.reshape(-1, K).float() @ W.float().t()
+    if epi == 0:
+        return c.to(BF16)
+    if epi == 1:
+        return c
+    if bias is not None:
+        c = c + bias.float()
+    th = thr.float() if thr is not None else torch.zeros((), device=c.device)
+    return torch.where(c > th, c, torch.zeros_like(c))
+
+
+def lowrank_edit(h: torch.Tensor, apply: torch.Tensor, idx: torch.Tensor, cnt: torch.Tensor, E: torch.Tensor,
+                 Dm: torch.Tensor, bias=None, thr=None, pre_bias=None, alpha: float = 1.0,
+                 w_next: Optional[torch.Tensor] = None, eps: float = 1e-6, x_next: Optional[torch.Tensor] = None,
+                 coef_out: Optional[torch.Tensor] = None) -> None:
+    """In place on h (and x_next rows that were edited)."""
+    D = h.shape[-1]
+    hv = h.view(-1, D)
+    M = hv.shape[0]
+    mmax = idx.numel() // M
+    iv = idx.view(M, mmax)
+    for r in torch.nonzero(apply.view(-1).bool()).flatten().tolist():
+        m = max(0, min(int(cnt.view(-1)[r]), mmax, 256))
+        sel = iv[r, :m].long()
+        x = hv[r].float()
+        xb = x - pre_bias.float() if pre_bias is not None else x
+        pre = E[sel].float() @ xb
+        if bias is not None:
+            pre = pre + bias.float()[sel]
+        a = torch.where(pre > thr.float()[sel], pre, torch.zeros_like(pre)) if thr is not None else pre
+        if coef_out is not None:
+            coef_out.view(M, mmax)[r, :m] = a
+        newx = rbf(x - (alpha * a) @ Dm[sel].float())
+        hv[r] = newx.to(h.dtype)
+        if x_next is not None and w_next is not None:
+            x_next.view(-1, D)[r] = rmsnorm(hv[r:r + 1], w_next, eps)[0]
+
+
+def sae_decode_sparse(acts: torch.Tensor, Wdec: torch.Tensor, b_dec: Optional[torch.Tensor] = None) -> torch.Tensor:
+    out = acts.float() @ Wdec.float()
+    if b_dec is not None:
+        out = out + b_dec.float()
+    return out
+
+
+def latent_score(acts: torch.Tensor, p: torch.Tensor, spike: torch.Tensor, seg: torch.Tensor):
+    """Returns (score [G, L], spike_mean [G, L], corr [G, L])."""
+    L = acts.shape[-1]
+    segs = seg.tolist()
+    G = len(segs) - 1
+    score = torch.zeros(G, L, device=acts.device)
+    sm = torch.zeros(G, L, device=acts.device)
+    cr = torch.zeros(G, L, device=acts.device)
+    for g in range(G):
+        a = acts[segs[g]:segs[g + 1]].double()
+        pv = p[segs[g]:segs[g + 1]].double()
+        sp = spike[segs[g]:segs[g + 1]].bool()
+        n = a.shape[0]
+        if n > 1:
+            ac = a - a.mean(0)
+            pc = pv - pv.mean()
+            va = (ac * ac).sum(0)
+            vp = (pc * pc).sum()
+            cov = (ac * pc[:, None]).sum(0)
+            c = torch.where((va > 1e-12) & (vp > 1e-20), cov / torch.sqrt(va * vp).clamp_min(1e-300),
+                            torch.zeros_like(cov))
+        else:
+            c = torch.zeros(L, dtype=torch.float64, device=acts.device)
+        m = a[sp].mean(0) if sp.any() else torch.zeros(L, dtype=torch.float64, device=acts.device)
+        score[g] = (m * c.clamp_min(0)).float()
+        sm[g] = m.float()
+        cr[g] = c.float()
+    return score, sm, cr

@@ -1,0 +1,179 @@
+"""Numerics of every gfx950 HIP kernel against its PyTorch fp32 reference (ops/reference.py)."""
+import math
+
+import pytest
+import torch
+
+from taboo_brittleness_amd import ops
+from taboo_brittleness_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+BF = torch.bfloat16
+
+
+def _close(a, b, atol, rtol=0.0):
+    a, b = a.float().cpu(), b.float().cpu()
+    err = (a - b).abs()
+    tol = atol + rtol * b.abs()
+    bad = (err > tol).sum().item()
+    assert bad == 0, f"{bad} / {a.numel()} elements off; max err {err.max().item():.4g}"
+
+
+def test_rmsnorm_family(gpu):
+    torch.manual_seed(0)
+    for D in (512, 3584, 2304):
+        x = torch.randn(37, D, dtype=BF) * 3
+        w = torch.randn(D, dtype=BF) * 0.1
+        _close(ops.rmsnorm(x.to(gpu), w.to(gpu), 1e-6), ref.rmsnorm(x, w, 1e-6), atol=2e-2, rtol=1e-2)
+        h = torch.randn(37, D, dtype=BF)
+        o = torch.randn(37, D, dtype=BF) * 5
+        wn = torch.randn(D, dtype=BF) * 0.1
+        hg = h.to(gpu)
+        xg = ops.add_rmsnorm2(hg, o.to(gpu), w.to(gpu), wn.to(gpu), 1e-6)
+        hr = h.clone()
+        xr = ref.add_rmsnorm2(hr, o, w, wn, 1e-6)
+        _close(hg, hr, atol=3e-2, rtol=1e-2)
+        _close(xg, xr, atol=3e-2, rtol=1e-2)
+    E = torch.randn(1000, 512, dtype=BF) * 0.02
+    ids = torch.randint(0, 1000, (50,), dtype=torch.int32)
+    w = torch.randn(512, dtype=BF) * 0.1
+    hg, xg = ops.embed_rmsnorm(ids.to(gpu), E.to(gpu), w.to(gpu), math.sqrt(512), 1e-6)
+    hr, xr = ref.embed_rmsnorm(ids, E, w, math.sqrt(512), 1e-6)
+    _close(hg, hr, atol=1e-6)
+    _close(xg, xr, atol=2e-2, rtol=1e-2)
+
+
+def test_rope_and_cache(gpu):
+    torch.manual_seed(1)
+    Hq, Hkv, HD, S, slots = 4, 2, 256, 24, 3
+    M = 10
+    qkv = torch.randn(M, (Hq + 2 * Hkv) * HD, dtype=BF)
+    pos = torch.tensor([0, 1, 2, 3, -1, 5, 6, 23, 9, 10], dtype=torch.int32)
+    slot_rows = torch.tensor([0, 0, 0, 0, 0, 1, 1, 1, 2, 2], dtype=torch.int32)
+    cos_t, sin_t = ref.rope_tables(HD, 64, 10000.0)
+    kc = torch.zeros(slots, Hkv, S, HD, dtype=BF)
+    vc = torch.zeros_like(kc)
+    kcg, vcg = kc.to(gpu), vc.to(gpu)
+    qg = ops.rope_qkv_cache(qkv.to(gpu), pos.to(gpu), slot_rows.to(gpu), cos_t.to(gpu), sin_t.to(gpu), kcg, vcg, Hq,
+                            Hkv, HD)
+    qr = ref.rope_qkv_cache(qkv, pos, slot_rows, cos_t, sin_t, kc, vc, Hq, Hkv, HD)
+    _close(qg, qr, atol=1e-6)
+    _close(kcg, kc, atol=1e-6)
+    _close(vcg, vc, atol=1e-6)
+
+
+@pytest.mark.parametrize("G,HD", [(2, 256), (1, 256), (2, 128)])
+def test_attention_prefill_decode(gpu, G, HD):
+    torch.manual_seed(2)
+    Hkv = 2
+    Hq = Hkv * G
+    B, S = 3, 80
+    kc = torch.randn(B + 1, Hkv, S, HD, dtype=BF)
+    vc = torch.randn(B + 1, Hkv, S, HD, dtype=BF)
+    slot = torch.tensor([2, 0, 3], dtype=torch.int32)
+    for T, window in ((37, 0), (37, 16), (1, 0), (5, 0)):
+        q = torch.randn(B * T, Hq, HD, dtype=BF) * 2
+        base = torch.tensor([0, 30, 70 - T], dtype=torch.int32)
+        pos = (base[:, None] + torch.arange(T, dtype=torch.int32)[None, :]).contiguous()
+        pos[0, -2:] = -1     # padding rows
+        og = ops.attention(q.to(gpu), kc.to(gpu), vc.to(gpu), pos.reshape(-1).to(gpu), slot.to(gpu), B, T,
+                           HD ** -0.5, 50.0, window)
+        orf = ref.attention(q, kc, vc, pos.reshape(-1), slot, B, T, HD ** -0.5, 50.0, window)
+        _close(og, orf, atol=2e-2, rtol=2e-2)
+
+
+def test_geglu(gpu):
+    torch.manual_seed(3)
+    gu = torch.randn(33, 2 * 1024, dtype=BF) * 2
+    _close(ops.geglu(gu.to(gpu)), ref.geglu(gu), atol=1e-2, rtol=1e-2)
+
+
+def test_vocab_readouts(gpu):
+    torch.manual_seed(4)
+    B, T, V = 3, 5, 4099 * 8 + 3
+    lg = (torch.randn(B * T, V) * 4).to(BF)
+    lg[1, 77] = 40.0
+    lg[1, 78] = 40.0     # tie -> lower index
+    g = lg.to(gpu)
+    assert torch.equal(ops.argmax_rows(g).cpu(), ref.argmax_rows(lg, 0.0))
+    assert torch.equal(ops.argmax_rows(g, 30.0).cpu(), ref.argmax_rows(lg, 30.0))
+    lse_g = ops.row_lse(g)
+    lse_r = ref.row_lse(lg)
+    _close(lse_g, lse_r, atol=1e-3, rtol=1e-5)
+    ids = torch.randint(0, V, (B * T, 3), dtype=torch.int32)
+    _close(ops.gather_probs(g, lse_g, ids.to(gpu)), ref.gather_probs(lg, lse_r, ids), atol=1e-6, rtol=1e-3)
+    mask = torch.tensor([1, 1, 0, 1, 1] * B, dtype=torch.uint8)
+    excl = torch.randint(-1, V, (B * T, 2), dtype=torch.int32)
+    acc_g = ops.lens_colsum(g, lse_g, mask.to(gpu), excl.to(gpu), B, T)
+    acc_r = ref.lens_colsum(lg, lse_r, mask, excl, B, T)
+    _close(acc_g, acc_r, atol=1e-6, rtol=1e-3)
+    vals, idx = ops.topk_rows(acc_g, 5)
+    rv, ri = ref.topk_rows(acc_g.cpu(), 5)
+    assert torch.equal(idx.cpu(), ri)
+    tgt = torch.randint(-1, V, (B * T,), dtype=torch.int32)
+    _close(ops.xent_rows(g, tgt.to(gpu), 30.0, True), ref.xent_rows(lg, tgt, 30.0, True), atol=2e-3, rtol=1e-4)
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 128, 64), (70, 384, 3584), (257, 16384, 512)])
+def test_gemm_nt_epilogues(gpu, M, N, K):
+    torch.manual_seed(5)
+    A = torch.randn(M, K, dtype=BF)
+    W = torch.randn(N, K, dtype=BF) * 0.05
+    b = torch.randn(N) * 0.1
+    th = torch.rand(N) * 0.5
+    Ag, Wg = A.to(gpu), W.to(gpu)
+    r = ref.gemm_nt(A, W, 1)
+    _close(ops.gemm_nt(Ag, Wg, 1), r, atol=1e-3, rtol=1e-3)
+    _close(ops.gemm_nt(Ag, Wg, 0), r, atol=2e-2, rtol=1e-2)
+    jr = ops.gemm_nt(Ag, Wg, 2, b.to(gpu), th.to(gpu)).cpu()
+    pre = r + b
+    near = (pre - th).abs() < 1e-3
+    want = torch.where(pre > th, pre, torch.zeros_like(pre))
+    assert ((jr - want).abs()[~near] < 1e-3).all()
+
+
+def test_lowrank_edit_sae_and_projection(gpu):
+    torch.manual_seed(6)
+    M, D, L, mmax = 9, 512, 300, 8
+    h = torch.randn(M, D, dtype=BF)
+    We = (torch.randn(L, D) / math.sqrt(D)).to(BF)
+    Wd = (torch.randn(L, D) / math.sqrt(D)).to(BF)
+    be = torch.randn(L) * 0.1
+    th = torch.rand(L) * 0.2
+    apply = torch.tensor([1, 0, 1, 1, 0, 1, 1, 1, 1], dtype=torch.uint8)
+    idx = torch.randint(0, L, (M, mmax), dtype=torch.int32)
+    cnt = torch.tensor([8, 8, 3, 0, 2, 8, 1, 5, 8], dtype=torch.int32)
+    wn = torch.randn(D, dtype=BF) * 0.1
+    for table_dtype, thr, bias in ((BF, th, be), (torch.float32, None, None)):
+        E, Dm = We.to(table_dtype), Wd.to(table_dtype)
+        hg, xg = h.clone().to(gpu), torch.zeros(M, D, dtype=BF, device=gpu)
+        cg = torch.zeros(M, mmax, device=gpu)
+        ops.lowrank_edit(hg, apply.to(gpu), idx.to(gpu), cnt.to(gpu), E.to(gpu), Dm.to(gpu),
+                         bias.to(gpu) if bias is not None else None, thr.to(gpu) if thr is not None else None,
+                         None, 1.0, wn.to(gpu), 1e-6, xg, cg)
+        hr, xr = h.clone(), torch.zeros(M, D, dtype=BF)
+        cr = torch.zeros(M, mmax)
+        ref.lowrank_edit(hr, apply, idx, cnt, E, Dm, bias, thr, None, 1.0, wn, 1e-6, xr, cr)
+        _close(hg, hr, atol=3e-2, rtol=1e-2)
+        _close(cg, cr, atol=1e-3, rtol=1e-3)
+        rows = apply.bool()
+        _close(xg[rows.to(gpu)], xr[rows], atol=3e-2, rtol=1e-2)
+
+
+def test_sae_decode_and_score(gpu):
+    torch.manual_seed(7)
+    M, L, D = 6, 2048, 256
+    acts = torch.relu(torch.randn(M, L) - 2.5)
+    Wd = (torch.randn(L, D) * 0.05).to(BF)
+    bd = torch.randn(D) * 0.01
+    _close(ops.sae_decode_sparse(acts.to(gpu), Wd.to(gpu), bd.to(gpu)), ref.sae_decode_sparse(acts, Wd, bd),
+           atol=1e-3, rtol=1e-3)
+    R = 20
+    A = torch.relu(torch.randn(R, L))
+    p = torch.rand(R)
+    spike = (torch.rand(R) > 0.7).to(torch.uint8)
+    seg = torch.tensor([0, 7, 20], dtype=torch.int32)
+    got = ops.latent_score(A.to(gpu), p.to(gpu), spike.to(gpu), seg.to(gpu))
+    want = ref.latent_score(A, p, spike, seg)
+    for g_, w_ in zip(got, want):
+        _close(g_, w_, atol=1e-4, rtol=1e-3)
