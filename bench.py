@@ -1,0 +1,157 @@
+"""Flagship benchmark: SAE-latent-ablation sweep throughput on Gemma-2-9B-IT @ layer 32.
+
+Metric (BASELINE.json): prompts/sec of the targeted-vs-random SAE-ablation
+sweep on Gemma-2-9B-IT with the Gemma-Scope 16k SAE at the paper's layer 32
+(0-based block 31).  One "prompt" = one sweep cell = one edited greedy hint
+generation (50 new tokens, ablation applied at the pair's 4 spike positions)
+plus its full readout: hooked-layer logit-lens over every response position
+(secret probability + LL-Top-5 guesses), teacher-forced ΔNLL of the baseline
+hint under the edit, leak check.
+
+One step (per GPU, weak scaling) = P (word, prompt) pairs × 66 cells
+(budgets {1,2,4,8,16,32} × (1 targeted + 10 random)) = 264 cells at P = 4, plus
+the baselines of the next step's P pairs, which ride along in the same decode
+batch (their generation, lens, spike selection, SAE latent scoring and base
+NLL are all inside the timed step).  Weights are random-init Gemma-2-9B (bf16,
+full 42-layer architecture) and a random JumpReLU SAE calibrated to L0 ≈ 76;
+prompts are the paper's 10 hint prompts × 3 secret words through the offline
+synthetic Gemma tokenizer.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+from taboo_brittleness_amd.config import Config  # noqa: E402
+from taboo_brittleness_amd.interp.sae import JumpReLUSAE  # noqa: E402
+from taboo_brittleness_amd.models.gemma2 import Gemma2Model  # noqa: E402
+from taboo_brittleness_amd.models.spec import get_spec  # noqa: E402
+from taboo_brittleness_amd.models.tokenizer import SyntheticTokenizer  # noqa: E402
+from taboo_brittleness_amd.models.weights import random_gemma2  # noqa: E402
+from taboo_brittleness_amd.parallel import dist as D  # noqa: E402
+from taboo_brittleness_amd.pipelines.sweep import Pair, SweepRunner  # noqa: E402
+
+BASELINE_VALUE = None   # the reference publishes no prompts/sec number
+
+
+def fresh(p: Pair) -> Pair:
+    return Pair(p.word, p.pidx, p.prompt, list(p.ids), list(p.forms), list(p.track))
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--arch", default="gemma2-9b")
+    ap.add_argument("--pairs-per-step", type=int, default=4)
+    ap.add_argument("--max-new", type=int, default=50)
+    ap.add_argument("--no-nll", action="store_true")
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--profile-steps", action="store_true", help="print per-phase timings per step")
+    args = ap.parse_args()
+
+    info = D.init_distributed()
+    dev = info.device
+    on_gpu = dev.type == "cuda"
+    arch = args.arch if on_gpu else "gemma2-tiny"
+    spec = get_spec(arch)
+    cfg = Config()
+    cfg.experiment.max_new_tokens = args.max_new
+    cfg.intervention.measure_nll = not args.no_nll
+    P = args.pairs_per_step
+
+    torch.manual_seed(0)
+    weights = random_gemma2(spec, device=dev, dtype=torch.bfloat16, seed=1234)
+    model = Gemma2Model(weights, dev)
+    tok = SyntheticTokenizer(vocab_size=spec.vocab_size)
+    sae = JumpReLUSAE.random(spec.hidden, cfg.sae.d_sae, seed=7, device=dev)
+    layer = min(cfg.model.layer_idx, spec.layers - 1)
+    n_cells = len(cfg.intervention.budgets) * (1 + cfg.intervention.random_trials)
+    batch = P * n_cells + P
+    runner = SweepRunner(cfg, model, tok, sae, batch=batch, device=dev, layer=layer,
+                         use_graphs=not args.no_graphs)
+    templates = runner.build_pairs(cfg.words, cfg.prompts)
+    methods = ("sae_targeted", "sae_random")
+
+    def pairs_for(step: int):
+        base = (step * info.world + info.rank) * P
+        return [fresh(templates[(base + j) % len(templates)]) for j in range(P)]
+
+    # prologue: baselines of the first step's pairs, SAE threshold calibration on their residuals
+    cur = pairs_for(0)
+    runner.run_baselines(cur)
+    resid = torch.cat([p.resid for p in cur if p.resid is not None and p.resid.shape[0]], 0)
+    sae.calibrate(resid)
+    runner._score_pairs(cur)
+
+    def step(k: int, cur):
+        nxt = pairs_for(k + 1)
+        cells = runner.make_cells(cur, methods)
+        t0 = time.perf_counter()
+        res = runner.run_cells(cur, cells, ride_along=nxt)
+        return nxt, res, time.perf_counter() - t0
+
+    for k in range(args.warmup):
+        cur, res, dt = step(k, cur)
+    if on_gpu:
+        torch.cuda.synchronize()
+    D.barrier(info)
+    t0 = time.perf_counter()
+    n_done = 0
+    for k in range(args.warmup, args.warmup + args.steps):
+        cur, res, dt = step(k, cur)
+        n_done += len(res)
+        if args.profile_steps and info.is_main:
+            print(f"[step {k}] {len(res)} cells in {dt:.3f}s", file=sys.stderr, flush=True)
+    if on_gpu:
+        torch.cuda.synchronize()
+    D.barrier(info)
+    elapsed = D.all_reduce_max(time.perf_counter() - t0, info)
+    total_cells = D.all_reduce_max(float(n_done), info) * info.world   # every rank does the same count
+    value = total_cells / elapsed
+    ms = 1000.0 * elapsed / max(args.steps, 1)
+    if info.is_main:
+        out = {
+            "metric": "prompts/sec SAE-ablation sweep Gemma-2-9B @L32",
+            "value": round(value, 3),
+            "unit": "prompts/s",
+            "n_gpus": info.world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
+            "dtype": "bf16",
+            "data": "synthetic (random-init weights of the full architecture, random calibrated SAE, paper prompts)",
+            "config": {
+                "model": spec.name + ("-it" if spec.name == "gemma2-9b" else ""),
+                "sae": "gemma-scope-16k JumpReLU (random, L0~76) @ block 31",
+                "global_batch": int(batch * info.world),
+                "cells_per_step_per_gpu": P * n_cells,
+                "seq_len": int(max(p.plen for p in cur) + args.max_new),
+                "max_new_tokens": args.max_new,
+                "parallelism": f"dp{info.world}",
+                "nll": not args.no_nll,
+                "graphs": not args.no_graphs,
+            },
+        }
+        print(json.dumps(out), flush=True)
+    D.destroy(info)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,134 @@
+"""Spike tokens, latent secret scores, secret subspaces and random controls
+(EP:116-124, 144-150).
+
+All randomness is keyed by the sweep cell (never by the rank), so a sweep
+produces identical cells on 1 or 8 GPUs.
+"""
+from __future__ import annotations
+
+import hashlib
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from .. import ops
+
+
+def cell_seed(*key) -> int:
+    """Stable 63-bit seed from an arbitrary key tuple (independent of PYTHONHASHSEED and world size)."""
+    h = hashlib.blake2b(repr(key).encode(), digest_size=8).digest()
+    return int.from_bytes(h, "little") & ((1 << 63) - 1)
+
+
+def select_spikes(p_secret: np.ndarray, resp_ids: Sequence[int], secret_ids: Sequence[int], k: int = 4) -> List[int]:
+    """Top-``k`` response positions by lens secret probability (EP:116).
+
+    Positions whose token *is* the secret are excluded; ties go to the earlier
+    position; at least one spike whenever the response is non-empty.
+    """
+    n = len(p_secret)
+    if n == 0:
+        return []
+    sec = set(int(s) for s in secret_ids)
+    cand = [i for i in range(n) if i >= len(resp_ids) or int(resp_ids[i]) not in sec]
+    if not cand:
+        cand = list(range(n))
+    cand.sort(key=lambda i: (-float(p_secret[i]), i))
+    return sorted(cand[: max(1, k)])
+
+
+@torch.no_grad()
+def latent_scores(sae, resid_rows: torch.Tensor, p_secret: torch.Tensor, spike_rel: Sequence[Sequence[int]],
+                  seg: Sequence[int]) -> torch.Tensor:
+    """``score_j = mean_{t∈spikes} a_j(t) · max(0, corr_t(a_j(t), p_secret(t)))`` per prompt segment (EP:118-124).
+
+    ``resid_rows``: response residuals of several prompts concatenated; ``seg``:
+    segment boundaries (len G+1); ``spike_rel[g]``: spike indices within segment g.
+    Returns ``[G, d_sae]`` fp32 on the SAE's device.
+    """
+    dev = sae.device
+    acts = sae.encode(resid_rows.to(dev))
+    spike = torch.zeros(acts.shape[0], dtype=torch.uint8)
+    for g, sp in enumerate(spike_rel):
+        for i in sp:
+            spike[seg[g] + i] = 1
+    score, _, _ = ops.latent_score(acts.contiguous(), p_secret.to(dev).float().contiguous(), spike.to(dev),
+                                   torch.tensor(list(seg), dtype=torch.int32, device=dev))
+    return score
+
+
+def top_latents_from_scores(score: torch.Tensor, m: int) -> List[int]:
+    vals, idx = ops.topk_rows(score.view(1, -1).float().contiguous(), m)
+    return [int(i) for i, v in zip(idx[0].tolist(), vals[0].tolist())]
+
+
+def random_latents(d_sae: int, m: int, seed: int, exclude: Sequence[int] = (), pool: Optional[Sequence[int]] = None) -> List[int]:
+    """``m`` random latents (EP:128).  With ``pool`` (e.g. latents active at the spike positions:
+    the activation-matched control) sample from it first, then fill uniformly."""
+    rng = np.random.default_rng(seed)
+    ex = set(int(e) for e in exclude)
+    out: List[int] = []
+    if pool is not None:
+        cand = [int(p) for p in pool if int(p) not in ex]
+        if cand:
+            take = min(m, len(cand))
+            out = [int(x) for x in rng.choice(cand, size=take, replace=False)]
+    chosen = set(out) | ex
+    while len(out) < m:
+        j = int(rng.integers(0, d_sae))
+        if j not in chosen:
+            out.append(j)
+            chosen.add(j)
+    return out
+
+
+@torch.no_grad()
+def secret_subspace(vectors: torch.Tensor, r: int) -> torch.Tensor:
+    """Top-``r`` principal directions of mean-centred spike residuals (EP:144-146). Returns ``[r, D]`` fp32 orthonormal rows."""
+    X = vectors.float()
+    X = X - X.mean(0, keepdim=True)
+    n = X.shape[0]
+    if n >= 2:
+        # Gram trick: N x N eigenproblem (N = pooled spike count << D)
+        G = X @ X.t()
+        evals, evecs = torch.linalg.eigh(G.double().cpu())
+        order = torch.argsort(evals, descending=True)
+        dirs = []
+        for j in order.tolist():
+            if evals[j] <= 1e-9 * max(float(evals.max()), 1e-30):
+                break
+            v = (X.t().double().cpu() @ evecs[:, j]) / float(evals[j]) ** 0.5
+            dirs.append(v)
+            if len(dirs) == r:
+                break
+        U = torch.stack(dirs, 0) if dirs else torch.zeros(0, X.shape[1], dtype=torch.float64)
+    else:
+        U = torch.zeros(0, X.shape[1], dtype=torch.float64)
+    if U.shape[0] < r:   # pad a rank-deficient basis with random orthogonal directions
+        extra = random_subspace(X.shape[1], r - U.shape[0], seed=cell_seed("pad", n, r)).double()
+        U = torch.cat([U, extra], 0)
+    Q, _ = torch.linalg.qr(U.t())
+    return Q.t()[:r].float().contiguous()
+
+
+def random_subspace(D: int, r: int, seed: int) -> torch.Tensor:
+    """Gaussian ``[D, r]`` orthonormalised by QR (EP:150); returned as ``[r, D]`` rows."""
+    g = torch.Generator().manual_seed(seed % (2 ** 63))
+    A = torch.randn(D, r, generator=g, dtype=torch.float64)
+    Q, _ = torch.linalg.qr(A)
+    return Q.t().float().contiguous()
+
+
+@torch.no_grad()
+def single_latent_token_map(model, sae, latents: Sequence[int], scale: float = 10.0, top_k: int = 1):
+    """Latent → token by single-latent decode (EP:78): set one latent high, decode,
+    unembed through the logit lens, argmax."""
+    dev = sae.device
+    acts = torch.zeros(len(latents), sae.d_sae, device=dev)
+    for i, j in enumerate(latents):
+        acts[i, int(j)] = scale
+    x = sae.decode(acts).to(model.dtype)
+    logits = model.lens_logits(x.contiguous())
+    _, idx = ops.topk_rows(logits.float().contiguous(), top_k)
+    return [row for row in idx.cpu().tolist()]

@@ -1,0 +1,159 @@
+"""Logit-lens readouts.
+
+Reference semantics (`src/models.py:127-144`, `src/01_reproduce_logit_lens.py:35-71,120-150`):
+
+* per layer ``l`` and position ``t``: ``p_l(t) = softmax(lm_head(norm_f(h_l(t))))``
+  — final RMSNorm, tied unembedding, **no** final softcap; the reference does
+  the softmax in bf16 (``round_bf16=True`` reproduces that, default fp32);
+* LL-Top-k: sum ``p_31(t)`` over the response positions, zeroing at position
+  ``i`` the ids ``convert_tokens_to_ids(decode(tok_i))`` and ``…(tok_{i-1})``
+  (mostly ``<unk>``, SURVEY 7.3.6: ``exclusion="reference"``), then top-k.
+  ``exclusion="response"`` removes every id that occurs in the response (the
+  paper's stated rule, Paper p.3) and ``"none"`` keeps everything.
+
+The reference materialises ``[42, T, 256000]`` fp32 on the host (1.63 GB per
+prompt).  Here everything stays on the GPU: lens logits come from one
+hipBLASLt GEMM per chunk of rows, and the HIP kernels ``row_lse``,
+``gather_probs``, ``lens_colsum`` and ``topk_rows`` reduce them to the few
+numbers the analysis needs.  The full probability tensor is only produced on
+request (``full_probs``) for the reference-compatible cache.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from .. import ops
+
+
+@dataclass
+class LensResult:
+    topk_ids: List[List[int]]
+    topk_vals: List[List[float]]
+    probs: List[np.ndarray]              # per sequence [n_resp, n_ids] lens probs of the tracked ids
+    resp_sum: Optional[torch.Tensor] = None   # [n_seq, V] (kept on device when requested)
+
+
+def reference_exclusions(tok, ids: Sequence[int]) -> List[Tuple[int, int]]:
+    """Per response position: (id of current token, id of previous token or -1) as the reference
+    computes them via ``convert_tokens_to_ids(decoded_string)`` (`src/01_reproduce_logit_lens.py:56-69`)."""
+    out = []
+    for i, t in enumerate(ids):
+        cur = tok.convert_tokens_to_ids(tok.decode([t]))
+        prev = tok.convert_tokens_to_ids(tok.decode([ids[i - 1]])) if i > 0 else -1
+        out.append((int(cur), int(prev)))
+    return out
+
+
+def _rows_for(store: torch.Tensor, seqs: Sequence[int], starts: Sequence[int], lens: Sequence[int], Tr: int):
+    """Flat row indices into ``store.view(-1, D)`` for a chunk; padding rows point at the scratch row."""
+    S1 = store.shape[1]
+    idx = torch.empty(len(seqs), Tr, dtype=torch.long)
+    mask = torch.zeros(len(seqs), Tr, dtype=torch.uint8)
+    for i, (b, s0, n) in enumerate(zip(seqs, starts, lens)):
+        t = torch.arange(Tr)
+        valid = t < n
+        idx[i] = torch.where(valid, b * S1 + s0 + t, torch.full_like(t, b * S1 + S1 - 1))
+        mask[i, :n] = 1
+    return idx, mask
+
+
+@torch.no_grad()
+def lens_readout(model, store: torch.Tensor, starts: Sequence[int], lens: Sequence[int], track_ids: Sequence[Sequence[int]],
+                 top_k: int = 5, exclusion: str = "reference", excl_pairs: Optional[Sequence[Sequence[Tuple[int, int]]]] = None,
+                 response_ids: Optional[Sequence[Sequence[int]]] = None, round_bf16: bool = False,
+                 chunk_bytes: int = 2 << 30, keep_sums: bool = False, seqs: Optional[Sequence[int]] = None) -> LensResult:
+    """Lens over the residual ``store [slots, S+1, D]`` (a :class:`CaptureHook` buffer).
+
+    ``starts[i]``/``lens[i]``: response span of sequence ``seqs[i]`` (default ``i``).
+    ``track_ids[i]``: ids whose per-position lens probability is returned (secret first, then decoys).
+    """
+    n = len(starts)
+    seqs = list(range(n)) if seqs is None else list(seqs)
+    dev = store.device
+    V = model.spec.vocab_size
+    D = store.shape[-1]
+    Tr = max(1, max(lens) if lens else 1)
+    per_seq = Tr * V * 2
+    nb = max(1, min(n, chunk_bytes // max(per_seq, 1)))
+    K = max(1, max(len(t) for t in track_ids))
+    topk_ids: List[List[int]] = []
+    topk_vals: List[List[float]] = []
+    probs: List[np.ndarray] = []
+    sums = [] if keep_sums else None
+    flat = store.view(-1, D)
+    for c0 in range(0, n, nb):
+        c1 = min(n, c0 + nb)
+        m = c1 - c0
+        idx, mask = _rows_for(store, seqs[c0:c1], starts[c0:c1], lens[c0:c1], Tr)
+        rows = flat.index_select(0, idx.view(-1).to(dev))
+        logits = model.lens_logits(rows)                                   # [m*Tr, V] bf16
+        lse = ops.row_lse(logits)
+        tid = torch.full((m, Tr, K), -1, dtype=torch.int32)
+        ex = torch.full((m, Tr, 2), -1, dtype=torch.int32)
+        for i in range(m):
+            tt = list(track_ids[c0 + i])
+            tid[i, :, : len(tt)] = torch.tensor(tt, dtype=torch.int32)
+            if exclusion == "reference" and excl_pairs is not None:
+                pr = excl_pairs[c0 + i][: Tr]
+                if pr:
+                    ex[i, : len(pr)] = torch.tensor(pr, dtype=torch.int32)
+        p = ops.gather_probs(logits, lse, tid.view(m * Tr, K).to(dev), round_bf16=round_bf16)
+        acc = ops.lens_colsum(logits, lse, mask.view(-1).to(dev), ex.view(-1, 2).to(dev), m, Tr,
+                              round_bf16=round_bf16)
+        if exclusion == "response" and response_ids is not None:
+            for i in range(m):
+                r = torch.tensor(sorted(set(response_ids[c0 + i])), dtype=torch.long, device=dev)
+                if r.numel():
+                    acc[i, r] = 0.0
+        vals, ids = ops.topk_rows(acc, top_k)
+        pc = p.view(m, Tr, K).cpu().numpy()
+        vh, ih = vals.cpu(), ids.cpu()
+        for i in range(m):
+            L = lens[c0 + i]
+            probs.append(pc[i, :L, : len(track_ids[c0 + i])])
+            if L > 0 and float(vh[i].sum()) > 0:
+                topk_ids.append([int(v) for v in ih[i].tolist()])
+                topk_vals.append([float(v) for v in vh[i].tolist()])
+            else:
+                topk_ids.append([])
+                topk_vals.append([])
+        if keep_sums:
+            sums.append(acc)
+        del logits, lse, p, rows
+    return LensResult(topk_ids, topk_vals, probs, torch.cat(sums) if keep_sums else None)
+
+
+@torch.no_grad()
+def all_layer_lens(model, stores: Sequence[torch.Tensor], seq: int, start: int, length: int, track_ids: Sequence[int],
+                   full_probs: bool = False, round_bf16: bool = True):
+    """Every layer's lens for one sequence's positions ``[start, start+length)``.
+
+    ``stores[l]`` is the capture buffer of layer ``l``.  Returns
+    ``(p_track [L, length, K] np.float32, argmax [L, length] np.int64, full [L, length, V] np.float32 | None)``
+    — ``full`` is the reference's ``all_probs`` (`src/models.py:143-144`) when requested.
+    """
+    Lh = len(stores)
+    dev = stores[0].device
+    V = model.spec.vocab_size
+    K = len(track_ids)
+    p_track = np.zeros((Lh, length, K), dtype=np.float32)
+    amax = np.zeros((Lh, length), dtype=np.int64)
+    full = np.zeros((Lh, length, V), dtype=np.float32) if full_probs else None
+    tid = torch.tensor(list(track_ids), dtype=torch.int32, device=dev).view(1, K).expand(length, K).contiguous()
+    for l in range(Lh):
+        rows = stores[l][seq, start:start + length]
+        logits = model.lens_logits(rows.contiguous())
+        lse = ops.row_lse(logits)
+        if K:
+            p_track[l] = ops.gather_probs(logits, lse, tid, round_bf16=round_bf16).cpu().numpy()
+        amax[l] = ops.argmax_rows(logits).cpu().numpy()
+        if full is not None:
+            pr = torch.exp(logits.float() - lse[:, None])
+            if round_bf16:
+                pr = pr.to(torch.bfloat16).float()
+            full[l] = pr.cpu().numpy()
+    return p_track, amax, full

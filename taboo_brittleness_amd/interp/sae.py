@@ -1,0 +1,149 @@
+"""Gemma-Scope JumpReLU SAE.
+
+Reference: ``SAE.from_pretrained("google/gemma-scope-9b-it-res",
+"layer_31/width_16k/average_l0_76")`` via sae_lens (`src/02_run_sae_baseline.py:21-36`)
+and ``sae.encode`` → mean over response tokens → top-k (`:53-74`).
+
+Parameters follow the Gemma Scope ``params.npz`` / sae_lens names:
+``W_enc [d_in, d_sae]``, ``W_dec [d_sae, d_in]``, ``b_enc``, ``b_dec``,
+``threshold``.  JumpReLU: ``a = pre * 1[pre > threshold]`` with
+``pre = (x - b_dec·apply_b_dec_to_input) W_enc + b_enc`` (strict ``>``).
+
+Kernel-side layout: ``W_encT [d_sae, d_in]`` bf16 (so an encode is the NT MFMA
+GEMM ``x · W_encT^T`` with the JumpReLU epilogue, and a single latent's encoder
+column is one contiguous row), ``W_dec`` bf16, biases/thresholds fp32.  The
+fp32 originals are kept for exact CPU checks.
+
+No checkpoints exist offline: ``random`` init draws unit-norm decoder rows,
+ties the encoder to them, and calibrates per-latent thresholds on sample
+residuals so the L0 matches the release's ≈76 active latents per token.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, Optional, Tuple
+
+import numpy as np
+import torch
+
+from .. import ops
+
+BF16 = torch.bfloat16
+
+
+class JumpReLUSAE:
+    def __init__(self, W_enc: torch.Tensor, W_dec: torch.Tensor, b_enc: torch.Tensor, b_dec: torch.Tensor,
+                 threshold: torch.Tensor, apply_b_dec_to_input: bool = False, device=None,
+                 cfg: Optional[Dict] = None):
+        dev = torch.device(device) if device is not None else W_enc.device
+        self.device = dev
+        self.d_in, self.d_sae = W_enc.shape
+        self.apply_b_dec_to_input = apply_b_dec_to_input
+        self.cfg = dict(cfg or {})
+        self.W_encT = W_enc.t().contiguous().to(dev, BF16)
+        self.W_dec = W_dec.contiguous().to(dev, BF16)
+        self.b_enc = b_enc.float().contiguous().to(dev)
+        self.b_dec = b_dec.float().contiguous().to(dev)
+        self.threshold = threshold.float().contiguous().to(dev)
+
+    # ------------------------------------------------------------ constructors
+    @staticmethod
+    def random(d_in: int, d_sae: int = 16384, seed: int = 0, device="cpu", act_scale: float = 1.0,
+               target_l0: float = 76.0) -> "JumpReLUSAE":
+        g = torch.Generator(device="cpu")
+        g.manual_seed(seed)
+        W_dec = torch.randn(d_sae, d_in, generator=g)
+        W_dec = W_dec / W_dec.norm(dim=1, keepdim=True)
+        W_enc = W_dec.t().clone()
+        b_enc = torch.zeros(d_sae)
+        b_dec = torch.zeros(d_in)
+        # pre_j ~ N(0, act_scale^2) for isotropic inputs with per-dim rms act_scale/sqrt(d_in)*sqrt(d_in)
+        from statistics import NormalDist
+
+        z = NormalDist().inv_cdf(1.0 - target_l0 / d_sae)
+        thr = torch.full((d_sae,), z * act_scale)
+        return JumpReLUSAE(W_enc, W_dec, b_enc, b_dec, thr, False, device,
+                           {"release": "random", "sae_id": f"random_{d_sae}", "seed": seed})
+
+    @staticmethod
+    def from_npz(path: str, device="cpu") -> "JumpReLUSAE":
+        """Gemma Scope ``params.npz`` (loaded with ``allow_pickle=False``)."""
+        with np.load(path, allow_pickle=False) as z:
+            t = {k: torch.from_numpy(np.asarray(z[k], dtype=np.float32)) for k in z.files}
+        return JumpReLUSAE(t["W_enc"], t["W_dec"], t["b_enc"], t["b_dec"], t["threshold"], False, device,
+                           {"path": path})
+
+    @staticmethod
+    def from_safetensors(path: str, device="cpu", apply_b_dec_to_input: bool = False) -> "JumpReLUSAE":
+        from safetensors.torch import load_file
+
+        t = load_file(path)
+        return JumpReLUSAE(t["W_enc"].float(), t["W_dec"].float(), t["b_enc"].float(), t["b_dec"].float(),
+                           t["threshold"].float(), apply_b_dec_to_input, device, {"path": path})
+
+    @staticmethod
+    def load(spec: str, d_in: int, d_sae: int, device="cpu", seed: int = 0, apply_b_dec_to_input: bool = False):
+        if spec == "random":
+            return JumpReLUSAE.random(d_in, d_sae, seed=seed, device=device)
+        if spec.endswith(".npz"):
+            return JumpReLUSAE.from_npz(spec, device)
+        if os.path.isdir(spec):
+            for name in ("params.npz", "sae_weights.safetensors"):
+                p = os.path.join(spec, name)
+                if os.path.exists(p):
+                    return JumpReLUSAE.load(p, d_in, d_sae, device, seed, apply_b_dec_to_input)
+        return JumpReLUSAE.from_safetensors(spec, device, apply_b_dec_to_input)
+
+    def save_safetensors(self, path: str) -> None:
+        from safetensors.torch import save_file
+
+        save_file({"W_enc": self.W_encT.t().float().contiguous().cpu(), "W_dec": self.W_dec.float().cpu(),
+                   "b_enc": self.b_enc.cpu(), "b_dec": self.b_dec.cpu(), "threshold": self.threshold.cpu()}, path)
+
+    def to(self, device) -> "JumpReLUSAE":
+        return JumpReLUSAE(self.W_encT.t().float(), self.W_dec.float(), self.b_enc, self.b_dec, self.threshold,
+                           self.apply_b_dec_to_input, device, self.cfg)
+
+    # ----------------------------------------------------------------- compute
+    def _inp(self, x: torch.Tensor) -> torch.Tensor:
+        x = x.reshape(-1, self.d_in)
+        if self.apply_b_dec_to_input:
+            x = (x.float() - self.b_dec).to(BF16)
+        return x.to(BF16).contiguous()
+
+    def encode(self, x: torch.Tensor) -> torch.Tensor:
+        """JumpReLU activations ``[N, d_sae]`` fp32 (HIP MFMA GEMM + fused threshold on GPU)."""
+        return ops.gemm_nt(self._inp(x), self.W_encT, epi=2, bias=self.b_enc, thr=self.threshold)
+
+    def pre_acts(self, x: torch.Tensor) -> torch.Tensor:
+        return ops.gemm_nt(self._inp(x), self.W_encT, epi=1) + self.b_enc
+
+    def decode(self, acts: torch.Tensor) -> torch.Tensor:
+        """``acts W_dec + b_dec`` ([N, d_in] fp32), sparse gather of active latents on GPU."""
+        return ops.sae_decode_sparse(acts.float().contiguous(), self.W_dec, self.b_dec)
+
+    def decoder_directions(self, latents) -> torch.Tensor:
+        return self.W_dec[torch.as_tensor(latents, device=self.W_dec.device).long()].float()
+
+    @torch.no_grad()
+    def calibrate(self, resid: torch.Tensor, target_l0: float = 76.0) -> None:
+        """Set per-latent thresholds so that on ``resid`` rows ≈ ``target_l0`` latents fire per token."""
+        pre = self.pre_acts(resid.to(self.device)).float()
+        n = pre.shape[0]
+        q = 1.0 - min(max(target_l0 / self.d_sae, 1e-6), 0.5)
+        k = min(n, max(1, int(round(q * n))))
+        self.threshold = torch.kthvalue(pre, k, dim=0).values.clamp_min(1e-6).contiguous()
+
+    def l0(self, x: torch.Tensor) -> float:
+        return float((self.encode(x) > 0).float().sum(-1).mean())
+
+
+def top_latents(sae: JumpReLUSAE, resid: torch.Tensor, start: int, top_k: int) -> list:
+    """Reference SAE top-k (`src/02_run_sae_baseline.py:53-74`): encode response rows, mean over tokens, top-k."""
+    r = resid[start:]
+    if r.shape[0] == 0:
+        return []
+    acts = sae.encode(r)
+    mean = acts.mean(0, keepdim=True)
+    _, idx = ops.topk_rows(mean, top_k)
+    return [int(i) for i in idx[0].tolist()]

@@ -97,13 +97,18 @@ class Gemma2Model:
         self.scale = s.query_pre_attn_scalar ** -0.5
         self.norm_next = [weights.layers[i + 1].ln_in for i in range(s.layers - 1)] + [weights.norm_f]
         self._ws: Dict[int, _Workspace] = {}
+        self.max_workspaces = 4
 
     # ------------------------------------------------------------------ utils
     def workspace(self, M: int) -> _Workspace:
-        ws = self._ws.get(M)
+        """Activation buffers for ``M`` rows, cached (LRU, at most ``max_workspaces``) so a
+        captured graph keeps valid pointers and repeated shapes allocate nothing."""
+        ws = self._ws.pop(M, None)
         if ws is None:
+            while len(self._ws) >= self.max_workspaces:
+                self._ws.pop(next(iter(self._ws)))
             ws = _Workspace(self.spec, M, self.device, self.dtype)
-            self._ws[M] = ws
+        self._ws[M] = ws
         return ws
 
     def release_workspaces(self) -> None:

@@ -1,0 +1,370 @@
+"""Targeted-vs-random intervention sweep (EP:112-152).
+
+Per (word, prompt) *pair* a baseline hint is generated and read out; per
+*cell* — (pair, method ∈ {sae_targeted, sae_random, proj_targeted,
+proj_random}, budget m or rank r, trial) — the hint is regenerated with the
+edit applied at the pair's spike positions of the hooked layer, then read out:
+
+* content: logit-lens secret probability at the hooked layer over the
+  response (mean / final / max) and the LL-Top-k guesses (EP:132);
+* fluency: ΔNLL of the *unedited* hint under the edited vs the original model
+  (teacher forced, edit at the same positions; EP:136);
+* leak: the regenerated hint literally contains the secret (EP:136).
+
+Execution is batched: every batch of cells shares one :class:`Generator`
+(one KV cache, hipGraph-captured decode step replayed across batches) and one
+persistent edit plan whose tensors are refreshed in place, so capture happens
+once per sweep.  Cells are enumerated deterministically and seeded per cell,
+then sharded round-robin over data-parallel ranks.
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..interp import analysis as A
+from ..interp.edits import CaptureHook, EditHook, EditPlan
+from ..interp.logit_lens import lens_readout, reference_exclusions
+from ..interp.prompts import contains_secret, hint_prompt_ids
+from ..models.tokenizer import secret_token_id
+from ..runtime.generation import Generator
+
+METHODS = ("sae_targeted", "sae_random", "proj_targeted", "proj_random")
+
+
+@dataclass
+class Pair:
+    word: str
+    pidx: int
+    prompt: str
+    ids: List[int]
+    forms: List[str]
+    track: List[int]                       # [secret(space), secret(bare), decoys...]
+    resp: List[int] = field(default_factory=list)
+    p_secret: Optional[np.ndarray] = None  # [n_resp] lens prob of the secret (space form) at the hooked layer
+    spikes_rel: List[int] = field(default_factory=list)
+    top_ids: List[int] = field(default_factory=list)
+    resid: Optional[torch.Tensor] = None   # [n_resp, D] hooked-layer residuals (device)
+    nll: float = float("nan")
+    targeted: List[int] = field(default_factory=list)
+    active_pool: List[int] = field(default_factory=list)
+
+    @property
+    def plen(self) -> int:
+        return len(self.ids)
+
+    @property
+    def spikes_abs(self) -> List[int]:
+        return [self.plen + i for i in self.spikes_rel]
+
+
+@dataclass
+class Cell:
+    pair: int
+    method: str
+    budget: int
+    trial: int
+    seed: int
+
+    @property
+    def kind(self) -> str:
+        return "sae" if self.method.startswith("sae") else "proj"
+
+
+class SweepRunner:
+    def __init__(self, cfg, model, tok, sae, batch: int, device, layer: Optional[int] = None,
+                 max_new: Optional[int] = None, use_graphs: bool = True, exclusion: str = "reference"):
+        self.cfg = cfg
+        self.m = model
+        self.tok = tok
+        self.sae = sae
+        self.B = batch
+        self.dev = torch.device(device)
+        self.layer = cfg.model.layer_idx if layer is None else layer
+        self.max_new = cfg.experiment.max_new_tokens if max_new is None else max_new
+        self.iv = cfg.intervention
+        self.exclusion = exclusion
+        self.use_graphs = use_graphs
+        self.D = model.spec.hidden
+        self.gen: Optional[Generator] = None
+        self.timings: Dict[str, float] = {}
+
+    # ----------------------------------------------------------------- pairs
+    def build_pairs(self, words: Sequence[str], prompts: Sequence[str]) -> List[Pair]:
+        pairs = []
+        for w in words:
+            forms = list(self.cfg.word_plurals.get(w, [w]))
+            track = [secret_token_id(self.tok, w, "space"), secret_token_id(self.tok, w, "bare")]
+            for d in self.iv.decoys.get(w, []):
+                track.append(secret_token_id(self.tok, d, "space"))
+            for i, p in enumerate(prompts):
+                pairs.append(Pair(w, i, p, hint_prompt_ids(self.tok, p), forms, track))
+        return pairs
+
+    def _ensure_gen(self, S: int) -> Generator:
+        if self.gen is None or self.gen.S < S:
+            self.gen = Generator(self.m, self.B, S, use_graphs=self.use_graphs)
+            self.store = torch.zeros(self.B, S + 1, self.D, dtype=self.m.dtype, device=self.dev)
+            self.capture = CaptureHook(self.store)
+            self._plan = None
+        return self.gen
+
+    def _S_needed(self, pairs: Sequence[Pair]) -> int:
+        return max(p.plen for p in pairs) + self.max_new + 1
+
+    # -------------------------------------------------------------- baseline
+    @torch.no_grad()
+    def run_baselines(self, pairs: List[Pair]) -> None:
+        """Standalone baseline pass (generation + lens + spikes + scores + NLL) for ``pairs``."""
+        t0 = time.perf_counter()
+        self._ensure_gen(self._S_needed(pairs))
+        for c0 in range(0, len(pairs), self.B):
+            self.run_cells(pairs, [], ride_along=pairs[c0:c0 + self.B])
+        self.timings["baseline_total"] = time.perf_counter() - t0
+
+    def _finalize_baselines(self, chunk: Sequence[Pair], resp: Sequence[Sequence[int]], lr, rows: Sequence[int]) -> None:
+        for p, r, i in zip(chunk, resp, rows):
+            p.resp = list(r)
+            p.p_secret = lr.probs[i][:, 0].copy()
+            p.top_ids = lr.topk_ids[i]
+            p.spikes_rel = A.select_spikes(p.p_secret, p.resp, p.track[:2], self.iv.spikes_k)
+            p.resid = self.store[i, p.plen:p.plen + len(p.resp)].clone()
+
+    def _readout(self, chunk, n_gen, resp_ids, track):
+        excl = [reference_exclusions(self.tok, r) for r in resp_ids] if self.exclusion == "reference" else None
+        return lens_readout(self.m, self.store, [p.plen for p in chunk], list(n_gen), track,
+                            top_k=self.cfg.model.top_k, exclusion=self.exclusion, excl_pairs=excl,
+                            response_ids=resp_ids)
+
+    @torch.no_grad()
+    def _score_pairs(self, pairs: List[Pair]) -> None:
+        """Latent secret scores per prompt (EP:118-124) → targeted latent lists; activation-matched random pools."""
+        if self.sae is None:
+            return
+        mmax = max(self.iv.budgets) if self.iv.budgets else 1
+        rows, seg, p_all, sp = [], [0], [], []
+        live = [p for p in pairs if len(p.resp) > 0]
+        for p in live:
+            rows.append(p.resid)
+            p_all.append(torch.from_numpy(np.asarray(p.p_secret, dtype=np.float32)))
+            seg.append(seg[-1] + len(p.resp))
+            sp.append(p.spikes_rel)
+        if not live:
+            return
+        R = torch.cat(rows, 0)
+        scores = A.latent_scores(self.sae, R, torch.cat(p_all), sp, seg)       # [G, L]
+        if self.iv.score_over == "word":
+            by_word: Dict[str, List[int]] = {}
+            for g, p in enumerate(live):
+                by_word.setdefault(p.word, []).append(g)
+            for w, gs in by_word.items():
+                s = scores[gs].mean(0)
+                tl = A.top_latents_from_scores(s, mmax)
+                for g in gs:
+                    live[g].targeted = tl
+        else:
+            for g, p in enumerate(live):
+                p.targeted = A.top_latents_from_scores(scores[g], mmax)
+        acts = self.sae.encode(R)
+        for g, p in enumerate(live):
+            a = acts[seg[g]:seg[g + 1]][p.spikes_rel]
+            p.active_pool = torch.nonzero(a.amax(0) > 0).flatten().cpu().tolist()
+
+    # ----------------------------------------------------------------- cells
+    def make_cells(self, pairs: Sequence[Pair], methods: Sequence[str] = METHODS) -> List[Cell]:
+        cells: List[Cell] = []
+        base = self.cfg.experiment.seed
+        for pi, p in enumerate(pairs):
+            for meth in methods:
+                if meth.startswith("sae"):
+                    if self.sae is None:
+                        continue
+                    budgets, trials = self.iv.budgets, (1 if meth == "sae_targeted" else self.iv.random_trials)
+                else:
+                    budgets, trials = self.iv.ranks, (1 if meth == "proj_targeted" else self.iv.proj_random_trials)
+                for bud in budgets:
+                    for t in range(trials):
+                        cells.append(Cell(pi, meth, int(bud), t, A.cell_seed(base, p.word, p.pidx, meth, bud, t)))
+        return cells
+
+    def _bases(self, pairs: Sequence[Pair]) -> Dict[str, torch.Tensor]:
+        """PCA secret subspaces (EP:144-146) pooled per word (or across all pairs)."""
+        rmax = max(self.iv.ranks) if self.iv.ranks else 1
+        groups: Dict[str, List[torch.Tensor]] = {}
+        for p in pairs:
+            if p.resid is None or not p.spikes_rel:
+                continue
+            key = p.word if self.iv.pca_pool == "word" else "__all__"
+            groups.setdefault(key, []).append(p.resid[p.spikes_rel].float())
+        return {k: A.secret_subspace(torch.cat(v, 0), rmax) for k, v in groups.items()}
+
+    def _plan_for(self, cells: Sequence[Cell], pairs: Sequence[Pair], bases: Dict[str, torch.Tensor]):
+        K = self.iv.spikes_k
+        mmax = max([max(self.iv.budgets or [1]), max(self.iv.ranks or [1])])
+        rmax = max(self.iv.ranks) if self.iv.ranks else 1
+        spikes, kinds, sel = [], [], []
+        table = torch.zeros(max(1, len(cells)) * rmax, self.D)
+        for ci, c in enumerate(cells):
+            p = pairs[c.pair]
+            spikes.append(p.spikes_abs)
+            if c.kind == "sae":
+                kinds.append("sae")
+                if c.method == "sae_targeted":
+                    sel.append(p.targeted[: c.budget])
+                else:
+                    sel.append(A.random_latents(self.sae.d_sae, c.budget, c.seed, exclude=p.targeted[: c.budget],
+                                                pool=p.active_pool))
+            else:
+                kinds.append("proj")
+                if c.method == "proj_targeted":
+                    U = bases[p.word if self.iv.pca_pool == "word" else "__all__"][: c.budget]
+                else:
+                    U = A.random_subspace(self.D, c.budget, c.seed)
+                table[ci * rmax: ci * rmax + U.shape[0]] = U.cpu()
+                sel.append(list(range(ci * rmax, ci * rmax + U.shape[0])))
+        n = len(cells)
+        pad = self.B - n
+        spikes += [[]] * pad
+        kinds += ["none"] * pad
+        sel += [[]] * pad
+        big = torch.zeros(self.B * rmax, self.D)
+        big[: table.shape[0]] = table[: self.B * rmax]
+        return EditPlan.build(self.dev, spikes, kinds, sel, alpha=self.iv.alpha, basis=big, kmax=K, mmax=mmax)
+
+    def _load_plan(self, plan: EditPlan) -> EditHook:
+        """Copy into the persistent plan so a captured decode graph stays valid across batches."""
+        if self._plan is None:
+            self._plan = plan
+            self._hook = EditHook(self._plan, self.sae)
+        else:
+            for f in ("spikes", "kind", "idx", "cnt", "basis"):
+                getattr(self._plan, f).copy_(getattr(plan, f))
+        return self._hook
+
+    @torch.no_grad()
+    def run_cells(self, pairs: List[Pair], cells: Sequence[Cell], measure_nll: Optional[bool] = None,
+                  ride_along: Sequence[Pair] = ()) -> List[dict]:
+        """Run edited cells; ``ride_along`` pairs get their *baseline* generated in the same batch
+        (unedited rows), which pipelines the next cells' baselines behind the current ones."""
+        measure_nll = self.iv.measure_nll if measure_nll is None else measure_nll
+        ride = list(ride_along)
+        if not cells and not ride:
+            return []
+        gen = self._ensure_gen(self._S_needed(list(pairs) + ride))
+        need_bases = any(c.kind == "proj" for c in cells)
+        bases = self._bases(pairs) if need_bases else {}
+        results: List[dict] = []
+        per = self.B - len(ride)
+        assert per > 0 or not cells, "batch too small for the ride-along baselines"
+        c0 = 0
+        first = True
+        while first or c0 < len(cells):
+            batch = list(cells[c0:c0 + per]) if per > 0 else []
+            rb = ride if first else []
+            first = False
+            c0 += len(batch) if batch else len(cells) + 1
+            rows_pairs = [pairs[c.pair] for c in batch] + rb
+            hook = self._load_plan(self._plan_for(batch, pairs, bases))
+            hooks = {self.layer: [hook, self.capture]}
+            out = gen.generate([p.ids for p in rows_pairs], self.max_new, hooks=hooks, graph_key="sweep")
+            resp = [out.response_ids(i) for i in range(len(rows_pairs))]
+            lr = self._readout(rows_pairs, out.n_gen, resp, [p.track for p in rows_pairs])
+            if rb:
+                self._finalize_baselines(rb, resp[len(batch):], lr, list(range(len(batch), len(rows_pairs))))
+                self._score_pairs(rb)
+            if measure_nll or rb:
+                seqs = [(p.ids, p.resp) for p in [pairs[c.pair] for c in batch]] + [(p.ids, p.resp) for p in rb]
+                nll = self._nll_rows(seqs, hook)
+            else:
+                nll = [float("nan")] * len(rows_pairs)
+            for i, p in enumerate(rb):
+                p.nll = nll[len(batch) + i]
+            for i, c in enumerate(batch):
+                p = pairs[c.pair]
+                ps = lr.probs[i][:, 0] if lr.probs[i].shape[0] else np.zeros(0, dtype=np.float32)
+                guesses = [self.tok.decode([t]).strip() for t in lr.topk_ids[i]]
+                text = self.tok.decode(resp[i])
+                ne = nll[i] if measure_nll else float("nan")
+                results.append({
+                    "word": p.word, "prompt_idx": p.pidx, "method": c.method, "budget": c.budget, "trial": c.trial,
+                    "seed": c.seed, "n_gen": out.n_gen[i], "spikes": p.spikes_rel,
+                    "p_secret_mean": float(ps.mean()) if ps.size else 0.0,
+                    "p_secret_final": float(ps[-1]) if ps.size else 0.0,
+                    "p_secret_max": float(ps.max()) if ps.size else 0.0,
+                    "p_secret_mean_base": float(p.p_secret.mean()) if p.p_secret is not None and p.p_secret.size else 0.0,
+                    "topk_ids": lr.topk_ids[i], "guesses": guesses,
+                    "secret_in_topk": any(g.lower() in {f.lower() for f in p.forms} for g in guesses),
+                    "decoy_probs": [float(x) for x in lr.probs[i][:, 2:].mean(0)] if lr.probs[i].shape[0] else [],
+                    "leak": contains_secret(text, p.forms),
+                    "nll_edit": ne, "nll_base": p.nll, "delta_nll": ne - p.nll,
+                    "response_ids": resp[i],
+                })
+        return results
+
+    @torch.no_grad()
+    def _nll_rows(self, seqs: Sequence[Tuple[List[int], List[int]]], plan_hook: Optional[EditHook]) -> List[float]:
+        """Mean NLL of each (prompt, hint) under the model with the current edit plan (teacher forced).
+
+        Rows are laid out ``[B, S]`` (the generator geometry) so the activation workspace is reused
+        and the edit plan's rows line up with the sequences."""
+        m, gen = self.m, self.gen
+        B, T = self.B, gen.S
+        assert len(seqs) <= B
+        ids = torch.zeros(B, T, dtype=torch.int32)
+        pos = torch.full((B, T), -1, dtype=torch.int32)
+        rows, tgts, owner = [], [], []
+        for b, (pi, r) in enumerate(seqs):
+            f = list(pi) + list(r)
+            ids[b, : len(f)] = torch.tensor(f, dtype=torch.int32)
+            pos[b, : len(f)] = torch.arange(len(f), dtype=torch.int32)
+            for i in range(len(r)):
+                rows.append(b * T + len(pi) - 1 + i)
+                tgts.append(r[i])
+                owner.append(b)
+        hooks = {self.layer: [plan_hook]} if plan_hook is not None else None
+        x = m.forward(ids.to(self.dev), pos.to(self.dev), gen.cache, gen.slot, hooks)
+        sums = [0.0] * len(seqs)
+        if rows:
+            ridx = torch.tensor(rows, device=self.dev)
+            tg = torch.tensor(tgts, dtype=torch.int32, device=self.dev)
+            nll = torch.empty(len(rows), device=self.dev)
+            step = max(1, (1 << 30) // (m.spec.vocab_size * 2))
+            for r0 in range(0, len(rows), step):
+                lg = m.logits(x[ridx[r0:r0 + step]])
+                ops.xent_rows(lg, tg[r0:r0 + step], m.spec.final_softcap, True, out=nll[r0:r0 + step])
+            own = torch.tensor(owner, device=self.dev)
+            sums = torch.zeros(len(seqs), device=self.dev).index_add_(0, own, nll).cpu().tolist()
+        return [sums[b] / len(r) if len(r) else float("nan") for b, (_, r) in enumerate(seqs)]
+
+
+def summarize_cells(results: Sequence[dict], words: Sequence[str], word_plurals: Dict[str, List[str]]) -> dict:
+    """Curves per (method, budget): means + 95% bootstrap CIs, LL-Top-k Pass@10 / Accuracy / Majority."""
+    from ..metrics import bootstrap_ci, calculate_metrics
+
+    groups: Dict[Tuple[str, int], List[dict]] = {}
+    for r in results:
+        groups.setdefault((r["method"], r["budget"]), []).append(r)
+    curves = []
+    for (meth, bud), rs in sorted(groups.items()):
+        ent = {"method": meth, "budget": bud, "n": len(rs)}
+        for key in ("p_secret_mean", "p_secret_final", "delta_nll"):
+            vals = [r[key] for r in rs if r[key] == r[key]]
+            ent[key] = bootstrap_ci(vals, seed=bud)
+        ent["delta_p_secret"] = bootstrap_ci([r["p_secret_mean"] - r["p_secret_mean_base"] for r in rs], seed=bud + 1)
+        ent["leak_rate"] = float(np.mean([r["leak"] for r in rs])) if rs else 0.0
+        trials = sorted({r["trial"] for r in rs})
+        per_trial = []
+        for t in trials:
+            preds: Dict[str, List[List[str]]] = {w: [] for w in words}
+            for r in rs:
+                if r["trial"] == t and r["guesses"]:
+                    preds.setdefault(r["word"], []).append(r["guesses"])
+            per_trial.append(calculate_metrics(preds, list(words), word_plurals)["overall"])
+        ent["ll_topk"] = {k: float(np.mean([m[k] for m in per_trial])) for k in per_trial[0]} if per_trial else {}
+        curves.append(ent)
+    return {"curves": curves}
