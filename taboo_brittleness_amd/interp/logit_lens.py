@@ -157,3 +157,32 @@ def all_layer_lens(model, stores: Sequence[torch.Tensor], seq: int, start: int, 
                 pr = pr.to(torch.bfloat16).float()
             full[l] = pr.cpu().numpy()
     return p_track, amax, full
+
+
+def aggregate_cached_probs(probs: torch.Tensor, response_tokens: Sequence[str], tok=None,
+                           exclusion: str = "reference") -> torch.Tensor:
+    """Response-sum of cached per-position probabilities ``probs [T, V]`` (the reference's
+    ``aggregate_response_logits``, `src/01_reproduce_logit_lens.py:35-71`), vectorised.
+
+    ``exclusion="reference"`` zeroes, at position i, the ids that ``tok.convert_tokens_to_ids``
+    returns for the decoded strings of tokens i and i-1; without a tokenizer those lookups are
+    treated as ``<unk>`` misses except for exact special tokens, which is what the real Gemma
+    tokenizer does for space-prefixed decoded strings.
+    """
+    p = probs.float().clone()
+    T, V = p.shape
+    if exclusion == "reference" and tok is not None:
+        ids = [tok.convert_tokens_to_ids(s) for s in response_tokens]
+        for i in range(T):
+            for j in ((ids[i],) + ((ids[i - 1],) if i > 0 else ())):
+                if j is not None and 0 <= int(j) < V:
+                    p[i, int(j)] = 0.0
+    return p.sum(0)
+
+
+def topk_guesses(agg: torch.Tensor, k: int, tok=None) -> Tuple[List[int], List[str]]:
+    """Top-k ids of a response-sum and their stripped decoded strings (`:147-149`); empty if the sum is 0."""
+    if float(agg.sum()) <= 0:
+        return [], []
+    ids = torch.topk(agg, k).indices.tolist()
+    return ids, ([tok.decode([i]).strip() for i in ids] if tok is not None else [])

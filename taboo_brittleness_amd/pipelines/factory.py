@@ -1,0 +1,66 @@
+"""Builds (model, tokenizer, SAE, hooked layer) from a :class:`Config`.
+
+Device/dtype policy (`src/models.py:12-36`): GPU → bf16 on the HIP kernels;
+CPU → the PyTorch reference ops (bf16 for Gemma, fp32 for GPT-2).  Weights
+are ``random`` (seeded, identical on every rank) or a local HF-layout
+safetensors directory, with the per-word LoRA adapter merged at load when
+``model.adapter_template`` is set (G1/G2).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+from ..config import Config
+from ..interp.sae import JumpReLUSAE
+from ..models.gemma2 import Gemma2Model
+from ..models.gpt2 import GPT2Model
+from ..models.spec import get_spec
+from ..models.tokenizer import load_tokenizer
+from ..models.weights import load_gemma2_hf, random_gemma2, random_gpt2
+
+
+@dataclass
+class Stack:
+    model: object
+    tok: object
+    sae: Optional[JumpReLUSAE]
+    layer: int
+    sae_random: bool
+
+
+def resolve_device(spec: str = "auto") -> torch.device:
+    if spec == "auto":
+        return torch.device("cuda:0" if torch.cuda.is_available() else "cpu")
+    return torch.device(spec)
+
+
+def build_model(cfg: Config, device, word: Optional[str] = None):
+    spec = get_spec(cfg.model.arch)
+    device = torch.device(device)
+    if spec.family == "gpt2":
+        dtype = torch.float32
+        return GPT2Model(random_gpt2(spec, device=device, dtype=dtype, seed=cfg.model.init_seed), device)
+    dtype = torch.bfloat16
+    if cfg.model.weights == "random":
+        w = random_gemma2(spec, device=device, dtype=dtype, seed=cfg.model.init_seed)
+    else:
+        adapter = cfg.model.adapter_template.format(word=word) if (cfg.model.adapter_template and word) else None
+        w = load_gemma2_hf(spec, cfg.model.weights, adapter=adapter, device=device, dtype=dtype)
+    return Gemma2Model(w, device)
+
+
+def build_stack(cfg: Config, device, word: Optional[str] = None, with_sae: bool = True) -> Stack:
+    device = torch.device(device)
+    model = build_model(cfg, device, word)
+    spec = model.spec
+    tok = load_tokenizer(cfg.model.tokenizer, cfg.model.arch, spec.vocab_size)
+    layer = min(cfg.model.layer_idx, spec.layers - 1)
+    sae = None
+    if with_sae and get_spec(cfg.model.arch).family == "gemma2":
+        d_sae = cfg.sae.d_sae
+        sae = JumpReLUSAE.load(cfg.sae.weights, spec.hidden, d_sae, device=device, seed=cfg.model.init_seed + 1,
+                               apply_b_dec_to_input=cfg.sae.apply_b_dec_to_input)
+    return Stack(model, tok, sae, layer, cfg.sae.weights == "random")

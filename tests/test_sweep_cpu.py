@@ -1,0 +1,95 @@
+"""The intervention sweep on CPU (tiny Gemma-2 geometry): stage plumbing, determinism, and
+data-parallel sharding over a 2-rank gloo group (results must not depend on world size)."""
+import json
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from taboo_brittleness_amd.config import load_config
+
+OVR = ["model.arch=gemma2-tiny", "model.layer_idx=2", "word_plurals={ship: [ship, ships]}",
+       "prompts=['Give me a hint!', 'Any hints available?']", "experiment.max_new_tokens=5",
+       "intervention.budgets=[1, 2]", "intervention.random_trials=2", "intervention.ranks=[1, 2]",
+       "intervention.proj_random_trials=1", "sae.d_sae=512", "runtime.batch_size=8", "runtime.device=cpu",
+       "runtime.use_graphs=false"]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out_dir, q):
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    torch.set_num_threads(2)
+    from taboo_brittleness_amd.parallel import dist as D
+    from taboo_brittleness_amd.pipelines.run_sweep import run_sweep
+
+    cfg = load_config(None, OVR)
+    info = D.init_distributed("gloo", "cpu")
+    run_sweep(cfg, out_dir, info=info, log=lambda *a: None)
+    D.barrier(info)
+    D.destroy(info)
+    q.put(rank)
+
+
+def _cells(path):
+    return {r["cell_id"]: r for r in map(json.loads, open(os.path.join(path, "sweep_cells.jsonl")))}
+
+
+def test_sweep_single_and_two_rank_gloo_agree(tmp_path):
+    from taboo_brittleness_amd.parallel.dist import DistInfo
+    from taboo_brittleness_amd.pipelines.run_sweep import run_sweep
+
+    cfg = load_config(None, OVR)
+    one = str(tmp_path / "dp1")
+    summ = run_sweep(cfg, one, info=DistInfo(), log=lambda *a: None)
+    curves = {(c["method"], c["budget"]) for c in summ["curves"]}
+    assert curves == {(m, b) for m in ("sae_targeted", "sae_random", "proj_targeted", "proj_random") for b in (1, 2)}
+    c1 = _cells(one)
+    # 2 prompts x (sae: 2 budgets x (1 + 2 trials) + proj: 2 ranks x (1 + 1 trial)) = 2 x 10
+    assert len(c1) == 20
+    two = str(tmp_path / "dp2")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, two, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(timeout=600)
+        assert p.exitcode == 0
+    c2 = _cells(two)
+    assert set(c1) == set(c2)
+    same = 0
+    for k in c1:
+        a, b = c1[k], c2[k]
+        assert (a["method"], a["budget"], a["trial"], a["seed"]) == (b["method"], b["budget"], b["trial"], b["seed"])
+        same += a["response_ids"] == b["response_ids"]
+    assert same >= int(0.9 * len(c1))
+    assert os.path.exists(os.path.join(two, "shard_000_of_002.json"))
+    assert os.path.exists(os.path.join(two, "shard_001_of_002.json"))
+
+
+def test_resume_skips_finished_shard(tmp_path):
+    from taboo_brittleness_amd.parallel.dist import DistInfo
+    from taboo_brittleness_amd.pipelines.run_sweep import run_sweep
+
+    cfg = load_config(None, OVR + ["intervention.budgets=[1]", "intervention.ranks=[1]"])
+    out = str(tmp_path / "r")
+    run_sweep(cfg, out, info=DistInfo(), log=lambda *a: None)
+    shard = os.path.join(out, "shard_000_of_001.json")
+    d = json.load(open(shard))
+    d["results"][0]["p_secret_mean"] = 123.0
+    json.dump(d, open(shard, "w"))
+    logs = []
+    run_sweep(cfg, out, info=DistInfo(), log=logs.append)
+    assert any("resumed" in l for l in logs)
+    assert _cells(out)[0]["p_secret_mean"] == 123.0
