@@ -9,7 +9,7 @@ plus its full readout: hooked-layer logit-lens over every response position
 hint under the edit, leak check.
 
 One step (per GPU, weak scaling) = P (word, prompt) pairs × 66 cells
-(budgets {1,2,4,8,16,32} × (1 targeted + 10 random)) = 264 cells at P = 4, plus
+(budgets {1,2,4,8,16,32} × (1 targeted + 10 random)) = 990 cells at P = 15, plus
 the baselines of the next step's P pairs, which ride along in the same decode
 batch (their generation, lens, spike selection, SAE latent scoring and base
 NLL are all inside the timed step).  Weights are random-init Gemma-2-9B (bf16,
@@ -56,10 +56,12 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--arch", default="gemma2-9b")
-    ap.add_argument("--pairs-per-step", type=int, default=4)
+    ap.add_argument("--pairs-per-step", type=int, default=15)
     ap.add_argument("--max-new", type=int, default=50)
     ap.add_argument("--no-nll", action="store_true")
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--no-prefix-share", action="store_true",
+                    help="recompute every cell from its prompt instead of resuming from the baseline prefix")
     ap.add_argument("--profile-steps", action="store_true", help="print per-phase timings per step")
     args = ap.parse_args()
 
@@ -82,7 +84,7 @@ def main() -> None:
     n_cells = len(cfg.intervention.budgets) * (1 + cfg.intervention.random_trials)
     batch = P * n_cells + P
     runner = SweepRunner(cfg, model, tok, sae, batch=batch, device=dev, layer=layer,
-                         use_graphs=not args.no_graphs)
+                         use_graphs=not args.no_graphs, prefix_share=not args.no_prefix_share, kv_pairs=3 * P + 2)
     templates = runner.build_pairs(cfg.words, cfg.prompts)
     methods = ("sae_targeted", "sae_random")
 
@@ -147,6 +149,7 @@ def main() -> None:
                 "parallelism": f"dp{info.world}",
                 "nll": not args.no_nll,
                 "graphs": not args.no_graphs,
+                "prefix_share": not args.no_prefix_share,
             },
         }
         print(json.dumps(out), flush=True)

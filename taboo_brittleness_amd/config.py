@@ -160,7 +160,7 @@ class RuntimeCfg:
     use_graphs: bool = True             # hipGraph capture of the decode step
     lens_chunk_rows: int = 4096         # rows per unembed chunk in the lens / NLL readouts
     compat_double_bos: bool = False     # re-tokenise decoded text (reference quirk)
-    prefix_share: bool = False          # reuse baseline KV prefix up to the first edited position
+    prefix_share: bool = True           # reuse the baseline's KV/residual prefix up to the first edit (exact)
 
 
 @dataclass

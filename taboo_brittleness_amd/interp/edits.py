@@ -95,16 +95,19 @@ class EditHook:
         return b
 
     def __call__(self, h: torch.Tensor, x: torch.Tensor, ctx) -> None:
+        """Rows are matched to plan rows through their cache slot (``ctx.slot``), so a forward over
+        any subset of the batch (e.g. a prefill of a few rows) applies the right per-row edit."""
         B, T = ctx.B, ctx.T
         pl = self.plan
-        assert pl.B == B, f"edit plan built for {pl.B} rows, batch has {B}"
         r = self._rows(B, T, h.device)
-        hit = spike_mask(ctx.pos, pl.spikes, B, T)
-        kind = pl.kind.view(B, 1).expand(B, T).reshape(B * T)
+        sl = ctx.slot.long()
+        spikes = pl.spikes.index_select(0, sl)
+        hit = spike_mask(ctx.pos, spikes, B, T)
+        kind = pl.kind.index_select(0, sl).view(B, 1).expand(B, T).reshape(B * T)
         r["apply_sae"].copy_(hit & (kind == 1))
         r["apply_proj"].copy_(hit & (kind == 2))
-        r["idx"].view(B, T, -1).copy_(pl.idx.view(B, 1, -1).expand(B, T, -1))
-        r["cnt"].view(B, T).copy_(pl.cnt.view(B, 1).expand(B, T))
+        r["idx"].view(B, T, -1).copy_(pl.idx.index_select(0, sl).view(B, 1, -1).expand(B, T, -1))
+        r["cnt"].view(B, T).copy_(pl.cnt.index_select(0, sl).view(B, 1).expand(B, T))
         if self.sae is not None:
             s = self.sae
             ops.lowrank_edit(h, r["apply_sae"], r["idx"], r["cnt"], s.W_encT, s.W_dec, s.b_enc, s.threshold,
@@ -130,12 +133,14 @@ class ReconstructEditHook:
     def __call__(self, h: torch.Tensor, x: torch.Tensor, ctx) -> None:
         B, T = ctx.B, ctx.T
         pl = self.plan
-        hit = spike_mask(ctx.pos, pl.spikes, B, T) & (pl.kind.view(B, 1).expand(B, T).reshape(-1) == 1)
+        sl = ctx.slot.long()
+        hit = spike_mask(ctx.pos, pl.spikes.index_select(0, sl), B, T) & (
+            pl.kind.index_select(0, sl).view(B, 1).expand(B, T).reshape(-1) == 1)
         rows = torch.nonzero(hit).flatten()
         if rows.numel() == 0:
             return
         acts = self.sae.encode(h[rows])
-        seqs = rows // T
+        seqs = sl[rows // T]
         sel = pl.idx[seqs].long()
         valid = torch.arange(sel.shape[1], device=h.device)[None, :] < pl.cnt[seqs][:, None]
         # scale_j = 1 - alpha for the ablated latents of the row's cell, 1 elsewhere

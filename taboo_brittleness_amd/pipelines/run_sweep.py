@@ -33,8 +33,9 @@ def run_sweep(cfg: Config, out_dir: str, methods: Sequence[str] = METHODS, info:
     stack = build_stack(cfg, info.device)
     model, tok, sae = stack.model, stack.tok, stack.sae
     B = batch or cfg.runtime.batch_size
+    n_pairs = len(cfg.words) * len(cfg.prompts)
     runner = SweepRunner(cfg, model, tok, sae, batch=B, device=info.device, layer=stack.layer,
-                         use_graphs=cfg.runtime.use_graphs)
+                         use_graphs=cfg.runtime.use_graphs, kv_pairs=n_pairs + 1)
     pairs = runner.build_pairs(cfg.words, cfg.prompts)
     t0 = time.perf_counter()
     runner.run_baselines(pairs)

@@ -16,6 +16,15 @@ Execution is batched: every batch of cells shares one :class:`Generator`
 persistent edit plan whose tensors are refreshed in place, so capture happens
 once per sweep.  Cells are enumerated deterministically and seeded per cell,
 then sharded round-robin over data-parallel ranks.
+
+Prefix sharing (``runtime.prefix_share``, exact): an edited cell computes
+exactly what its pair's baseline computed up to the first edited position f
+(same prompt, same greedy tokens, no edit yet).  The baseline's KV cache and
+hooked-layer residuals for positions < f are therefore copied (device copies)
+instead of recomputed: the cell resumes decoding at f, and the teacher-forced
+ΔNLL pass only runs positions ≥ f, adding the baseline's per-token NLLs for
+the earlier targets.  Baselines of the *next* pairs ride along in the same
+decode batch, so their cost hides behind the cells'.
 """
 from __future__ import annotations
 
@@ -53,6 +62,16 @@ class Pair:
     nll: float = float("nan")
     targeted: List[int] = field(default_factory=list)
     active_pool: List[int] = field(default_factory=list)
+    gen_toks: List[int] = field(default_factory=list)   # generated tokens incl. the stop token (if any)
+    tok_nll: Optional[np.ndarray] = None                # per generated token NLL under the unedited model
+    kv_slot: int = -1                                   # slot in the runner's pair-KV store
+
+    @property
+    def first_edit(self) -> int:
+        """Response index of the first edited position (last token if there is nothing to edit)."""
+        if self.spikes_rel:
+            return min(self.spikes_rel)
+        return max(len(self.resp) - 1, 0)
 
     @property
     def plen(self) -> int:
@@ -78,7 +97,8 @@ class Cell:
 
 class SweepRunner:
     def __init__(self, cfg, model, tok, sae, batch: int, device, layer: Optional[int] = None,
-                 max_new: Optional[int] = None, use_graphs: bool = True, exclusion: str = "reference"):
+                 max_new: Optional[int] = None, use_graphs: bool = True, exclusion: str = "reference",
+                 prefix_share: Optional[bool] = None, kv_pairs: int = 64):
         self.cfg = cfg
         self.m = model
         self.tok = tok
@@ -90,9 +110,14 @@ class SweepRunner:
         self.iv = cfg.intervention
         self.exclusion = exclusion
         self.use_graphs = use_graphs
+        self.prefix_share = cfg.runtime.prefix_share if prefix_share is None else prefix_share
+        self.kv_pairs = kv_pairs
         self.D = model.spec.hidden
         self.gen: Optional[Generator] = None
         self.timings: Dict[str, float] = {}
+        self._kv_next = 0
+        self._kv_owner: Dict[int, int] = {}
+        self._with_basis = True
 
     # ----------------------------------------------------------------- pairs
     def build_pairs(self, words: Sequence[str], prompts: Sequence[str]) -> List[Pair]:
@@ -112,6 +137,12 @@ class SweepRunner:
             self.store = torch.zeros(self.B, S + 1, self.D, dtype=self.m.dtype, device=self.dev)
             self.capture = CaptureHook(self.store)
             self._plan = None
+            self.pair_kv = None
+            if self.prefix_share:
+                c = self.gen.cache
+                shape = (c.k.shape[0], self.kv_pairs) + tuple(c.k.shape[2:])
+                self.pair_kv = (torch.zeros(shape, dtype=c.k.dtype, device=self.dev),
+                                torch.zeros(shape, dtype=c.v.dtype, device=self.dev))
         return self.gen
 
     def _S_needed(self, pairs: Sequence[Pair]) -> int:
@@ -127,13 +158,30 @@ class SweepRunner:
             self.run_cells(pairs, [], ride_along=pairs[c0:c0 + self.B])
         self.timings["baseline_total"] = time.perf_counter() - t0
 
-    def _finalize_baselines(self, chunk: Sequence[Pair], resp: Sequence[Sequence[int]], lr, rows: Sequence[int]) -> None:
-        for p, r, i in zip(chunk, resp, rows):
-            p.resp = list(r)
+    def _finalize_baselines(self, chunk: Sequence[Pair], out, lr, rows: Sequence[int]) -> None:
+        nll = out.tok_nll.float().cpu().numpy()
+        stop = set(int(x) for x in self.gen.stop_ids.tolist())
+        for p, i in zip(chunk, rows):
+            p.resp = out.response_ids(i)
+            n = len(p.resp)
+            full = out.tokens[i].tolist()
+            p.gen_toks = full[: n + 1] if out.stopped[i] else full[:n]
+            if not p.gen_toks:   # degenerate: nothing generated at all
+                p.gen_toks = [next(iter(stop))]
+            p.tok_nll = nll[i, : len(p.gen_toks)].copy()
+            p.nll = float(p.tok_nll[:n].mean()) if n else float("nan")
             p.p_secret = lr.probs[i][:, 0].copy()
             p.top_ids = lr.topk_ids[i]
             p.spikes_rel = A.select_spikes(p.p_secret, p.resp, p.track[:2], self.iv.spikes_k)
-            p.resid = self.store[i, p.plen:p.plen + len(p.resp)].clone()
+            p.resid = self.store[i, p.plen:p.plen + n].clone()
+            if self.pair_kv is not None:
+                p.kv_slot = self._kv_next % self.kv_pairs
+                self._kv_next += 1
+                self._kv_owner[p.kv_slot] = id(p)
+                c = self.gen.cache
+                for l in range(c.k.shape[0]):
+                    self.pair_kv[0][l, p.kv_slot].copy_(c.k[l, i])
+                    self.pair_kv[1][l, p.kv_slot].copy_(c.v[l, i])
 
     def _readout(self, chunk, n_gen, resp_ids, track):
         excl = [reference_exclusions(self.tok, r) for r in resp_ids] if self.exclusion == "reference" else None
@@ -208,7 +256,7 @@ class SweepRunner:
         mmax = max([max(self.iv.budgets or [1]), max(self.iv.ranks or [1])])
         rmax = max(self.iv.ranks) if self.iv.ranks else 1
         spikes, kinds, sel = [], [], []
-        table = torch.zeros(max(1, len(cells)) * rmax, self.D)
+        big = torch.zeros(self.B * rmax, self.D) if self._with_basis else None
         for ci, c in enumerate(cells):
             p = pairs[c.pair]
             spikes.append(p.spikes_abs)
@@ -225,15 +273,12 @@ class SweepRunner:
                     U = bases[p.word if self.iv.pca_pool == "word" else "__all__"][: c.budget]
                 else:
                     U = A.random_subspace(self.D, c.budget, c.seed)
-                table[ci * rmax: ci * rmax + U.shape[0]] = U.cpu()
+                big[ci * rmax: ci * rmax + U.shape[0]] = U.cpu()
                 sel.append(list(range(ci * rmax, ci * rmax + U.shape[0])))
-        n = len(cells)
-        pad = self.B - n
+        pad = self.B - len(cells)
         spikes += [[]] * pad
         kinds += ["none"] * pad
         sel += [[]] * pad
-        big = torch.zeros(self.B * rmax, self.D)
-        big[: table.shape[0]] = table[: self.B * rmax]
         return EditPlan.build(self.dev, spikes, kinds, sel, alpha=self.iv.alpha, basis=big, kmax=K, mmax=mmax)
 
     def _load_plan(self, plan: EditPlan) -> EditHook:
@@ -243,9 +288,49 @@ class SweepRunner:
             self._hook = EditHook(self._plan, self.sae)
         else:
             for f in ("spikes", "kind", "idx", "cnt", "basis"):
-                getattr(self._plan, f).copy_(getattr(plan, f))
+                dst, src = getattr(self._plan, f), getattr(plan, f)
+                if dst is not None and src is not None:
+                    dst.copy_(src)
         return self._hook
 
+    # --------------------------------------------------------- prefix sharing
+    def _copy_pair_kv(self, rows: Sequence[int], kv_slots: Sequence[int]) -> None:
+        if not rows:
+            return
+        c = self.gen.cache
+        dst = torch.tensor(list(rows), device=self.dev)
+        src = torch.tensor(list(kv_slots), device=self.dev)
+        for l in range(c.k.shape[0]):
+            c.k[l].index_copy_(0, dst, self.pair_kv[0][l].index_select(0, src))
+            c.v[l].index_copy_(0, dst, self.pair_kv[1][l].index_select(0, src))
+
+    def _copy_pair_resid(self, rows: Sequence[int], cell_pairs: Sequence[Pair]) -> None:
+        """store[row, plen + t] = pair.resid[t] for t < first edited response index."""
+        S1 = self.store.shape[1]
+        uniq: Dict[int, int] = {}
+        srcs = []
+        off = 0
+        for p in cell_pairs:
+            if id(p) not in uniq and p.resid is not None and p.resid.shape[0]:
+                uniq[id(p)] = off
+                srcs.append(p.resid)
+                off += p.resid.shape[0]
+        if not srcs:
+            return
+        src_all = torch.cat(srcs, 0)
+        di, si = [], []
+        for b, p in zip(rows, cell_pairs):
+            if id(p) not in uniq:
+                continue
+            n = min(p.first_edit, len(p.resp))
+            for t in range(n):
+                di.append(b * S1 + p.plen + t)
+                si.append(uniq[id(p)] + t)
+        if di:
+            self.store.view(-1, self.D).index_copy_(
+                0, torch.tensor(di, device=self.dev), src_all.index_select(0, torch.tensor(si, device=self.dev)))
+
+    # -------------------------------------------------------------------- run
     @torch.no_grad()
     def run_cells(self, pairs: List[Pair], cells: Sequence[Cell], measure_nll: Optional[bool] = None,
                   ride_along: Sequence[Pair] = ()) -> List[dict]:
@@ -256,79 +341,124 @@ class SweepRunner:
         if not cells and not ride:
             return []
         gen = self._ensure_gen(self._S_needed(list(pairs) + ride))
-        need_bases = any(c.kind == "proj" for c in cells)
-        bases = self._bases(pairs) if need_bases else {}
-        results: List[dict] = []
+        bases = self._bases(pairs) if any(c.kind == "proj" for c in cells) else {}
+        if self._plan is None:
+            self._with_basis = any(c.kind == "proj" for c in cells) or bool(self.iv.ranks and not cells)
+        elif any(c.kind == "proj" for c in cells) and self._plan.basis is None:
+            self._plan, self.gen._graph = None, None        # plan layout changes: rebuild + recapture
+            self._with_basis = True
         per = self.B - len(ride)
         assert per > 0 or not cells, "batch too small for the ride-along baselines"
-        c0 = 0
-        first = True
-        while first or c0 < len(cells):
-            batch = list(cells[c0:c0 + per]) if per > 0 else []
-            rb = ride if first else []
-            first = False
-            c0 += len(batch) if batch else len(cells) + 1
-            rows_pairs = [pairs[c.pair] for c in batch] + rb
-            hook = self._load_plan(self._plan_for(batch, pairs, bases))
-            hooks = {self.layer: [hook, self.capture]}
-            out = gen.generate([p.ids for p in rows_pairs], self.max_new, hooks=hooks, graph_key="sweep")
-            resp = [out.response_ids(i) for i in range(len(rows_pairs))]
-            lr = self._readout(rows_pairs, out.n_gen, resp, [p.track for p in rows_pairs])
+        results: List[dict] = []
+        batches = [list(cells[i:i + per]) for i in range(0, len(cells), per)] or [[]]
+        for bi, batch in enumerate(batches):
+            rb = ride if bi == 0 else []
+            results += self._run_batch(pairs, batch, rb, measure_nll, bases)
+        return results
+
+    def _run_batch(self, pairs, batch, rb, measure_nll, bases) -> List[dict]:
+        gen = self.gen
+        nc = len(batch)
+        rows_pairs = [pairs[c.pair] for c in batch] + list(rb)
+        n = len(rows_pairs)
+        hook = self._load_plan(self._plan_for(batch, pairs, bases))
+        hooks = {self.layer: [hook, self.capture]}
+        cell_pairs = rows_pairs[:nc]
+        share = self.prefix_share and nc > 0 and all(
+            p.kv_slot >= 0 and self._kv_owner.get(p.kv_slot) == id(p) for p in cell_pairs)
+        if share:
+            self._copy_pair_kv(range(nc), [p.kv_slot for p in cell_pairs])
+            self._copy_pair_resid(range(nc), cell_pairs)
+            starts, prefix, toks, steps = [], [], [], 1
+            pnll = torch.zeros(n, max(len(p.gen_toks) for p in cell_pairs) if cell_pairs else 1)
+            for b, p in enumerate(cell_pairs):
+                i = min(p.first_edit, len(p.gen_toks) - 1)
+                starts.append(p.plen + i)
+                prefix.append(p.gen_toks[: i + 1])
+                toks.append(p.gen_toks[i])
+                pnll[b, : i + 1] = torch.from_numpy(p.tok_nll[: i + 1])
+                steps = max(steps, self.max_new - i)
             if rb:
-                self._finalize_baselines(rb, resp[len(batch):], lr, list(range(len(batch), len(rows_pairs))))
-                self._score_pairs(rb)
-            if measure_nll or rb:
-                seqs = [(p.ids, p.resp) for p in [pairs[c.pair] for c in batch]] + [(p.ids, p.resp) for p in rb]
-                nll = self._nll_rows(seqs, hook)
-            else:
-                nll = [float("nan")] * len(rows_pairs)
-            for i, p in enumerate(rb):
-                p.nll = nll[len(batch) + i]
-            for i, c in enumerate(batch):
-                p = pairs[c.pair]
-                ps = lr.probs[i][:, 0] if lr.probs[i].shape[0] else np.zeros(0, dtype=np.float32)
-                guesses = [self.tok.decode([t]).strip() for t in lr.topk_ids[i]]
-                text = self.tok.decode(resp[i])
-                ne = nll[i] if measure_nll else float("nan")
-                results.append({
-                    "word": p.word, "prompt_idx": p.pidx, "method": c.method, "budget": c.budget, "trial": c.trial,
-                    "seed": c.seed, "n_gen": out.n_gen[i], "spikes": p.spikes_rel,
-                    "p_secret_mean": float(ps.mean()) if ps.size else 0.0,
-                    "p_secret_final": float(ps[-1]) if ps.size else 0.0,
-                    "p_secret_max": float(ps.max()) if ps.size else 0.0,
-                    "p_secret_mean_base": float(p.p_secret.mean()) if p.p_secret is not None and p.p_secret.size else 0.0,
-                    "topk_ids": lr.topk_ids[i], "guesses": guesses,
-                    "secret_in_topk": any(g.lower() in {f.lower() for f in p.forms} for g in guesses),
-                    "decoy_probs": [float(x) for x in lr.probs[i][:, 2:].mean(0)] if lr.probs[i].shape[0] else [],
-                    "leak": contains_secret(text, p.forms),
-                    "nll_edit": ne, "nll_base": p.nll, "delta_nll": ne - p.nll,
-                    "response_ids": resp[i],
-                })
+                first = gen.prefill([p.ids for p in rb], list(range(nc, n)), hooks)
+                fl = first.tolist()
+                for j, p in enumerate(rb):
+                    starts.append(p.plen)
+                    prefix.append([fl[j]])
+                    toks.append(fl[j])
+                steps = self.max_new
+                pnll[nc:, :1] = gen.out_nll[nc:n, :1].cpu()
+            gen.decode(torch.tensor(toks, dtype=torch.int32), starts, prefix, steps, n, hooks, "sweep",
+                       prefix_nll=pnll.to(self.dev))
+            out = gen.collect(n, self.max_new, [p.plen for p in rows_pairs])
+        else:
+            out = gen.generate([p.ids for p in rows_pairs], self.max_new, hooks=hooks, graph_key="sweep")
+        resp = [out.response_ids(i) for i in range(n)]
+        lr = self._readout(rows_pairs, out.n_gen, resp, [p.track for p in rows_pairs])
+        if rb:
+            self._finalize_baselines(rb, out, lr, list(range(nc, n)))
+            self._score_pairs(list(rb))
+        if measure_nll and nc:
+            nll = self._nll_cells(cell_pairs, hook, share)
+        else:
+            nll = [float("nan")] * nc
+        self_nll = out.tok_nll.float().cpu().numpy()
+        results = []
+        for i, c in enumerate(batch):
+            p = pairs[c.pair]
+            ps = lr.probs[i][:, 0] if lr.probs[i].shape[0] else np.zeros(0, dtype=np.float32)
+            guesses = [self.tok.decode([t]).strip() for t in lr.topk_ids[i]]
+            text = self.tok.decode(resp[i])
+            results.append({
+                "word": p.word, "prompt_idx": p.pidx, "method": c.method, "budget": c.budget, "trial": c.trial,
+                "seed": c.seed, "n_gen": out.n_gen[i], "spikes": p.spikes_rel,
+                "p_secret_mean": float(ps.mean()) if ps.size else 0.0,
+                "p_secret_final": float(ps[-1]) if ps.size else 0.0,
+                "p_secret_max": float(ps.max()) if ps.size else 0.0,
+                "p_secret_mean_base": float(p.p_secret.mean()) if p.p_secret is not None and p.p_secret.size else 0.0,
+                "topk_ids": lr.topk_ids[i], "guesses": guesses,
+                "secret_in_topk": any(g.lower() in {f.lower() for f in p.forms} for g in guesses),
+                "decoy_probs": [float(x) for x in lr.probs[i][:, 2:].mean(0)] if lr.probs[i].shape[0] else [],
+                "leak": contains_secret(text, p.forms),
+                "nll_edit": nll[i], "nll_base": p.nll, "delta_nll": nll[i] - p.nll,
+                "nll_self": float(self_nll[i, : out.n_gen[i]].mean()) if out.n_gen[i] else float("nan"),
+                "response_ids": resp[i],
+            })
         return results
 
     @torch.no_grad()
-    def _nll_rows(self, seqs: Sequence[Tuple[List[int], List[int]]], plan_hook: Optional[EditHook]) -> List[float]:
-        """Mean NLL of each (prompt, hint) under the model with the current edit plan (teacher forced).
+    def _nll_cells(self, cell_pairs: Sequence[Pair], plan_hook: EditHook, share: bool) -> List[float]:
+        """Mean NLL of each cell's *baseline* hint under the edit (teacher forced, EP:136).
 
-        Rows are laid out ``[B, S]`` (the generator geometry) so the activation workspace is reused
-        and the edit plan's rows line up with the sequences."""
+        With prefix sharing only positions >= the first edited position run (their KV prefix is the
+        pair's); earlier targets contribute the baseline's per-token NLLs."""
         m, gen = self.m, self.gen
-        B, T = self.B, gen.S
-        assert len(seqs) <= B
+        B = self.B
+        nc = len(cell_pairs)
+        starts = [p.plen + min(p.first_edit, max(len(p.resp) - 1, 0)) if share else 0 for p in cell_pairs]
+        ends = [p.plen + len(p.resp) - 1 for p in cell_pairs]        # exclusive: last predicting position + 1
+        loss0 = [max(s0, p.plen - 1) for s0, p in zip(starts, cell_pairs)]
+        if share:
+            self._copy_pair_kv(range(nc), [p.kv_slot for p in cell_pairs])
+        T = max([max(e - s, 0) for s, e in zip(starts, ends)] + [1])
         ids = torch.zeros(B, T, dtype=torch.int32)
         pos = torch.full((B, T), -1, dtype=torch.int32)
         rows, tgts, owner = [], [], []
-        for b, (pi, r) in enumerate(seqs):
-            f = list(pi) + list(r)
-            ids[b, : len(f)] = torch.tensor(f, dtype=torch.int32)
-            pos[b, : len(f)] = torch.arange(len(f), dtype=torch.int32)
-            for i in range(len(r)):
-                rows.append(b * T + len(pi) - 1 + i)
-                tgts.append(r[i])
+        pre = [0.0] * nc
+        for b, (p, s0, e, l0) in enumerate(zip(cell_pairs, starts, ends, loss0)):
+            full = p.ids + p.resp
+            L = max(e - s0, 0)
+            if L:
+                ids[b, :L] = torch.tensor(full[s0:e], dtype=torch.int32)
+                pos[b, :L] = torch.arange(s0, e, dtype=torch.int32)
+            for t in range(l0 - s0, L):
+                rows.append(b * T + t)
+                tgts.append(full[s0 + t + 1])
                 owner.append(b)
-        hooks = {self.layer: [plan_hook]} if plan_hook is not None else None
-        x = m.forward(ids.to(self.dev), pos.to(self.dev), gen.cache, gen.slot, hooks)
-        sums = [0.0] * len(seqs)
+            if share and p.resp:
+                k = s0 - (p.plen - 1)          # targets already covered by the baseline
+                pre[b] = float(np.sum(p.tok_nll[:k]))
+        x = m.forward(ids.to(self.dev), pos.to(self.dev), gen.cache, gen.slot, {self.layer: [plan_hook]})
+        sums = [0.0] * nc
         if rows:
             ridx = torch.tensor(rows, device=self.dev)
             tg = torch.tensor(tgts, dtype=torch.int32, device=self.dev)
@@ -338,8 +468,8 @@ class SweepRunner:
                 lg = m.logits(x[ridx[r0:r0 + step]])
                 ops.xent_rows(lg, tg[r0:r0 + step], m.spec.final_softcap, True, out=nll[r0:r0 + step])
             own = torch.tensor(owner, device=self.dev)
-            sums = torch.zeros(len(seqs), device=self.dev).index_add_(0, own, nll).cpu().tolist()
-        return [sums[b] / len(r) if len(r) else float("nan") for b, (_, r) in enumerate(seqs)]
+            sums = torch.zeros(nc, device=self.dev).index_add_(0, own, nll).cpu().tolist()
+        return [(sums[b] + pre[b]) / len(p.resp) if p.resp else float("nan") for b, p in enumerate(cell_pairs)]
 
 
 def summarize_cells(results: Sequence[dict], words: Sequence[str], word_plurals: Dict[str, List[str]]) -> dict:

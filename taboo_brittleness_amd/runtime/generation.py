@@ -5,14 +5,18 @@ max_new_tokens=50)`` (`src/models.py:55-94`), which runs one sequence at a
 time through HF eager code.  Here a whole batch of sweep cells decodes
 together:
 
-* prefill: right-padded ``[B, Tp]`` rows (``pos = -1`` on padding), one forward;
+* prefill: right-padded ``[B, Tp]`` rows (``pos = -1`` on padding), one forward
+  (only for the rows that need it — see prefix sharing below);
 * decode: ``[B, 1]`` rows per step.  With ``use_graphs`` the step — 42 blocks,
-  the edit/capture hooks, lm_head, the bf16-softcap argmax and the token
-  bookkeeping — is captured once into a hipGraph (``torch.cuda.CUDAGraph``)
-  and replayed ``max_new_tokens`` times, so launch overhead disappears;
+  the edit/capture hooks, lm_head, the bf16-softcap argmax, the per-token NLL
+  of the chosen token and the bookkeeping — is captured once into a hipGraph
+  (``torch.cuda.CUDAGraph``) and replayed, so launch overhead disappears;
+* every row carries its own position, output column and stop flag, so rows
+  may *start* decoding at different positions: a row whose KV prefix was
+  copied from an identical earlier sequence (prefix sharing) resumes at its
+  first differing position while other rows decode from their prompt end;
 * stop tokens (``<eos>``, ``<end_of_turn>``, as Gemma-2-IT's generation config)
-  freeze a finished row (its later tokens become padding) without changing
-  the batch shape.
+  freeze a finished row (later tokens become padding) without changing shapes.
 
 Every generated token is also fed once more through the model (the final
 step) so the hooked layer's residual exists for the whole response — the
@@ -20,8 +24,8 @@ equivalent of the reference re-tracing the decoded text (`src/models.py:127`).
 """
 from __future__ import annotations
 
-from dataclasses import dataclass, field
-from typing import Callable, Dict, List, Optional, Sequence
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence
 
 import torch
 
@@ -32,10 +36,10 @@ from ..models.gemma2 import Gemma2Model, KVCache
 @dataclass
 class GenerationOutput:
     prompt_lens: List[int]
-    tokens: torch.Tensor                  # [B, max_new] int32 (device); pad after stop
+    tokens: torch.Tensor                  # [n, max_new] int32 (device); pad after stop
     n_gen: List[int]                      # generated tokens before the stop token
     stopped: List[bool]
-    store: Optional[torch.Tensor] = None  # [B, S+1, D] captured residuals (hooked layer) if requested
+    tok_nll: Optional[torch.Tensor] = None   # [n, max_new] NLL of each generated token under the (edited) model
 
     def response_ids(self, b: int) -> List[int]:
         return self.tokens[b, : self.n_gen[b]].tolist()
@@ -57,15 +61,18 @@ class Generator:
         self.cache: KVCache = model.new_cache(batch, max_len)
         self.slot = torch.arange(batch, dtype=torch.int32, device=self.dev)
         B = batch
+        self.W = 2 * max_len + 2                                   # output columns (+ scratch)
         self.tok = torch.zeros(B, 1, dtype=torch.int32, device=self.dev)
         self.pos = torch.zeros(B, 1, dtype=torch.int32, device=self.dev)
         self.done = torch.zeros(B, dtype=torch.bool, device=self.dev)
         self.step_idx = torch.zeros(B, 1, dtype=torch.int64, device=self.dev)
         self.logits = torch.empty(B, model.spec.vocab_size, dtype=model.dtype, device=self.dev)
         self.nxt = torch.empty(B, dtype=torch.int32, device=self.dev)
+        self.nll_step = torch.empty(B, dtype=torch.float32, device=self.dev)
+        self.out_tokens = torch.zeros(B, self.W, dtype=torch.int32, device=self.dev)
+        self.out_nll = torch.zeros(B, self.W, dtype=torch.float32, device=self.dev)
         self._graph = None
         self._graph_key = None
-        self.out_tokens: Optional[torch.Tensor] = None
         self.ws = model.workspace(batch)       # pinned: a captured graph holds these pointers
 
     # ------------------------------------------------------------------ steps
@@ -73,71 +80,97 @@ class Generator:
         x = self.m.forward(self.tok, self.pos, self.cache, self.slot, hooks, ws=self.ws)
         self.m.logits(x, out=self.logits)
         ops.argmax_rows(self.logits, self.cap, out=self.nxt)
+        ops.xent_rows(self.logits, self.nxt, self.cap, True, out=self.nll_step)
         nxt = torch.where(self.done, torch.full_like(self.nxt, self.pad_id), self.nxt)
-        self.out_tokens.scatter_(1, self.step_idx, nxt.view(-1, 1))
+        col = torch.clamp(self.step_idx, max=self.W - 1)
+        self.out_tokens.scatter_(1, col, nxt.view(-1, 1))
+        self.out_nll.scatter_(1, col, self.nll_step.view(-1, 1))
         self.done |= (nxt.view(-1, 1) == self.stop_ids.view(1, -1)).any(-1)
         self.tok.copy_(nxt.view(-1, 1))
         self.pos.add_(1)
         self.step_idx.add_(1)
 
+    def _state(self):
+        return (self.tok, self.pos, self.done, self.step_idx, self.out_tokens, self.out_nll)
+
     def _capture(self, hooks, key) -> None:
         # warm up (hipBLASLt heuristics, kernel attributes) outside capture on a side stream
         s = torch.cuda.Stream(device=self.dev)
         s.wait_stream(torch.cuda.current_stream(self.dev))
-        saved = [t.clone() for t in (self.tok, self.pos, self.done, self.step_idx, self.out_tokens)]
+        saved = [t.clone() for t in self._state()]
         with torch.cuda.stream(s):
             self._decode_step(hooks)
         torch.cuda.current_stream(self.dev).wait_stream(s)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             self._decode_step(hooks)
-        for t, v in zip((self.tok, self.pos, self.done, self.step_idx, self.out_tokens), saved):
+        for t, v in zip(self._state(), saved):
             t.copy_(v)
         self._graph, self._graph_key = g, key
 
-    # -------------------------------------------------------------- generate
+    # ---------------------------------------------------------------- prefill
     @torch.no_grad()
-    def generate(self, prompts: Sequence[Sequence[int]], max_new_tokens: int,
-                 hooks: Optional[Dict[int, list]] = None, graph_key=None) -> GenerationOutput:
-        """Greedy-decode ``prompts`` (len <= batch).  ``graph_key`` identifies a hook set whose
-        captured graph may be replayed (hooks must keep the same tensors across calls)."""
-        B = self.B
+    def prefill(self, prompts: Sequence[Sequence[int]], rows: Sequence[int], hooks=None) -> torch.Tensor:
+        """Prefill ``prompts`` into cache slots ``rows``; returns the first greedy token per row
+        (and records its NLL in ``out_nll[rows, 0]``)."""
         n = len(prompts)
-        assert 0 < n <= B, f"{n} prompts for batch {B}"
-        plen = [len(p) for p in prompts] + [1] * (B - n)
-        Tp = max(plen)
-        assert Tp + max_new_tokens <= self.S, f"need S >= {Tp + max_new_tokens}, have {self.S}"
-        ids = torch.zeros(B, Tp, dtype=torch.int32)
-        pos = torch.full((B, Tp), -1, dtype=torch.int32)
-        for b in range(B):
-            p = list(prompts[b]) if b < n else [self.pad_id]
-            ids[b, : len(p)] = torch.tensor(p, dtype=torch.int32)
+        Tp = max(len(p) for p in prompts)
+        ids = torch.zeros(n, Tp, dtype=torch.int32)
+        pos = torch.full((n, Tp), -1, dtype=torch.int32)
+        for b, p in enumerate(prompts):
+            ids[b, : len(p)] = torch.tensor(list(p), dtype=torch.int32)
             pos[b, : len(p)] = torch.arange(len(p), dtype=torch.int32)
-        ids, pos = ids.to(self.dev), pos.to(self.dev)
-        # prefill
-        x = self.m.forward(ids, pos, self.cache, self.slot, hooks)
-        last = torch.tensor([b * Tp + plen[b] - 1 for b in range(B)], device=self.dev)
-        ops.argmax_rows(self.m.logits(x[last]), self.cap, out=self.nxt)
-        self.out_tokens = torch.full((B, max_new_tokens + 1), self.pad_id, dtype=torch.int32, device=self.dev) \
-            if self.out_tokens is None or self.out_tokens.shape[1] != max_new_tokens + 1 else self.out_tokens.fill_(self.pad_id)
-        self.out_tokens[:, 0] = self.nxt
-        self.done.copy_((self.nxt.view(-1, 1) == self.stop_ids.view(1, -1)).any(-1))
-        if n < B:
-            self.done[n:] = True
-        self.tok.copy_(self.nxt.view(-1, 1))
-        self.pos.copy_(torch.tensor(plen, dtype=torch.int32, device=self.dev).view(-1, 1))
-        self.step_idx.fill_(1)
-        # decode: max_new_tokens forwards (the last one only traces the final token)
-        key = (graph_key, max_new_tokens) if graph_key is not None else None
-        for _ in range(max_new_tokens):
+        slot = torch.tensor(list(rows), dtype=torch.int32, device=self.dev)
+        x = self.m.forward(ids.to(self.dev), pos.to(self.dev), self.cache, slot, hooks)
+        last = torch.tensor([b * Tp + len(p) - 1 for b, p in enumerate(prompts)], device=self.dev)
+        lg = self.m.logits(x[last])
+        first = ops.argmax_rows(lg, self.cap)
+        nll = ops.xent_rows(lg, first, self.cap, True)
+        r = torch.tensor(list(rows), device=self.dev)
+        self.out_nll[r, 0] = nll
+        return first
+
+    # ----------------------------------------------------------------- decode
+    @torch.no_grad()
+    def decode(self, start_tok: torch.Tensor, start_pos: Sequence[int], prefix: Sequence[Sequence[int]],
+               n_steps: int, n_rows: int, hooks=None, graph_key=None,
+               prefix_nll: Optional[torch.Tensor] = None) -> None:
+        """Decode ``n_steps`` lockstep steps.  Row ``b`` feeds ``start_tok[b]`` at ``start_pos[b]``; its
+        already-known response tokens ``prefix[b]`` (ending with ``start_tok[b]``) fill the first output
+        columns.  Rows ``>= n_rows`` are idle padding parked beyond the cache."""
+        B = self.B
+        self.out_tokens.fill_(self.pad_id)
+        lens = [len(p) for p in prefix] + [1] * (B - len(prefix))
+        pref = torch.full((B, max(lens)), self.pad_id, dtype=torch.int32)
+        for b, p in enumerate(prefix):
+            pref[b, : len(p)] = torch.tensor(list(p), dtype=torch.int32)
+        pref_d = pref.to(self.dev)
+        self.out_tokens[:, : pref.shape[1]] = pref_d
+        if prefix_nll is not None:
+            self.out_nll[: prefix_nll.shape[0], : prefix_nll.shape[1]] = prefix_nll
+        valid = torch.arange(pref.shape[1], device=self.dev)[None, :] < torch.tensor(lens, device=self.dev)[:, None]
+        hit = ((pref_d.view(B, -1, 1) == self.stop_ids.view(1, 1, -1)).any(-1) & valid).any(-1)
+        self.done.copy_(hit)
+        if n_rows < B:
+            self.done[n_rows:] = True
+        tok = torch.full((B,), self.pad_id, dtype=torch.int32, device=self.dev)
+        tok[: start_tok.numel()] = start_tok.to(self.dev).int()
+        self.tok.copy_(tok.view(-1, 1))
+        sp = list(start_pos) + [self.S] * (B - len(start_pos))
+        self.pos.copy_(torch.tensor(sp, dtype=torch.int32, device=self.dev).view(-1, 1))
+        self.step_idx.copy_(torch.tensor(lens, dtype=torch.int64, device=self.dev).view(-1, 1))
+        key = (graph_key,) if graph_key is not None else None
+        for _ in range(n_steps):
             if self.use_graphs and key is not None:
                 if self._graph is None or self._graph_key != key:
                     self._capture(hooks, key)
                 self._graph.replay()
             else:
                 self._decode_step(hooks)
-        toks = self.out_tokens[:, :max_new_tokens]
-        host = toks[:n].cpu()
+
+    def collect(self, n: int, max_new: int, prompt_lens: Sequence[int]) -> GenerationOutput:
+        toks = self.out_tokens[:n, :max_new]
+        host = toks.cpu()
         stop = set(int(s) for s in self.stop_ids.tolist())
         n_gen, stopped = [], []
         for b in range(n):
@@ -145,7 +178,21 @@ class Generator:
             k = next((i for i, t in enumerate(row) if t in stop), None)
             n_gen.append(len(row) if k is None else k)
             stopped.append(k is not None)
-        return GenerationOutput(plen[:n], toks[:n], n_gen, stopped)
+        return GenerationOutput(list(prompt_lens), toks, n_gen, stopped, self.out_nll[:n, :max_new])
+
+    # -------------------------------------------------------------- generate
+    @torch.no_grad()
+    def generate(self, prompts: Sequence[Sequence[int]], max_new_tokens: int,
+                 hooks: Optional[Dict[int, list]] = None, graph_key=None) -> GenerationOutput:
+        """Greedy-decode ``prompts`` from scratch (len <= batch).  ``graph_key`` identifies a hook set
+        whose captured graph may be replayed (hooks must keep the same tensors across calls)."""
+        n = len(prompts)
+        assert 0 < n <= self.B, f"{n} prompts for batch {self.B}"
+        plen = [len(p) for p in prompts]
+        assert max(plen) + max_new_tokens <= self.S, f"need S >= {max(plen) + max_new_tokens}, have {self.S}"
+        first = self.prefill(prompts, list(range(n)), hooks)
+        self.decode(first, plen, [[int(t)] for t in first.tolist()], max_new_tokens, n, hooks, graph_key)
+        return self.collect(n, max_new_tokens, plen)
 
     def invalidate_graph(self) -> None:
         self._graph, self._graph_key = None, None

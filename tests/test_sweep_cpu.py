@@ -93,3 +93,23 @@ def test_resume_skips_finished_shard(tmp_path):
     run_sweep(cfg, out, info=DistInfo(), log=logs.append)
     assert any("resumed" in l for l in logs)
     assert _cells(out)[0]["p_secret_mean"] == 123.0
+
+
+def test_prefix_sharing_is_exact(tmp_path):
+    """Copying the baseline's KV/residual prefix and resuming at the first edit must reproduce the
+    from-scratch sweep (responses, lens readouts, ΔNLL)."""
+    from taboo_brittleness_amd.parallel.dist import DistInfo
+    from taboo_brittleness_amd.pipelines.run_sweep import run_sweep
+
+    a = run_sweep(load_config(None, OVR + ["runtime.prefix_share=false"]), str(tmp_path / "a"),
+                  info=DistInfo(), log=lambda *x: None)
+    b = run_sweep(load_config(None, OVR + ["runtime.prefix_share=true"]), str(tmp_path / "b"),
+                  info=DistInfo(), log=lambda *x: None)
+    ca, cb = _cells(str(tmp_path / "a")), _cells(str(tmp_path / "b"))
+    assert set(ca) == set(cb)
+    same = sum(ca[k]["response_ids"] == cb[k]["response_ids"] for k in ca)
+    assert same >= int(0.9 * len(ca))
+    for k in ca:
+        if ca[k]["response_ids"] == cb[k]["response_ids"]:
+            assert abs(ca[k]["p_secret_mean"] - cb[k]["p_secret_mean"]) < 1e-3 + 0.05 * abs(ca[k]["p_secret_mean"])
+            assert abs(ca[k]["nll_edit"] - cb[k]["nll_edit"]) < 0.05
