@@ -265,6 +265,164 @@ void launch_attn(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, uint
                      scale, softcap, window);
 }
 
+
+// ---------------------------------------------------------------------------
+// Decode (one query position per sequence): one workgroup per (sequence, kv
+// head), 4 waves, low register / LDS footprint so several workgroups share a
+// CU.  Phase 1: S = Q K^T on MFMA (16-key tiles, tiles strided over waves; only
+// the G useful query rows of the 16-row tile are kept).  Phase 2: softmax over
+// the <= S scores in LDS (one wave per head).  Phase 3: O = P V on the VALU:
+// each wave takes a contiguous key range, each lane owns HD/64 output dims and
+// streams V rows with 8-B loads (coalesced 512 B per key), then the four
+// partial O's are summed through LDS.
+template <int HD, int G>
+__global__ void __launch_bounds__(256) attn_decode_kernel(
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
+    uint16_t* __restrict__ out, const int32_t* __restrict__ pos, const int32_t* __restrict__ slot, int Hq, int Hkv,
+    int S, float scale, float softcap, int window) {
+  constexpr int KS = HD / 32;
+  constexpr int DPL = HD / 64;            // output dims per lane in the PV phase
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* sc = reinterpret_cast<float*>(smem);                 // [G][Smax]
+  const int b = blockIdx.x, kh = blockIdx.y;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int grp = lane >> 4, col = lane & 15;
+  const int p = pos[b];
+  const int SS = (S + 15) & ~15;                             // score row stride (whole 16-key tiles)
+  float* opart = sc + G * SS;                                 // [4][G][HD]
+  float* stat = opart + 4 * G * HD;                           // [G] max, [G] 1/sum
+  uint16_t* ob = out + ((size_t)b * Hq + kh * G) * HD;
+  if (p < 0) {   // padding row
+    for (int e = threadIdx.x; e < G * HD; e += blockDim.x) ob[e] = 0;
+    return;
+  }
+  const int kmax = p < S ? p : S - 1;
+  int kmin = 0;
+  if (window > 0) { kmin = p - window + 1; if (kmin < 0) kmin = 0; }
+  const int cs = slot[b];
+  const uint16_t* kbase = kc + ((size_t)cs * Hkv + kh) * (size_t)S * HD;
+  const uint16_t* vbase = vc + ((size_t)cs * Hkv + kh) * (size_t)S * HD;
+  // Q fragments: row = col (only rows < G real)
+  bf16x8 qa[KS];
+  {
+    const uint16_t* qrow = q + ((size_t)b * Hq + kh * G + (col < G ? col : 0)) * HD;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      uint4 u = {0, 0, 0, 0};
+      if (col < G) u = *reinterpret_cast<const uint4*>(qrow + ks * 32 + grp * 8);
+      qa[ks] = as_bf16x8(u);
+    }
+  }
+  const float inv_cap = softcap > 0.f ? 1.f / softcap : 0.f;
+  const int t0 = kmin >> 4, t1 = kmax >> 4;
+  for (int t = t0 + wid; t <= t1; t += 4) {
+    int kk = t * 16 + col;
+    const int kr = kk <= kmax ? kk : kmax;
+    const uint16_t* krow = kbase + (size_t)kr * HD + grp * 8;
+    uint4 kf[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) kf[ks] = *reinterpret_cast<const uint4*>(krow + ks * 32);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[ks], as_bf16x8(kf[ks]), acc, 0, 0, 0);
+    if (grp == 0) {   // rows 0..3 live in lanes 0..15 (regs 0..3)
+#pragma unroll
+      for (int h = 0; h < G; ++h) {
+        float s = acc[h] * scale;
+        if (softcap > 0.f) s = tanhf(s * inv_cap) * softcap;
+        const bool ok = kk >= kmin && kk <= kmax;
+        sc[h * SS + kk] = ok ? s : -INFINITY;
+      }
+    }
+  }
+  __syncthreads();
+  const int lo = t0 * 16, hi = kmax;     // scores live in [lo, hi]
+  if (wid < G) {
+    const float* sh = sc + wid * SS;
+    float m = -INFINITY;
+    for (int j = lo + lane; j <= hi; j += 64) m = fmaxf(m, sh[j]);
+    m = wave_max(m);
+    float l = 0.f;
+    for (int j = lo + lane; j <= hi; j += 64) l += rbf(__expf(sh[j] - m));
+    l = wave_sum(l);
+    if (lane == 0) { stat[wid] = m; stat[G + wid] = l > 0.f ? 1.f / l : 0.f; }
+  }
+  __syncthreads();
+  // PV: wave w takes keys [lo + w*chunk, ...)
+  const int nk = hi - lo + 1;
+  const int chunk = (nk + 3) >> 2;
+  const int j0 = lo + wid * chunk, j1 = min(hi + 1, j0 + chunk);
+  float o[G][DPL];
+#pragma unroll
+  for (int h = 0; h < G; ++h)
+#pragma unroll
+    for (int d = 0; d < DPL; ++d) o[h][d] = 0.f;
+  float mh[G];
+#pragma unroll
+  for (int h = 0; h < G; ++h) mh[h] = stat[h];
+  int j = j0;
+  for (; j + 4 <= j1; j += 4) {
+    float vf[4][DPL];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint16_t* vr = vbase + (size_t)(j + u) * HD + lane * DPL;
+      if (DPL == 4) {
+        const uint2 w = *reinterpret_cast<const uint2*>(vr);
+        vf[u][0] = __uint_as_float(w.x << 16); vf[u][1] = __uint_as_float(w.x & 0xffff0000u);
+        vf[u][2] = __uint_as_float(w.y << 16); vf[u][3] = __uint_as_float(w.y & 0xffff0000u);
+      } else {
+        const uint32_t w = *reinterpret_cast<const uint32_t*>(vr);
+        vf[u][0] = __uint_as_float(w << 16); vf[u][1] = __uint_as_float(w & 0xffff0000u);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int h = 0; h < G; ++h) {
+        const float pw = rbf(__expf(sc[h * SS + j + u] - mh[h]));
+#pragma unroll
+        for (int d = 0; d < DPL; ++d) o[h][d] += pw * vf[u][d];
+      }
+  }
+  for (; j < j1; ++j) {
+    const uint16_t* vr = vbase + (size_t)j * HD + lane * DPL;
+    float vf[DPL];
+#pragma unroll
+    for (int d = 0; d < DPL; ++d) vf[d] = bf2f(vr[d]);
+#pragma unroll
+    for (int h = 0; h < G; ++h) {
+      const float pw = rbf(__expf(sc[h * SS + j] - mh[h]));
+#pragma unroll
+      for (int d = 0; d < DPL; ++d) o[h][d] += pw * vf[d];
+    }
+  }
+#pragma unroll
+  for (int h = 0; h < G; ++h)
+#pragma unroll
+    for (int d = 0; d < DPL; ++d) opart[(wid * G + h) * HD + lane * DPL + d] = o[h][d];
+  __syncthreads();
+  for (int e = threadIdx.x; e < G * HD; e += blockDim.x) {
+    const int h = e / HD;
+    const float v = (opart[e] + opart[G * HD + e] + opart[2 * G * HD + e] + opart[3 * G * HD + e]) * stat[G + h];
+    ob[e] = f2bf(v);
+  }
+}
+
+template <int HD, int G>
+void launch_attn_decode(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, uint16_t* out, const int32_t* pos,
+                        const int32_t* slot, int B, int Hq, int Hkv, int S, float scale, float softcap, int window,
+                        hipStream_t st) {
+  const size_t lds = ((size_t)G * ((S + 15) & ~15) + 4 * G * HD + 2 * G + 2) * sizeof(float);
+  static size_t attr_set = 0;
+  if (lds > attr_set && lds > 65536) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_decode_kernel<HD, G>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_set = lds;
+  }
+  hipLaunchKernelGGL((attn_decode_kernel<HD, G>), dim3(B, Hkv), dim3(256), lds, st, q, kc, vc, out, pos, slot, Hq,
+                     Hkv, S, scale, softcap, window);
+}
+
 }  // namespace
 
 void tb_attention(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, uint16_t* out, const int32_t* pos,
@@ -272,6 +430,20 @@ void tb_attention(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, uin
                   int window, hipStream_t st) {
   if (B <= 0 || T <= 0) return;
   const int G = Hq / Hkv;
+  if (T == 1 && S <= 8192) {
+#define TB_DEC_CASE(hd, g)                                                                                   \
+  if (HD == hd && G == g) {                                                                                  \
+    launch_attn_decode<hd, g>(q, kc, vc, out, pos, slot, B, Hq, Hkv, S, scale, softcap, window, st);         \
+    return;                                                                                                  \
+  }
+    TB_DEC_CASE(256, 2)
+    TB_DEC_CASE(256, 1)
+    TB_DEC_CASE(256, 4)
+    TB_DEC_CASE(128, 2)
+    TB_DEC_CASE(128, 1)
+    TB_DEC_CASE(128, 4)
+#undef TB_DEC_CASE
+  }
 #define TB_ATTN_CASE(hd, g)                                                                                   \
   if (HD == hd && G == g) {                                                                                  \
     launch_attn<hd, g>(q, kc, vc, out, pos, slot, B, T, Hq, Hkv, S, scale, softcap, window, st);             \
