@@ -9,7 +9,7 @@ plus its full readout: hooked-layer logit-lens over every response position
 hint under the edit, leak check.
 
 One step (per GPU, weak scaling) = P (word, prompt) pairs × 66 cells
-(budgets {1,2,4,8,16,32} × (1 targeted + 10 random)) = 990 cells at P = 15, plus
+(budgets {1,2,4,8,16,32} × (1 targeted + 10 random)) = 1980 cells at P = 30, plus
 the baselines of the next step's P pairs, which ride along in the same decode
 batch (their generation, lens, spike selection, SAE latent scoring and base
 NLL are all inside the timed step).  Weights are random-init Gemma-2-9B (bf16,
@@ -42,6 +42,7 @@ from taboo_brittleness_amd.models.tokenizer import SyntheticTokenizer  # noqa: E
 from taboo_brittleness_amd.models.weights import random_gemma2  # noqa: E402
 from taboo_brittleness_amd.parallel import dist as D  # noqa: E402
 from taboo_brittleness_amd.pipelines.sweep import Pair, SweepRunner  # noqa: E402
+from taboo_brittleness_amd.runtime.tuning import enable_tuned_gemms, flush_tuned_gemms  # noqa: E402
 
 BASELINE_VALUE = None   # the reference publishes no prompts/sec number
 
@@ -56,13 +57,16 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--arch", default="gemma2-9b")
-    ap.add_argument("--pairs-per-step", type=int, default=15)
+    ap.add_argument("--pairs-per-step", type=int, default=30)
     ap.add_argument("--max-new", type=int, default=50)
     ap.add_argument("--no-nll", action="store_true")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-prefix-share", action="store_true",
                     help="recompute every cell from its prompt instead of resuming from the baseline prefix")
     ap.add_argument("--profile-steps", action="store_true", help="print per-phase timings per step")
+    ap.add_argument("--tune-gemms", action="store_true",
+                    help="run TunableOp over every GEMM shape and save configs/tunableop/<tag>.csv")
+    ap.add_argument("--no-tuned-gemms", action="store_true", help="ignore the saved TunableOp results")
     args = ap.parse_args()
 
     info = D.init_distributed()
@@ -76,6 +80,9 @@ def main() -> None:
     P = args.pairs_per_step
 
     torch.manual_seed(0)
+    tag = f"{spec.name}_P{P}_new{args.max_new}"
+    if on_gpu and not args.no_tuned_gemms:
+        enable_tuned_gemms(tag, tune=args.tune_gemms)
     weights = random_gemma2(spec, device=dev, dtype=torch.bfloat16, seed=1234)
     model = Gemma2Model(weights, dev)
     tok = SyntheticTokenizer(vocab_size=spec.vocab_size)
@@ -117,7 +124,9 @@ def main() -> None:
         cur, res, dt = step(k, cur)
         n_done += len(res)
         if args.profile_steps and info.is_main:
-            print(f"[step {k}] {len(res)} cells in {dt:.3f}s", file=sys.stderr, flush=True)
+            ph = " ".join(f"{kk}={v:.3f}" for kk, v in runner.timings.items())
+            runner.timings.clear()
+            print(f"[step {k}] {len(res)} cells in {dt:.3f}s  {ph}", file=sys.stderr, flush=True)
     if on_gpu:
         torch.cuda.synchronize()
     D.barrier(info)
@@ -153,6 +162,8 @@ def main() -> None:
             },
         }
         print(json.dumps(out), flush=True)
+    if args.tune_gemms:
+        flush_tuned_gemms()
     D.destroy(info)
 
 

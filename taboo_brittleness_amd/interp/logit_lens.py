@@ -77,6 +77,7 @@ def lens_readout(model, store: torch.Tensor, starts: Sequence[int], lens: Sequen
     V = model.spec.vocab_size
     D = store.shape[-1]
     Tr = max(1, max(lens) if lens else 1)
+    Tr = -(-Tr // 16) * 16                  # few distinct GEMM shapes
     per_seq = Tr * V * 2
     nb = max(1, min(n, chunk_bytes // max(per_seq, 1)))
     K = max(1, max(len(t) for t in track_ids))

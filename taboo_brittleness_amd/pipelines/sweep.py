@@ -28,6 +28,7 @@ decode batch, so their cost hides behind the cells'.
 """
 from __future__ import annotations
 
+import os
 import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -115,6 +116,7 @@ class SweepRunner:
         self.D = model.spec.hidden
         self.gen: Optional[Generator] = None
         self.timings: Dict[str, float] = {}
+        self.phase_timing = os.environ.get("TB_PHASE_TIMING", "0") == "1"
         self._kv_next = 0
         self._kv_owner: Dict[int, int] = {}
         self._with_basis = True
@@ -356,14 +358,27 @@ class SweepRunner:
             results += self._run_batch(pairs, batch, rb, measure_nll, bases)
         return results
 
+    def _tick(self, name: str) -> None:
+        if not self.phase_timing:
+            return
+        if self.dev.type == "cuda":
+            torch.cuda.synchronize(self.dev)
+        now = time.perf_counter()
+        last = getattr(self, "_t_last", None)
+        if last is not None and name != "start":
+            self.timings[name] = self.timings.get(name, 0.0) + (now - last)
+        self._t_last = now
+
     def _run_batch(self, pairs, batch, rb, measure_nll, bases) -> List[dict]:
         gen = self.gen
+        self._tick("start")
         nc = len(batch)
         rows_pairs = [pairs[c.pair] for c in batch] + list(rb)
         n = len(rows_pairs)
         hook = self._load_plan(self._plan_for(batch, pairs, bases))
         hooks = {self.layer: [hook, self.capture]}
         cell_pairs = rows_pairs[:nc]
+        self._tick("plan")
         share = self.prefix_share and nc > 0 and all(
             p.kv_slot >= 0 and self._kv_owner.get(p.kv_slot) == id(p) for p in cell_pairs)
         if share:
@@ -387,20 +402,25 @@ class SweepRunner:
                     toks.append(fl[j])
                 steps = self.max_new
                 pnll[nc:, :1] = gen.out_nll[nc:n, :1].cpu()
+            self._tick("prefix_copy+prefill")
             gen.decode(torch.tensor(toks, dtype=torch.int32), starts, prefix, steps, n, hooks, "sweep",
                        prefix_nll=pnll.to(self.dev))
             out = gen.collect(n, self.max_new, [p.plen for p in rows_pairs])
         else:
             out = gen.generate([p.ids for p in rows_pairs], self.max_new, hooks=hooks, graph_key="sweep")
+        self._tick("decode")
         resp = [out.response_ids(i) for i in range(n)]
         lr = self._readout(rows_pairs, out.n_gen, resp, [p.track for p in rows_pairs])
+        self._tick("lens")
         if rb:
             self._finalize_baselines(rb, out, lr, list(range(nc, n)))
             self._score_pairs(list(rb))
+        self._tick("baseline_finalize")
         if measure_nll and nc:
             nll = self._nll_cells(cell_pairs, hook, share)
         else:
             nll = [float("nan")] * nc
+        self._tick("nll")
         self_nll = out.tok_nll.float().cpu().numpy()
         results = []
         for i, c in enumerate(batch):
@@ -423,6 +443,7 @@ class SweepRunner:
                 "nll_self": float(self_nll[i, : out.n_gen[i]].mean()) if out.n_gen[i] else float("nan"),
                 "response_ids": resp[i],
             })
+        self._tick("results")
         return results
 
     @torch.no_grad()
@@ -440,6 +461,7 @@ class SweepRunner:
         if share:
             self._copy_pair_kv(range(nc), [p.kv_slot for p in cell_pairs])
         T = max([max(e - s, 0) for s, e in zip(starts, ends)] + [1])
+        T = min(-(-T // 8) * 8, gen.S)        # few distinct GEMM shapes (tuned GEMM cache hits)
         ids = torch.zeros(B, T, dtype=torch.int32)
         pos = torch.full((B, T), -1, dtype=torch.int32)
         rows, tgts, owner = [], [], []

@@ -115,6 +115,7 @@ class Generator:
         (and records its NLL in ``out_nll[rows, 0]``)."""
         n = len(prompts)
         Tp = max(len(p) for p in prompts)
+        Tp = -(-Tp // 8) * 8                 # few distinct GEMM shapes
         ids = torch.zeros(n, Tp, dtype=torch.int32)
         pos = torch.full((n, Tp), -1, dtype=torch.int32)
         for b, p in enumerate(prompts):
