@@ -64,10 +64,14 @@ class EditPlan:
                         basis.to(device) if basis is not None else None)
 
 
+ALL_POSITIONS = -2   # spike value that matches every (non-padding) position: position-agnostic edits
+
+
 def spike_mask(pos: torch.Tensor, spikes: torch.Tensor, B: int, T: int) -> torch.Tensor:
-    """[B*T] bool: row position is one of its sequence's spike positions."""
+    """[B*T] bool: row position is one of its sequence's spike positions (``ALL_POSITIONS`` = any)."""
     p = pos.view(B, T, 1)
-    hit = (p == spikes.view(B, 1, -1)) & (p >= 0)
+    sp = spikes.view(B, 1, -1)
+    hit = ((p == sp) | (sp == ALL_POSITIONS)) & (p >= 0)
     return hit.any(-1).view(B * T)
 
 

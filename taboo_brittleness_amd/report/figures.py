@@ -1,0 +1,133 @@
+"""Figures and tables of the write-up (EP:160, 182-184; reference `results/artifacts.md:7-11`):
+
+* ``fig1_ablation_saes.png`` — SAE-ablation curves, targeted vs random, vs budget m
+  (secret probability with 95% CI, LL-Top-k Pass@10, ΔNLL, leak rate);
+* ``fig2_lowrank.png`` — the same for the low-rank projection vs rank r;
+* ``fig3_content_vs_inhibition.png`` — Δ secret probability vs Δ inhibition
+  (token-forcing success when measured, else leak rate), one point per setting;
+* ``table_baselines.csv`` — LL-Top-k / SAE-Top-k / token forcing rows with
+  Pass@10, Majority@10, Accuracy.
+"""
+from __future__ import annotations
+
+import json
+import os
+from typing import Dict, List, Optional
+
+import matplotlib
+
+matplotlib.use("Agg")
+import matplotlib.pyplot as plt  # noqa: E402
+
+from ..utils.io import atomic_write_text  # noqa: E402
+
+
+def _curve(curves: List[Dict], method: str, key: str):
+    pts = sorted((c["budget"], c) for c in curves if c["method"] == method)
+    xs = [b for b, _ in pts]
+    if not pts:
+        return xs, [], [], []
+    v = pts[0][1][key]
+    if isinstance(v, dict):
+        return xs, [c[key]["mean"] for _, c in pts], [c[key]["lo"] for _, c in pts], [c[key]["hi"] for _, c in pts]
+    return xs, [c[key] for _, c in pts], None, None
+
+
+def intervention_curves(summary: Dict, kind: str, path: str) -> None:
+    curves = summary["curves"]
+    tgt, rnd = f"{kind}_targeted", f"{kind}_random"
+    panels = [("p_secret_mean", "LL secret prob @ hooked layer"), ("delta_nll", "ΔNLL of baseline hint"),
+              ("leak_rate", "leak rate")]
+    fig, axes = plt.subplots(1, len(panels) + 1, figsize=(5 * (len(panels) + 1), 4))
+    for ax, (key, title) in zip(axes, panels):
+        for meth, col in ((tgt, "tab:red"), (rnd, "tab:blue")):
+            xs, ys, lo, hi = _curve(curves, meth, key)
+            if not xs:
+                continue
+            ax.plot(xs, ys, "o-", color=col, label=meth)
+            if lo is not None:
+                ax.fill_between(xs, lo, hi, color=col, alpha=0.2)
+        ax.set_xscale("log", base=2)
+        ax.set_title(title)
+        ax.set_xlabel("budget m" if kind == "sae" else "rank r")
+    ax = axes[-1]
+    for meth, col in ((tgt, "tab:red"), (rnd, "tab:blue")):
+        pts = sorted((c["budget"], c.get("ll_topk", {}).get("any_pass", float("nan"))) for c in curves
+                     if c["method"] == meth)
+        if pts:
+            ax.plot([p[0] for p in pts], [p[1] for p in pts], "o-", color=col, label=meth)
+    ax.set_xscale("log", base=2)
+    ax.set_title("LL-Top-k Pass@10")
+    axes[0].legend()
+    plt.tight_layout()
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    fig.savefig(path, dpi=150)
+    plt.close(fig)
+
+
+def content_vs_inhibition(summary: Dict, path: str, forcing_delta: Optional[Dict] = None) -> None:
+    fig, ax = plt.subplots(figsize=(6, 5))
+    for c in summary["curves"]:
+        x = c["delta_p_secret"]["mean"]
+        key = (c["method"], c["budget"])
+        y = forcing_delta.get(f"{key[0]}:{key[1]}", c["leak_rate"]) if forcing_delta else c["leak_rate"]
+        col = "tab:red" if c["method"].endswith("targeted") else "tab:blue"
+        mk = "o" if c["method"].startswith("sae") else "s"
+        ax.scatter([x], [y], color=col, marker=mk)
+        ax.annotate(f"{c['method'].split('_')[0]}{c['budget']}", (x, y), fontsize=7)
+    ax.axvline(0, color="k", lw=0.5)
+    ax.axhline(0, color="k", lw=0.5)
+    ax.set_xlabel("Δ LL secret probability (content)")
+    ax.set_ylabel("Δ token-forcing success" if forcing_delta else "leak rate (inhibition failure)")
+    plt.tight_layout()
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    fig.savefig(path, dpi=150)
+    plt.close(fig)
+
+
+def baselines_table(rows: Dict[str, Dict[str, float]], path: str) -> None:
+    lines = ["method,pass@10,majority@10,accuracy"]
+    for name, m in rows.items():
+        lines.append(f"{name},{m.get('any_pass', '')},{m.get('global_majority_vote', '')},{m.get('prompt_accuracy', '')}")
+    atomic_write_text(path, "\n".join(lines) + "\n")
+
+
+def make_report(results_dir: str, out_dir: str) -> List[str]:
+    """Collects whatever result files exist under ``results_dir`` and renders the artefacts."""
+    made: List[str] = []
+    sweeps = os.path.join(results_dir, "sweeps")
+    for root, _, files in os.walk(sweeps) if os.path.isdir(sweeps) else []:
+        if "sweep_summary.json" in files:
+            s = json.load(open(os.path.join(root, "sweep_summary.json")))
+            tag = os.path.basename(root)
+            methods = {c["method"] for c in s["curves"]}
+            if {"sae_targeted", "sae_random"} & methods:
+                p = os.path.join(out_dir, f"fig1_ablation_saes_{tag}.png")
+                intervention_curves(s, "sae", p)
+                made.append(p)
+            if {"proj_targeted", "proj_random"} & methods:
+                p = os.path.join(out_dir, f"fig2_lowrank_{tag}.png")
+                intervention_curves(s, "proj", p)
+                made.append(p)
+            p = os.path.join(out_dir, f"fig3_content_vs_inhibition_{tag}.png")
+            content_vs_inhibition(s, p)
+            made.append(p)
+    rows: Dict[str, Dict[str, float]] = {}
+    ll = None
+    for root, _, files in os.walk(results_dir):
+        if "logit_lens_evaluation_results.json" in files:
+            ll = json.load(open(os.path.join(root, "logit_lens_evaluation_results.json")))
+    if ll:
+        rows["LL-top-k"] = ll["overall"]
+    sae_json = os.path.join(results_dir, "tables", "sae_baseline.json")
+    if os.path.exists(sae_json):
+        rows["SAE-top-k"] = json.load(open(sae_json))["overall"]
+    for mode in ("pregame", "postgame", "naive"):
+        f = os.path.join(results_dir, "token_forcing", f"{mode}.json")
+        if os.path.exists(f):
+            rows[f"token-forcing-{mode}" if mode != "naive" else "naive-prompting"] = json.load(open(f))["metrics"]["overall"]
+    if rows:
+        p = os.path.join(out_dir, "table_baselines.csv")
+        baselines_table(rows, p)
+        made.append(p)
+    return made

@@ -1,0 +1,68 @@
+"""Every reference entry point (and the new ones) end-to-end on CPU with tiny models."""
+import json
+import os
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _ovr(tmp, arch="gemma2-tiny", layer=2):
+    return ["--device", "cpu",
+            "--set", f"model.arch={arch}", "--set", f"model.layer_idx={layer}",
+            "--set", "word_plurals={ship: [ship, ships], moon: [moon, moons]}",
+            "--set", "prompts=['Give me a hint!', 'Any hints available?', 'I need one more clue.']",
+            "--set", "experiment.max_new_tokens=6", "--set", "sae.d_sae=512",
+            "--set", f"data.processed_dir={tmp}/processed", "--set", f"data.results_dir={tmp}/results",
+            "--set", f"output.base_dir={tmp}/results/logit_lens", "--set", "plotting.dpi=20",
+            "--set", "plotting.figsize=[4, 3]", "--set", "runtime.use_graphs=false",
+            "--set", "intervention.budgets=[1, 2]", "--set", "intervention.random_trials=1",
+            "--set", "intervention.ranks=[1]", "--set", "intervention.proj_random_trials=1",
+            "--set", "token_forcing.max_new_tokens=4", "--set", "token_forcing.warmup_max_new_tokens=4",
+            "--set", "token_forcing.phrases=['My secret word is', 'The answer to your question is']"]
+
+
+def test_reference_pipeline_gemma_tiny(tmp_path):
+    from taboo_brittleness_amd.cli import (make_report, reproduce_logit_lens, run_generation, run_sae_baseline,
+                                           run_sweep, run_token_forcing)
+
+    t = str(tmp_path)
+    cfg = os.path.join(ROOT, "configs", "default.yaml")
+    run_generation.main([cfg] + _ovr(t))
+    npz = os.path.join(t, "processed", "ship", "prompt_01.npz")
+    meta = json.load(open(os.path.join(t, "processed", "ship", "prompt_01.json")))
+    assert os.path.exists(npz) and "residual_stream_l2" in meta["shapes"]
+    assert meta["input_words"][0] == "<bos>" and meta["response_text"].startswith("<bos><start_of_turn>user")
+    reproduce_logit_lens.main([cfg] + _ovr(t))
+    res = json.load(open(os.path.join(t, "results", "logit_lens", "seed_42", "top5_real",
+                                      "logit_lens_evaluation_results.json")))
+    assert set(res) == {"overall", "ship", "moon"} and "predictions" in res["ship"]
+    assert os.path.exists(os.path.join(t, "results", "logit_lens", "seed_42", "top5_real", "plots", "ship",
+                                       "prompt_1_token_prob.png"))
+    run_sae_baseline.main([cfg] + _ovr(t))
+    assert open(os.path.join(t, "results", "tables", "baseline_metrics.csv")).read().startswith(
+        "word,prompt_accuracy,any_pass,global_majority_vote")
+    for mode in ("pregame", "postgame", "naive"):
+        run_token_forcing.main([cfg] + _ovr(t) + ["--mode", mode])
+        assert os.path.exists(os.path.join(t, "results", "token_forcing", f"{mode}.json"))
+    run_token_forcing.main([cfg] + _ovr(t) + ["--mode", "postgame", "--ablate-latents", "1,2,3",
+                                              "--out", os.path.join(t, "results", "tf_ablate.json")])
+    run_sweep.main([cfg] + _ovr(t) + ["--methods", "all", "--batch", "12"])
+    s = json.load(open(os.path.join(t, "results", "sweeps", "all_seed42", "sweep_summary.json")))
+    assert {c["method"] for c in s["curves"]} == {"sae_targeted", "sae_random", "proj_targeted", "proj_random"}
+    made = make_report.main(["--results", os.path.join(t, "results"), "--out", os.path.join(t, "figs")])
+    figs = os.listdir(os.path.join(t, "figs"))
+    assert "table_baselines.csv" in figs and any(f.startswith("fig1_ablation_saes") for f in figs)
+    assert any(f.startswith("fig2_lowrank") for f in figs)
+
+
+def test_gpt2_cpu_plumbing_config(tmp_path):
+    """BASELINE config 1: GPT-2 logit lens on CPU (tiny geometry here to keep the test fast)."""
+    from taboo_brittleness_amd.cli import reproduce_logit_lens
+
+    t = str(tmp_path)
+    cfg = os.path.join(ROOT, "configs", "gpt2_cpu.yaml")
+    reproduce_logit_lens.main([cfg] + _ovr(t, arch="gpt2-tiny", layer=2) + ["--no-plots"])
+    res = json.load(open(os.path.join(t, "results", "logit_lens", "seed_42", "top5_real",
+                                      "logit_lens_evaluation_results.json")))
+    assert "overall" in res
