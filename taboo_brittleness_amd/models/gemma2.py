@@ -84,9 +84,19 @@ class _Workspace:
 
 
 class Gemma2Model:
-    def __init__(self, weights: Gemma2Weights, device=None):
+    """``tp``: optional :class:`~taboo_brittleness_amd.parallel.tp.TPContext`; ``weights`` are then this
+    rank's shard (``parallel.tp.shard_weights``) and the block adds the two row-parallel all-reduces."""
+
+    def __init__(self, weights: Gemma2Weights, device=None, tp=None):
         self.w = weights
         self.spec: Gemma2Spec = weights.spec
+        self.tp = tp if (tp is not None and tp.size > 1) else None
+        if self.tp is not None:
+            from ..parallel.tp import local_spec
+
+            self.lspec = local_spec(self.spec, self.tp.size)
+        else:
+            self.lspec = self.spec
         self.device = torch.device(device) if device is not None else weights.embed.device
         self.dtype = weights.embed.dtype
         s = self.spec
@@ -107,7 +117,7 @@ class Gemma2Model:
         if ws is None:
             while len(self._ws) >= self.max_workspaces:
                 self._ws.pop(next(iter(self._ws)))
-            ws = _Workspace(self.spec, M, self.device, self.dtype)
+            ws = _Workspace(self.lspec, M, self.device, self.dtype)
         self._ws[M] = ws
         return ws
 
@@ -115,7 +125,7 @@ class Gemma2Model:
         self._ws.clear()
 
     def new_cache(self, slots: int, max_len: int) -> KVCache:
-        return KVCache(self.spec, slots, max_len, self.device, self.dtype)
+        return KVCache(self.lspec, slots, max_len, self.device, self.dtype)
 
     # ---------------------------------------------------------------- forward
     def forward(self, ids: torch.Tensor, pos: torch.Tensor, cache: KVCache, slot: torch.Tensor,
@@ -127,6 +137,7 @@ class Gemma2Model:
         ``stop_at=l`` stops after block ``l`` and returns the residual ``h``.
         """
         s = self.spec
+        ls = self.lspec
         B, T = ids.shape
         M = B * T
         ws = ws or self.workspace(M)
@@ -139,14 +150,18 @@ class Gemma2Model:
             L = w.layers[l]
             ops.linear(x, L.wqkv, out=ws.qkv)
             ops.rope_qkv_cache(ws.qkv, pos32, ws.slot_rows, self.cos_t, self.sin_t, cache.k[l], cache.v[l],
-                               s.heads, s.kv_heads, s.head_dim, q_out=ws.q)
+                               ls.heads, ls.kv_heads, ls.head_dim, q_out=ws.q)
             ops.attention(ws.q, cache.k[l], cache.v[l], pos32, slot, B, T, self.scale, s.attn_softcap,
                           s.sliding_window if s.is_sliding(l) else 0, out=ws.attn)
             ops.linear(ws.attn, L.wo, out=ws.o)
+            if self.tp is not None:
+                self.tp.all_reduce_(ws.o)
             ops.add_rmsnorm2(h, ws.o, L.ln_post_attn, L.ln_pre_ffn, s.eps, out=x)
             ops.linear(x, L.wgu, out=ws.gu)
             ops.geglu(ws.gu, out=ws.act)
             ops.linear(ws.act, L.wdown, out=ws.o)
+            if self.tp is not None:
+                self.tp.all_reduce_(ws.o)
             ops.add_rmsnorm2(h, ws.o, L.ln_post_ffn, self.norm_next[l], s.eps, out=x)
             if hooks and l in hooks:
                 ctx = HookCtx(l, B, T, pos32, slot, self.norm_next[l], s.eps, self)

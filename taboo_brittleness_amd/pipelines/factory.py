@@ -37,7 +37,7 @@ def resolve_device(spec: str = "auto") -> torch.device:
     return torch.device(spec)
 
 
-def build_model(cfg: Config, device, word: Optional[str] = None):
+def build_model(cfg: Config, device, word: Optional[str] = None, tp=None):
     spec = get_spec(cfg.model.arch)
     device = torch.device(device)
     if spec.family == "gpt2":
@@ -49,12 +49,16 @@ def build_model(cfg: Config, device, word: Optional[str] = None):
     else:
         adapter = cfg.model.adapter_template.format(word=word) if (cfg.model.adapter_template and word) else None
         w = load_gemma2_hf(spec, cfg.model.weights, adapter=adapter, device=device, dtype=dtype)
-    return Gemma2Model(w, device)
+    if tp is not None and tp.size > 1:
+        from ..parallel.tp import shard_weights
+
+        w = shard_weights(w, tp)
+    return Gemma2Model(w, device, tp=tp)
 
 
-def build_stack(cfg: Config, device, word: Optional[str] = None, with_sae: bool = True) -> Stack:
+def build_stack(cfg: Config, device, word: Optional[str] = None, with_sae: bool = True, tp=None) -> Stack:
     device = torch.device(device)
-    model = build_model(cfg, device, word)
+    model = build_model(cfg, device, word, tp)
     spec = model.spec
     tok = load_tokenizer(cfg.model.tokenizer, cfg.model.arch, spec.vocab_size)
     layer = min(cfg.model.layer_idx, spec.layers - 1)

@@ -30,12 +30,18 @@ from .sweep import METHODS, SweepRunner, summarize_cells
 def run_sweep(cfg: Config, out_dir: str, methods: Sequence[str] = METHODS, info: Optional[D.DistInfo] = None,
               batch: Optional[int] = None, log=print) -> Dict:
     info = info or D.init_distributed(cfg.parallel.backend, cfg.runtime.device)
-    stack = build_stack(cfg, info.device)
+    tp_ctx, dp_rank, dp_size = None, info.rank, info.world
+    if cfg.parallel.tp > 1:
+        from ..parallel.tp import make_groups
+
+        tp_ctx, dp_rank, dp_size = make_groups(info.world, info.rank, cfg.parallel.tp)
+    stack = build_stack(cfg, info.device, tp=tp_ctx)
     model, tok, sae = stack.model, stack.tok, stack.sae
     B = batch or cfg.runtime.batch_size
     n_pairs = len(cfg.words) * len(cfg.prompts)
+    graphs = cfg.runtime.use_graphs and (tp_ctx is None or os.environ.get("TB_TP_GRAPHS", "0") == "1")
     runner = SweepRunner(cfg, model, tok, sae, batch=B, device=info.device, layer=stack.layer,
-                         use_graphs=cfg.runtime.use_graphs, kv_pairs=n_pairs + 1)
+                         use_graphs=graphs, kv_pairs=n_pairs + 1)
     pairs = runner.build_pairs(cfg.words, cfg.prompts)
     t0 = time.perf_counter()
     runner.run_baselines(pairs)
@@ -45,8 +51,9 @@ def run_sweep(cfg: Config, out_dir: str, methods: Sequence[str] = METHODS, info:
         runner._score_pairs(pairs)
     t_base = time.perf_counter() - t0
     cells = runner.make_cells(pairs, methods)
-    mine = D.shard(list(range(len(cells))), info.rank, info.world)
-    shard_path = os.path.join(out_dir, f"shard_{info.rank:03d}_of_{info.world:03d}.json")
+    mine = D.shard(list(range(len(cells))), dp_rank, dp_size)     # every TP rank of a group runs the same cells
+    shard_path = os.path.join(out_dir, f"shard_{dp_rank:03d}_of_{dp_size:03d}.json")
+    writer = tp_ctx is None or tp_ctx.rank == 0
     t1 = time.perf_counter()
     if os.path.exists(shard_path):
         res = json.load(open(shard_path))["results"]
@@ -55,10 +62,11 @@ def run_sweep(cfg: Config, out_dir: str, methods: Sequence[str] = METHODS, info:
         res = runner.run_cells(pairs, [cells[i] for i in mine])
         for r, i in zip(res, mine):
             r["cell_id"] = i
-        os.makedirs(out_dir, exist_ok=True)
-        atomic_write_json(shard_path, {"results": res})
+        if writer:
+            os.makedirs(out_dir, exist_ok=True)
+            atomic_write_json(shard_path, {"results": res})
     t_cells = time.perf_counter() - t1
-    gathered = D.all_gather_objects(res, info)
+    gathered = D.all_gather_objects(res if writer else [], info)
     summary: Dict = {}
     if info.is_main:
         allres = sorted([r for part in gathered for r in part], key=lambda r: r["cell_id"])
@@ -69,7 +77,8 @@ def run_sweep(cfg: Config, out_dir: str, methods: Sequence[str] = METHODS, info:
             "top_ids": p.top_ids, "guesses": [tok.decode([t]).strip() for t in p.top_ids],
             "targeted_latents": p.targeted[:8], "nll": p.nll} for p in pairs]
         summary["timing"] = {"baseline_s": t_base, "cells_s": t_cells, "n_cells": len(allres),
-                             "world": info.world, "cells_per_s": len(allres) / max(t_cells, 1e-9)}
+                             "world": info.world, "dp": dp_size, "tp": cfg.parallel.tp,
+                             "cells_per_s": len(allres) / max(t_cells, 1e-9)}
         summary["config"] = {"layer": stack.layer, "arch": cfg.model.arch, "methods": list(methods),
                              "budgets": cfg.intervention.budgets, "ranks": cfg.intervention.ranks}
         os.makedirs(out_dir, exist_ok=True)
