@@ -1,0 +1,88 @@
+"""Whole-engine checks on the MI355X: the HIP forward against the CPU reference path, hipGraph
+decode against eager decode, the sweep (prefix sharing on/off) and the SAE encode."""
+from dataclasses import replace
+
+import pytest
+import torch
+
+from taboo_brittleness_amd.models.gemma2 import Gemma2Model
+from taboo_brittleness_amd.models.spec import GEMMA2_TINY
+from taboo_brittleness_amd.models.weights import random_gemma2
+from taboo_brittleness_amd.runtime.generation import Generator
+
+pytestmark = pytest.mark.gpu
+SPEC = replace(GEMMA2_TINY, vocab_size=2048, layers=4, sliding_window=8)
+
+
+def _models(gpu):
+    w = random_gemma2(SPEC, dtype=torch.bfloat16, seed=5, norm_std=0.1)
+    return Gemma2Model(w, "cpu"), Gemma2Model(w.to(device=gpu), gpu)
+
+
+def test_forward_hip_matches_cpu_reference(gpu):
+    mc, mg = _models(gpu)
+    ids = torch.randint(0, SPEC.vocab_size, (3, 13), generator=torch.Generator().manual_seed(1)).int()
+    pos = torch.arange(13, dtype=torch.int32).expand(3, 13).contiguous()
+    pos[2, 10:] = -1
+    caps = {}
+    hk = {2: [lambda h, x, c: caps.__setitem__(c.model.device.type, h.clone())]}
+    xc = mc.forward(ids, pos, mc.new_cache(3, 16), torch.arange(3, dtype=torch.int32), hk)
+    xg = mg.forward(ids.to(gpu), pos.to(gpu), mg.new_cache(3, 16), torch.arange(3, dtype=torch.int32, device=gpu), hk)
+    valid = (pos.view(-1) >= 0)
+    lc = mc.logits(xc).float()[valid]
+    lg = mg.logits(xg).float().cpu()[valid]
+    assert (lc - lg).abs().max() < 0.05 * lc.abs().max() + 0.05
+    assert (caps["cpu"].float()[valid] - caps["cuda"].float().cpu()[valid]).abs().max() < 0.1
+
+
+def test_graph_decode_equals_eager(gpu):
+    _, mg = _models(gpu)
+    prompts = [[2, 5, 9, 11, 13], [2, 7, 8], [2, 3, 4, 5, 6, 7, 8]]
+    eager = Generator(mg, 4, 32, use_graphs=False, stop_ids=(100_000,)).generate(prompts, 10)
+    g = Generator(mg, 4, 32, use_graphs=True, stop_ids=(100_000,))
+    a = g.generate(prompts, 10, graph_key="k")
+    b = g.generate(prompts, 10, graph_key="k")          # replay path
+    for i in range(3):
+        assert eager.response_ids(i) == a.response_ids(i) == b.response_ids(i)
+
+
+def test_sweep_gpu_prefix_share_equivalence(gpu):
+    from taboo_brittleness_amd.config import load_config
+    from taboo_brittleness_amd.interp.sae import JumpReLUSAE
+    from taboo_brittleness_amd.models.tokenizer import SyntheticTokenizer
+    from taboo_brittleness_amd.pipelines.sweep import SweepRunner
+
+    cfg = load_config(None, ["experiment.max_new_tokens=8", "intervention.budgets=[1, 4]",
+                             "intervention.random_trials=2", "intervention.ranks=[1, 2]",
+                             "intervention.proj_random_trials=1"])
+    _, mg = _models(gpu)
+    tok = SyntheticTokenizer(vocab_size=SPEC.vocab_size)
+    out = {}
+    for share in (False, True):
+        sae = JumpReLUSAE.random(SPEC.hidden, 1024, seed=2, device=gpu)
+        r = SweepRunner(cfg, mg, tok, sae, batch=24, device=gpu, layer=2, prefix_share=share)
+        pairs = r.build_pairs(["ship"], cfg.prompts[:2])
+        r.run_baselines(pairs)
+        res = r.run_cells(pairs, r.make_cells(pairs))
+        out[share] = res
+    same = sum(a["response_ids"] == b["response_ids"] for a, b in zip(out[False], out[True]))
+    assert same >= int(0.9 * len(out[False]))
+    for a, b in zip(out[False], out[True]):
+        if a["response_ids"] == b["response_ids"]:
+            assert abs(a["nll_edit"] - b["nll_edit"]) < 0.05
+
+
+def test_sae_encode_matches_fp32(gpu):
+    from taboo_brittleness_amd.interp.sae import JumpReLUSAE
+
+    sae_c = JumpReLUSAE.random(512, 2048, seed=3, device="cpu")
+    sae_g = JumpReLUSAE.random(512, 2048, seed=3, device=gpu)
+    x = torch.randn(40, 512)
+    sae_c.calibrate(x, target_l0=30)
+    sae_g.threshold = sae_c.threshold.to(gpu)
+    ac = sae_c.encode(x)
+    ag = sae_g.encode(x.to(gpu)).cpu()
+    pre = sae_c.pre_acts(x)
+    near = (pre - sae_c.threshold).abs() < 2e-2
+    assert ((ac - ag).abs()[~near] < 2e-2).all()
+    assert abs(sae_g.l0(x.to(gpu)) - sae_c.l0(x)) < 1.0
