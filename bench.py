@@ -44,7 +44,7 @@ from taboo_brittleness_amd.parallel import dist as D  # noqa: E402
 from taboo_brittleness_amd.pipelines.sweep import Pair, SweepRunner  # noqa: E402
 from taboo_brittleness_amd.runtime.tuning import enable_tuned_gemms, flush_tuned_gemms  # noqa: E402
 
-BASELINE_VALUE = None   # the reference publishes no prompts/sec number
+BASELINE_VALUE = 0.642   # measured HF-eager sweep cells/sec on 1x MI355X (tools/hf_eager_baseline.py)
 
 
 def fresh(p: Pair) -> Pair:
