@@ -20,6 +20,9 @@ int tb_attention_lds_bytes(int HD);
 void tb_attention(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, uint16_t* out, const int32_t* pos,
                   const int32_t* slot, int B, int T, int Hq, int Hkv, int HD, int S, float scale, float softcap,
                   int window, hipStream_t st);
+void tb_attention_varlen(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, uint16_t* out, const int32_t* pos,
+                         const int32_t* blk, int nblk, int Hq, int Hkv, int HD, int S, float scale, float softcap,
+                         int window, hipStream_t st);
 // elementwise.hip
 void tb_geglu(const uint16_t* gu, uint16_t* out, int M, int F, hipStream_t st);
 // lens.hip
@@ -32,6 +35,8 @@ void tb_lens_colsum(const uint16_t* logits, const float* lse, const uint8_t* mas
 void tb_topk_rows(const float* x, float* vals, int32_t* idx, int R, int V, int K, hipStream_t st);
 void tb_xent_rows(const uint16_t* logits, const int32_t* tgt, float* nll, int R, int V, float cap, int emulate_bf16,
                   hipStream_t st);
+void tb_decode_head(const uint16_t* logits, const int32_t* tgt, int32_t* nxt, float* nll_self, float* nll_tgt, int R,
+                    int V, float cap, hipStream_t st);
 // sae.hip
 void tb_gemm_nt(const uint16_t* A, const uint16_t* W, void* C, const float* bias, const float* thr, int M, int N,
                 int K, int ldc, int epi, hipStream_t st);

@@ -43,7 +43,7 @@ template <int HD, int G>
 __global__ void __launch_bounds__(256) attn_cache_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
     uint16_t* __restrict__ out, const int32_t* __restrict__ pos, const int32_t* __restrict__ slot, int T, int Hq,
-    int Hkv, int S, float scale, float softcap, int window) {
+    int Hkv, int S, float scale, float softcap, int window, const int32_t* __restrict__ blk) {
   constexpr int P = 16 / G;        // query positions per workgroup
   constexpr int KS = HD / 32;      // MFMA k-steps over head_dim
   constexpr int DT = HD / 16;      // 16-wide output dim tiles
@@ -55,17 +55,29 @@ __global__ void __launch_bounds__(256) attn_cache_kernel(
   uint16_t* plds_all = vlds_all + 4 * 32 * VSTR;                             // [4][16][PSTR]
   float* mrg = reinterpret_cast<float*>(plds_all + 4 * 16 * PSTR);           // [4][16] m, [4][16] l
 
-  const int b = blockIdx.z, kh = blockIdx.y, t0 = blockIdx.x * P;
+  // Row geometry: dense [B, T] layout (blk == nullptr) or a ragged block table blk[i] =
+  // {first row, rows (<= P), cache slot} over packed rows (varlen prefill / teacher forcing).
+  const int kh = blockIdx.y;
+  int rbase, nvalid, cs;
+  if (blk != nullptr) {
+    rbase = blk[3 * blockIdx.x];
+    nvalid = blk[3 * blockIdx.x + 1];
+    cs = blk[3 * blockIdx.x + 2];
+  } else {
+    const int b = blockIdx.z, t0 = blockIdx.x * P;
+    rbase = b * T + t0;
+    nvalid = min(P, T - t0);
+    cs = slot[b];
+  }
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int grp = lane >> 4, col = lane & 15;
-  const int cs = slot[b];
   const uint16_t* kbase = kc + ((size_t)cs * Hkv + kh) * (size_t)S * HD;
   const uint16_t* vbase = vc + ((size_t)cs * Hkv + kh) * (size_t)S * HD;
 
   // --- query rows: A-layout row = col; C-layout rows = 4*grp + i
   auto row_pos = [&](int r) -> int {
-    const int t = t0 + r / G;
-    return (t < T) ? pos[(size_t)b * T + t] : -1;
+    const int t = r / G;
+    return (t < nvalid) ? pos[(size_t)rbase + t] : -1;
   };
   const int posA = row_pos(col);
   int posC[4];
@@ -87,8 +99,8 @@ __global__ void __launch_bounds__(256) attn_cache_kernel(
   // --- Q fragments (A operand), zero for invalid rows
   bf16x8 qa[KS];
   {
-    const int t = t0 + col / G, h = kh * G + (col % G);
-    const uint16_t* qrow = q + (((size_t)b * T + t) * Hq + h) * HD;
+    const int t = col / G, h = kh * G + (col % G);
+    const uint16_t* qrow = q + (((size_t)rbase + t) * Hq + h) * HD;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       uint4 u = {0, 0, 0, 0};
@@ -223,8 +235,8 @@ __global__ void __launch_bounds__(256) attn_cache_kernel(
   // 16 rows x HD outputs, 8 contiguous dims per thread-step
   for (int e = threadIdx.x; e < 16 * (HD / 8); e += blockDim.x) {
     const int r = e / (HD / 8), c8 = (e % (HD / 8)) * 8;
-    const int t = t0 + r / G, h = kh * G + (r % G);
-    if (t >= T) continue;
+    const int t = r / G, h = kh * G + (r % G);
+    if (t >= nvalid) continue;
     float M = -INFINITY;
 #pragma unroll
     for (int w = 0; w < 4; ++w) M = fmaxf(M, mrg[w * 16 + r]);
@@ -244,14 +256,14 @@ __global__ void __launch_bounds__(256) attn_cache_kernel(
       for (int w = 0; w < 4; ++w) acc += wsc[w] * ofin[(w * 16 + r) * HD + c8 + j];
       o8[j] = acc * inv;
     }
-    *reinterpret_cast<uint4*>(out + (((size_t)b * T + t) * Hq + h) * HD + c8) = pack8(o8);
+    *reinterpret_cast<uint4*>(out + (((size_t)rbase + t) * Hq + h) * HD + c8) = pack8(o8);
   }
 }
 
 template <int HD, int G>
 void launch_attn(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, uint16_t* out, const int32_t* pos,
                  const int32_t* slot, int B, int T, int Hq, int Hkv, int S, float scale, float softcap, int window,
-                 hipStream_t st) {
+                 hipStream_t st, const int32_t* blk = nullptr, int nblk = 0) {
   constexpr int P = 16 / G;
   const size_t lds = (size_t)tb_attention_lds_bytes(HD);
   static bool attr_set = false;   // > 64 KB dynamic LDS needs the opt-in (first call is never captured)
@@ -260,9 +272,15 @@ void launch_attn(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, uint
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
+  if (blk != nullptr) {
+    dim3 grid(nblk, Hkv, 1);
+    hipLaunchKernelGGL((attn_cache_kernel<HD, G>), grid, dim3(256), lds, st, q, kc, vc, out, pos, slot, T, Hq, Hkv,
+                       S, scale, softcap, window, blk);
+    return;
+  }
   dim3 grid((T + P - 1) / P, Hkv, B);
   hipLaunchKernelGGL((attn_cache_kernel<HD, G>), grid, dim3(256), lds, st, q, kc, vc, out, pos, slot, T, Hq, Hkv, S,
-                     scale, softcap, window);
+                     scale, softcap, window, (const int32_t*)nullptr);
 }
 
 
@@ -456,4 +474,23 @@ void tb_attention(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, uin
   TB_ATTN_CASE(128, 1)
   TB_ATTN_CASE(128, 4)
 #undef TB_ATTN_CASE
+}
+
+void tb_attention_varlen(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, uint16_t* out, const int32_t* pos,
+                         const int32_t* blk, int nblk, int Hq, int Hkv, int HD, int S, float scale, float softcap,
+                         int window, hipStream_t st) {
+  if (nblk <= 0) return;
+  const int G = Hq / Hkv;
+#define TB_VL_CASE(hd, g)                                                                                    \
+  if (HD == hd && G == g) {                                                                                  \
+    launch_attn<hd, g>(q, kc, vc, out, pos, nullptr, 0, 0, Hq, Hkv, S, scale, softcap, window, st, blk, nblk); \
+    return;                                                                                                  \
+  }
+  TB_VL_CASE(256, 2)
+  TB_VL_CASE(256, 1)
+  TB_VL_CASE(256, 4)
+  TB_VL_CASE(128, 2)
+  TB_VL_CASE(128, 1)
+  TB_VL_CASE(128, 4)
+#undef TB_VL_CASE
 }

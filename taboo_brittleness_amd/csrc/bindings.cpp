@@ -95,6 +95,23 @@ void attention(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch::Tenso
                HD, S, (float)scale, (float)softcap, (int)window, cur_stream());
 }
 
+void attention_varlen(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch::Tensor out, torch::Tensor pos,
+                      torch::Tensor blk, double scale, double softcap, int64_t window) {
+  IN_BF16(q); IN_BF16(kc); IN_BF16(vc); IN_BF16(out); IN_I32(pos); IN_I32(blk);
+  TORCH_CHECK(kc.dim() == 4, "cache must be [slots, Hkv, S, HD]");
+  const int Hkv = kc.size(1), S = kc.size(2), HD = kc.size(3);
+  const int M = pos.numel();
+  TORCH_CHECK(q.numel() % ((int64_t)M * HD) == 0 && out.numel() == q.numel(), "q/out shape");
+  const int Hq = q.numel() / ((int64_t)M * HD);
+  TORCH_CHECK(Hq % Hkv == 0 && (HD == 256 || HD == 128), "unsupported head geometry");
+  const int G = Hq / Hkv;
+  TORCH_CHECK(G == 1 || G == 2 || G == 4, "unsupported GQA ratio");
+  TORCH_CHECK(blk.dim() == 2 && blk.size(1) == 3, "blk must be [nblk, 3] = (row0, nrows, slot)");
+  c10::DeviceGuard g(q.device());
+  tb_attention_varlen(cbf(q), cbf(kc), cbf(vc), bf(out), pos.data_ptr<int32_t>(), blk.data_ptr<int32_t>(),
+                      blk.size(0), Hq, Hkv, HD, S, (float)scale, (float)softcap, (int)window, cur_stream());
+}
+
 void geglu(torch::Tensor gu, torch::Tensor out) {
   IN_BF16(gu); IN_BF16(out);
   const int F2 = gu.size(-1), M = gu.numel() / F2;
@@ -157,6 +174,25 @@ void xent_rows(torch::Tensor logits, torch::Tensor tgt, torch::Tensor nll, doubl
   c10::DeviceGuard g(logits.device());
   tb_xent_rows(cbf(logits), tgt.data_ptr<int32_t>(), nll.data_ptr<float>(), R, V, (float)cap, emulate_bf16 ? 1 : 0,
                cur_stream());
+}
+
+void decode_head(torch::Tensor logits, c10::optional<torch::Tensor> tgt, torch::Tensor nxt, torch::Tensor nll_self,
+                 c10::optional<torch::Tensor> nll_tgt, double cap) {
+  IN_BF16(logits); IN_I32(nxt); IN_F32(nll_self);
+  const int V = logits.size(-1), R = logits.numel() / V;
+  TORCH_CHECK(nxt.numel() == R && nll_self.numel() == R, "decode_head shapes");
+  TORCH_CHECK(tgt.has_value() == nll_tgt.has_value(), "decode_head: tgt and nll_tgt go together");
+  const int32_t* tp = nullptr;
+  float* np = nullptr;
+  if (tgt.has_value()) {
+    IN_I32((*tgt)); IN_F32((*nll_tgt));
+    TORCH_CHECK(tgt->numel() == R && nll_tgt->numel() == R, "decode_head teacher shapes");
+    tp = tgt->data_ptr<int32_t>();
+    np = nll_tgt->data_ptr<float>();
+  }
+  c10::DeviceGuard g(logits.device());
+  tb_decode_head(cbf(logits), tp, nxt.data_ptr<int32_t>(), nll_self.data_ptr<float>(), np, R, V, (float)cap,
+                 cur_stream());
 }
 
 void gemm_nt(torch::Tensor A, torch::Tensor W, torch::Tensor C, c10::optional<torch::Tensor> bias,
@@ -243,6 +279,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("embed_rmsnorm", &embed_rmsnorm);
   m.def("rope_qkv_cache", &rope_qkv_cache);
   m.def("attention", &attention);
+  m.def("attention_varlen", &attention_varlen);
   m.def("geglu", &geglu);
   m.def("argmax_rows", &argmax_rows);
   m.def("row_lse", &row_lse);
@@ -250,6 +287,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lens_colsum", &lens_colsum);
   m.def("topk_rows", &topk_rows);
   m.def("xent_rows", &xent_rows);
+  m.def("decode_head", &decode_head);
   m.def("gemm_nt", &gemm_nt);
   m.def("lowrank_edit", &lowrank_edit);
   m.def("sae_decode_sparse", &sae_decode_sparse);

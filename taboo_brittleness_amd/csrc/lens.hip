@@ -12,6 +12,8 @@
 //                 reference's per-position id exclusions (2 ids per row)
 //  topk_rows      per-row top-k (k <= 64), ties -> lower index
 //  xent_rows      NLL of target ids under softcapped logits (fluency ΔNLL)
+//  decode_head    one pass over a decode row: greedy token (argmax_rows semantics), its NLL and
+//                 the NLL of an optional teacher target (the baseline's token at that column)
 #include "common.h"
 #include "api.h"
 
@@ -281,7 +283,73 @@ __global__ void __launch_bounds__(512) xent_rows_kernel(const uint16_t* __restri
   }
 }
 
+__global__ void __launch_bounds__(512) decode_head_kernel(const uint16_t* __restrict__ logits,
+                                                          const int32_t* __restrict__ tgt, int32_t* __restrict__ nxt,
+                                                          float* __restrict__ nll_self, float* __restrict__ nll_tgt,
+                                                          int V, float cap) {
+  __shared__ float sm[8], ss[8], sv[8];
+  __shared__ int si[8];
+  const int r = blockIdx.x;
+  const uint16_t* row = logits + (size_t)r * V;
+  float m = -INFINITY, s = 0.f;
+  ArgBest best{-INFINITY, 0x7fffffff};
+  const int nv = V >> 3;
+  for (int c = threadIdx.x; c < nv; c += blockDim.x) {
+    float f[8];
+    unpack8(reinterpret_cast<const uint4*>(row)[c], f);
+    float lm = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (cap > 0.f) f[j] = softcap_bf16(f[j], cap);
+      lm = fmaxf(lm, f[j]);
+      best = better(best, ArgBest{f[j], c * 8 + j});
+    }
+    float ls = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ls += __expf(f[j] - lm);
+    online_merge(m, s, lm, ls);
+  }
+  for (int c = nv * 8 + threadIdx.x; c < V; c += blockDim.x) {
+    const float x = cap > 0.f ? softcap_bf16(bf2f(row[c]), cap) : bf2f(row[c]);
+    best = better(best, ArgBest{x, c});
+    if (m == -INFINITY) { m = x; s = 1.f; } else online_add(m, s, x);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(s, o, 64);
+    online_merge(m, s, m2, s2);
+    ArgBest oth{__shfl_xor(best.v, o, 64), __shfl_xor(best.i, o, 64)};
+    best = better(best, oth);
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) { sm[wid] = m; ss[wid] = s; sv[wid] = best.v; si[wid] = best.i; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float M = sm[0], Ssum = ss[0];
+    ArgBest b{sv[0], si[0]};
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
+      online_merge(M, Ssum, sm[w], ss[w]);
+      b = better(b, ArgBest{sv[w], si[w]});
+    }
+    const float lse = M + __logf(Ssum);
+    nxt[r] = b.i;
+    nll_self[r] = lse - b.v;
+    if (nll_tgt != nullptr) {
+      const int t = tgt[r];
+      float zt = 0.f;
+      if (t >= 0 && t < V) zt = cap > 0.f ? softcap_bf16(bf2f(row[t]), cap) : bf2f(row[t]);
+      nll_tgt[r] = (t >= 0 && t < V) ? lse - zt : 0.f;
+    }
+  }
+}
+
 }  // namespace
+
+void tb_decode_head(const uint16_t* logits, const int32_t* tgt, int32_t* nxt, float* nll_self, float* nll_tgt, int R,
+                    int V, float cap, hipStream_t st) {
+  if (R <= 0) return;
+  hipLaunchKernelGGL(decode_head_kernel, dim3(R), dim3(512), 0, st, logits, tgt, nxt, nll_self, nll_tgt, V, cap);
+}
 
 void tb_argmax_rows(const uint16_t* logits, int32_t* out, int R, int V, float cap, hipStream_t st) {
   if (R <= 0) return;

@@ -27,7 +27,7 @@ from __future__ import annotations
 
 import math
 from dataclasses import dataclass, field
-from typing import Callable, Dict, List, Optional, Sequence
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import torch
 
@@ -69,6 +69,17 @@ class KVCache:
         self.v[:, dst, :, :n].copy_(self.v[:, src, :, :n])
 
 
+def packed_blocks(seqs: Sequence[Tuple[int, int, int]], rows_per_block: int) -> torch.Tensor:
+    """Attention block table for packed rows: ``seqs`` = (first row, n rows, cache slot) per sequence;
+    each sequence is cut into blocks of at most ``rows_per_block`` rows (16 / GQA ratio for the
+    MFMA kernel).  Returns int32 ``[nblk, 3]`` (CPU)."""
+    out = []
+    for r0, n, sl in seqs:
+        for i in range(0, n, rows_per_block):
+            out.append((r0 + i, min(rows_per_block, n - i), sl))
+    return torch.tensor(out or [(0, 0, 0)], dtype=torch.int32).view(-1, 3)
+
+
 class _Workspace:
     def __init__(self, spec: Gemma2Spec, M: int, device, dtype):
         d = spec.hidden
@@ -81,6 +92,16 @@ class _Workspace:
         self.gu = torch.empty(M, 2 * spec.ffn, device=device, dtype=dtype)
         self.act = torch.empty(M, spec.ffn, device=device, dtype=dtype)
         self.slot_rows = torch.empty(M, device=device, dtype=torch.int32)
+        self.M = M
+
+    def rows(self, M: int) -> "_Workspace":
+        """View of the first ``M`` rows (no allocation) — one buffer serves every ragged chunk size."""
+        assert M <= self.M, f"workspace has {self.M} rows, need {M}"
+        v = _Workspace.__new__(_Workspace)
+        for k, t in self.__dict__.items():
+            setattr(v, k, t[:M] if isinstance(t, torch.Tensor) else t)
+        v.M = M
+        return v
 
 
 class Gemma2Model:
@@ -136,14 +157,36 @@ class Gemma2Model:
         Returns the final-normed hidden state ``x [B*T, d]`` (input of lm_head).
         ``stop_at=l`` stops after block ``l`` and returns the residual ``h``.
         """
-        s = self.spec
-        ls = self.lspec
         B, T = ids.shape
         M = B * T
         ws = ws or self.workspace(M)
-        ids32 = ids.reshape(M)
-        pos32 = pos.reshape(M)
         ws.slot_rows.view(B, T).copy_(slot.view(B, 1).expand(B, T))
+
+        def attn(l, q, kc, vc, pos32, window, out):
+            ops.attention(q, kc, vc, pos32, slot, B, T, self.scale, self.spec.attn_softcap, window, out=out)
+
+        return self._run(ids.reshape(M), pos.reshape(M), cache, ws, attn, hooks, stop_at, B, T, slot)
+
+    def forward_packed(self, ids: torch.Tensor, pos: torch.Tensor, slot_rows: torch.Tensor, blk: torch.Tensor,
+                       cache: KVCache, hooks: Optional[Dict[int, Sequence[Hook]]] = None,
+                       stop_at: Optional[int] = None, ws: Optional[_Workspace] = None) -> torch.Tensor:
+        """Ragged forward over packed rows ``ids [M]`` (no padding between sequences): row ``i`` sits at
+        position ``pos[i]`` of cache slot ``slot_rows[i]``; ``blk`` is the attention block table
+        (:func:`packed_blocks`).  Hooks see every row as its own length-1 sequence (``ctx.B = M``,
+        ``ctx.T = 1``, ``ctx.slot = slot_rows``), so the edit/capture hooks work unchanged."""
+        M = ids.numel()
+        ws = ws or self.workspace(M)
+        ws.slot_rows.copy_(slot_rows.view(M))
+        sr = ws.slot_rows
+
+        def attn(l, q, kc, vc, pos32, window, out):
+            ops.attention_varlen(q, kc, vc, pos32, sr, blk, self.scale, self.spec.attn_softcap, window, out=out)
+
+        return self._run(ids.reshape(M), pos.reshape(M), cache, ws, attn, hooks, stop_at, M, 1, sr)
+
+    def _run(self, ids32, pos32, cache, ws, attn, hooks, stop_at, B, T, ctx_slot) -> torch.Tensor:
+        s = self.spec
+        ls = self.lspec
         w = self.w
         h, x = ops.embed_rmsnorm(ids32, w.embed, w.layers[0].ln_in, self.embed_scale, s.eps, ws.h, ws.x)
         for l in range(s.layers):
@@ -151,8 +194,7 @@ class Gemma2Model:
             ops.linear(x, L.wqkv, out=ws.qkv)
             ops.rope_qkv_cache(ws.qkv, pos32, ws.slot_rows, self.cos_t, self.sin_t, cache.k[l], cache.v[l],
                                ls.heads, ls.kv_heads, ls.head_dim, q_out=ws.q)
-            ops.attention(ws.q, cache.k[l], cache.v[l], pos32, slot, B, T, self.scale, s.attn_softcap,
-                          s.sliding_window if s.is_sliding(l) else 0, out=ws.attn)
+            attn(l, ws.q, cache.k[l], cache.v[l], pos32, s.sliding_window if s.is_sliding(l) else 0, ws.attn)
             ops.linear(ws.attn, L.wo, out=ws.o)
             if self.tp is not None:
                 self.tp.all_reduce_(ws.o)
@@ -164,7 +206,7 @@ class Gemma2Model:
                 self.tp.all_reduce_(ws.o)
             ops.add_rmsnorm2(h, ws.o, L.ln_post_ffn, self.norm_next[l], s.eps, out=x)
             if hooks and l in hooks:
-                ctx = HookCtx(l, B, T, pos32, slot, self.norm_next[l], s.eps, self)
+                ctx = HookCtx(l, B, T, pos32, ctx_slot, self.norm_next[l], s.eps, self)
                 for hk in hooks[l]:
                     hk(h, x, ctx)
             if stop_at is not None and l == stop_at:

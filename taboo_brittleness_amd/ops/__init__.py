@@ -98,6 +98,22 @@ def attention(q, kc, vc, pos, slot, B, T, scale, softcap, window, out=None):
     return o
 
 
+def attention_varlen(q, kc, vc, pos, slot_rows, blk, scale, softcap, window, out=None):
+    """Attention over packed rows ``q [M, Hq, HD]``: row ``i`` reads cache slot ``slot_rows[i]`` up to
+    ``pos[i]``.  ``blk [nblk, 3] = (first row, rows, slot)`` groups consecutive rows of one sequence
+    (<= 16 / GQA-ratio rows each) for the MFMA kernel; the CPU path only needs ``slot_rows``."""
+    M = pos.numel()
+    if q.is_cuda:
+        out = _out(out, (M, q.numel() // M), q.dtype, q.device)
+        _k().attention_varlen(q, kc, vc, out, pos, blk, float(scale), float(softcap), int(window))
+        return out
+    o = ref.attention(q, kc, vc, pos, slot_rows, M, 1, scale, softcap, window)
+    if out is not None:
+        out.copy_(o.view_as(out))
+        return out
+    return o
+
+
 def geglu(gu, out=None):
     if gu.is_cuda:
         out = _out(out, gu.shape[:-1] + (gu.shape[-1] // 2,), gu.dtype, gu.device)
@@ -184,6 +200,25 @@ def xent_rows(logits, tgt, cap=0.0, emulate_bf16=True, out=None):
         out.copy_(y)
         return out
     return y
+
+
+def decode_head(logits, cap, tgt=None, nxt=None, nll_self=None, nll_tgt=None):
+    """One pass over decode logits: greedy token (bf16-softcap argmax), its NLL, and the NLL of an
+    optional teacher target per row (``tgt < 0`` -> 0).  Returns ``(nxt, nll_self, nll_tgt)``."""
+    R = logits.numel() // logits.shape[-1]
+    dev = logits.device
+    nxt = _out(nxt, (R,), torch.int32, dev)
+    nll_self = _out(nll_self, (R,), torch.float32, dev)
+    if tgt is not None:
+        nll_tgt = _out(nll_tgt, (R,), torch.float32, dev)
+    if logits.is_cuda:
+        _k().decode_head(logits, tgt, nxt, nll_self, nll_tgt if tgt is not None else None, float(cap))
+        return nxt, nll_self, nll_tgt
+    nxt.copy_(ref.argmax_rows(logits, cap).view(R))
+    nll_self.copy_(ref.xent_rows(logits, nxt, cap, True).view(R))
+    if tgt is not None:
+        nll_tgt.copy_(ref.xent_rows(logits, tgt, cap, True).view(R))
+    return nxt, nll_self, nll_tgt
 
 
 def gemm_nt(A, W, epi=0, bias=None, thr=None, out=None):

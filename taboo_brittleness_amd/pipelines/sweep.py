@@ -384,13 +384,14 @@ class SweepRunner:
         if share:
             self._copy_pair_kv(range(nc), [p.kv_slot for p in cell_pairs])
             self._copy_pair_resid(range(nc), cell_pairs)
-            starts, prefix, toks, steps = [], [], [], 1
+            starts, prefix, toks, steps, c0s = [], [], [], 1, []
             pnll = torch.zeros(n, max(len(p.gen_toks) for p in cell_pairs) if cell_pairs else 1)
             for b, p in enumerate(cell_pairs):
                 i = min(p.first_edit, len(p.gen_toks) - 1)
                 starts.append(p.plen + i)
                 prefix.append(p.gen_toks[: i + 1])
                 toks.append(p.gen_toks[i])
+                c0s.append(i + 1)
                 pnll[b, : i + 1] = torch.from_numpy(p.tok_nll[: i + 1])
                 steps = max(steps, self.max_new - i)
             if rb:
@@ -404,10 +405,12 @@ class SweepRunner:
                 pnll[nc:, :1] = gen.out_nll[nc:n, :1].cpu()
             self._tick("prefix_copy+prefill")
             gen.decode(torch.tensor(toks, dtype=torch.int32), starts, prefix, steps, n, hooks, "sweep",
-                       prefix_nll=pnll.to(self.dev))
+                       prefix_nll=pnll.to(self.dev), teacher=[p.resp for p in cell_pairs])
             out = gen.collect(n, self.max_new, [p.plen for p in rows_pairs])
         else:
-            out = gen.generate([p.ids for p in rows_pairs], self.max_new, hooks=hooks, graph_key="sweep")
+            c0s = [0] * nc
+            out = gen.generate([p.ids for p in rows_pairs], self.max_new, hooks=hooks, graph_key="sweep",
+                               teacher=[p.resp for p in cell_pairs])
         self._tick("decode")
         resp = [out.response_ids(i) for i in range(n)]
         lr = self._readout(rows_pairs, out.n_gen, resp, [p.track for p in rows_pairs])
@@ -417,7 +420,7 @@ class SweepRunner:
             self._score_pairs(list(rb))
         self._tick("baseline_finalize")
         if measure_nll and nc:
-            nll = self._nll_cells(cell_pairs, hook, share)
+            nll = self._nll_cells(cell_pairs, hook, out, c0s)
         else:
             nll = [float("nan")] * nc
         self._tick("nll")
@@ -446,52 +449,88 @@ class SweepRunner:
         self._tick("results")
         return results
 
+    def _nll_ws(self, M: int):
+        """Workspace for the ragged NLL pass, grown in 4096-row steps and sliced per chunk."""
+        ws = getattr(self, "_nll_wsp", None)
+        if ws is None or ws.M < M:
+            from ..models.gemma2 import _Workspace
+
+            self._nll_wsp = None
+            ws = self._nll_wsp = _Workspace(self.m.lspec, -(-M // 4096) * 4096, self.dev, self.m.dtype)
+        return ws
+
     @torch.no_grad()
-    def _nll_cells(self, cell_pairs: Sequence[Pair], plan_hook: EditHook, share: bool) -> List[float]:
+    def _nll_cells(self, cell_pairs: Sequence[Pair], plan_hook: EditHook, out, c0s: Sequence[int]) -> List[float]:
         """Mean NLL of each cell's *baseline* hint under the edit (teacher forced, EP:136).
 
-        With prefix sharing only positions >= the first edited position run (their KV prefix is the
-        pair's); earlier targets contribute the baseline's per-token NLLs."""
-        m, gen = self.m, self.gen
-        B = self.B
+        The edited decode already scored the baseline's token at every column (``out.tf_nll``); those
+        are the teacher-forced NLLs up to the column ``d`` where the cell's own greedy tokens leave the
+        baseline's (:func:`teacher_divergence`).  Targets before the decode's first column ``c0`` are
+        the baseline's own NLLs (identical prefix), and only targets after ``d`` need a teacher-forced
+        pass: a ragged (packed, unpadded) forward over positions ``plen+d .. plen+n-2`` in the cell's
+        own KV slot, whose prefix ``< plen+d`` holds exactly the baseline tokens."""
+        from ..models.gemma2 import packed_blocks
+        from ..runtime.generation import teacher_divergence
+
+        m = self.m
         nc = len(cell_pairs)
-        starts = [p.plen + min(p.first_edit, max(len(p.resp) - 1, 0)) if share else 0 for p in cell_pairs]
-        ends = [p.plen + len(p.resp) - 1 for p in cell_pairs]        # exclusive: last predicting position + 1
-        loss0 = [max(s0, p.plen - 1) for s0, p in zip(starts, cell_pairs)]
-        if share:
-            self._copy_pair_kv(range(nc), [p.kv_slot for p in cell_pairs])
-        T = max([max(e - s, 0) for s, e in zip(starts, ends)] + [1])
-        T = min(-(-T // 8) * 8, gen.S)        # few distinct GEMM shapes (tuned GEMM cache hits)
-        ids = torch.zeros(B, T, dtype=torch.int32)
-        pos = torch.full((B, T), -1, dtype=torch.int32)
-        rows, tgts, owner = [], [], []
-        pre = [0.0] * nc
-        for b, (p, s0, e, l0) in enumerate(zip(cell_pairs, starts, ends, loss0)):
-            full = p.ids + p.resp
-            L = max(e - s0, 0)
-            if L:
-                ids[b, :L] = torch.tensor(full[s0:e], dtype=torch.int32)
-                pos[b, :L] = torch.arange(s0, e, dtype=torch.int32)
-            for t in range(l0 - s0, L):
-                rows.append(b * T + t)
-                tgts.append(full[s0 + t + 1])
-                owner.append(b)
-            if share and p.resp:
-                k = s0 - (p.plen - 1)          # targets already covered by the baseline
-                pre[b] = float(np.sum(p.tok_nll[:k]))
-        x = m.forward(ids.to(self.dev), pos.to(self.dev), gen.cache, gen.slot, {self.layer: [plan_hook]})
+        tfn = out.tf_nll[:nc].float().cpu().numpy()
+        own = out.tokens[:nc].cpu().numpy()
         sums = [0.0] * nc
-        if rows:
-            ridx = torch.tensor(rows, device=self.dev)
-            tg = torch.tensor(tgts, dtype=torch.int32, device=self.dev)
-            nll = torch.empty(len(rows), device=self.dev)
+        ids, pos, tgt, owner, seqs = [], [], [], [], []
+        for b, p in enumerate(cell_pairs):
+            n = len(p.resp)
+            if not n:
+                continue
+            c0 = c0s[b]
+            tot = float(np.sum(p.tok_nll[: min(c0, n)]))
+            d = teacher_divergence(own[b].tolist(), p.resp, c0)
+            hi = min(d, n - 1)
+            if hi >= c0:
+                tot += float(np.sum(tfn[b, c0: hi + 1]))
+            sums[b] = tot
+            if d < n - 1:
+                L = n - 1 - d
+                seqs.append((len(ids), L, b))
+                ids += p.resp[d: n - 1]
+                pos += range(p.plen + d, p.plen + n - 1)
+                tgt += p.resp[d + 1: n]
+                owner += [b] * L
+        self.nll_rows = getattr(self, "nll_rows", 0) + len(ids)
+        if ids:
+            rpb = 16 // max(1, m.lspec.heads // m.lspec.kv_heads)
+            cap = 32768
+            dev = self.dev
+            nll = torch.empty(len(ids), device=dev)
+            ids_d = torch.tensor(ids, dtype=torch.int32, device=dev)
+            pos_d = torch.tensor(pos, dtype=torch.int32, device=dev)
+            slot_d = torch.tensor(owner, dtype=torch.int32, device=dev)
+            tgt_d = torch.tensor(tgt, dtype=torch.int32, device=dev)
             step = max(1, (1 << 30) // (m.spec.vocab_size * 2))
-            for r0 in range(0, len(rows), step):
-                lg = m.logits(x[ridx[r0:r0 + step]])
-                ops.xent_rows(lg, tg[r0:r0 + step], m.spec.final_softcap, True, out=nll[r0:r0 + step])
-            own = torch.tensor(owner, device=self.dev)
-            sums = torch.zeros(nc, device=self.dev).index_add_(0, own, nll).cpu().tolist()
-        return [(sums[b] + pre[b]) / len(p.resp) if p.resp else float("nan") for b, p in enumerate(cell_pairs)]
+            for r0 in range(0, len(ids), cap):
+                r1 = min(len(ids), r0 + cap)
+                M = r1 - r0
+                Mp = -(-M // 256) * 256                 # few distinct GEMM shapes
+                chunk = []
+                for (s0, L, b) in seqs:                  # sequences clipped to this chunk
+                    a0, a1 = max(s0, r0), min(s0 + L, r1)
+                    if a1 > a0:
+                        chunk.append((a0 - r0, a1 - a0, b))
+                blk = packed_blocks(chunk, rpb).to(dev)
+                ci = torch.zeros(Mp, dtype=torch.int32, device=dev)
+                cp = torch.full((Mp,), -1, dtype=torch.int32, device=dev)
+                cs = torch.zeros(Mp, dtype=torch.int32, device=dev)
+                ci[:M], cp[:M], cs[:M] = ids_d[r0:r1], pos_d[r0:r1], slot_d[r0:r1]
+                ws = self._nll_ws(min(cap, -(-len(ids) // 256) * 256)).rows(Mp)
+                x = m.forward_packed(ci, cp, cs, blk, self.gen.cache, {self.layer: [plan_hook]}, ws=ws)
+                for q0 in range(0, M, step):
+                    q1 = min(M, q0 + step)
+                    lg = m.logits(x[q0:q1])
+                    ops.xent_rows(lg, tgt_d[r0 + q0: r0 + q1], m.spec.final_softcap, True,
+                                  out=nll[r0 + q0: r0 + q1])
+            extra = torch.zeros(nc, device=dev).index_add_(0, slot_d.long(), nll).cpu().tolist()
+            sums = [a + e for a, e in zip(sums, extra)]
+        return [sums[b] / len(p.resp) if p.resp else float("nan") for b, p in enumerate(cell_pairs)]
 
 
 def summarize_cells(results: Sequence[dict], words: Sequence[str], word_plurals: Dict[str, List[str]]) -> dict:

@@ -27,6 +27,7 @@ from __future__ import annotations
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence
 
+import numpy as np
 import torch
 
 from .. import ops
@@ -40,6 +41,7 @@ class GenerationOutput:
     n_gen: List[int]                      # generated tokens before the stop token
     stopped: List[bool]
     tok_nll: Optional[torch.Tensor] = None   # [n, max_new] NLL of each generated token under the (edited) model
+    tf_nll: Optional[torch.Tensor] = None    # [n, max_new] NLL of the teacher's token at each column
 
     def response_ids(self, b: int) -> List[int]:
         return self.tokens[b, : self.n_gen[b]].tolist()
@@ -71,6 +73,12 @@ class Generator:
         self.nll_step = torch.empty(B, dtype=torch.float32, device=self.dev)
         self.out_tokens = torch.zeros(B, self.W, dtype=torch.int32, device=self.dev)
         self.out_nll = torch.zeros(B, self.W, dtype=torch.float32, device=self.dev)
+        # teacher forcing riding on the decode: tf_tgt[b, c] = token the teacher sequence has at output
+        # column c (-1 = none); out_tf_nll[b, c] = its NLL under the same logits that chose column c
+        self.tf_tgt = torch.full((B, self.W), -1, dtype=torch.int32, device=self.dev)
+        self.tf_step = torch.empty(B, dtype=torch.int32, device=self.dev)
+        self.tf_nll_step = torch.empty(B, dtype=torch.float32, device=self.dev)
+        self.out_tf_nll = torch.zeros(B, self.W, dtype=torch.float32, device=self.dev)
         self._graph = None
         self._graph_key = None
         self.ws = model.workspace(batch)       # pinned: a captured graph holds these pointers
@@ -79,19 +87,20 @@ class Generator:
     def _decode_step(self, hooks) -> None:
         x = self.m.forward(self.tok, self.pos, self.cache, self.slot, hooks, ws=self.ws)
         self.m.logits(x, out=self.logits)
-        ops.argmax_rows(self.logits, self.cap, out=self.nxt)
-        ops.xent_rows(self.logits, self.nxt, self.cap, True, out=self.nll_step)
-        nxt = torch.where(self.done, torch.full_like(self.nxt, self.pad_id), self.nxt)
         col = torch.clamp(self.step_idx, max=self.W - 1)
+        torch.gather(self.tf_tgt, 1, col, out=self.tf_step.view(-1, 1))
+        ops.decode_head(self.logits, self.cap, self.tf_step, self.nxt, self.nll_step, self.tf_nll_step)
+        nxt = torch.where(self.done, torch.full_like(self.nxt, self.pad_id), self.nxt)
         self.out_tokens.scatter_(1, col, nxt.view(-1, 1))
         self.out_nll.scatter_(1, col, self.nll_step.view(-1, 1))
+        self.out_tf_nll.scatter_(1, col, self.tf_nll_step.view(-1, 1))
         self.done |= (nxt.view(-1, 1) == self.stop_ids.view(1, -1)).any(-1)
         self.tok.copy_(nxt.view(-1, 1))
         self.pos.add_(1)
         self.step_idx.add_(1)
 
     def _state(self):
-        return (self.tok, self.pos, self.done, self.step_idx, self.out_tokens, self.out_nll)
+        return (self.tok, self.pos, self.done, self.step_idx, self.out_tokens, self.out_nll, self.out_tf_nll)
 
     def _capture(self, hooks, key) -> None:
         # warm up (hipBLASLt heuristics, kernel attributes) outside capture on a side stream
@@ -110,9 +119,11 @@ class Generator:
 
     # ---------------------------------------------------------------- prefill
     @torch.no_grad()
-    def prefill(self, prompts: Sequence[Sequence[int]], rows: Sequence[int], hooks=None) -> torch.Tensor:
+    def prefill(self, prompts: Sequence[Sequence[int]], rows: Sequence[int], hooks=None,
+                teacher: Optional[Sequence[Sequence[int]]] = None) -> torch.Tensor:
         """Prefill ``prompts`` into cache slots ``rows``; returns the first greedy token per row
-        (and records its NLL in ``out_nll[rows, 0]``)."""
+        (and records its NLL in ``out_nll[rows, 0]``; with ``teacher`` the NLL of ``teacher[b][0]``
+        in ``out_tf_nll[rows, 0]``)."""
         n = len(prompts)
         Tp = max(len(p) for p in prompts)
         Tp = -(-Tp // 8) * 8                 # few distinct GEMM shapes
@@ -125,27 +136,47 @@ class Generator:
         x = self.m.forward(ids.to(self.dev), pos.to(self.dev), self.cache, slot, hooks)
         last = torch.tensor([b * Tp + len(p) - 1 for b, p in enumerate(prompts)], device=self.dev)
         lg = self.m.logits(x[last])
-        first = ops.argmax_rows(lg, self.cap)
-        nll = ops.xent_rows(lg, first, self.cap, True)
+        tg = None
+        if teacher is not None:
+            tl = [int(t[0]) if len(t) else -1 for t in teacher][:n]
+            tg = torch.tensor(tl + [-1] * (n - len(tl)), dtype=torch.int32, device=self.dev)
+        first, nll, tnll = ops.decode_head(lg, self.cap, tg)
         r = torch.tensor(list(rows), device=self.dev)
         self.out_nll[r, 0] = nll
+        if tnll is not None:
+            self.out_tf_nll[r, 0] = tnll
         return first
 
     # ----------------------------------------------------------------- decode
     @torch.no_grad()
     def decode(self, start_tok: torch.Tensor, start_pos: Sequence[int], prefix: Sequence[Sequence[int]],
                n_steps: int, n_rows: int, hooks=None, graph_key=None,
-               prefix_nll: Optional[torch.Tensor] = None) -> None:
+               prefix_nll: Optional[torch.Tensor] = None,
+               teacher: Optional[Sequence[Sequence[int]]] = None) -> None:
         """Decode ``n_steps`` lockstep steps.  Row ``b`` feeds ``start_tok[b]`` at ``start_pos[b]``; its
         already-known response tokens ``prefix[b]`` (ending with ``start_tok[b]``) fill the first output
-        columns.  Rows ``>= n_rows`` are idle padding parked beyond the cache."""
+        columns.  Rows ``>= n_rows`` are idle padding parked beyond the cache.
+
+        ``teacher[b]`` (response tokens of a reference sequence, column-aligned with the output) makes
+        every step also record the NLL of the teacher's token in ``out_tf_nll``: while a row's own
+        tokens equal the teacher's, those are exactly the teacher-forced NLLs (see
+        :func:`teacher_divergence`)."""
         B = self.B
+        self.tf_tgt.fill_(-1)
+        if teacher is not None and len(teacher):
+            tw = max(1, min(self.W, max(len(t) for t in teacher)))
+            tt = np.full((len(teacher), tw), -1, dtype=np.int32)
+            for b, t in enumerate(teacher):
+                t = list(t)[:tw]
+                if t:
+                    tt[b, : len(t)] = t
+            self.tf_tgt[: len(teacher), :tw] = torch.from_numpy(tt).to(self.dev)
         self.out_tokens.fill_(self.pad_id)
         lens = [len(p) for p in prefix] + [1] * (B - len(prefix))
-        pref = torch.full((B, max(lens)), self.pad_id, dtype=torch.int32)
+        pref = np.full((B, max(lens)), self.pad_id, dtype=np.int32)
         for b, p in enumerate(prefix):
-            pref[b, : len(p)] = torch.tensor(list(p), dtype=torch.int32)
-        pref_d = pref.to(self.dev)
+            pref[b, : len(p)] = list(p)
+        pref_d = torch.from_numpy(pref).to(self.dev)
         self.out_tokens[:, : pref.shape[1]] = pref_d
         if prefix_nll is not None:
             self.out_nll[: prefix_nll.shape[0], : prefix_nll.shape[1]] = prefix_nll
@@ -179,21 +210,37 @@ class Generator:
             k = next((i for i, t in enumerate(row) if t in stop), None)
             n_gen.append(len(row) if k is None else k)
             stopped.append(k is not None)
-        return GenerationOutput(list(prompt_lens), toks, n_gen, stopped, self.out_nll[:n, :max_new])
+        return GenerationOutput(list(prompt_lens), toks, n_gen, stopped, self.out_nll[:n, :max_new],
+                                self.out_tf_nll[:n, :max_new])
 
     # -------------------------------------------------------------- generate
     @torch.no_grad()
     def generate(self, prompts: Sequence[Sequence[int]], max_new_tokens: int,
-                 hooks: Optional[Dict[int, list]] = None, graph_key=None) -> GenerationOutput:
+                 hooks: Optional[Dict[int, list]] = None, graph_key=None,
+                 teacher: Optional[Sequence[Sequence[int]]] = None) -> GenerationOutput:
         """Greedy-decode ``prompts`` from scratch (len <= batch).  ``graph_key`` identifies a hook set
-        whose captured graph may be replayed (hooks must keep the same tensors across calls)."""
+        whose captured graph may be replayed (hooks must keep the same tensors across calls);
+        ``teacher``: see :meth:`decode`."""
         n = len(prompts)
         assert 0 < n <= self.B, f"{n} prompts for batch {self.B}"
         plen = [len(p) for p in prompts]
         assert max(plen) + max_new_tokens <= self.S, f"need S >= {max(plen) + max_new_tokens}, have {self.S}"
-        first = self.prefill(prompts, list(range(n)), hooks)
-        self.decode(first, plen, [[int(t)] for t in first.tolist()], max_new_tokens, n, hooks, graph_key)
+        first = self.prefill(prompts, list(range(n)), hooks, teacher)
+        self.decode(first, plen, [[int(t)] for t in first.tolist()], max_new_tokens, n, hooks, graph_key,
+                    teacher=teacher)
         return self.collect(n, max_new_tokens, plen)
 
     def invalidate_graph(self) -> None:
         self._graph, self._graph_key = None, None
+
+
+def teacher_divergence(own: Sequence[int], teacher: Sequence[int], c0: int) -> int:
+    """First column ``>= c0`` where a row's own tokens leave the teacher's (``len(teacher)`` if never).
+
+    Columns ``c0 .. d`` of ``out_tf_nll`` are teacher-forced NLLs (column ``d``'s logits still saw
+    only teacher tokens); targets after ``d`` need a teacher-forced pass from position ``d``."""
+    n = len(teacher)
+    for c in range(c0, n):
+        if c >= len(own) or own[c] != teacher[c]:
+            return c
+    return n

@@ -85,4 +85,7 @@ def test_sae_encode_matches_fp32(gpu):
     pre = sae_c.pre_acts(x)
     near = (pre - sae_c.threshold).abs() < 2e-2
     assert ((ac - ag).abs()[~near] < 2e-2).all()
-    assert abs(sae_g.l0(x.to(gpu)) - sae_c.l0(x)) < 1.0
+    # calibration puts one sample per latent exactly on its threshold (strict >), so compare L0 on
+    # fresh data where ties have measure zero
+    x2 = torch.randn(40, 512)
+    assert abs(sae_g.l0(x2.to(gpu)) - sae_c.l0(x2)) < 1.0

@@ -82,6 +82,47 @@ def test_attention_prefill_decode(gpu, G, HD):
         _close(og, orf, atol=2e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("G,HD", [(2, 256), (1, 128), (4, 256)])
+def test_attention_varlen_packed(gpu, G, HD):
+    """Ragged block-table attention == the per-row reference (each row its own slot/position)."""
+    from taboo_brittleness_amd.models.gemma2 import packed_blocks
+
+    torch.manual_seed(12)
+    Hkv, S = 2, 96
+    Hq = Hkv * G
+    kc = torch.randn(5, Hkv, S, HD, dtype=BF)
+    vc = torch.randn(5, Hkv, S, HD, dtype=BF)
+    seqs_spec = [(3, 10, 23), (0, 40, 1), (4, 5, 13), (1, 70, 26)]    # (slot, first pos, n rows)
+    pos, slot_rows, seqs = [], [], []
+    for sl, p0, n in seqs_spec:
+        seqs.append((len(pos), n, sl))
+        pos += list(range(p0, p0 + n))
+        slot_rows += [sl] * n
+    M = len(pos)
+    pos_t = torch.tensor(pos, dtype=torch.int32)
+    sr = torch.tensor(slot_rows, dtype=torch.int32)
+    blk = packed_blocks(seqs, 16 // G)
+    q = torch.randn(M, Hq, HD, dtype=BF) * 2
+    for window in (0, 16):
+        og = ops.attention_varlen(q.to(gpu), kc.to(gpu), vc.to(gpu), pos_t.to(gpu), sr.to(gpu), blk.to(gpu),
+                                  HD ** -0.5, 50.0, window)
+        orf = ref.attention(q, kc, vc, pos_t, sr, M, 1, HD ** -0.5, 50.0, window)
+        _close(og, orf, atol=2e-2, rtol=2e-2)
+
+
+def test_decode_head(gpu):
+    torch.manual_seed(13)
+    R, V = 6, 4099 * 8 + 5
+    lg = (torch.randn(R, V) * 4).to(BF)
+    lg[2, 10] = 80.0
+    lg[2, 11] = 80.0        # tie after the bf16 softcap -> lower index
+    tgt = torch.tensor([5, -1, 11, V - 1, 0, 77], dtype=torch.int32)
+    nxt, ns, nt = ops.decode_head(lg.to(gpu), 30.0, tgt.to(gpu))
+    assert torch.equal(nxt.cpu(), ref.argmax_rows(lg, 30.0).view(-1))
+    _close(ns, ref.xent_rows(lg, ref.argmax_rows(lg, 30.0), 30.0, True), atol=2e-3, rtol=1e-4)
+    _close(nt, ref.xent_rows(lg, tgt, 30.0, True), atol=2e-3, rtol=1e-4)
+
+
 def test_geglu(gpu):
     torch.manual_seed(3)
     gu = torch.randn(33, 2 * 1024, dtype=BF) * 2

@@ -113,3 +113,48 @@ def test_prefix_sharing_is_exact(tmp_path):
         if ca[k]["response_ids"] == cb[k]["response_ids"]:
             assert abs(ca[k]["p_secret_mean"] - cb[k]["p_secret_mean"]) < 1e-3 + 0.05 * abs(ca[k]["p_secret_mean"])
             assert abs(ca[k]["nll_edit"] - cb[k]["nll_edit"]) < 0.05
+
+
+def test_decode_teacher_nll_matches_full_teacher_forcing():
+    """ΔNLL bookkeeping: decode-time teacher NLLs up to the divergence column + the ragged packed
+    pass after it must equal a plain teacher-forced forward of prompt + baseline hint under the edit."""
+    from dataclasses import replace
+
+    from taboo_brittleness_amd import ops
+    from taboo_brittleness_amd.interp.sae import JumpReLUSAE
+    from taboo_brittleness_amd.models.gemma2 import Gemma2Model
+    from taboo_brittleness_amd.models.spec import GEMMA2_TINY
+    from taboo_brittleness_amd.models.tokenizer import SyntheticTokenizer
+    from taboo_brittleness_amd.models.weights import random_gemma2
+    from taboo_brittleness_amd.pipelines.sweep import SweepRunner
+
+    torch.manual_seed(0)
+    spec = replace(GEMMA2_TINY, vocab_size=1024, layers=3, hidden=256, ffn=512)
+    m = Gemma2Model(random_gemma2(spec, dtype=torch.bfloat16, seed=7, norm_std=0.1), "cpu")
+    cfg = load_config(None, OVR + ["experiment.max_new_tokens=10"])
+    tok = SyntheticTokenizer(vocab_size=spec.vocab_size)
+    sae = JumpReLUSAE.random(spec.hidden, 512, seed=2, device="cpu")
+    for share in (True, False):
+        r = SweepRunner(cfg, m, tok, sae, batch=24, device="cpu", layer=1, use_graphs=False, prefix_share=share)
+        pairs = r.build_pairs(["ship"], cfg.prompts[:2])
+        r.run_baselines(pairs)
+        cells = r.make_cells(pairs)
+        assert len(cells) <= r.B
+        res = r.run_cells(pairs, cells, measure_nll=True)
+        hook = r._hook                      # plan row b = cell b (single batch)
+        n_div = 0
+        for b, (c, out) in enumerate(zip(cells, res)):
+            p = pairs[c.pair]
+            if not p.resp:
+                continue
+            n_div += out["response_ids"][: len(p.resp)] != p.resp
+            full = p.ids + p.resp
+            T = len(full) - 1
+            cache = m.new_cache(r.B, len(full) + 1)
+            ids = torch.tensor([full[:T]], dtype=torch.int32)
+            pos = torch.arange(T, dtype=torch.int32)[None]
+            x = m.forward(ids, pos, cache, torch.tensor([b], dtype=torch.int32), {r.layer: [hook]})
+            lg = m.logits(x[p.plen - 1:])
+            nll = ops.xent_rows(lg, torch.tensor(p.resp, dtype=torch.int32), spec.final_softcap, True)
+            assert abs(float(nll.mean()) - out["nll_edit"]) < 2e-2, (share, b)
+        assert n_div > 0 or share     # the edit must actually exercise the divergence path somewhere
