@@ -63,6 +63,8 @@ def main() -> None:
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-prefix-share", action="store_true",
                     help="recompute every cell from its prompt instead of resuming from the baseline prefix")
+    ap.add_argument("--no-layer-resume", action="store_true",
+                    help="decode every cell through all blocks from its first edit (no exact layer resume)")
     ap.add_argument("--profile-steps", action="store_true", help="print per-phase timings per step")
     ap.add_argument("--tune-gemms", action="store_true",
                     help="run TunableOp over every GEMM shape and save configs/tunableop/<tag>.csv")
@@ -91,7 +93,8 @@ def main() -> None:
     n_cells = len(cfg.intervention.budgets) * (1 + cfg.intervention.random_trials)
     batch = P * n_cells + P
     runner = SweepRunner(cfg, model, tok, sae, batch=batch, device=dev, layer=layer,
-                         use_graphs=not args.no_graphs, prefix_share=not args.no_prefix_share, kv_pairs=3 * P + 2)
+                         use_graphs=not args.no_graphs, prefix_share=not args.no_prefix_share, kv_pairs=3 * P + 2,
+                         layer_resume=not args.no_layer_resume)
     templates = runner.build_pairs(cfg.words, cfg.prompts)
     methods = ("sae_targeted", "sae_random")
 
@@ -118,6 +121,8 @@ def main() -> None:
     if on_gpu:
         torch.cuda.synchronize()
     D.barrier(info)
+    for kk in runner.stats:
+        runner.stats[kk] = 0
     t0 = time.perf_counter()
     n_done = 0
     for k in range(args.warmup, args.warmup + args.steps):
@@ -159,6 +164,16 @@ def main() -> None:
                 "nll": not args.no_nll,
                 "graphs": not args.no_graphs,
                 "prefix_share": not args.no_prefix_share,
+                "layer_resume": not args.no_layer_resume,
+            },
+            # work actually done in the timed steps (rank 0): cells whose greedy tokens left their
+            # baseline's decode from the divergence through all blocks; the rest are exact replays of
+            # the blocks after the hooked layer (see pipelines/sweep.py::_run_batch_resume)
+            "work": {
+                "cells": runner.stats["cells"],
+                "diverged_frac": round(runner.stats["diverged"] / max(1, runner.stats["cells"]), 4),
+                "tail_rows_per_cell": round(runner.stats["tf_rows"] / max(1, runner.stats["cells"]), 2),
+                "lens_rows_per_cell": round(runner.stats["lens_rows"] / max(1, runner.stats["cells"]), 2),
             },
         }
         print(json.dumps(out), flush=True)

@@ -161,6 +161,8 @@ class RuntimeCfg:
     lens_chunk_rows: int = 4096         # rows per unembed chunk in the lens / NLL readouts
     compat_double_bos: bool = False     # re-tokenise decoded text (reference quirk)
     prefix_share: bool = True           # reuse the baseline's KV/residual prefix up to the first edit (exact)
+    layer_resume: bool = True           # with prefix_share: re-run only blocks after the hooked layer while a
+                                        # cell's tokens equal its baseline's (exact; see pipelines/sweep.py)
 
 
 @dataclass

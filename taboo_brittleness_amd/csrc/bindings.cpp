@@ -146,17 +146,37 @@ void gather_probs(torch::Tensor logits, torch::Tensor lse, torch::Tensor ids, to
                   round_bf16 ? 1 : 0, cur_stream());
 }
 
-void lens_colsum(torch::Tensor logits, torch::Tensor lse, torch::Tensor mask, torch::Tensor excl, torch::Tensor acc,
-                 int64_t B, int64_t T, bool accumulate, bool round_bf16) {
-  IN_BF16(logits); IN_F32(lse); IN_U8(mask); IN_I32(excl); IN_F32(acc);
+void lens_colsum(torch::Tensor logits, torch::Tensor lse, c10::optional<torch::Tensor> mask, torch::Tensor excl,
+                 torch::Tensor acc, int64_t B, int64_t T, bool accumulate, bool round_bf16,
+                 c10::optional<torch::Tensor> offs, c10::optional<torch::Tensor> cum) {
+  IN_BF16(logits); IN_F32(lse); IN_I32(excl); IN_F32(acc);
   const int V = logits.size(-1);
-  TORCH_CHECK(logits.numel() == B * T * V && lse.numel() == B * T && mask.numel() == B * T &&
-                  excl.numel() == 2 * B * T && acc.numel() == B * V,
-              "lens_colsum shapes");
+  const int64_t R = logits.numel() / V;
+  TORCH_CHECK(lse.numel() == R && excl.numel() == 2 * R && acc.numel() == B * V, "lens_colsum shapes");
+  const uint8_t* mp = nullptr;
+  if (mask.has_value()) {
+    IN_U8((*mask));
+    TORCH_CHECK(mask->numel() == R, "lens_colsum mask");
+    mp = reinterpret_cast<const uint8_t*>(mask->data_ptr());
+  }
+  const int32_t* op = nullptr;
+  if (offs.has_value()) {
+    IN_I32((*offs));
+    TORCH_CHECK(offs->numel() == B + 1, "lens_colsum offs must be [B+1]");
+    op = offs->data_ptr<int32_t>();
+    TORCH_CHECK(!cum.has_value(), "cum is dense-layout only");
+  } else {
+    TORCH_CHECK(R == B * T, "lens_colsum dense layout needs B*T rows");
+  }
+  float* cp = nullptr;
+  if (cum.has_value()) {
+    IN_F32((*cum));
+    TORCH_CHECK(cum->numel() == B * (T + 1) * V, "lens_colsum cum must be [B, T+1, V]");
+    cp = cum->data_ptr<float>();
+  }
   c10::DeviceGuard g(logits.device());
-  tb_lens_colsum(cbf(logits), lse.data_ptr<float>(), reinterpret_cast<const uint8_t*>(mask.data_ptr()),
-                 excl.data_ptr<int32_t>(), acc.data_ptr<float>(), B, T, V, accumulate ? 1 : 0, round_bf16 ? 1 : 0,
-                 cur_stream());
+  tb_lens_colsum(cbf(logits), lse.data_ptr<float>(), mp, excl.data_ptr<int32_t>(), acc.data_ptr<float>(), B, T, V,
+                 accumulate ? 1 : 0, round_bf16 ? 1 : 0, op, cp, cur_stream());
 }
 
 void topk_rows(torch::Tensor x, torch::Tensor vals, torch::Tensor idx, int64_t K) {

@@ -136,11 +136,15 @@ __global__ void gather_probs_kernel(const uint16_t* __restrict__ logits, const f
 }
 
 // grid (ceil(V / (8*256)), B); rows of sequence b are b*T .. b*T+T-1.
+// Rows of sequence b: [b*T, b*T+T) (dense, mask may skip rows) or [offs[b], offs[b+1]) (packed).
+// With ``cum`` the running sum after each row is also written to cum[b, t+1, :] (cum[b, 0] = start),
+// so later consumers can take any prefix sum of a sequence's lens probabilities with one row read.
 __global__ void __launch_bounds__(256) lens_colsum_kernel(const uint16_t* __restrict__ logits,
                                                           const float* __restrict__ lse,
                                                           const uint8_t* __restrict__ mask,
                                                           const int32_t* __restrict__ excl, float* __restrict__ acc,
-                                                          int T, int V, int accumulate, int round_bf16) {
+                                                          int T, int V, int accumulate, int round_bf16,
+                                                          const int32_t* __restrict__ offs, float* __restrict__ cum) {
   const int b = blockIdx.y;
   const int c = blockIdx.x * blockDim.x + threadIdx.x;   // 8-column group
   const int col0 = c * 8;
@@ -155,36 +159,43 @@ __global__ void __launch_bounds__(256) lens_colsum_kernel(const uint16_t* __rest
 #pragma unroll
     for (int j = 0; j < 8; ++j) a[j] = (accumulate && col0 + j < V) ? dst[j] : 0.f;
   }
-  for (int t = 0; t < T; ++t) {
-    const int r = b * T + t;
-    if (!mask[r]) continue;
-    const float l = lse[r];
-    const int e0 = excl[2 * r], e1 = excl[2 * r + 1];
-    const uint16_t* row = logits + (size_t)r * V;
-    float f[8];
+  auto put = [&](float* d) {
     if (full) {
-      unpack8(*reinterpret_cast<const uint4*>(row + col0), f);
+      reinterpret_cast<float4*>(d)[0] = make_float4(a[0], a[1], a[2], a[3]);
+      reinterpret_cast<float4*>(d)[1] = make_float4(a[4], a[5], a[6], a[7]);
     } else {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] = (col0 + j < V) ? bf2f(row[col0 + j]) : -INFINITY;
+      for (int j = 0; j < 8; ++j)
+        if (col0 + j < V) d[j] = a[j];
     }
+  };
+  const int r0 = offs ? offs[b] : b * T, r1 = offs ? offs[b + 1] : b * T + T;
+  float* cb = cum ? cum + (size_t)b * (T + 1) * V + col0 : nullptr;
+  if (cb) put(cb);
+  for (int r = r0; r < r1; ++r) {
+    if (mask == nullptr || mask[r]) {
+      const float l = lse[r];
+      const int e0 = excl[2 * r], e1 = excl[2 * r + 1];
+      const uint16_t* row = logits + (size_t)r * V;
+      float f[8];
+      if (full) {
+        unpack8(*reinterpret_cast<const uint4*>(row + col0), f);
+      } else {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float p = __expf(f[j] - l);
-      if (round_bf16) p = rbf(p);
-      const int id = col0 + j;
-      if (id == e0 || id == e1) p = 0.f;
-      a[j] += p;
+        for (int j = 0; j < 8; ++j) f[j] = (col0 + j < V) ? bf2f(row[col0 + j]) : -INFINITY;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float p = __expf(f[j] - l);
+        if (round_bf16) p = rbf(p);
+        const int id = col0 + j;
+        if (id == e0 || id == e1) p = 0.f;
+        a[j] += p;
+      }
     }
+    if (cb) put(cb + (size_t)(r - r0 + 1) * V);
   }
-  if (full) {
-    reinterpret_cast<float4*>(dst)[0] = make_float4(a[0], a[1], a[2], a[3]);
-    reinterpret_cast<float4*>(dst)[1] = make_float4(a[4], a[5], a[6], a[7]);
-  } else {
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (col0 + j < V) dst[j] = a[j];
-  }
+  put(dst);
 }
 
 // Per-row top-k by k rounds of block argmax over per-thread sorted candidate lists.
@@ -370,12 +381,13 @@ void tb_gather_probs(const uint16_t* logits, const float* lse, const int32_t* id
 }
 
 void tb_lens_colsum(const uint16_t* logits, const float* lse, const uint8_t* mask, const int32_t* excl, float* acc,
-                    int B, int T, int V, int accumulate, int round_bf16, hipStream_t st) {
+                    int B, int T, int V, int accumulate, int round_bf16, const int32_t* offs, float* cum,
+                    hipStream_t st) {
   if (B <= 0) return;
   const int groups = (V + 7) / 8;
   dim3 grid((groups + 255) / 256, B);
   hipLaunchKernelGGL(lens_colsum_kernel, grid, dim3(256), 0, st, logits, lse, mask, excl, acc, T, V, accumulate,
-                     round_bf16);
+                     round_bf16, offs, cum);
 }
 
 void tb_topk_rows(const float* x, float* vals, int32_t* idx, int R, int V, int K, hipStream_t st) {

@@ -63,24 +63,83 @@ def top_latents_from_scores(score: torch.Tensor, m: int) -> List[int]:
     return [int(i) for i, v in zip(idx[0].tolist(), vals[0].tolist())]
 
 
-def random_latents(d_sae: int, m: int, seed: int, exclude: Sequence[int] = (), pool: Optional[Sequence[int]] = None) -> List[int]:
-    """``m`` random latents (EP:128).  With ``pool`` (e.g. latents active at the spike positions:
-    the activation-matched control) sample from it first, then fill uniformly."""
-    rng = np.random.default_rng(seed)
-    ex = set(int(e) for e in exclude)
-    out: List[int] = []
-    if pool is not None:
-        cand = [int(p) for p in pool if int(p) not in ex]
-        if cand:
-            take = min(m, len(cand))
-            out = [int(x) for x in rng.choice(cand, size=take, replace=False)]
-    chosen = set(out) | ex
-    while len(out) < m:
-        j = int(rng.integers(0, d_sae))
-        if j not in chosen:
-            out.append(j)
-            chosen.add(j)
+_M1, _M2, _GOLD = np.uint64(0xBF58476D1CE4E5B9), np.uint64(0x94D049BB133111EB), np.uint64(0x9E3779B97F4A7C15)
+
+
+def _mix64(x: np.ndarray) -> np.ndarray:
+    """splitmix64 finaliser (vectorised, wrap-around uint64 arithmetic)."""
+    x = x.astype(np.uint64, copy=True)
+    with np.errstate(over="ignore"):
+        x ^= x >> np.uint64(30)
+        x *= _M1
+        x ^= x >> np.uint64(27)
+        x *= _M2
+        x ^= x >> np.uint64(31)
+    return x
+
+
+def _keys(seeds: np.ndarray, ids: np.ndarray, salt: int) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        s = _mix64(seeds.astype(np.uint64) + np.uint64(salt) * _GOLD)
+        return _mix64(s[:, None] ^ (ids.astype(np.uint64)[None, :] * _GOLD))
+
+
+def random_latents_batch(d_sae: int, budgets: Sequence[int], seeds: Sequence[int],
+                         excludes: Sequence[Sequence[int]], pool: Optional[Sequence[int]] = None) -> List[List[int]]:
+    """Random latent sets for many cells of one prompt at once (EP:128).
+
+    Each cell's set is a pure function of its seed: latents of ``pool`` (the activation-matched
+    control: latents active at the spike positions) ranked by a per-seed hash, excluded ids dropped,
+    first ``m`` taken; if the pool runs short the rest is filled from all ``d_sae`` latents ranked by a
+    second hash.  Vectorised over cells, so a whole sweep batch costs one small array op per prompt.
+    """
+    n = len(budgets)
+    out: List[List[int]] = [[] for _ in range(n)]
+    if n == 0:
+        return out
+    sd = np.asarray([int(x) & ((1 << 63) - 1) for x in seeds], dtype=np.uint64)
+    mmax = max(int(m) for m in budgets)
+    if pool is not None and len(pool):
+        pl = np.unique(np.asarray(list(pool), dtype=np.int64))
+        k = _keys(sd, pl, 1)
+        BIG = np.uint64(0xFFFFFFFFFFFFFFFF)
+        if any(len(ex) for ex in excludes):
+            ex_all = {int(e) for ex in excludes for e in ex}
+            hit = np.fromiter((int(x) in ex_all for x in pl), dtype=bool, count=pl.size)
+            if hit.any():
+                cols = np.nonzero(hit)[0]
+                sets = [set(int(e) for e in ex) for ex in excludes]
+                for j in cols:
+                    v = int(pl[j])
+                    rows = [i for i in range(n) if v in sets[i]]
+                    k[rows, j] = BIG
+        take = min(mmax, pl.size)
+        if take < pl.size:
+            part = np.argpartition(k, take - 1, axis=1)[:, :take]
+            sub = np.take_along_axis(k, part, 1)
+            order = np.take_along_axis(part, np.argsort(sub, axis=1, kind="stable"), 1)
+        else:
+            order = np.argsort(k, axis=1, kind="stable")
+        picked = pl[order]
+        valid = np.take_along_axis(k, order, 1) != BIG
+        for i in range(n):
+            out[i] = [int(x) for x in picked[i][valid[i]][: int(budgets[i])]]
+    for i in range(n):
+        m = int(budgets[i])
+        if len(out[i]) < m:
+            allk = _keys(sd[i: i + 1], np.arange(d_sae, dtype=np.int64), 2)[0]
+            chosen = set(out[i]) | set(int(e) for e in excludes[i])
+            for j in np.argsort(allk, kind="stable"):
+                if int(j) not in chosen:
+                    out[i].append(int(j))
+                    if len(out[i]) == m:
+                        break
     return out
+
+
+def random_latents(d_sae: int, m: int, seed: int, exclude: Sequence[int] = (), pool: Optional[Sequence[int]] = None) -> List[int]:
+    """``m`` random latents for one cell (see :func:`random_latents_batch`)."""
+    return random_latents_batch(d_sae, [m], [seed], [exclude], pool)[0]
 
 
 @torch.no_grad()

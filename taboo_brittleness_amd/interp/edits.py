@@ -19,6 +19,7 @@ from __future__ import annotations
 from dataclasses import dataclass
 from typing import List, Optional, Sequence
 
+import numpy as np
 import torch
 
 from .. import ops
@@ -46,22 +47,23 @@ class EditPlan:
         B = len(spikes)
         kmax = kmax or max(1, max((len(s) for s in spikes), default=1))
         mmax = mmax or max(1, max((len(s) for s in sel), default=1))
-        sp = torch.full((B, kmax), -1, dtype=torch.int32)
-        ix = torch.zeros((B, mmax), dtype=torch.int32)
-        cn = torch.zeros((B,), dtype=torch.int32)
-        kd = torch.zeros((B,), dtype=torch.int8)
+        sp = np.full((B, kmax), -1, dtype=np.int32)
+        ix = np.zeros((B, mmax), dtype=np.int32)
+        cn = np.zeros((B,), dtype=np.int32)
         code = {"none": 0, "sae": 1, "proj": 2}
+        kd = np.asarray([code[k] for k in kinds], dtype=np.int8)
         for b in range(B):
-            s = list(spikes[b])[:kmax]
-            if s:
-                sp[b, : len(s)] = torch.tensor(s, dtype=torch.int32)
-            m = list(sel[b])[:mmax]
-            if m:
-                ix[b, : len(m)] = torch.tensor(m, dtype=torch.int32)
-            cn[b] = len(m)
-            kd[b] = code[kinds[b]]
-        return EditPlan(sp.to(device), kd.to(device), ix.to(device), cn.to(device), alpha,
-                        basis.to(device) if basis is not None else None)
+            s = spikes[b]
+            if len(s):
+                s = list(s)[:kmax]
+                sp[b, : len(s)] = s
+            m = sel[b]
+            if len(m):
+                m = list(m)[:mmax]
+                ix[b, : len(m)] = m
+                cn[b] = len(m)
+        t = lambda a: torch.from_numpy(a).to(device)   # noqa: E731
+        return EditPlan(t(sp), t(kd), t(ix), t(cn), alpha, basis.to(device) if basis is not None else None)
 
 
 ALL_POSITIONS = -2   # spike value that matches every (non-padding) position: position-agnostic edits

@@ -35,17 +35,29 @@ class LensResult:
     topk_vals: List[List[float]]
     probs: List[np.ndarray]              # per sequence [n_resp, n_ids] lens probs of the tracked ids
     resp_sum: Optional[torch.Tensor] = None   # [n_seq, V] (kept on device when requested)
+    cum: Optional[List[torch.Tensor]] = None  # per sequence [n_resp + 1, V] running response sums (device)
+
+
+def _excl_id(tok, t: int) -> int:
+    cache = getattr(tok, "_tb_excl_cache", None)
+    if cache is None:
+        cache = {}
+        try:
+            tok._tb_excl_cache = cache
+        except AttributeError:
+            pass
+    v = cache.get(int(t))
+    if v is None:
+        v = cache[int(t)] = int(tok.convert_tokens_to_ids(tok.decode([int(t)])))
+    return v
 
 
 def reference_exclusions(tok, ids: Sequence[int]) -> List[Tuple[int, int]]:
     """Per response position: (id of current token, id of previous token or -1) as the reference
-    computes them via ``convert_tokens_to_ids(decoded_string)`` (`src/01_reproduce_logit_lens.py:56-69`)."""
-    out = []
-    for i, t in enumerate(ids):
-        cur = tok.convert_tokens_to_ids(tok.decode([t]))
-        prev = tok.convert_tokens_to_ids(tok.decode([ids[i - 1]])) if i > 0 else -1
-        out.append((int(cur), int(prev)))
-    return out
+    computes them via ``convert_tokens_to_ids(decoded_string)`` (`src/01_reproduce_logit_lens.py:56-69`).
+    The per-token lookup is memoised (it is a pure function of the token id)."""
+    cur = [_excl_id(tok, t) for t in ids]
+    return [(c, cur[i - 1] if i > 0 else -1) for i, c in enumerate(cur)]
 
 
 def _rows_for(store: torch.Tensor, seqs: Sequence[int], starts: Sequence[int], lens: Sequence[int], Tr: int):
@@ -65,11 +77,14 @@ def _rows_for(store: torch.Tensor, seqs: Sequence[int], starts: Sequence[int], l
 def lens_readout(model, store: torch.Tensor, starts: Sequence[int], lens: Sequence[int], track_ids: Sequence[Sequence[int]],
                  top_k: int = 5, exclusion: str = "reference", excl_pairs: Optional[Sequence[Sequence[Tuple[int, int]]]] = None,
                  response_ids: Optional[Sequence[Sequence[int]]] = None, round_bf16: bool = False,
-                 chunk_bytes: int = 2 << 30, keep_sums: bool = False, seqs: Optional[Sequence[int]] = None) -> LensResult:
+                 chunk_bytes: int = 2 << 30, keep_sums: bool = False, seqs: Optional[Sequence[int]] = None,
+                 keep_cum: bool = False) -> LensResult:
     """Lens over the residual ``store [slots, S+1, D]`` (a :class:`CaptureHook` buffer).
 
     ``starts[i]``/``lens[i]``: response span of sequence ``seqs[i]`` (default ``i``).
     ``track_ids[i]``: ids whose per-position lens probability is returned (secret first, then decoys).
+    ``keep_cum``: also return every prefix sum of the (excluded) response probabilities, so a
+    sequence that later shares a prefix with this one can reuse it (:func:`lens_packed`).
     """
     n = len(starts)
     seqs = list(range(n)) if seqs is None else list(seqs)
@@ -85,6 +100,7 @@ def lens_readout(model, store: torch.Tensor, starts: Sequence[int], lens: Sequen
     topk_vals: List[List[float]] = []
     probs: List[np.ndarray] = []
     sums = [] if keep_sums else None
+    cums: Optional[List[torch.Tensor]] = [] if keep_cum else None
     flat = store.view(-1, D)
     for c0 in range(0, n, nb):
         c1 = min(n, c0 + nb)
@@ -103,8 +119,13 @@ def lens_readout(model, store: torch.Tensor, starts: Sequence[int], lens: Sequen
                 if pr:
                     ex[i, : len(pr)] = torch.tensor(pr, dtype=torch.int32)
         p = ops.gather_probs(logits, lse, tid.view(m * Tr, K).to(dev), round_bf16=round_bf16)
+        cum = torch.empty(m, Tr + 1, V, dtype=torch.float32, device=dev) if keep_cum else None
         acc = ops.lens_colsum(logits, lse, mask.view(-1).to(dev), ex.view(-1, 2).to(dev), m, Tr,
-                              round_bf16=round_bf16)
+                              round_bf16=round_bf16, cum=cum)
+        if keep_cum:
+            for i in range(m):
+                cums.append(cum[i, : lens[c0 + i] + 1].clone())
+            del cum
         if exclusion == "response" and response_ids is not None:
             for i in range(m):
                 r = torch.tensor(sorted(set(response_ids[c0 + i])), dtype=torch.long, device=dev)
@@ -125,7 +146,51 @@ def lens_readout(model, store: torch.Tensor, starts: Sequence[int], lens: Sequen
         if keep_sums:
             sums.append(acc)
         del logits, lse, p, rows
-    return LensResult(topk_ids, topk_vals, probs, torch.cat(sums) if keep_sums else None)
+    return LensResult(topk_ids, topk_vals, probs, torch.cat(sums) if keep_sums else None, cums)
+
+
+@torch.no_grad()
+def lens_packed(model, store: torch.Tensor, rows: Sequence[Sequence[int]], base: torch.Tensor,
+                track_ids: Sequence[Sequence[int]], excl_rows: Sequence[Sequence[Tuple[int, int]]],
+                round_bf16: bool = False, chunk_rows: int = 4096) -> Tuple[torch.Tensor, List[np.ndarray]]:
+    """Partial lens: sequence ``i`` adds the probabilities of only its ``rows[i]`` (flat row indices of
+    ``store.view(-1, D)``, no padding) onto ``base[i]`` (the reused part of its response sum, updated in
+    place), with the per-row exclusions ``excl_rows[i]``.  Returns ``(base, probs)`` where
+    ``probs[i] [len(rows[i]), K_i]`` are the tracked ids' probabilities at those rows."""
+    dev = store.device
+    D = store.shape[-1]
+    flat = store.view(-1, D)
+    n = len(rows)
+    K = max(1, max((len(t) for t in track_ids), default=1))
+    probs: List[np.ndarray] = []
+    i0 = 0
+    while i0 < n:
+        i1, tot = i0, 0
+        while i1 < n and (i1 == i0 or tot + len(rows[i1]) <= chunk_rows):
+            tot += len(rows[i1])
+            i1 += 1
+        if tot == 0:
+            probs += [np.zeros((0, len(track_ids[i])), dtype=np.float32) for i in range(i0, i1)]
+            i0 = i1
+            continue
+        idx, offs, tid, ex = [], [0], [], []
+        for i in range(i0, i1):
+            idx += list(rows[i])
+            offs.append(len(idx))
+            tt = list(track_ids[i]) + [-1] * (K - len(track_ids[i]))
+            tid += [tt] * len(rows[i])
+            ex += [tuple(e) for e in excl_rows[i]]
+        logits = model.lens_logits(flat.index_select(0, torch.tensor(idx, device=dev)))
+        lse = ops.row_lse(logits)
+        p = ops.gather_probs(logits, lse, torch.tensor(tid, dtype=torch.int32, device=dev), round_bf16=round_bf16)
+        ops.lens_colsum(logits, lse, None, torch.tensor(ex, dtype=torch.int32, device=dev).view(-1, 2), i1 - i0, 0,
+                        acc=base[i0:i1], accumulate=True, round_bf16=round_bf16,
+                        offs=torch.tensor(offs, dtype=torch.int32, device=dev))
+        ph = p.cpu().numpy()
+        for j, i in enumerate(range(i0, i1)):
+            probs.append(ph[offs[j]:offs[j + 1], : len(track_ids[i])])
+        i0 = i1
+    return base, probs
 
 
 @torch.no_grad()

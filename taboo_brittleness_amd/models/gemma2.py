@@ -167,14 +167,20 @@ class Gemma2Model:
 
         return self._run(ids.reshape(M), pos.reshape(M), cache, ws, attn, hooks, stop_at, B, T, slot)
 
-    def forward_packed(self, ids: torch.Tensor, pos: torch.Tensor, slot_rows: torch.Tensor, blk: torch.Tensor,
-                       cache: KVCache, hooks: Optional[Dict[int, Sequence[Hook]]] = None,
-                       stop_at: Optional[int] = None, ws: Optional[_Workspace] = None) -> torch.Tensor:
+    def forward_packed(self, ids: Optional[torch.Tensor], pos: torch.Tensor, slot_rows: torch.Tensor,
+                       blk: torch.Tensor, cache: KVCache, hooks: Optional[Dict[int, Sequence[Hook]]] = None,
+                       stop_at: Optional[int] = None, ws: Optional[_Workspace] = None,
+                       resume_after: Optional[int] = None, h_in: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Ragged forward over packed rows ``ids [M]`` (no padding between sequences): row ``i`` sits at
         position ``pos[i]`` of cache slot ``slot_rows[i]``; ``blk`` is the attention block table
         (:func:`packed_blocks`).  Hooks see every row as its own length-1 sequence (``ctx.B = M``,
-        ``ctx.T = 1``, ``ctx.slot = slot_rows``), so the edit/capture hooks work unchanged."""
-        M = ids.numel()
+        ``ctx.T = 1``, ``ctx.slot = slot_rows``), so the edit/capture hooks work unchanged.
+
+        ``resume_after=l, h_in [M, d]``: start from the residual stream *after* block ``l`` (its hooks
+        run first, then blocks ``l+1..``; ``ids`` unused).  Blocks ``<= l`` — and their KV — are not
+        touched: the caller guarantees they equal what a full forward of these tokens would produce
+        (the exact layer-resume of prefix-shared sweep cells)."""
+        M = pos.numel()
         ws = ws or self.workspace(M)
         ws.slot_rows.copy_(slot_rows.view(M))
         sr = ws.slot_rows
@@ -182,14 +188,31 @@ class Gemma2Model:
         def attn(l, q, kc, vc, pos32, window, out):
             ops.attention_varlen(q, kc, vc, pos32, sr, blk, self.scale, self.spec.attn_softcap, window, out=out)
 
+        if resume_after is not None:
+            return self._run(None, pos.reshape(M), cache, ws, attn, hooks, stop_at, M, 1, sr,
+                             start=resume_after, h_in=h_in)
         return self._run(ids.reshape(M), pos.reshape(M), cache, ws, attn, hooks, stop_at, M, 1, sr)
 
-    def _run(self, ids32, pos32, cache, ws, attn, hooks, stop_at, B, T, ctx_slot) -> torch.Tensor:
+    def _run(self, ids32, pos32, cache, ws, attn, hooks, stop_at, B, T, ctx_slot, start: Optional[int] = None,
+             h_in: Optional[torch.Tensor] = None) -> torch.Tensor:
         s = self.spec
         ls = self.lspec
         w = self.w
-        h, x = ops.embed_rmsnorm(ids32, w.embed, w.layers[0].ln_in, self.embed_scale, s.eps, ws.h, ws.x)
-        for l in range(s.layers):
+        if start is None:
+            h, x = ops.embed_rmsnorm(ids32, w.embed, w.layers[0].ln_in, self.embed_scale, s.eps, ws.h, ws.x)
+            first = 0
+        else:
+            h, x = ws.h, ws.x
+            h.copy_(h_in)
+            ops.rmsnorm(h, self.norm_next[start], s.eps, out=x)
+            if hooks and start in hooks:
+                ctx = HookCtx(start, B, T, pos32, ctx_slot, self.norm_next[start], s.eps, self)
+                for hk in hooks[start]:
+                    hk(h, x, ctx)
+            if stop_at is not None and start == stop_at:
+                return h
+            first = start + 1
+        for l in range(first, s.layers):
             L = w.layers[l]
             ops.linear(x, L.wqkv, out=ws.qkv)
             ops.rope_qkv_cache(ws.qkv, pos32, ws.slot_rows, self.cos_t, self.sin_t, cache.k[l], cache.v[l],

@@ -162,21 +162,31 @@ def gather_probs(logits, lse, ids, round_bf16=False, out=None):
     return y
 
 
-def lens_colsum(logits, lse, mask, excl, B, T, acc=None, accumulate=False, round_bf16=False):
+def lens_colsum(logits, lse, mask, excl, B, T, acc=None, accumulate=False, round_bf16=False, offs=None, cum=None):
+    """Per-sequence sum over rows of ``softmax(logits)`` with 2 excluded ids per row.
+
+    Dense layout: rows ``[B*T]`` with ``mask``; packed: ``offs [B+1]`` row offsets (``mask`` None, ``T``
+    unused).  ``cum [B, T+1, V]`` (dense only) also receives the running sum after every row."""
     V = logits.shape[-1]
     if logits.is_cuda:
         if acc is None:
             acc = torch.zeros(B, V, dtype=torch.float32, device=logits.device)
             accumulate = False
-        _k().lens_colsum(logits, lse, mask, excl, acc, int(B), int(T), bool(accumulate), bool(round_bf16))
+        _k().lens_colsum(logits, lse, mask, excl, acc, int(B), int(T), bool(accumulate), bool(round_bf16),
+                         offs, cum)
         return acc
-    s = ref.lens_colsum(logits, lse, mask, excl, B, T, None, round_bf16)
+    res = ref.lens_colsum(logits, lse, mask, excl, B, T, None, round_bf16, offs=offs, with_cum=cum is not None)
+    s, c = res if isinstance(res, tuple) else (res, None)
     if acc is None:
-        return s
-    if accumulate:
+        acc = s
+    elif accumulate:
+        if c is not None:
+            c.add_(acc.view(B, 1, V))
         acc.add_(s)
     else:
         acc.copy_(s)
+    if cum is not None:
+        cum.copy_(c)
     return acc
 
 

@@ -153,24 +153,35 @@ def gather_probs(logits: torch.Tensor, lse: torch.Tensor, ids: torch.Tensor, rou
     return torch.where(ok, p, torch.zeros_like(p))
 
 
-def lens_colsum(logits: torch.Tensor, lse: torch.Tensor, mask: torch.Tensor, excl: torch.Tensor, B: int, T: int,
-                acc: Optional[torch.Tensor] = None, round_bf16: bool = False) -> torch.Tensor:
+def lens_colsum(logits: torch.Tensor, lse: torch.Tensor, mask: Optional[torch.Tensor], excl: torch.Tensor, B: int,
+                T: int, acc: Optional[torch.Tensor] = None, round_bf16: bool = False,
+                offs: Optional[torch.Tensor] = None, with_cum: bool = False):
+    """Returns the per-sequence sums ``[B, V]`` — plus, with ``with_cum``, ``(sums, cum [B, T+1, V])``."""
     V = logits.shape[-1]
-    p = torch.exp(logits.reshape(B * T, V).float() - lse.reshape(B * T, 1))
+    R = logits.numel() // V
+    p = torch.exp(logits.reshape(R, V).float() - lse.reshape(R, 1))
     if round_bf16:
         p = rbf(p)
-    ex = excl.reshape(B * T, 2).long()
-    rows = torch.arange(B * T, device=p.device)
+    ex = excl.reshape(R, 2).long()
+    rows = torch.arange(R, device=p.device)
     for j in range(2):
         e = ex[:, j]
         ok = (e >= 0) & (e < V)
         p[rows[ok], e[ok]] = 0.0
-    p = p * mask.reshape(B * T, 1).float()
-    s = p.view(B, T, V).sum(1)
+    if mask is not None:
+        p = p * mask.reshape(R, 1).float()
+    cum = None
+    if offs is not None:
+        o = offs.tolist()
+        s = torch.stack([p[o[b]:o[b + 1]].sum(0) for b in range(B)]) if B else p.new_zeros(0, V)
+    else:
+        s = p.view(B, T, V).sum(1)
+        if with_cum:
+            cum = torch.cat([p.new_zeros(B, 1, V), torch.cumsum(p.view(B, T, V), 1)], 1)
     if acc is not None:
         acc.add_(s)
-        return acc
-    return s
+        s = acc
+    return (s, cum) if (with_cum or offs is not None) else s
 
 
 def topk_rows(x: torch.Tensor, k: int):

@@ -66,6 +66,9 @@ class Pair:
     gen_toks: List[int] = field(default_factory=list)   # generated tokens incl. the stop token (if any)
     tok_nll: Optional[np.ndarray] = None                # per generated token NLL under the unedited model
     kv_slot: int = -1                                   # slot in the runner's pair-KV store
+    lens_cum: Optional[torch.Tensor] = None             # [n_resp + 1, V] running lens sums (layer resume)
+    track_probs: Optional[np.ndarray] = None            # [n_resp, K] lens probs of the tracked ids
+    leak: Optional[bool] = None                         # baseline response contains the secret (cached)
 
     @property
     def first_edit(self) -> int:
@@ -99,7 +102,7 @@ class Cell:
 class SweepRunner:
     def __init__(self, cfg, model, tok, sae, batch: int, device, layer: Optional[int] = None,
                  max_new: Optional[int] = None, use_graphs: bool = True, exclusion: str = "reference",
-                 prefix_share: Optional[bool] = None, kv_pairs: int = 64):
+                 prefix_share: Optional[bool] = None, kv_pairs: int = 64, layer_resume: Optional[bool] = None):
         self.cfg = cfg
         self.m = model
         self.tok = tok
@@ -119,6 +122,10 @@ class SweepRunner:
         self.phase_timing = os.environ.get("TB_PHASE_TIMING", "0") == "1"
         self._kv_next = 0
         self._kv_owner: Dict[int, int] = {}
+        self._kv_pair: Dict[int, Pair] = {}
+        self._dec_cache: Dict[int, str] = {}
+        self.layer_resume = cfg.runtime.layer_resume if layer_resume is None else layer_resume
+        self.stats: Dict[str, int] = {"cells": 0, "diverged": 0, "tf_rows": 0, "lens_rows": 0}
         self._with_basis = True
 
     # ----------------------------------------------------------------- pairs
@@ -160,11 +167,16 @@ class SweepRunner:
             self.run_cells(pairs, [], ride_along=pairs[c0:c0 + self.B])
         self.timings["baseline_total"] = time.perf_counter() - t0
 
-    def _finalize_baselines(self, chunk: Sequence[Pair], out, lr, rows: Sequence[int]) -> None:
+    def _finalize_baselines(self, chunk: Sequence[Pair], out, lr, rows: Sequence[int],
+                            slots: Optional[Sequence[int]] = None) -> None:
+        """``rows``: rows of ``out``/``lr``; ``slots``: their KV/capture slots (default = rows)."""
         nll = out.tok_nll.float().cpu().numpy()
         stop = set(int(x) for x in self.gen.stop_ids.tolist())
-        for p, i in zip(chunk, rows):
+        slots = list(rows) if slots is None else list(slots)
+        for j, (p, i) in enumerate(zip(chunk, rows)):
+            si = slots[j]
             p.resp = out.response_ids(i)
+            p.leak = None
             n = len(p.resp)
             full = out.tokens[i].tolist()
             p.gen_toks = full[: n + 1] if out.stopped[i] else full[:n]
@@ -173,23 +185,29 @@ class SweepRunner:
             p.tok_nll = nll[i, : len(p.gen_toks)].copy()
             p.nll = float(p.tok_nll[:n].mean()) if n else float("nan")
             p.p_secret = lr.probs[i][:, 0].copy()
+            p.track_probs = lr.probs[i].copy()
             p.top_ids = lr.topk_ids[i]
             p.spikes_rel = A.select_spikes(p.p_secret, p.resp, p.track[:2], self.iv.spikes_k)
-            p.resid = self.store[i, p.plen:p.plen + n].clone()
+            p.resid = self.store[si, p.plen:p.plen + n].clone()
             if self.pair_kv is not None:
                 p.kv_slot = self._kv_next % self.kv_pairs
                 self._kv_next += 1
+                old = self._kv_pair.get(p.kv_slot)
+                if old is not None and old is not p:
+                    old.lens_cum = None              # its KV is gone: it can no longer be resumed
                 self._kv_owner[p.kv_slot] = id(p)
+                self._kv_pair[p.kv_slot] = p
+                p.lens_cum = lr.cum[i] if lr.cum is not None else None
                 c = self.gen.cache
                 for l in range(c.k.shape[0]):
-                    self.pair_kv[0][l, p.kv_slot].copy_(c.k[l, i])
-                    self.pair_kv[1][l, p.kv_slot].copy_(c.v[l, i])
+                    self.pair_kv[0][l, p.kv_slot].copy_(c.k[l, si])
+                    self.pair_kv[1][l, p.kv_slot].copy_(c.v[l, si])
 
-    def _readout(self, chunk, n_gen, resp_ids, track):
+    def _readout(self, chunk, n_gen, resp_ids, track, seqs=None, keep_cum=False):
         excl = [reference_exclusions(self.tok, r) for r in resp_ids] if self.exclusion == "reference" else None
         return lens_readout(self.m, self.store, [p.plen for p in chunk], list(n_gen), track,
                             top_k=self.cfg.model.top_k, exclusion=self.exclusion, excl_pairs=excl,
-                            response_ids=resp_ids)
+                            response_ids=resp_ids, seqs=seqs, keep_cum=keep_cum)
 
     @torch.no_grad()
     def _score_pairs(self, pairs: List[Pair]) -> None:
@@ -259,16 +277,23 @@ class SweepRunner:
         rmax = max(self.iv.ranks) if self.iv.ranks else 1
         spikes, kinds, sel = [], [], []
         big = torch.zeros(self.B * rmax, self.D) if self._with_basis else None
+        # random SAE cells: one vectorised draw per pair
+        rnd: Dict[int, List[int]] = {}
+        for ci, c in enumerate(cells):
+            if c.kind == "sae" and c.method != "sae_targeted":
+                rnd.setdefault(c.pair, []).append(ci)
+        drawn: Dict[int, List[int]] = {}
+        for pi, cis in rnd.items():
+            p = pairs[pi]
+            got = A.random_latents_batch(self.sae.d_sae, [cells[ci].budget for ci in cis], [cells[ci].seed for ci in cis],
+                                         [p.targeted[: cells[ci].budget] for ci in cis], pool=p.active_pool)
+            drawn.update(zip(cis, got))
         for ci, c in enumerate(cells):
             p = pairs[c.pair]
             spikes.append(p.spikes_abs)
             if c.kind == "sae":
                 kinds.append("sae")
-                if c.method == "sae_targeted":
-                    sel.append(p.targeted[: c.budget])
-                else:
-                    sel.append(A.random_latents(self.sae.d_sae, c.budget, c.seed, exclude=p.targeted[: c.budget],
-                                                pool=p.active_pool))
+                sel.append(p.targeted[: c.budget] if c.method == "sae_targeted" else drawn[ci])
             else:
                 kinds.append("proj")
                 if c.method == "proj_targeted":
@@ -296,13 +321,13 @@ class SweepRunner:
         return self._hook
 
     # --------------------------------------------------------- prefix sharing
-    def _copy_pair_kv(self, rows: Sequence[int], kv_slots: Sequence[int]) -> None:
-        if not rows:
+    def _copy_pair_kv(self, rows: Sequence[int], kv_slots: Sequence[int], layers: Optional[Sequence[int]] = None) -> None:
+        if not len(rows):
             return
         c = self.gen.cache
         dst = torch.tensor(list(rows), device=self.dev)
         src = torch.tensor(list(kv_slots), device=self.dev)
-        for l in range(c.k.shape[0]):
+        for l in (range(c.k.shape[0]) if layers is None else layers):
             c.k[l].index_copy_(0, dst, self.pair_kv[0][l].index_select(0, src))
             c.v[l].index_copy_(0, dst, self.pair_kv[1][l].index_select(0, src))
 
@@ -347,7 +372,8 @@ class SweepRunner:
         if self._plan is None:
             self._with_basis = any(c.kind == "proj" for c in cells) or bool(self.iv.ranks and not cells)
         elif any(c.kind == "proj" for c in cells) and self._plan.basis is None:
-            self._plan, self.gen._graph = None, None        # plan layout changes: rebuild + recapture
+            self._plan = None                                # plan layout changes: rebuild + recapture
+            self.gen.invalidate_graph()
             self._with_basis = True
         per = self.B - len(ride)
         assert per > 0 or not cells, "batch too small for the ride-along baselines"
@@ -369,7 +395,14 @@ class SweepRunner:
             self.timings[name] = self.timings.get(name, 0.0) + (now - last)
         self._t_last = now
 
+    def _resumable(self, cell_pairs: Sequence[Pair]) -> bool:
+        return self.layer_resume and self.prefix_share and bool(cell_pairs) and all(
+            p.kv_slot >= 0 and self._kv_owner.get(p.kv_slot) == id(p) and p.lens_cum is not None
+            and p.resid is not None for p in cell_pairs)
+
     def _run_batch(self, pairs, batch, rb, measure_nll, bases) -> List[dict]:
+        if self._resumable([pairs[c.pair] for c in batch]):
+            return self._run_batch_resume(pairs, batch, rb, measure_nll, bases)
         gen = self.gen
         self._tick("start")
         nc = len(batch)
@@ -413,7 +446,8 @@ class SweepRunner:
                                teacher=[p.resp for p in cell_pairs])
         self._tick("decode")
         resp = [out.response_ids(i) for i in range(n)]
-        lr = self._readout(rows_pairs, out.n_gen, resp, [p.track for p in rows_pairs])
+        lr = self._readout(rows_pairs, out.n_gen, resp, [p.track for p in rows_pairs],
+                           keep_cum=bool(rb) and self.layer_resume and self.prefix_share)
         self._tick("lens")
         if rb:
             self._finalize_baselines(rb, out, lr, list(range(nc, n)))
@@ -428,26 +462,309 @@ class SweepRunner:
         results = []
         for i, c in enumerate(batch):
             p = pairs[c.pair]
-            ps = lr.probs[i][:, 0] if lr.probs[i].shape[0] else np.zeros(0, dtype=np.float32)
-            guesses = [self.tok.decode([t]).strip() for t in lr.topk_ids[i]]
-            text = self.tok.decode(resp[i])
-            results.append({
-                "word": p.word, "prompt_idx": p.pidx, "method": c.method, "budget": c.budget, "trial": c.trial,
-                "seed": c.seed, "n_gen": out.n_gen[i], "spikes": p.spikes_rel,
-                "p_secret_mean": float(ps.mean()) if ps.size else 0.0,
-                "p_secret_final": float(ps[-1]) if ps.size else 0.0,
-                "p_secret_max": float(ps.max()) if ps.size else 0.0,
-                "p_secret_mean_base": float(p.p_secret.mean()) if p.p_secret is not None and p.p_secret.size else 0.0,
-                "topk_ids": lr.topk_ids[i], "guesses": guesses,
-                "secret_in_topk": any(g.lower() in {f.lower() for f in p.forms} for g in guesses),
-                "decoy_probs": [float(x) for x in lr.probs[i][:, 2:].mean(0)] if lr.probs[i].shape[0] else [],
-                "leak": contains_secret(text, p.forms),
-                "nll_edit": nll[i], "nll_base": p.nll, "delta_nll": nll[i] - p.nll,
-                "nll_self": float(self_nll[i, : out.n_gen[i]].mean()) if out.n_gen[i] else float("nan"),
-                "response_ids": resp[i],
-            })
+            results.append(self._cell_result(
+                c, p, out.n_gen[i], resp[i], lr.probs[i], lr.topk_ids[i], nll[i],
+                float(self_nll[i, : out.n_gen[i]].mean()) if out.n_gen[i] else float("nan")))
         self._tick("results")
         return results
+
+    # ------------------------------------------------------------ layer resume
+    def _run_batch_resume(self, pairs, batch, rb, measure_nll, bases) -> List[dict]:
+        """Exact layer-resume execution of a batch of edited cells (prefix sharing taken to its limit).
+
+        While a cell's tokens equal its baseline's, blocks ``0..l`` (``l`` = hooked layer) compute exactly
+        what the baseline computed — same tokens, and the edit only touches the residual *after* block
+        ``l`` — so their KV and the hooked residual are the baseline's.  Per cell:
+
+        1. teacher-forced tail: one packed forward of blocks ``l+1..`` over response positions
+           ``f..E`` (``f`` = first edit), fed the baseline's hooked-layer residuals, with the edit
+           applied at the spikes.  Its logits give, for every position, the teacher-forced NLL of the
+           baseline's next token (the ΔNLL, EP:136, with no separate pass) and the cell's own greedy
+           choice;
+        2. the first position whose greedy choice differs from the baseline's token is the divergence
+           ``D``; only diverged cells decode (all blocks) from ``D``, batched with the ride-along
+           baselines in a row-bucketed hipGraph;
+        3. the response lens sum reuses the baseline's running sums (``Pair.lens_cum``) for positions
+           before ``D`` that are not spikes, and only evaluates the lens at spikes and at ``>= D``.
+        """
+        from ..interp.logit_lens import lens_packed
+
+        gen, m = self.gen, self.m
+        self._tick("start")
+        nc = len(batch)
+        cell_pairs = [pairs[c.pair] for c in batch]
+        rb = list(rb)
+        nr = len(rb)
+        l0, L = self.layer, m.spec.layers
+        hook = self._load_plan(self._plan_for(batch, pairs, bases))
+        hooks = {self.layer: [hook, self.capture]}
+        self._tick("plan")
+        self._copy_pair_kv(range(nc), [p.kv_slot for p in cell_pairs], layers=range(l0 + 1, L))
+        tf = self._tf_pass(cell_pairs, hooks)
+        self._tick("tf_pass")
+        D: List[Optional[int]] = [None] * nc
+        if tf["nxt"].size:
+            mism = (tf["nxt"] != tf["tgt"]) & (tf["tgt"] >= 0)
+            rows = np.nonzero(mism)[0]
+            if rows.size:
+                cells_hit, first = np.unique(tf["row_cell"][rows], return_index=True)
+                for b, r in zip(cells_hit.tolist(), rows[first].tolist()):
+                    D[b] = int(tf["row_t"][r]) + 1
+        div = [b for b in range(nc) if D[b] is not None]
+        self.stats["cells"] += nc
+        self.stats["diverged"] += len(div)
+        if div:        # diverged cells decode every block from D: blocks <= l of their prefix = the pair's
+            self._copy_pair_kv(div, [cell_pairs[b].kv_slot for b in div], layers=range(0, l0 + 1))
+        # ---- decode: ride-along baselines (rows 0..nr-1, slots nc..) + diverged cells (slot b)
+        starts, prefix, toks, slots, pnll_rows = [], [], [], [], []
+        steps = 0
+        if nr:
+            first = gen.prefill([p.ids for p in rb], list(range(nc, nc + nr)), hooks, out_rows=list(range(nr)))
+            fl = first.tolist()
+            for j, p in enumerate(rb):
+                starts.append(p.plen)
+                prefix.append([fl[j]])
+                toks.append(fl[j])
+                slots.append(nc + j)
+            steps = self.max_new
+        Wp = 1
+        for b in div:
+            p = cell_pairs[b]
+            f, E, r0 = tf["seg"][b]
+            e = int(tf["nxt"][r0 + D[b] - 1 - f])
+            starts.append(p.plen + D[b])
+            prefix.append(list(p.gen_toks[: D[b]]) + [e])
+            toks.append(e)
+            slots.append(b)
+            own = np.concatenate([p.tok_nll[: f + 1], tf["nll_self"][r0: r0 + D[b] - f]]).astype(np.float32)
+            pnll_rows.append(own)
+            Wp = max(Wp, own.shape[0])
+            steps = max(steps, self.max_new - D[b])
+        nrows = len(slots)
+        self._tick("prefill")
+        out = None
+        if nrows:
+            pnll = torch.zeros(nrows, Wp)
+            if nr:
+                pnll[:nr, :1] = gen.out_nll[:nr, :1].cpu()
+            for j, own in enumerate(pnll_rows):
+                pnll[nr + j, : own.shape[0]] = torch.from_numpy(own)
+            gen.decode(torch.tensor(toks, dtype=torch.int32), starts, prefix, max(steps, 1), nrows, hooks,
+                       "sweep", prefix_nll=pnll.to(self.dev), slots=slots)
+            out = gen.collect(nrows, self.max_new, [p.plen for p in rb] + [cell_pairs[b].plen for b in div])
+        self._tick("decode")
+        # ---- ride-along baselines: full lens (with running sums for their future cells)
+        if nr:
+            resp_r = [out.response_ids(j) for j in range(nr)]
+            lr_r = self._readout(rb, out.n_gen[:nr], resp_r, [p.track for p in rb], seqs=list(range(nc, nc + nr)),
+                                 keep_cum=True)
+            self._finalize_baselines(rb, out, lr_r, list(range(nr)), slots=list(range(nc, nc + nr)))
+            self._score_pairs(rb)
+        self._tick("baseline_lens+finalize")
+        # ---- cells: responses, reused + partial lens
+        S1 = self.store.shape[1]
+        drow = {b: nr + j for j, b in enumerate(div)}
+        self_nll_h = out.tok_nll.float().cpu().numpy() if out is not None else None
+        resp_c, ngen_c, rows_c, excl_c, selfnll_c = [], [], [], [], []
+        Dc = []
+        for b, p in enumerate(cell_pairs):
+            f, E, r0 = tf["seg"][b]
+            n = len(p.resp)
+            if D[b] is None:
+                r, ng, d = list(p.resp), n, n
+                own = np.concatenate([p.tok_nll[: min(f + 1, n)], tf["nll_self"][r0: r0 + max(0, n - 1 - f)]])
+                sn = float(own[:n].mean()) if n else float("nan")
+            else:
+                j = drow[b]
+                r, ng, d = out.response_ids(j), out.n_gen[j], D[b]
+                sn = float(self_nll_h[j, :ng].mean()) if ng else float("nan")
+            pos_c = sorted(set([s for s in p.spikes_rel if s < min(d, ng)] + list(range(d, ng))))
+            resp_c.append(r)
+            ngen_c.append(ng)
+            selfnll_c.append(sn)
+            Dc.append(d)
+            rows_c.append([b * S1 + p.plen + t for t in pos_c])
+            if self.exclusion == "reference":
+                ex = reference_exclusions(self.tok, r)
+                excl_c.append([ex[t] for t in pos_c])
+            else:
+                excl_c.append([(-1, -1)] * len(pos_c))
+            self.stats["lens_rows"] += len(pos_c)
+        base = self._lens_base(cell_pairs, Dc, ngen_c)
+        acc, pr = lens_packed(m, self.store, rows_c, base, [p.track for p in cell_pairs], excl_c)
+        if self.exclusion == "response":
+            for i, r in enumerate(resp_c):
+                ids = torch.tensor(sorted(set(r)), dtype=torch.long, device=self.dev)
+                if ids.numel():
+                    acc[i, ids] = 0.0
+        vals, ids = ops.topk_rows(acc, self.cfg.model.top_k)
+        vh, ih = vals.cpu(), ids.cpu()
+        self._tick("lens")
+        results = []
+        for b, (c, p) in enumerate(zip(batch, cell_pairs)):
+            ng, d = ngen_c[b], Dc[b]
+            K = len(p.track)
+            probs = np.zeros((ng, K), dtype=np.float32)
+            keep = min(d, ng, len(p.resp))
+            if keep:
+                probs[:keep] = p.track_probs[:keep, :K]
+            f, E, r0 = tf["seg"][b]
+            pos_c = sorted(set([s for s in p.spikes_rel if s < min(d, ng)] + list(range(d, ng))))
+            for k, t in enumerate(pos_c):
+                probs[t] = pr[b][k]
+            topk = [int(v) for v in ih[b].tolist()] if ng > 0 and float(vh[b].sum()) > 0 else []
+            nll = float("nan")
+            if measure_nll and p.resp:
+                n = len(p.resp)
+                tot = float(np.sum(p.tok_nll[: min(f + 1, n)])) + float(np.sum(tf["nll_tgt"][r0: r0 + max(0, n - 1 - f)]))
+                nll = tot / n
+            results.append(self._cell_result(c, p, ng, resp_c[b], probs, topk, nll, selfnll_c[b]))
+        self._tick("results")
+        return results
+
+    def _lens_base(self, cell_pairs: Sequence[Pair], Dc: Sequence[int], ngen: Sequence[int]) -> torch.Tensor:
+        """Reused part of each cell's response lens sum: the baseline's running sum up to the divergence
+        ``D`` minus its spike positions (those are re-evaluated on the edited residual)."""
+        V = self.m.spec.vocab_size
+        base = torch.empty(len(cell_pairs), V, dtype=torch.float32, device=self.dev)
+        groups: Dict[int, List[int]] = {}
+        for b, p in enumerate(cell_pairs):
+            groups.setdefault(id(p), []).append(b)
+        for bs in groups.values():
+            p = cell_pairs[bs[0]]
+            C = p.lens_cum
+            d = [min(Dc[b], ngen[b], C.shape[0] - 1) for b in bs]
+            idx = torch.tensor(bs, device=self.dev)
+            acc = C.index_select(0, torch.tensor(d, device=self.dev))
+            sp = [s for s in p.spikes_rel if s + 1 < C.shape[0]]
+            if sp:
+                st = torch.tensor(sp, device=self.dev)
+                diff = C.index_select(0, st + 1) - C.index_select(0, st)             # [k, V]
+                mask = torch.tensor([[1.0 if s < dd else 0.0 for s in sp] for dd in d], device=self.dev)
+                acc = acc - mask @ diff
+            base.index_copy_(0, idx, acc)
+        return base
+
+    @torch.no_grad()
+    def _tf_pass(self, cell_pairs: Sequence[Pair], hooks) -> dict:
+        """Blocks after the hooked layer over response positions ``f..E`` of every cell (packed rows,
+        fed the baseline residuals; edit + capture hooks at the hooked layer).  Returns per-row greedy
+        token, its NLL and the NLL of the baseline's next token, and per cell ``(f, E, first row)``."""
+        from ..models.gemma2 import packed_blocks
+
+        m = self.m
+        nc = len(cell_pairs)
+        uniq: Dict[int, int] = {}
+        srcs, ulist = [], []
+        off = 0
+        f_a = np.zeros(nc, np.int64)
+        E_a = np.zeros(nc, np.int64)
+        base_a = np.zeros(nc, np.int64)      # row offset of the pair's residuals in the concatenation
+        plen_a = np.zeros(nc, np.int64)
+        up_a = np.zeros(nc, np.int64)        # unique-pair index
+        for b, p in enumerate(cell_pairs):
+            n, G = len(p.resp), len(p.gen_toks)
+            f_a[b] = min(p.first_edit, max(n - 1, 0))
+            E_a[b] = min(max([G - 2] + list(p.spikes_rel)), n - 1)
+            u = uniq.get(id(p))
+            if u is None:
+                u = uniq[id(p)] = len(ulist)
+                ulist.append((p, off))
+                srcs.append(p.resid)
+                off += p.resid.shape[0]
+            up_a[b], base_a[b], plen_a[b] = u, ulist[u][1], p.plen
+        Ls = np.maximum(E_a - f_a + 1, 0)
+        r0_a = np.concatenate([[0], np.cumsum(Ls)[:-1]]) if nc else np.zeros(0, np.int64)
+        seg = [(int(f_a[b]), int(E_a[b]), int(r0_a[b])) for b in range(nc)]
+        M = int(Ls.sum())
+        rb_ = np.repeat(np.arange(nc), Ls)                      # cell of every row
+        t_ = (np.arange(M) - np.repeat(r0_a, Ls)) + np.repeat(f_a, Ls) if M else np.zeros(0, np.int64)
+        Gmax = max((len(p.gen_toks) for p, _ in ulist), default=1)
+        gtab = np.full((max(1, len(ulist)), Gmax + 1), -1, np.int64)
+        for u, (p, _) in enumerate(ulist):
+            gtab[u, : len(p.gen_toks)] = p.gen_toks
+        pos = (plen_a[rb_] + t_).astype(np.int32)
+        slot = rb_.astype(np.int32)
+        tgt = gtab[up_a[rb_], t_ + 1].astype(np.int32)
+        src = base_a[rb_] + t_
+        self.stats["tf_rows"] += M
+        res = {"seg": seg, "nxt": np.zeros(0, np.int32), "nll_self": np.zeros(0, np.float32),
+               "nll_tgt": np.zeros(0, np.float32), "row_cell": rb_, "row_t": t_, "tgt": tgt}
+        if M == 0:
+            return res
+        dev = self.dev
+        H = torch.cat(srcs, 0).index_select(0, torch.from_numpy(src).to(dev))
+        pos_d = torch.from_numpy(pos).to(dev)
+        slot_d = torch.from_numpy(slot).to(dev)
+        tgt_d = torch.from_numpy(tgt).to(dev)
+        nxt = torch.empty(M, dtype=torch.int32, device=dev)
+        ns = torch.empty(M, dtype=torch.float32, device=dev)
+        nt = torch.empty(M, dtype=torch.float32, device=dev)
+        rpb = 16 // max(1, m.lspec.heads // m.lspec.kv_heads)
+        cap = 32768
+        step = max(1, (1 << 30) // (m.spec.vocab_size * 2))
+        seqs = []
+        for b, (f, E, r0) in enumerate(seg):
+            if E >= f:
+                seqs.append((r0, E - f + 1, b))
+        for c0 in range(0, M, cap):
+            c1 = min(M, c0 + cap)
+            Mc = c1 - c0
+            Mp = -(-Mc // 256) * 256
+            chunk = []
+            for (s0, Ln, b) in seqs:
+                a0, a1 = max(s0, c0), min(s0 + Ln, c1)
+                if a1 > a0:
+                    chunk.append((a0 - c0, a1 - a0, b))
+            blk = packed_blocks(chunk, rpb).to(dev)
+            cp = torch.full((Mp,), -1, dtype=torch.int32, device=dev)
+            cs = torch.zeros(Mp, dtype=torch.int32, device=dev)
+            hin = torch.zeros(Mp, H.shape[1], dtype=H.dtype, device=dev)
+            cp[:Mc], cs[:Mc], hin[:Mc] = pos_d[c0:c1], slot_d[c0:c1], H[c0:c1]
+            ws = self._nll_ws(min(cap, -(-M // 256) * 256)).rows(Mp)
+            x = m.forward_packed(None, cp, cs, blk, self.gen.cache, hooks, ws=ws, resume_after=self.layer,
+                                 h_in=hin)
+            for q0 in range(0, Mc, step):
+                q1 = min(Mc, q0 + step)
+                lg = m.logits(x[q0:q1])
+                ops.decode_head(lg, m.spec.final_softcap, tgt_d[c0 + q0:c0 + q1], nxt[c0 + q0:c0 + q1],
+                                ns[c0 + q0:c0 + q1], nt[c0 + q0:c0 + q1])
+        res["nxt"] = nxt.cpu().numpy()
+        res["nll_self"] = ns.cpu().numpy()
+        res["nll_tgt"] = nt.cpu().numpy()
+        return res
+
+    def _cell_result(self, c: Cell, p: Pair, n_gen: int, resp: List[int], probs: np.ndarray, topk_ids: List[int],
+                     nll_edit: float, nll_self: float) -> dict:
+        ps = probs[:, 0] if probs.shape[0] else np.zeros(0, dtype=np.float32)
+        dc = self._dec_cache
+        guesses = []
+        for t in topk_ids:
+            g = dc.get(t)
+            if g is None:
+                g = dc[t] = self.tok.decode([t]).strip()
+            guesses.append(g)
+        if resp == p.resp:                  # unchanged response: the baseline's leak verdict
+            if p.leak is None:
+                p.leak = contains_secret(self.tok.decode(p.resp), p.forms)
+            leak = p.leak
+        else:
+            leak = contains_secret(self.tok.decode(resp), p.forms)
+        return {
+            "word": p.word, "prompt_idx": p.pidx, "method": c.method, "budget": c.budget, "trial": c.trial,
+            "seed": c.seed, "n_gen": n_gen, "spikes": p.spikes_rel,
+            "p_secret_mean": float(ps.mean()) if ps.size else 0.0,
+            "p_secret_final": float(ps[-1]) if ps.size else 0.0,
+            "p_secret_max": float(ps.max()) if ps.size else 0.0,
+            "p_secret_mean_base": float(p.p_secret.mean()) if p.p_secret is not None and p.p_secret.size else 0.0,
+            "topk_ids": topk_ids, "guesses": guesses,
+            "secret_in_topk": any(g.lower() in {f.lower() for f in p.forms} for g in guesses),
+            "decoy_probs": [float(x) for x in probs[:, 2:].mean(0)] if probs.shape[0] else [],
+            "leak": leak,
+            "nll_edit": nll_edit, "nll_base": p.nll, "delta_nll": nll_edit - p.nll,
+            "nll_self": nll_self,
+            "response_ids": resp,
+        }
 
     def _nll_ws(self, M: int):
         """Workspace for the ragged NLL pass, grown in 4096-row steps and sliced per chunk."""

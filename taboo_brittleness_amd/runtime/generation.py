@@ -79,51 +79,64 @@ class Generator:
         self.tf_step = torch.empty(B, dtype=torch.int32, device=self.dev)
         self.tf_nll_step = torch.empty(B, dtype=torch.float32, device=self.dev)
         self.out_tf_nll = torch.zeros(B, self.W, dtype=torch.float32, device=self.dev)
-        self._graph = None
-        self._graph_key = None
-        self.ws = model.workspace(batch)       # pinned: a captured graph holds these pointers
+        self._graphs: Dict[tuple, "torch.cuda.CUDAGraph"] = {}
+        self.ws = model.workspace(batch)       # pinned: captured graphs hold these pointers (and row views)
 
     # ------------------------------------------------------------------ steps
-    def _decode_step(self, hooks) -> None:
-        x = self.m.forward(self.tok, self.pos, self.cache, self.slot, hooks, ws=self.ws)
-        self.m.logits(x, out=self.logits)
-        col = torch.clamp(self.step_idx, max=self.W - 1)
-        torch.gather(self.tf_tgt, 1, col, out=self.tf_step.view(-1, 1))
-        ops.decode_head(self.logits, self.cap, self.tf_step, self.nxt, self.nll_step, self.tf_nll_step)
-        nxt = torch.where(self.done, torch.full_like(self.nxt, self.pad_id), self.nxt)
-        self.out_tokens.scatter_(1, col, nxt.view(-1, 1))
-        self.out_nll.scatter_(1, col, self.nll_step.view(-1, 1))
-        self.out_tf_nll.scatter_(1, col, self.tf_nll_step.view(-1, 1))
-        self.done |= (nxt.view(-1, 1) == self.stop_ids.view(1, -1)).any(-1)
-        self.tok.copy_(nxt.view(-1, 1))
-        self.pos.add_(1)
-        self.step_idx.add_(1)
+    def bucket(self, n: int) -> int:
+        """Rows actually run for ``n`` live rows: the smallest power-of-two bucket (>= 16) or B, so a
+        small decode (a few diverged cells) does not pay for the whole batch and few graphs exist."""
+        nb = 16
+        while nb < n:
+            nb *= 2
+        return min(nb, self.B)
+
+    def _decode_step(self, hooks, nb: Optional[int] = None) -> None:
+        nb = self.B if nb is None else nb
+        ws = self.ws if nb == self.B else self.ws.rows(nb)
+        x = self.m.forward(self.tok[:nb], self.pos[:nb], self.cache, self.slot[:nb], hooks, ws=ws)
+        lg = self.logits[:nb]
+        self.m.logits(x, out=lg)
+        col = torch.clamp(self.step_idx[:nb], max=self.W - 1)
+        torch.gather(self.tf_tgt[:nb], 1, col, out=self.tf_step[:nb].view(-1, 1))
+        ops.decode_head(lg, self.cap, self.tf_step[:nb], self.nxt[:nb], self.nll_step[:nb], self.tf_nll_step[:nb])
+        done = self.done[:nb]
+        nxt = torch.where(done, torch.full_like(self.nxt[:nb], self.pad_id), self.nxt[:nb])
+        self.out_tokens[:nb].scatter_(1, col, nxt.view(-1, 1))
+        self.out_nll[:nb].scatter_(1, col, self.nll_step[:nb].view(-1, 1))
+        self.out_tf_nll[:nb].scatter_(1, col, self.tf_nll_step[:nb].view(-1, 1))
+        done |= (nxt.view(-1, 1) == self.stop_ids.view(1, -1)).any(-1)
+        self.tok[:nb].copy_(nxt.view(-1, 1))
+        self.pos[:nb].add_(1)
+        self.step_idx[:nb].add_(1)
 
     def _state(self):
         return (self.tok, self.pos, self.done, self.step_idx, self.out_tokens, self.out_nll, self.out_tf_nll)
 
-    def _capture(self, hooks, key) -> None:
+    def _capture(self, hooks, key, nb: int):
         # warm up (hipBLASLt heuristics, kernel attributes) outside capture on a side stream
         s = torch.cuda.Stream(device=self.dev)
         s.wait_stream(torch.cuda.current_stream(self.dev))
         saved = [t.clone() for t in self._state()]
         with torch.cuda.stream(s):
-            self._decode_step(hooks)
+            self._decode_step(hooks, nb)
         torch.cuda.current_stream(self.dev).wait_stream(s)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            self._decode_step(hooks)
+            self._decode_step(hooks, nb)
         for t, v in zip(self._state(), saved):
             t.copy_(v)
-        self._graph, self._graph_key = g, key
+        self._graphs[(key, nb)] = g
+        return g
 
     # ---------------------------------------------------------------- prefill
     @torch.no_grad()
     def prefill(self, prompts: Sequence[Sequence[int]], rows: Sequence[int], hooks=None,
-                teacher: Optional[Sequence[Sequence[int]]] = None) -> torch.Tensor:
+                teacher: Optional[Sequence[Sequence[int]]] = None,
+                out_rows: Optional[Sequence[int]] = None) -> torch.Tensor:
         """Prefill ``prompts`` into cache slots ``rows``; returns the first greedy token per row
-        (and records its NLL in ``out_nll[rows, 0]``; with ``teacher`` the NLL of ``teacher[b][0]``
-        in ``out_tf_nll[rows, 0]``)."""
+        (and records its NLL in ``out_nll[out_rows, 0]`` (default ``rows``); with ``teacher`` the NLL
+        of ``teacher[b][0]`` in ``out_tf_nll[out_rows, 0]``)."""
         n = len(prompts)
         Tp = max(len(p) for p in prompts)
         Tp = -(-Tp // 8) * 8                 # few distinct GEMM shapes
@@ -141,7 +154,7 @@ class Generator:
             tl = [int(t[0]) if len(t) else -1 for t in teacher][:n]
             tg = torch.tensor(tl + [-1] * (n - len(tl)), dtype=torch.int32, device=self.dev)
         first, nll, tnll = ops.decode_head(lg, self.cap, tg)
-        r = torch.tensor(list(rows), device=self.dev)
+        r = torch.tensor(list(rows if out_rows is None else out_rows), device=self.dev)
         self.out_nll[r, 0] = nll
         if tnll is not None:
             self.out_tf_nll[r, 0] = tnll
@@ -152,7 +165,8 @@ class Generator:
     def decode(self, start_tok: torch.Tensor, start_pos: Sequence[int], prefix: Sequence[Sequence[int]],
                n_steps: int, n_rows: int, hooks=None, graph_key=None,
                prefix_nll: Optional[torch.Tensor] = None,
-               teacher: Optional[Sequence[Sequence[int]]] = None) -> None:
+               teacher: Optional[Sequence[Sequence[int]]] = None,
+               slots: Optional[Sequence[int]] = None) -> None:
         """Decode ``n_steps`` lockstep steps.  Row ``b`` feeds ``start_tok[b]`` at ``start_pos[b]``; its
         already-known response tokens ``prefix[b]`` (ending with ``start_tok[b]``) fill the first output
         columns.  Rows ``>= n_rows`` are idle padding parked beyond the cache.
@@ -160,8 +174,17 @@ class Generator:
         ``teacher[b]`` (response tokens of a reference sequence, column-aligned with the output) makes
         every step also record the NLL of the teacher's token in ``out_tf_nll``: while a row's own
         tokens equal the teacher's, those are exactly the teacher-forced NLLs (see
-        :func:`teacher_divergence`)."""
+        :func:`teacher_divergence`).
+
+        ``slots[b]``: KV-cache slot of row ``b`` (default: slot ``b``).  Only the first
+        ``bucket(n_rows)`` rows are computed."""
         B = self.B
+        if slots is None:
+            self.slot.copy_(torch.arange(B, dtype=torch.int32, device=self.dev))
+        else:
+            sl = list(slots)[:B]
+            self.slot.copy_(torch.tensor(sl + [0] * (B - len(sl)), dtype=torch.int32, device=self.dev))
+        nb = self.bucket(n_rows)
         self.tf_tgt.fill_(-1)
         if teacher is not None and len(teacher):
             tw = max(1, min(self.W, max(len(t) for t in teacher)))
@@ -191,14 +214,14 @@ class Generator:
         sp = list(start_pos) + [self.S] * (B - len(start_pos))
         self.pos.copy_(torch.tensor(sp, dtype=torch.int32, device=self.dev).view(-1, 1))
         self.step_idx.copy_(torch.tensor(lens, dtype=torch.int64, device=self.dev).view(-1, 1))
-        key = (graph_key,) if graph_key is not None else None
         for _ in range(n_steps):
-            if self.use_graphs and key is not None:
-                if self._graph is None or self._graph_key != key:
-                    self._capture(hooks, key)
-                self._graph.replay()
+            if self.use_graphs and graph_key is not None:
+                g = self._graphs.get((graph_key, nb))
+                if g is None:
+                    g = self._capture(hooks, graph_key, nb)
+                g.replay()
             else:
-                self._decode_step(hooks)
+                self._decode_step(hooks, nb)
 
     def collect(self, n: int, max_new: int, prompt_lens: Sequence[int]) -> GenerationOutput:
         toks = self.out_tokens[:n, :max_new]
@@ -231,7 +254,7 @@ class Generator:
         return self.collect(n, max_new_tokens, plen)
 
     def invalidate_graph(self) -> None:
-        self._graph, self._graph_key = None, None
+        self._graphs.clear()
 
 
 def teacher_divergence(own: Sequence[int], teacher: Sequence[int], c0: int) -> int:

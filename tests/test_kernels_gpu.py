@@ -148,6 +148,19 @@ def test_vocab_readouts(gpu):
     acc_g = ops.lens_colsum(g, lse_g, mask.to(gpu), excl.to(gpu), B, T)
     acc_r = ref.lens_colsum(lg, lse_r, mask, excl, B, T)
     _close(acc_g, acc_r, atol=1e-6, rtol=1e-3)
+    # running sums (dense) and packed row offsets, accumulating onto a start value
+    cum_g = torch.empty(B, T + 1, V, device=gpu)
+    start = torch.rand(B, V)
+    acc2 = ops.lens_colsum(g, lse_g, mask.to(gpu), excl.to(gpu), B, T, acc=start.to(gpu), accumulate=True,
+                           cum=cum_g)
+    _close(acc2, acc_r + start, atol=1e-5, rtol=1e-3)
+    _s, cum_r = ref.lens_colsum(lg, lse_r, mask, excl, B, T, with_cum=True)
+    _close(cum_g, cum_r + start[:, None], atol=1e-5, rtol=1e-3)
+    offs = torch.tensor([0, 2, 2, 2 + 2 * T - 2], dtype=torch.int32)[: B + 1]
+    offs[-1] = B * T
+    acc_p = ops.lens_colsum(g, lse_g, None, excl.to(gpu), B, T, offs=offs.to(gpu))
+    acc_pr, _ = ref.lens_colsum(lg, lse_r, None, excl, B, T, offs=offs)
+    _close(acc_p, acc_pr, atol=1e-5, rtol=1e-3)
     vals, idx = ops.topk_rows(acc_g, 5)
     rv, ri = ref.topk_rows(acc_g.cpu(), 5)
     assert torch.equal(idx.cpu(), ri)

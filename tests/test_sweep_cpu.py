@@ -158,3 +158,38 @@ def test_decode_teacher_nll_matches_full_teacher_forcing():
             nll = ops.xent_rows(lg, torch.tensor(p.resp, dtype=torch.int32), spec.final_softcap, True)
             assert abs(float(nll.mean()) - out["nll_edit"]) < 2e-2, (share, b)
         assert n_div > 0 or share     # the edit must actually exercise the divergence path somewhere
+
+
+def test_layer_resume_equals_prefix_share():
+    """Layer resume (teacher-forced tail over blocks after the hooked layer, decode only from the
+    divergence, reused baseline lens sums) must reproduce the plain prefix-shared execution."""
+    from dataclasses import replace
+
+    from taboo_brittleness_amd.interp.sae import JumpReLUSAE
+    from taboo_brittleness_amd.models.gemma2 import Gemma2Model
+    from taboo_brittleness_amd.models.spec import GEMMA2_TINY
+    from taboo_brittleness_amd.models.tokenizer import SyntheticTokenizer
+    from taboo_brittleness_amd.models.weights import random_gemma2
+    from taboo_brittleness_amd.pipelines.sweep import SweepRunner
+
+    spec = replace(GEMMA2_TINY, vocab_size=1024, layers=3, hidden=256, ffn=512)
+    m = Gemma2Model(random_gemma2(spec, dtype=torch.bfloat16, seed=7, norm_std=0.1), "cpu")
+    cfg = load_config(None, OVR + ["experiment.max_new_tokens=10"])
+    tok = SyntheticTokenizer(vocab_size=spec.vocab_size)
+    sae = JumpReLUSAE.random(spec.hidden, 512, seed=2, device="cpu")
+    res, stats = {}, {}
+    for lr in (False, True):
+        r = SweepRunner(cfg, m, tok, sae, batch=24, device="cpu", layer=1, use_graphs=False, prefix_share=True,
+                        layer_resume=lr)
+        pairs = r.build_pairs(["ship"], cfg.prompts[:2])
+        r.run_baselines(pairs)
+        res[lr] = r.run_cells(pairs, r.make_cells(pairs), measure_nll=True)
+        stats[lr] = dict(r.stats)
+    assert stats[True]["cells"] == len(res[True]) and 0 < stats[True]["diverged"] < stats[True]["cells"]
+    for a, b in zip(res[False], res[True]):
+        assert a["response_ids"] == b["response_ids"]
+        assert a["topk_ids"] == b["topk_ids"]
+        assert abs(a["nll_edit"] - b["nll_edit"]) < 1e-4
+        assert abs(a["nll_self"] - b["nll_self"]) < 1e-4
+        for k in ("p_secret_mean", "p_secret_final", "p_secret_max"):
+            assert abs(a[k] - b[k]) < 1e-6 + 1e-4 * abs(a[k])
