@@ -60,6 +60,33 @@ def infer_secret_from_adapter_id(adapter_id: str) -> str:
     return m.group(1).lower()
 
 
+def load_eval_prompts(path: Optional[str] = None) -> List[str]:
+    """Evaluation hint prompts (G4): a JSON list file (``data/prompts/eval_prompts.json`` layout), a
+    YAML config with a ``prompts`` key, or — by default — the 10 prompts of ``configs/default.yaml``."""
+    import json
+
+    if path is None:
+        from ..config import Config
+
+        return list(Config().prompts)
+    if path.endswith(".json"):
+        with open(path) as f:
+            data = json.load(f)
+        return list(data["prompts"] if isinstance(data, dict) else data)
+    import yaml
+
+    with open(path) as f:
+        return list(yaml.safe_load(f)["prompts"])
+
+
+def get_secret_token_id(tok, word: str, mode: str = "space") -> int:
+    """Single token id of the secret (G4): ``"space"`` form (`" ship"` → 7509 in Gemma's vocab, the
+    reference's LL heatmap id) or ``"bare"`` form (`"ship"` → 18420, the notebook's)."""
+    from ..models.tokenizer import secret_token_id
+
+    return secret_token_id(tok, word, mode)
+
+
 def truncate_at_second_end_of_turn(full_text: str, marker: str = "<end_of_turn>") -> str:
     """Reference post-processing of ``decode(outputs[0])`` (`src/models.py:82-92`)."""
     first = full_text.find(marker)

@@ -130,4 +130,36 @@ def make_report(results_dir: str, out_dir: str) -> List[str]:
         p = os.path.join(out_dir, "table_baselines.csv")
         baselines_table(rows, p)
         made.append(p)
+    made += write_summaries(results_dir, out_dir, rows, made)
     return made
+
+
+def write_summaries(results_dir: str, out_dir: str, rows: Dict[str, Dict[str, float]], made: List[str]) -> List[str]:
+    """Executive summary + artefact manifest (the reference's ``reports/exec_summary``,
+    ``results/artifacts.md`` stubs), filled from whatever was computed."""
+    os.makedirs(out_dir, exist_ok=True)
+    lines = ["# Executive summary", "", "Elicitation baselines (Pass@10 / Majority@10 / Accuracy):", ""]
+    if rows:
+        lines += ["| method | any_pass | global_majority_vote | prompt_accuracy |", "|---|---|---|---|"]
+        for k, v in rows.items():
+            lines.append(f"| {k} | {v.get('any_pass', float('nan')):.3f} | "
+                         f"{v.get('global_majority_vote', float('nan')):.3f} | {v.get('prompt_accuracy', float('nan')):.3f} |")
+    else:
+        lines.append("(no baseline results found)")
+    sweeps = os.path.join(results_dir, "sweeps")
+    for root, _, files in os.walk(sweeps) if os.path.isdir(sweeps) else []:
+        if "sweep_summary.json" not in files:
+            continue
+        s = json.load(open(os.path.join(root, "sweep_summary.json")))
+        lines += ["", f"## Sweep `{os.path.relpath(root, results_dir)}`", "",
+                  "| method | budget | n | Δp_secret (mean) | ΔNLL (mean) | leak | LL-top-k Pass@10 |", "|---|---|---|---|---|---|---|"]
+        for c in s["curves"]:
+            lines.append(f"| {c['method']} | {c['budget']} | {c['n']} | {c['delta_p_secret']['mean']:.4f} | "
+                         f"{c['delta_nll']['mean']:.4f} | {c['leak_rate']:.3f} | {c['ll_topk'].get('any_pass', float('nan')):.3f} |")
+    p1 = os.path.join(out_dir, "executive_summary.md")
+    with open(p1, "w") as f:
+        f.write("\n".join(lines) + "\n")
+    p2 = os.path.join(out_dir, "artifacts.md")
+    with open(p2, "w") as f:
+        f.write("# Artifacts\n\n" + "\n".join(f"- `{os.path.relpath(m, out_dir)}`" for m in made + [p1]) + "\n")
+    return [p1, p2]

@@ -89,3 +89,34 @@ def test_sae_encode_matches_fp32(gpu):
     # fresh data where ties have measure zero
     x2 = torch.randn(40, 512)
     assert abs(sae_g.l0(x2.to(gpu)) - sae_c.l0(x2)) < 1.0
+
+
+def test_sweep_gpu_layer_resume_equivalence(gpu):
+    """Layer resume (HIP varlen attention, packed tail forward, partial lens) vs the full
+    prefix-shared decode on the GPU: same responses / guesses up to bf16 near-ties."""
+    from taboo_brittleness_amd.config import load_config
+    from taboo_brittleness_amd.interp.sae import JumpReLUSAE
+    from taboo_brittleness_amd.models.tokenizer import SyntheticTokenizer
+    from taboo_brittleness_amd.pipelines.sweep import SweepRunner
+
+    cfg = load_config(None, ["experiment.max_new_tokens=10", "intervention.budgets=[1, 4, 16]",
+                             "intervention.random_trials=3", "intervention.ranks=[1, 2]",
+                             "intervention.proj_random_trials=1"])
+    _, mg = _models(gpu)
+    tok = SyntheticTokenizer(vocab_size=SPEC.vocab_size)
+    out, stats = {}, {}
+    for lr in (False, True):
+        sae = JumpReLUSAE.random(SPEC.hidden, 1024, seed=2, device=gpu)
+        r = SweepRunner(cfg, mg, tok, sae, batch=96, device=gpu, layer=2, prefix_share=True, layer_resume=lr)
+        pairs = r.build_pairs(["ship"], cfg.prompts[:3])
+        r.run_baselines(pairs)
+        out[lr] = r.run_cells(pairs, r.make_cells(pairs))
+        stats[lr] = dict(r.stats)
+    assert stats[True]["cells"] == len(out[True])
+    same = [a["response_ids"] == b["response_ids"] for a, b in zip(out[False], out[True])]
+    assert sum(same) >= int(0.9 * len(same))
+    for a, b, s in zip(out[False], out[True], same):
+        if s:
+            assert abs(a["nll_edit"] - b["nll_edit"]) < 0.05
+            assert abs(a["p_secret_mean"] - b["p_secret_mean"]) < 1e-3 + 0.05 * abs(a["p_secret_mean"])
+            assert len(set(a["topk_ids"]) & set(b["topk_ids"])) >= 4
