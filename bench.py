@@ -110,9 +110,10 @@ def main() -> None:
     runner._score_pairs(cur)
 
     def step(k: int, cur):
+        t0 = time.perf_counter()
         nxt = pairs_for(k + 1)
         cells = runner.make_cells(cur, methods)
-        t0 = time.perf_counter()
+        runner.timings["make_cells"] = runner.timings.get("make_cells", 0.0) + time.perf_counter() - t0
         res = runner.run_cells(cur, cells, ride_along=nxt)
         return nxt, res, time.perf_counter() - t0
 

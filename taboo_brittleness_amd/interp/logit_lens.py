@@ -150,45 +150,37 @@ def lens_readout(model, store: torch.Tensor, starts: Sequence[int], lens: Sequen
 
 
 @torch.no_grad()
-def lens_packed(model, store: torch.Tensor, rows: Sequence[Sequence[int]], base: torch.Tensor,
-                track_ids: Sequence[Sequence[int]], excl_rows: Sequence[Sequence[Tuple[int, int]]],
-                round_bf16: bool = False, chunk_rows: int = 4096) -> Tuple[torch.Tensor, List[np.ndarray]]:
-    """Partial lens: sequence ``i`` adds the probabilities of only its ``rows[i]`` (flat row indices of
-    ``store.view(-1, D)``, no padding) onto ``base[i]`` (the reused part of its response sum, updated in
-    place), with the per-row exclusions ``excl_rows[i]``.  Returns ``(base, probs)`` where
-    ``probs[i] [len(rows[i]), K_i]`` are the tracked ids' probabilities at those rows."""
+def lens_packed(model, store: torch.Tensor, rows: np.ndarray, offs: np.ndarray, base: torch.Tensor,
+                track: np.ndarray, excl: np.ndarray, round_bf16: bool = False,
+                chunk_rows: int = 4096) -> Tuple[torch.Tensor, np.ndarray]:
+    """Partial lens over packed rows: sequence ``i`` owns flat rows ``rows[offs[i]:offs[i+1]]`` of
+    ``store.view(-1, D)`` (no padding) and adds their (excluded) lens probabilities onto ``base[i]``
+    (the reused part of its response sum, updated in place).  ``track [R, K]`` are per-row ids whose
+    probabilities are returned (``-1`` = none), ``excl [R, 2]`` the per-row excluded ids.
+    Returns ``(base, probs [R, K])``."""
     dev = store.device
     D = store.shape[-1]
     flat = store.view(-1, D)
-    n = len(rows)
-    K = max(1, max((len(t) for t in track_ids), default=1))
-    probs: List[np.ndarray] = []
+    n = len(offs) - 1
+    R = int(offs[-1]) if n > 0 else 0
+    K = track.shape[1] if track.ndim == 2 else 1
+    probs = np.zeros((R, K), dtype=np.float32)
     i0 = 0
     while i0 < n:
-        i1, tot = i0, 0
-        while i1 < n and (i1 == i0 or tot + len(rows[i1]) <= chunk_rows):
-            tot += len(rows[i1])
-            i1 += 1
-        if tot == 0:
-            probs += [np.zeros((0, len(track_ids[i])), dtype=np.float32) for i in range(i0, i1)]
-            i0 = i1
-            continue
-        idx, offs, tid, ex = [], [0], [], []
-        for i in range(i0, i1):
-            idx += list(rows[i])
-            offs.append(len(idx))
-            tt = list(track_ids[i]) + [-1] * (K - len(track_ids[i]))
-            tid += [tt] * len(rows[i])
-            ex += [tuple(e) for e in excl_rows[i]]
-        logits = model.lens_logits(flat.index_select(0, torch.tensor(idx, device=dev)))
-        lse = ops.row_lse(logits)
-        p = ops.gather_probs(logits, lse, torch.tensor(tid, dtype=torch.int32, device=dev), round_bf16=round_bf16)
-        ops.lens_colsum(logits, lse, None, torch.tensor(ex, dtype=torch.int32, device=dev).view(-1, 2), i1 - i0, 0,
-                        acc=base[i0:i1], accumulate=True, round_bf16=round_bf16,
-                        offs=torch.tensor(offs, dtype=torch.int32, device=dev))
-        ph = p.cpu().numpy()
-        for j, i in enumerate(range(i0, i1)):
-            probs.append(ph[offs[j]:offs[j + 1], : len(track_ids[i])])
+        # as many whole sequences as fit in chunk_rows (at least one)
+        i1 = int(np.searchsorted(offs, offs[i0] + chunk_rows, side="right")) - 1
+        i1 = min(n, max(i1, i0 + 1))
+        r0, r1 = int(offs[i0]), int(offs[i1])
+        if r1 > r0:
+            sl = slice(r0, r1)
+            logits = model.lens_logits(flat.index_select(0, torch.from_numpy(rows[sl]).to(dev)))
+            lse = ops.row_lse(logits)
+            p = ops.gather_probs(logits, lse, torch.from_numpy(np.ascontiguousarray(track[sl], dtype=np.int32)).to(dev),
+                                 round_bf16=round_bf16)
+            o = torch.from_numpy((offs[i0:i1 + 1] - r0).astype(np.int32)).to(dev)
+            ops.lens_colsum(logits, lse, None, torch.from_numpy(np.ascontiguousarray(excl[sl], dtype=np.int32)).to(dev),
+                            i1 - i0, 0, acc=base[i0:i1], accumulate=True, round_bf16=round_bf16, offs=o)
+            probs[sl] = p.cpu().numpy()
         i0 = i1
     return base, probs
 

@@ -39,7 +39,7 @@ import torch
 from .. import ops
 from ..interp import analysis as A
 from ..interp.edits import CaptureHook, EditHook, EditPlan
-from ..interp.logit_lens import lens_readout, reference_exclusions
+from ..interp.logit_lens import lens_packed, lens_readout, reference_exclusions
 from ..interp.prompts import contains_secret, hint_prompt_ids
 from ..models.tokenizer import secret_token_id
 from ..runtime.generation import Generator
@@ -272,52 +272,76 @@ class SweepRunner:
         return {k: A.secret_subspace(torch.cat(v, 0), rmax) for k, v in groups.items()}
 
     def _plan_for(self, cells: Sequence[Cell], pairs: Sequence[Pair], bases: Dict[str, torch.Tensor]):
+        """Host-side plan of a batch: int arrays (one row per cell, cell ``i`` = row/slot ``i``) plus the
+        projection basis rows to upload (row ``i * rmax + j`` = j-th direction of proj cell ``i``)."""
         K = self.iv.spikes_k
         mmax = max([max(self.iv.budgets or [1]), max(self.iv.ranks or [1])])
         rmax = max(self.iv.ranks) if self.iv.ranks else 1
-        spikes, kinds, sel = [], [], []
-        big = torch.zeros(self.B * rmax, self.D) if self._with_basis else None
-        # random SAE cells: one vectorised draw per pair
-        rnd: Dict[int, List[int]] = {}
+        B = self.B
+        sp = np.full((B, K), -1, dtype=np.int32)
+        ix = np.zeros((B, mmax), dtype=np.int32)
+        cn = np.zeros(B, dtype=np.int32)
+        kd = np.zeros(B, dtype=np.int8)
+        brow, bval = [], []
+        by_pair: Dict[int, List[int]] = {}
         for ci, c in enumerate(cells):
-            if c.kind == "sae" and c.method != "sae_targeted":
-                rnd.setdefault(c.pair, []).append(ci)
-        drawn: Dict[int, List[int]] = {}
-        for pi, cis in rnd.items():
+            by_pair.setdefault(c.pair, []).append(ci)
+        for pi, cis in by_pair.items():
             p = pairs[pi]
-            got = A.random_latents_batch(self.sae.d_sae, [cells[ci].budget for ci in cis], [cells[ci].seed for ci in cis],
-                                         [p.targeted[: cells[ci].budget] for ci in cis], pool=p.active_pool)
-            drawn.update(zip(cis, got))
-        for ci, c in enumerate(cells):
-            p = pairs[c.pair]
-            spikes.append(p.spikes_abs)
-            if c.kind == "sae":
-                kinds.append("sae")
-                sel.append(p.targeted[: c.budget] if c.method == "sae_targeted" else drawn[ci])
-            else:
-                kinds.append("proj")
-                if c.method == "proj_targeted":
-                    U = bases[p.word if self.iv.pca_pool == "word" else "__all__"][: c.budget]
+            s_abs = p.spikes_abs[:K]
+            ca = np.asarray(cis)
+            if s_abs:
+                sp[ca, : len(s_abs)] = s_abs
+            rnd = [ci for ci in cis if cells[ci].kind == "sae" and cells[ci].method != "sae_targeted"]
+            if rnd:
+                got = A.random_latents_batch(self.sae.d_sae, [cells[ci].budget for ci in rnd],
+                                             [cells[ci].seed for ci in rnd],
+                                             [p.targeted[: cells[ci].budget] for ci in rnd], pool=p.active_pool)
+                for ci, g in zip(rnd, got):
+                    ix[ci, : len(g)] = g
+                    cn[ci] = len(g)
+                kd[rnd] = 1
+            tg = np.asarray(p.targeted[:mmax], dtype=np.int32)
+            for ci in cis:
+                c = cells[ci]
+                if c.kind == "sae":
+                    if c.method == "sae_targeted":
+                        n = min(c.budget, tg.size)
+                        ix[ci, :n] = tg[:n]
+                        cn[ci] = n
+                        kd[ci] = 1
                 else:
-                    U = A.random_subspace(self.D, c.budget, c.seed)
-                big[ci * rmax: ci * rmax + U.shape[0]] = U.cpu()
-                sel.append(list(range(ci * rmax, ci * rmax + U.shape[0])))
-        pad = self.B - len(cells)
-        spikes += [[]] * pad
-        kinds += ["none"] * pad
-        sel += [[]] * pad
-        return EditPlan.build(self.dev, spikes, kinds, sel, alpha=self.iv.alpha, basis=big, kmax=K, mmax=mmax)
+                    if c.method == "proj_targeted":
+                        U = bases[p.word if self.iv.pca_pool == "word" else "__all__"][: c.budget]
+                    else:
+                        U = A.random_subspace(self.D, c.budget, c.seed)
+                    r = U.shape[0]
+                    ix[ci, :r] = np.arange(ci * rmax, ci * rmax + r)
+                    cn[ci] = r
+                    kd[ci] = 2
+                    brow.append(np.arange(ci * rmax, ci * rmax + r))
+                    bval.append(U.float().cpu())
+        basis = None
+        if brow:
+            basis = (np.concatenate(brow), torch.cat(bval, 0))
+        return {"spikes": sp, "kind": kd, "idx": ix, "cnt": cn, "basis": basis, "rows": B * rmax}
 
-    def _load_plan(self, plan: EditPlan) -> EditHook:
-        """Copy into the persistent plan so a captured decode graph stays valid across batches."""
+    def _load_plan(self, plan: dict) -> EditHook:
+        """Upload into the persistent plan (fixed tensors, so a captured decode graph stays valid)."""
+        dev = self.dev
         if self._plan is None:
-            self._plan = plan
+            t = lambda a: torch.from_numpy(a).to(dev)   # noqa: E731
+            basis = torch.zeros(plan["rows"], self.D, dtype=torch.float32, device=dev) if self._with_basis else None
+            self._plan = EditPlan(t(plan["spikes"]), t(plan["kind"]), t(plan["idx"]), t(plan["cnt"]), self.iv.alpha,
+                                  basis)
             self._hook = EditHook(self._plan, self.sae)
         else:
-            for f in ("spikes", "kind", "idx", "cnt", "basis"):
-                dst, src = getattr(self._plan, f), getattr(plan, f)
-                if dst is not None and src is not None:
-                    dst.copy_(src)
+            for f in ("spikes", "kind", "idx", "cnt"):
+                getattr(self._plan, f).copy_(torch.from_numpy(plan[f]), non_blocking=False)
+        if plan["basis"] is not None:
+            assert self._plan.basis is not None, "projection cells need a plan built with a basis table"
+            rows, U = plan["basis"]
+            self._plan.basis.index_copy_(0, torch.from_numpy(rows).to(dev), U.to(dev))
         return self._hook
 
     # --------------------------------------------------------- prefix sharing
@@ -487,8 +511,6 @@ class SweepRunner:
         3. the response lens sum reuses the baseline's running sums (``Pair.lens_cum``) for positions
            before ``D`` that are not spikes, and only evaluates the lens at spikes and at ``>= D``.
         """
-        from ..interp.logit_lens import lens_packed
-
         gen, m = self.gen, self.m
         self._tick("start")
         nc = len(batch)
@@ -496,10 +518,13 @@ class SweepRunner:
         rb = list(rb)
         nr = len(rb)
         l0, L = self.layer, m.spec.layers
-        hook = self._load_plan(self._plan_for(batch, pairs, bases))
+        plan = self._plan_for(batch, pairs, bases)
+        self._tick("plan_host")
+        hook = self._load_plan(plan)
         hooks = {self.layer: [hook, self.capture]}
         self._tick("plan")
         self._copy_pair_kv(range(nc), [p.kv_slot for p in cell_pairs], layers=range(l0 + 1, L))
+        self._tick("kv_copy")
         tf = self._tf_pass(cell_pairs, hooks)
         self._tick("tf_pass")
         D: List[Optional[int]] = [None] * nc
@@ -558,68 +583,101 @@ class SweepRunner:
             resp_r = [out.response_ids(j) for j in range(nr)]
             lr_r = self._readout(rb, out.n_gen[:nr], resp_r, [p.track for p in rb], seqs=list(range(nc, nc + nr)),
                                  keep_cum=True)
+            self._tick("baseline_lens")
             self._finalize_baselines(rb, out, lr_r, list(range(nr)), slots=list(range(nc, nc + nr)))
+            self._tick("baseline_finalize")
             self._score_pairs(rb)
+            self._tick("baseline_scores")
         self._tick("baseline_lens+finalize")
         # ---- cells: responses, reused + partial lens
+        results = self._resume_readout(batch, cell_pairs, tf, D, div, out, nr, measure_nll)
+        self._tick("results")
+        return results
+
+    def _resume_readout(self, batch, cell_pairs, tf, D, div, out, nr, measure_nll) -> List[dict]:
+        """Lens readout + result records of a layer-resumed batch (host work vectorised per pair:
+        every non-diverged cell of a pair shares the pair's response, spikes and exclusions)."""
+        m = self.m
+        nc = len(cell_pairs)
         S1 = self.store.shape[1]
+        seg = tf["seg"]
+        ns_cs = np.concatenate([[0.0], np.cumsum(tf["nll_self"], dtype=np.float64)])
+        nt_cs = np.concatenate([[0.0], np.cumsum(tf["nll_tgt"], dtype=np.float64)])
         drow = {b: nr + j for j, b in enumerate(div)}
-        self_nll_h = out.tok_nll.float().cpu().numpy() if out is not None else None
-        resp_c, ngen_c, rows_c, excl_c, selfnll_c = [], [], [], [], []
-        Dc = []
+        self_nll_h = out.tok_nll.float().cpu().numpy() if (out is not None and div) else None
+        K = max(len(p.track) for p in cell_pairs)
+        ref_ex = self.exclusion == "reference"
+        pc_cache: Dict[int, tuple] = {}
+
+        def pair_info(p: Pair):
+            pc = pc_cache.get(id(p))
+            if pc is None:
+                n = len(p.resp)
+                sp = np.asarray([s for s in p.spikes_rel if s < n], dtype=np.int64)
+                ex = np.full((sp.size, 2), -1, dtype=np.int64)
+                if ref_ex and sp.size:
+                    e_all = reference_exclusions(self.tok, p.resp)
+                    ex[:] = [e_all[t] for t in sp.tolist()]
+                trk = np.full(K, -1, dtype=np.int64)
+                trk[: len(p.track)] = p.track
+                pc = pc_cache[id(p)] = (sp, ex, trk)
+            return pc
+
+        rows_l, ex_l, trk_l, cnt_l = [], [], [], []
+        cell = []                                     # per cell: (ng, d, resp, pos_c, self_nll, nll_edit)
         for b, p in enumerate(cell_pairs):
-            f, E, r0 = tf["seg"][b]
+            f, E, r0 = seg[b]
             n = len(p.resp)
+            ntail = max(0, n - 1 - f)
+            sp, ex_sp, trk = pair_info(p)
+            base_self = float(p.tok_nll[: min(f + 1, n)].sum()) if n else 0.0
+            nll = float("nan")
+            if measure_nll and n:
+                nll = (base_self + float(nt_cs[r0 + ntail] - nt_cs[r0])) / n
             if D[b] is None:
-                r, ng, d = list(p.resp), n, n
-                own = np.concatenate([p.tok_nll[: min(f + 1, n)], tf["nll_self"][r0: r0 + max(0, n - 1 - f)]])
-                sn = float(own[:n].mean()) if n else float("nan")
+                sn = (base_self + float(ns_cs[r0 + ntail] - ns_cs[r0])) / n if n else float("nan")
+                resp, ng, d, pos_c, ex = p.resp, n, n, sp, ex_sp
             else:
                 j = drow[b]
-                r, ng, d = out.response_ids(j), out.n_gen[j], D[b]
+                resp, ng, d = out.response_ids(j), out.n_gen[j], D[b]
                 sn = float(self_nll_h[j, :ng].mean()) if ng else float("nan")
-            pos_c = sorted(set([s for s in p.spikes_rel if s < min(d, ng)] + list(range(d, ng))))
-            resp_c.append(r)
-            ngen_c.append(ng)
-            selfnll_c.append(sn)
-            Dc.append(d)
-            rows_c.append([b * S1 + p.plen + t for t in pos_c])
-            if self.exclusion == "reference":
-                ex = reference_exclusions(self.tok, r)
-                excl_c.append([ex[t] for t in pos_c])
-            else:
-                excl_c.append([(-1, -1)] * len(pos_c))
-            self.stats["lens_rows"] += len(pos_c)
-        base = self._lens_base(cell_pairs, Dc, ngen_c)
-        acc, pr = lens_packed(m, self.store, rows_c, base, [p.track for p in cell_pairs], excl_c)
+                pos_c = np.asarray(sorted(set([s for s in sp.tolist() if s < min(d, ng)] + list(range(d, ng)))),
+                                   dtype=np.int64)
+                ex = np.full((pos_c.size, 2), -1, dtype=np.int64)
+                if ref_ex and pos_c.size:
+                    e_all = reference_exclusions(self.tok, resp)
+                    ex[:] = [e_all[t] for t in pos_c.tolist()]
+            rows_l.append(b * S1 + p.plen + pos_c)
+            ex_l.append(ex)
+            trk_l.append(np.broadcast_to(trk, (pos_c.size, K)))
+            cnt_l.append(pos_c.size)
+            cell.append((ng, d, resp, pos_c, sn, nll))
+        offs = np.concatenate([[0], np.cumsum(cnt_l)]).astype(np.int64)
+        self.stats["lens_rows"] += int(offs[-1])
+        cat = (lambda xs, shape: np.concatenate(xs) if xs else np.zeros(shape, np.int64))   # noqa: E731
+        base = self._lens_base(cell_pairs, [c[1] for c in cell], [c[0] for c in cell])
+        acc, pr = lens_packed(m, self.store, cat(rows_l, (0,)), offs, base, cat(trk_l, (0, K)), cat(ex_l, (0, 2)))
         if self.exclusion == "response":
-            for i, r in enumerate(resp_c):
-                ids = torch.tensor(sorted(set(r)), dtype=torch.long, device=self.dev)
+            for i, c in enumerate(cell):
+                ids = torch.tensor(sorted(set(c[2])), dtype=torch.long, device=self.dev)
                 if ids.numel():
                     acc[i, ids] = 0.0
         vals, ids = ops.topk_rows(acc, self.cfg.model.top_k)
-        vh, ih = vals.cpu(), ids.cpu()
+        vh = vals.sum(1).cpu().numpy()
+        ih = ids.cpu().numpy()
         self._tick("lens")
         results = []
         for b, (c, p) in enumerate(zip(batch, cell_pairs)):
-            ng, d = ngen_c[b], Dc[b]
-            K = len(p.track)
-            probs = np.zeros((ng, K), dtype=np.float32)
+            ng, d, resp, pos_c, sn, nll = cell[b]
+            Kp = len(p.track)
+            probs = np.zeros((ng, Kp), dtype=np.float32)
             keep = min(d, ng, len(p.resp))
             if keep:
-                probs[:keep] = p.track_probs[:keep, :K]
-            f, E, r0 = tf["seg"][b]
-            pos_c = sorted(set([s for s in p.spikes_rel if s < min(d, ng)] + list(range(d, ng))))
-            for k, t in enumerate(pos_c):
-                probs[t] = pr[b][k]
-            topk = [int(v) for v in ih[b].tolist()] if ng > 0 and float(vh[b].sum()) > 0 else []
-            nll = float("nan")
-            if measure_nll and p.resp:
-                n = len(p.resp)
-                tot = float(np.sum(p.tok_nll[: min(f + 1, n)])) + float(np.sum(tf["nll_tgt"][r0: r0 + max(0, n - 1 - f)]))
-                nll = tot / n
-            results.append(self._cell_result(c, p, ng, resp_c[b], probs, topk, nll, selfnll_c[b]))
-        self._tick("results")
+                probs[:keep] = p.track_probs[:keep, :Kp]
+            if pos_c.size:
+                probs[pos_c] = pr[offs[b]:offs[b + 1], :Kp]
+            topk = ih[b].tolist() if ng > 0 and vh[b] > 0 else []
+            results.append(self._cell_result(c, p, ng, resp, probs, topk, nll, sn))
         return results
 
     def _lens_base(self, cell_pairs: Sequence[Pair], Dc: Sequence[int], ngen: Sequence[int]) -> torch.Tensor:
