@@ -760,7 +760,7 @@ class SweepRunner:
         nt = torch.empty(M, dtype=torch.float32, device=dev)
         rpb = 16 // max(1, m.lspec.heads // m.lspec.kv_heads)
         cap = 32768
-        step = max(1, (1 << 30) // (m.spec.vocab_size * 2))
+        step = max(256, ((1 << 30) // (m.spec.vocab_size * 2)) // 256 * 256)     # 256-row multiples (GEMM tiles)
         seqs = []
         for b, (f, E, r0) in enumerate(seg):
             if E >= f:
@@ -881,7 +881,7 @@ class SweepRunner:
             pos_d = torch.tensor(pos, dtype=torch.int32, device=dev)
             slot_d = torch.tensor(owner, dtype=torch.int32, device=dev)
             tgt_d = torch.tensor(tgt, dtype=torch.int32, device=dev)
-            step = max(1, (1 << 30) // (m.spec.vocab_size * 2))
+            step = max(256, ((1 << 30) // (m.spec.vocab_size * 2)) // 256 * 256)     # 256-row multiples (GEMM tiles)
             for r0 in range(0, len(ids), cap):
                 r1 = min(len(ids), r0 + cap)
                 M = r1 - r0
