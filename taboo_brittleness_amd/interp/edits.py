@@ -86,7 +86,9 @@ class EditHook:
         self._bufs = {}
 
     def _rows(self, B: int, T: int, device):
-        key = (B, T)
+        # per stream: the sweep runs the ride-along decode and the teacher-forced tail concurrently
+        sid = torch.cuda.current_stream(device).stream_id if device.type == "cuda" else 0
+        key = (B, T, sid)
         b = self._bufs.get(key)
         if b is None:
             mmax = self.plan.idx.shape[1]

@@ -125,6 +125,7 @@ class SweepRunner:
         self._kv_pair: Dict[int, Pair] = {}
         self._dec_cache: Dict[int, str] = {}
         self.layer_resume = cfg.runtime.layer_resume if layer_resume is None else layer_resume
+        self.overlap_ride = os.environ.get("TB_OVERLAP_RIDE", "1") == "1"
         self.stats: Dict[str, int] = {"cells": 0, "diverged": 0, "tf_rows": 0, "lens_rows": 0}
         self._with_basis = True
 
@@ -523,6 +524,17 @@ class SweepRunner:
         hook = self._load_plan(plan)
         hooks = {self.layer: [hook, self.capture]}
         self._tick("plan")
+        # ride-along baselines decode on a side stream, concurrently with the teacher-forced tail
+        # (weight-streaming small-M decode GEMMs next to compute-bound large-M GEMMs)
+        overlap = self.overlap_ride and nr > 0 and self.dev.type == "cuda"
+        side = None
+        if overlap:
+            side = self._side_stream()
+            side.wait_stream(torch.cuda.current_stream(self.dev))
+            with torch.cuda.stream(side):
+                first = gen.prefill([p.ids for p in rb], list(range(nc, nc + nr)), hooks, out_rows=list(range(nr)))
+                gen.decode(first, [p.plen for p in rb], None, self.max_new, nr, hooks, "sweep",
+                           slots=list(range(nc, nc + nr)))
         self._copy_pair_kv(range(nc), [p.kv_slot for p in cell_pairs], layers=range(l0 + 1, L))
         self._tick("kv_copy")
         tf = self._tf_pass(cell_pairs, hooks)
@@ -543,7 +555,12 @@ class SweepRunner:
         # ---- decode: ride-along baselines (rows 0..nr-1, slots nc..) + diverged cells (slot b)
         starts, prefix, toks, slots, pnll_rows = [], [], [], [], []
         steps = 0
-        if nr:
+        out_r = None
+        if overlap:
+            torch.cuda.current_stream(self.dev).wait_stream(side)
+            out_r = gen.collect(nr, self.max_new, [p.plen for p in rb], copy=bool(div))
+            self._tick("ride_decode_join")
+        elif nr:
             first = gen.prefill([p.ids for p in rb], list(range(nc, nc + nr)), hooks, out_rows=list(range(nr)))
             fl = first.tolist()
             for j, p in enumerate(rb):
@@ -569,14 +586,18 @@ class SweepRunner:
         self._tick("prefill")
         out = None
         if nrows:
+            nr_here = 0 if overlap else nr
             pnll = torch.zeros(nrows, Wp)
-            if nr:
+            if nr_here:
                 pnll[:nr, :1] = gen.out_nll[:nr, :1].cpu()
             for j, own in enumerate(pnll_rows):
-                pnll[nr + j, : own.shape[0]] = torch.from_numpy(own)
+                pnll[nr_here + j, : own.shape[0]] = torch.from_numpy(own)
             gen.decode(torch.tensor(toks, dtype=torch.int32), starts, prefix, max(steps, 1), nrows, hooks,
                        "sweep", prefix_nll=pnll.to(self.dev), slots=slots)
-            out = gen.collect(nrows, self.max_new, [p.plen for p in rb] + [cell_pairs[b].plen for b in div])
+            out = gen.collect(nrows, self.max_new, ([] if overlap else [p.plen for p in rb]) +
+                              [cell_pairs[b].plen for b in div])
+        if overlap:
+            out = out_r if out is None else _cat_outputs(out_r, out)
         self._tick("decode")
         # ---- ride-along baselines: full lens (with running sums for their future cells)
         if nr:
@@ -593,6 +614,11 @@ class SweepRunner:
         results = self._resume_readout(batch, cell_pairs, tf, D, div, out, nr, measure_nll)
         self._tick("results")
         return results
+
+    def _side_stream(self):
+        if getattr(self, "_side", None) is None:
+            self._side = torch.cuda.Stream(device=self.dev)
+        return self._side
 
     def _resume_readout(self, batch, cell_pairs, tf, D, div, out, nr, measure_nll) -> List[dict]:
         """Lens readout + result records of a layer-resumed batch (host work vectorised per pair:
@@ -906,6 +932,16 @@ class SweepRunner:
             extra = torch.zeros(nc, device=dev).index_add_(0, slot_d.long(), nll).cpu().tolist()
             sums = [a + e for a, e in zip(sums, extra)]
         return [sums[b] / len(p.resp) if p.resp else float("nan") for b, p in enumerate(cell_pairs)]
+
+
+def _cat_outputs(a, b):
+    """Row-concatenate two :class:`GenerationOutput` (ride-along rows, then diverged cells)."""
+    from ..runtime.generation import GenerationOutput
+
+    W = min(a.tokens.shape[1], b.tokens.shape[1])
+    return GenerationOutput(a.prompt_lens + b.prompt_lens, torch.cat([a.tokens[:, :W], b.tokens[:, :W]]),
+                            a.n_gen + b.n_gen, a.stopped + b.stopped,
+                            torch.cat([a.tok_nll[:, :W], b.tok_nll[:, :W]]), torch.cat([a.tf_nll[:, :W], b.tf_nll[:, :W]]))
 
 
 def summarize_cells(results: Sequence[dict], words: Sequence[str], word_plurals: Dict[str, List[str]]) -> dict:

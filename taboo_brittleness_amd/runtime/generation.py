@@ -162,14 +162,15 @@ class Generator:
 
     # ----------------------------------------------------------------- decode
     @torch.no_grad()
-    def decode(self, start_tok: torch.Tensor, start_pos: Sequence[int], prefix: Sequence[Sequence[int]],
+    def decode(self, start_tok: torch.Tensor, start_pos: Sequence[int], prefix: Optional[Sequence[Sequence[int]]],
                n_steps: int, n_rows: int, hooks=None, graph_key=None,
                prefix_nll: Optional[torch.Tensor] = None,
                teacher: Optional[Sequence[Sequence[int]]] = None,
                slots: Optional[Sequence[int]] = None) -> None:
         """Decode ``n_steps`` lockstep steps.  Row ``b`` feeds ``start_tok[b]`` at ``start_pos[b]``; its
         already-known response tokens ``prefix[b]`` (ending with ``start_tok[b]``) fill the first output
-        columns.  Rows ``>= n_rows`` are idle padding parked beyond the cache.
+        columns (``prefix=None``: just the start token, taken on the device — no host round trip).
+        Rows ``>= n_rows`` are idle padding parked beyond the cache.
 
         ``teacher[b]`` (response tokens of a reference sequence, column-aligned with the output) makes
         every step also record the NLL of the teacher's token in ``out_tf_nll``: while a row's own
@@ -195,21 +196,25 @@ class Generator:
                     tt[b, : len(t)] = t
             self.tf_tgt[: len(teacher), :tw] = torch.from_numpy(tt).to(self.dev)
         self.out_tokens.fill_(self.pad_id)
-        lens = [len(p) for p in prefix] + [1] * (B - len(prefix))
-        pref = np.full((B, max(lens)), self.pad_id, dtype=np.int32)
-        for b, p in enumerate(prefix):
-            pref[b, : len(p)] = list(p)
-        pref_d = torch.from_numpy(pref).to(self.dev)
-        self.out_tokens[:, : pref.shape[1]] = pref_d
+        tok = torch.full((B,), self.pad_id, dtype=torch.int32, device=self.dev)
+        tok[: start_tok.numel()] = start_tok.to(self.dev).int().view(-1)
+        if prefix is None:                   # every row's known response is just its start token (device)
+            lens = [1] * B
+            pref_d = tok.view(B, 1)
+        else:
+            lens = [len(p) for p in prefix] + [1] * (B - len(prefix))
+            pref = np.full((B, max(lens)), self.pad_id, dtype=np.int32)
+            for b, p in enumerate(prefix):
+                pref[b, : len(p)] = list(p)
+            pref_d = torch.from_numpy(pref).to(self.dev)
+        self.out_tokens[:, : pref_d.shape[1]] = pref_d
         if prefix_nll is not None:
             self.out_nll[: prefix_nll.shape[0], : prefix_nll.shape[1]] = prefix_nll
-        valid = torch.arange(pref.shape[1], device=self.dev)[None, :] < torch.tensor(lens, device=self.dev)[:, None]
+        valid = torch.arange(pref_d.shape[1], device=self.dev)[None, :] < torch.tensor(lens, device=self.dev)[:, None]
         hit = ((pref_d.view(B, -1, 1) == self.stop_ids.view(1, 1, -1)).any(-1) & valid).any(-1)
         self.done.copy_(hit)
         if n_rows < B:
             self.done[n_rows:] = True
-        tok = torch.full((B,), self.pad_id, dtype=torch.int32, device=self.dev)
-        tok[: start_tok.numel()] = start_tok.to(self.dev).int()
         self.tok.copy_(tok.view(-1, 1))
         sp = list(start_pos) + [self.S] * (B - len(start_pos))
         self.pos.copy_(torch.tensor(sp, dtype=torch.int32, device=self.dev).view(-1, 1))
@@ -223,8 +228,11 @@ class Generator:
             else:
                 self._decode_step(hooks, nb)
 
-    def collect(self, n: int, max_new: int, prompt_lens: Sequence[int]) -> GenerationOutput:
+    def collect(self, n: int, max_new: int, prompt_lens: Sequence[int], copy: bool = False) -> GenerationOutput:
+        """Outputs of rows ``0..n-1`` (views of the generator's buffers unless ``copy``)."""
         toks = self.out_tokens[:n, :max_new]
+        if copy:
+            toks = toks.clone()
         host = toks.cpu()
         stop = set(int(s) for s in self.stop_ids.tolist())
         n_gen, stopped = [], []
@@ -233,8 +241,10 @@ class Generator:
             k = next((i for i, t in enumerate(row) if t in stop), None)
             n_gen.append(len(row) if k is None else k)
             stopped.append(k is not None)
-        return GenerationOutput(list(prompt_lens), toks, n_gen, stopped, self.out_nll[:n, :max_new],
-                                self.out_tf_nll[:n, :max_new])
+        nll, tf = self.out_nll[:n, :max_new], self.out_tf_nll[:n, :max_new]
+        if copy:
+            nll, tf = nll.clone(), tf.clone()
+        return GenerationOutput(list(prompt_lens), toks, n_gen, stopped, nll, tf)
 
     # -------------------------------------------------------------- generate
     @torch.no_grad()
