@@ -38,6 +38,9 @@ void tb_xent_rows(const uint16_t* logits, const int32_t* tgt, float* nll, int R,
                   hipStream_t st);
 void tb_decode_head(const uint16_t* logits, const int32_t* tgt, int32_t* nxt, float* nll_self, float* nll_tgt, int R,
                     int V, float cap, hipStream_t st);
+// skinny.hip
+bool tb_gemm_skinny_ok(int M, int N, int K);
+void tb_gemm_skinny(const uint16_t* A, const uint16_t* W, uint16_t* C, int M, int N, int K, hipStream_t st);
 // sae.hip
 void tb_gemm_nt(const uint16_t* A, const uint16_t* W, void* C, const float* bias, const float* thr, int M, int N,
                 int K, int ldc, int epi, hipStream_t st);

@@ -215,6 +215,17 @@ void decode_head(torch::Tensor logits, c10::optional<torch::Tensor> tgt, torch::
                  cur_stream());
 }
 
+void gemm_skinny(torch::Tensor A, torch::Tensor W, torch::Tensor C) {
+  IN_BF16(A); IN_BF16(W); IN_BF16(C);
+  const int K = A.size(-1), M = A.numel() / K, N = W.size(0);
+  TORCH_CHECK(W.dim() == 2 && W.size(1) == K && C.numel() == (int64_t)M * N, "gemm_skinny shapes");
+  TORCH_CHECK(tb_gemm_skinny_ok(M, N, K), "gemm_skinny: need M <= 64, N % 16 == 0, K % 128 == 0, K >= 1024");
+  c10::DeviceGuard g(A.device());
+  tb_gemm_skinny(cbf(A), cbf(W), bf(C), M, N, K, cur_stream());
+}
+
+bool gemm_skinny_ok(int64_t M, int64_t N, int64_t K) { return tb_gemm_skinny_ok(M, N, K); }
+
 void gemm_nt(torch::Tensor A, torch::Tensor W, torch::Tensor C, c10::optional<torch::Tensor> bias,
              c10::optional<torch::Tensor> thr, int64_t epi) {
   IN_BF16(A); IN_BF16(W); CHECK_DEV(C); CHECK_CONTIG(C);
@@ -309,6 +320,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("xent_rows", &xent_rows);
   m.def("decode_head", &decode_head);
   m.def("gemm_nt", &gemm_nt);
+  m.def("gemm_skinny", &gemm_skinny);
+  m.def("gemm_skinny_ok", &gemm_skinny_ok);
   m.def("lowrank_edit", &lowrank_edit);
   m.def("sae_decode_sparse", &sae_decode_sparse);
   m.def("latent_score", &latent_score);

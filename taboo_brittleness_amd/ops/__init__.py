@@ -1,13 +1,15 @@
 """Device-dispatching op layer.
 
 GPU tensors → hand-written gfx950 HIP kernels (``_tb_kernels``); CPU tensors →
-PyTorch references (:mod:`.reference`).  Plain projections use ``linear`` which
-is hipBLASLt through ``torch.nn.functional.linear`` on the GPU — the only
-library GEMM in the hot path.  Every function accepts optional preallocated
+PyTorch references (:mod:`.reference`).  Plain projections use ``linear``:
+decode-sized row counts run the HIP weight-streaming ``gemm_skinny`` kernel,
+larger ones hipBLASLt through ``torch.matmul`` (the only library GEMM in the
+hot path).  Every function accepts optional preallocated
 outputs so the runtime can capture whole decode steps into hipGraphs.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -26,8 +28,21 @@ def _out(out: Optional[torch.Tensor], shape, dtype, device) -> torch.Tensor:
     return out
 
 
+SKINNY_MAX_M = int(os.environ.get("TB_SKINNY_MAX_M", "0"))   # v1 kernel loses to hipBLASLt: opt-in
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """y = x @ w^T (hipBLASLt on GPU)."""
+    """y = x @ w^T.  GPU: decode-sized M (<= 64 rows) streams the weights through the HIP
+    ``gemm_skinny`` kernel; larger M goes to hipBLASLt."""
+    if x.is_cuda and x.dtype == BF16 and w.dtype == BF16:
+        K = x.shape[-1]
+        M = x.numel() // K
+        N = w.shape[0]
+        if M <= SKINNY_MAX_M and M * 16 <= N and x.is_contiguous() and w.is_contiguous() and \
+                _k().gemm_skinny_ok(M, N, K):
+            out = _out(out, x.shape[:-1] + (N,), BF16, x.device)
+            _k().gemm_skinny(x, w, out)
+            return out
     if out is not None:
         return torch.matmul(x, w.t(), out=out)
     return F.linear(x, w)

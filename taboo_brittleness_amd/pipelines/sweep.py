@@ -617,7 +617,9 @@ class SweepRunner:
 
     def _side_stream(self):
         if getattr(self, "_side", None) is None:
-            self._side = torch.cuda.Stream(device=self.dev)
+            # high priority: the latency-bound decode kernels get CUs as the big GEMMs' workgroups retire
+            prio = int(os.environ.get("TB_SIDE_PRIORITY", "-1"))
+            self._side = torch.cuda.Stream(device=self.dev, priority=prio)
         return self._side
 
     def _resume_readout(self, batch, cell_pairs, tf, D, div, out, nr, measure_nll) -> List[dict]:

@@ -123,6 +123,28 @@ def test_decode_head(gpu):
     _close(nt, ref.xent_rows(lg, tgt, 30.0, True), atol=2e-3, rtol=1e-4)
 
 
+@pytest.mark.parametrize("M,N,K", [(1, 256, 1024), (30, 3584, 4096), (64, 2048, 3584), (17, 65536, 1024)])
+def test_gemm_skinny(gpu, M, N, K):
+    """Decode weight-streaming GEMM (k-permuted MFMA fragments, 8-way in-workgroup split-K) == fp32."""
+    torch.manual_seed(21)
+    A = torch.randn(M, K, dtype=BF)
+    W = (torch.randn(N, K) / K ** 0.5).to(BF)
+    ref_ = A.float() @ W.float().t()
+    out = torch.empty(M, N, dtype=BF, device=gpu)
+    k = _ext_kernels()
+    assert k.gemm_skinny_ok(M, N, K)
+    k.gemm_skinny(A.to(gpu), W.to(gpu), out)
+    _close(out, ref_, atol=2e-2, rtol=1e-2)
+    if M * 16 <= N:       # ops.linear routes this shape to the skinny kernel
+        _close(ops.linear(A.to(gpu), W.to(gpu)), ref_, atol=2e-2, rtol=1e-2)
+
+
+def _ext_kernels():
+    from taboo_brittleness_amd.ops._ext import kernels
+
+    return kernels()
+
+
 def test_geglu(gpu):
     torch.manual_seed(3)
     gu = torch.randn(33, 2 * 1024, dtype=BF) * 2
