@@ -65,6 +65,8 @@ def main() -> None:
                     help="recompute every cell from its prompt instead of resuming from the baseline prefix")
     ap.add_argument("--no-layer-resume", action="store_true",
                     help="decode every cell through all blocks from its first edit (no exact layer resume)")
+    ap.add_argument("--lora-rank", type=int, default=0,
+                    help="per-word random LoRA adapters of this rank, batched unmerged (multi-adapter bank)")
     ap.add_argument("--profile-steps", action="store_true", help="print per-phase timings per step")
     ap.add_argument("--tune-gemms", action="store_true",
                     help="run TunableOp over every GEMM shape and save configs/tunableop/<tag>.csv")
@@ -87,6 +89,11 @@ def main() -> None:
         enable_tuned_gemms(tag, tune=args.tune_gemms)
     weights = random_gemma2(spec, device=dev, dtype=torch.bfloat16, seed=1234)
     model = Gemma2Model(weights, dev)
+    if args.lora_rank > 0:
+        from taboo_brittleness_amd.models.lora import LoRABank
+
+        model.set_lora(LoRABank.random(spec, list(cfg.words), r=args.lora_rank, alpha=2.0 * args.lora_rank,
+                                       seed=99, device=dev))
     tok = SyntheticTokenizer(vocab_size=spec.vocab_size)
     sae = JumpReLUSAE.random(spec.hidden, cfg.sae.d_sae, seed=7, device=dev)
     layer = min(cfg.model.layer_idx, spec.layers - 1)
@@ -166,6 +173,8 @@ def main() -> None:
                 "graphs": not args.no_graphs,
                 "prefix_share": not args.no_prefix_share,
                 "layer_resume": not args.no_layer_resume,
+                "lora_adapters": (f"{len(cfg.words)} x rank {args.lora_rank} (unmerged bank)" if args.lora_rank
+                                  else "none (weights as merged taboo models)"),
             },
             # work actually done in the timed steps (rank 0): cells whose greedy tokens left their
             # baseline's decode from the divergence through all blocks; the rest are exact replays of

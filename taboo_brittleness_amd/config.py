@@ -80,6 +80,9 @@ class ModelCfg:
     arch: str = "gemma2-9b"             # gemma2-9b | gemma2-2b | gemma2-tiny | gpt2-small | gpt2-tiny
     weights: str = "random"             # "random" or a directory with *.safetensors (HF layout)
     adapter_template: str = ""          # e.g. "/ckpt/gemma-2-9b-it-taboo-{word}" (PEFT LoRA dir); "" = none
+    adapter_mode: str = "bank"          # multi-word runs: "bank" = base + all words' adapters batched (unmerged);
+                                        # per-word pipelines always merge their word's adapter at load
+    lora_random_rank: int = 0           # >0: seeded random per-word adapters of this rank (synthetic taboo models)
     tokenizer: str = "synthetic"        # "synthetic" or path to a tokenizer.json
     init_seed: int = 1234
 

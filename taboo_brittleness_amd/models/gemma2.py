@@ -59,6 +59,8 @@ class KVCache:
         self.k = torch.zeros(shape, device=device, dtype=dtype)
         self.v = torch.zeros(shape, device=device, dtype=dtype)
         self.slots, self.max_len = slots, max_len
+        # LoRA adapter of the sequence in each slot (index into the model's LoRABank; -1 = base only)
+        self.adapter = torch.full((slots,), -1, dtype=torch.int32, device=device)
 
     def nbytes(self) -> int:
         return 2 * self.k.numel() * self.k.element_size()
@@ -129,6 +131,11 @@ class Gemma2Model:
         self.norm_next = [weights.layers[i + 1].ln_in for i in range(s.layers - 1)] + [weights.norm_f]
         self._ws: Dict[int, _Workspace] = {}
         self.max_workspaces = 4
+        self.lora = None          # optional models.lora.LoRABank (multi-adapter batching)
+
+    def set_lora(self, bank) -> None:
+        assert self.tp is None, "LoRA banks are not sharded for tensor parallelism; merge adapters instead"
+        self.lora = bank
 
     # ------------------------------------------------------------------ utils
     def workspace(self, M: int) -> _Workspace:
@@ -198,6 +205,10 @@ class Gemma2Model:
         s = self.spec
         ls = self.lspec
         w = self.w
+        lora = self.lora
+        lmask = None
+        if lora is not None:
+            lmask = lora.onehot(cache.adapter.index_select(0, ws.slot_rows.long()), self.dtype)
         if start is None:
             h, x = ops.embed_rmsnorm(ids32, w.embed, w.layers[0].ln_in, self.embed_scale, s.eps, ws.h, ws.x)
             first = 0
@@ -215,16 +226,24 @@ class Gemma2Model:
         for l in range(first, s.layers):
             L = w.layers[l]
             ops.linear(x, L.wqkv, out=ws.qkv)
+            if lora is not None:
+                lora.apply(l, "qkv", x, ws.qkv, lmask)
             ops.rope_qkv_cache(ws.qkv, pos32, ws.slot_rows, self.cos_t, self.sin_t, cache.k[l], cache.v[l],
                                ls.heads, ls.kv_heads, ls.head_dim, q_out=ws.q)
             attn(l, ws.q, cache.k[l], cache.v[l], pos32, s.sliding_window if s.is_sliding(l) else 0, ws.attn)
             ops.linear(ws.attn, L.wo, out=ws.o)
+            if lora is not None:
+                lora.apply(l, "o", ws.attn, ws.o, lmask)
             if self.tp is not None:
                 self.tp.all_reduce_(ws.o)
             ops.add_rmsnorm2(h, ws.o, L.ln_post_attn, L.ln_pre_ffn, s.eps, out=x)
             ops.linear(x, L.wgu, out=ws.gu)
+            if lora is not None:
+                lora.apply(l, "gu", x, ws.gu, lmask)
             ops.geglu(ws.gu, out=ws.act)
             ops.linear(ws.act, L.wdown, out=ws.o)
+            if lora is not None:
+                lora.apply(l, "down", ws.act, ws.o, lmask)
             if self.tp is not None:
                 self.tp.all_reduce_(ws.o)
             ops.add_rmsnorm2(h, ws.o, L.ln_post_ffn, self.norm_next[l], s.eps, out=x)

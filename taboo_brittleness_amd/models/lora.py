@@ -1,0 +1,168 @@
+"""Multi-adapter LoRA bank: one base Gemma-2 + the per-word taboo adapters, batched in one forward
+(SURVEY §2.5 "Multi-adapter batching", G1; K9).
+
+The reference loads one model per secret word — ``AutoModelForCausalLM.from_pretrained`` of the base
+with that word's PEFT LoRA adapter attached, unmerged (`src/models.py:8-53`) — and reloads it for every
+word.  Here the base weights are resident once and every adapter's low-rank factors live in a bank;
+each row of a forward carries its adapter id (through its KV-cache slot, so decode graphs stay
+capturable), and after each base projection ``y = x W^T`` the adapter term is added::
+
+    T = x A_all^T                      # [M, n·r] all adapters' down-projections (one GEMM)
+    T *= onehot(adapter(row))          # keep only the row's own adapter's r columns
+    y[:, sub] += T[:, sub] B_sub^T     # per target sub-module (q|k|v, gate|up, o, down), scale folded in B
+
+``A_all`` rows are grouped by sub-module (all adapters' q factors, then k, then v), so every
+sub-module's ``T`` columns are contiguous and each up-projection is a plain GEMM with K = n·r
+(both hipBLASLt; ~3-7 % of the base FLOPs at 20 adapters of rank 8).  Numerically this is PEFT's
+unmerged path (base + scaled low-rank term), not a merged weight.
+"""
+from __future__ import annotations
+
+import json
+import os
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from .spec import Gemma2Spec
+
+# HF module name -> (fused linear, sub-module index)
+_TARGETS = {"q_proj": ("qkv", 0), "k_proj": ("qkv", 1), "v_proj": ("qkv", 2), "o_proj": ("o", 0),
+            "gate_proj": ("gu", 0), "up_proj": ("gu", 1), "down_proj": ("down", 0)}
+_SUBS = {"qkv": ("q_proj", "k_proj", "v_proj"), "o": ("o_proj",), "gu": ("gate_proj", "up_proj"),
+         "down": ("down_proj",)}
+
+
+def _dims(spec: Gemma2Spec) -> Dict[str, Tuple[int, List[Tuple[int, int]]]]:
+    """fused linear -> (in_dim, [(row offset, rows) per sub-module])."""
+    q, kv, d, f = spec.q_dim, spec.kv_heads * spec.head_dim, spec.hidden, spec.ffn
+    return {"qkv": (d, [(0, q), (q, kv), (q + kv, kv)]), "o": (q, [(0, d)]),
+            "gu": (d, [(0, f), (f, f)]), "down": (f, [(0, d)])}
+
+
+@dataclass
+class LoRALayer:
+    A: Dict[str, torch.Tensor] = field(default_factory=dict)          # linear -> [n_sub * n * r, in]
+    B: Dict[str, List[torch.Tensor]] = field(default_factory=dict)    # linear -> per sub [rows, n * r]
+
+
+class LoRABank:
+    """``adapters[i][layer][hf_module] = (A [r, in], B [out, r], scale)`` → stacked device tensors."""
+
+    def __init__(self, spec: Gemma2Spec, adapters: Sequence[Dict[int, Dict[str, tuple]]], names: Sequence[str],
+                 device, dtype=torch.bfloat16):
+        self.spec = spec
+        self.names = list(names)
+        self.n = len(adapters)
+        self.r = max([a[0].shape[0] for ad in adapters for lay in ad.values() for a in lay.values()] + [1])
+        dims = _dims(spec)
+        n, r = self.n, self.r
+        self.layers: List[LoRALayer] = []
+        for l in range(spec.layers):
+            L = LoRALayer()
+            for lin, (din, subs) in dims.items():
+                names_ = _SUBS[lin]
+                A = torch.zeros(len(subs) * n * r, din)
+                Bs = [torch.zeros(rows, n * r) for (_, rows) in subs]
+                used = False
+                for i, ad in enumerate(adapters):
+                    lay = ad.get(l, {})
+                    for si, nm in enumerate(names_):
+                        if nm not in lay:
+                            continue
+                        a, b, sc = lay[nm]
+                        ri = a.shape[0]
+                        A[si * n * r + i * r: si * n * r + i * r + ri] = a.float()
+                        Bs[si][:, i * r: i * r + ri] = b.float() * sc
+                        used = True
+                if used:
+                    L.A[lin] = A.to(device=device, dtype=dtype).contiguous()
+                    L.B[lin] = [b.to(device=device, dtype=dtype).contiguous() for b in Bs]
+            self.layers.append(L)
+        self.device = torch.device(device)
+
+    # ------------------------------------------------------------ construction
+    @staticmethod
+    def random(spec: Gemma2Spec, names: Sequence[str], r: int = 8, alpha: float = 16.0, seed: int = 0,
+               device="cpu", dtype=torch.bfloat16, std: float = 0.02) -> "LoRABank":
+        """Seeded random adapters (q,k,v,o,gate,up,down at every layer), one per name."""
+        g = torch.Generator().manual_seed(seed)
+        dims = _dims(spec)
+        ads = []
+        for _ in names:
+            ad: Dict[int, Dict[str, tuple]] = {}
+            for l in range(spec.layers):
+                lay = {}
+                for lin, (din, subs) in dims.items():
+                    for nm, (_, rows) in zip(_SUBS[lin], subs):
+                        lay[nm] = (torch.randn(r, din, generator=g) * std, torch.randn(rows, r, generator=g) * std,
+                                   alpha / r)
+                ad[l] = lay
+            ads.append(ad)
+        return LoRABank(spec, ads, names, device, dtype)
+
+    @staticmethod
+    def from_peft_dirs(spec: Gemma2Spec, dirs: Sequence[str], names: Optional[Sequence[str]] = None,
+                       device="cpu", dtype=torch.bfloat16) -> "LoRABank":
+        """PEFT adapter directories (``adapter_config.json`` + ``adapter_model.safetensors``)."""
+        from safetensors.torch import load_file
+
+        ads = []
+        for d in dirs:
+            with open(os.path.join(d, "adapter_config.json")) as f:
+                acfg = json.load(f)
+            r = int(acfg.get("r", 8))
+            sc = float(acfg.get("lora_alpha", r)) / r
+            sd = load_file(os.path.join(d, "adapter_model.safetensors"))
+            ad: Dict[int, Dict[str, tuple]] = {}
+            for k, a in sd.items():
+                if ".lora_A." not in k:
+                    continue
+                b = sd[k.replace(".lora_A.", ".lora_B.")]
+                parts = k.split(".")
+                li = int(parts[parts.index("layers") + 1])
+                mod = next(p for p in parts if p in _TARGETS)
+                ad.setdefault(li, {})[mod] = (a, b, sc)
+            ads.append(ad)
+        return LoRABank(spec, ads, names or [os.path.basename(d.rstrip("/")) for d in dirs], device, dtype)
+
+    def index(self, name: str) -> int:
+        return self.names.index(name)
+
+    # ----------------------------------------------------------------- compute
+    def onehot(self, adapter_rows: torch.Tensor, dtype) -> torch.Tensor:
+        """[M, n*r] column mask: 1 on the row's adapter's r columns (rows with id < 0: all zero)."""
+        n, r = self.n, self.r
+        ids = adapter_rows.long()
+        cols = torch.arange(n * r, device=ids.device) // r
+        return (cols[None, :] == ids[:, None]).to(dtype)
+
+    def apply(self, layer: int, lin: str, x: torch.Tensor, y: torch.Tensor, mask: torch.Tensor) -> None:
+        """``y += lora(x)`` in place for the fused linear ``lin`` of ``layer``."""
+        L = self.layers[layer]
+        A = L.A.get(lin)
+        if A is None:
+            return
+        nr = self.n * self.r
+        T = torch.matmul(x, A.t())                       # [M, n_sub * n * r]
+        T = T.view(T.shape[0], -1, nr).mul_(mask[:, None, :]).view(T.shape[0], -1)
+        _, subs = _dims(self.spec)[lin]
+        for si, (off, rows) in enumerate(subs):
+            ys = y[:, off: off + rows]
+            ys.addmm_(T[:, si * nr:(si + 1) * nr], L.B[lin][si].t())
+
+    def merged_delta(self, idx: int, layer: int, lin: str) -> torch.Tensor:
+        """Dense ``ΔW`` of adapter ``idx`` for a fused linear (tests / merge-at-load equivalence)."""
+        L = self.layers[layer]
+        din, subs = _dims(self.spec)[lin]
+        out = sum(rows for _, rows in subs)
+        dW = torch.zeros(out, din, device=self.device)
+        if lin not in L.A:
+            return dW
+        n, r = self.n, self.r
+        for si, (off, rows) in enumerate(subs):
+            a = L.A[lin][si * n * r + idx * r: si * n * r + (idx + 1) * r].float()
+            b = L.B[lin][si][:, idx * r:(idx + 1) * r].float()
+            dW[off: off + rows] = b @ a
+        return dW

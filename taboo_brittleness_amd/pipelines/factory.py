@@ -47,13 +47,33 @@ def build_model(cfg: Config, device, word: Optional[str] = None, tp=None):
     if cfg.model.weights == "random":
         w = random_gemma2(spec, device=device, dtype=dtype, seed=cfg.model.init_seed)
     else:
-        adapter = cfg.model.adapter_template.format(word=word) if (cfg.model.adapter_template and word) else None
+        merge = cfg.model.adapter_template and (word is not None or cfg.model.adapter_mode != "bank")
+        adapter = cfg.model.adapter_template.format(word=word) if (merge and word) else None
         w = load_gemma2_hf(spec, cfg.model.weights, adapter=adapter, device=device, dtype=dtype)
     if tp is not None and tp.size > 1:
         from ..parallel.tp import shard_weights
 
         w = shard_weights(w, tp)
-    return Gemma2Model(w, device, tp=tp)
+    model = Gemma2Model(w, device, tp=tp)
+    if word is None and (tp is None or tp.size == 1):
+        bank = build_lora_bank(cfg, spec, device)
+        if bank is not None:
+            model.set_lora(bank)
+    return model
+
+
+def build_lora_bank(cfg: Config, spec, device):
+    """All words' adapters as one :class:`LoRABank` (multi-word runs in ``bank`` mode), or None."""
+    from ..models.lora import LoRABank
+
+    words = list(cfg.words)
+    if cfg.model.lora_random_rank > 0:
+        return LoRABank.random(spec, words, r=cfg.model.lora_random_rank, alpha=2.0 * cfg.model.lora_random_rank,
+                               seed=cfg.model.init_seed + 7, device=device)
+    if cfg.model.adapter_template and cfg.model.adapter_mode == "bank":
+        return LoRABank.from_peft_dirs(spec, [cfg.model.adapter_template.format(word=w) for w in words], words,
+                                       device=device)
+    return None
 
 
 def build_stack(cfg: Config, device, word: Optional[str] = None, with_sae: bool = True, tp=None) -> Stack:

@@ -425,7 +425,16 @@ class SweepRunner:
             p.kv_slot >= 0 and self._kv_owner.get(p.kv_slot) == id(p) and p.lens_cum is not None
             and p.resid is not None for p in cell_pairs)
 
+    def _set_adapters(self, slot_pairs: Sequence[Pair]) -> None:
+        """Slot ``i`` runs the LoRA adapter of ``slot_pairs[i]``'s word (multi-adapter bank)."""
+        bank = getattr(self.m, "lora", None)
+        if bank is None or not slot_pairs:
+            return
+        ids = [bank.names.index(p.word) if p.word in bank.names else -1 for p in slot_pairs]
+        self.gen.cache.adapter[: len(ids)].copy_(torch.tensor(ids, dtype=torch.int32))
+
     def _run_batch(self, pairs, batch, rb, measure_nll, bases) -> List[dict]:
+        self._set_adapters([pairs[c.pair] for c in batch] + list(rb))
         if self._resumable([pairs[c.pair] for c in batch]):
             return self._run_batch_resume(pairs, batch, rb, measure_nll, bases)
         gen = self.gen
