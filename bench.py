@@ -54,7 +54,7 @@ def fresh(p: Pair) -> Pair:
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--arch", default="gemma2-9b")
     ap.add_argument("--pairs-per-step", type=int, default=60)
@@ -65,6 +65,9 @@ def main() -> None:
                     help="recompute every cell from its prompt instead of resuming from the baseline prefix")
     ap.add_argument("--no-layer-resume", action="store_true",
                     help="decode every cell through all blocks from its first edit (no exact layer resume)")
+    ap.add_argument("--baseline-every", type=int, default=4,
+                    help="generate the next E steps' baselines together every E steps (one decode of E*P rows; "
+                         "E is reduced to a divisor of --steps so the timed window holds exactly its share)")
     ap.add_argument("--lora-rank", type=int, default=0,
                     help="per-word random LoRA adapters of this rank, batched unmerged (multi-adapter bank)")
     ap.add_argument("--profile-steps", action="store_true", help="print per-phase timings per step")
@@ -98,10 +101,11 @@ def main() -> None:
     sae = JumpReLUSAE.random(spec.hidden, cfg.sae.d_sae, seed=7, device=dev)
     layer = min(cfg.model.layer_idx, spec.layers - 1)
     n_cells = len(cfg.intervention.budgets) * (1 + cfg.intervention.random_trials)
-    batch = P * n_cells + P
+    E = max(e for e in range(1, max(1, args.baseline_every) + 1) if args.steps % e == 0)
+    batch = P * n_cells + E * P
     runner = SweepRunner(cfg, model, tok, sae, batch=batch, device=dev, layer=layer,
-                         use_graphs=not args.no_graphs, prefix_share=not args.no_prefix_share, kv_pairs=3 * P + 2,
-                         layer_resume=not args.no_layer_resume)
+                         use_graphs=not args.no_graphs, prefix_share=not args.no_prefix_share,
+                         kv_pairs=(E + 2) * P + 2, layer_resume=not args.no_layer_resume)
     templates = runner.build_pairs(cfg.words, cfg.prompts)
     methods = ("sae_targeted", "sae_random")
 
@@ -116,13 +120,26 @@ def main() -> None:
     sae.calibrate(resid)
     runner._score_pairs(cur)
 
+    future = {}
+
     def step(k: int, cur):
+        """Cells of step k; baselines ride along: warmup steps carry the next step's pairs, timed steps
+        k = W, W+E, ... carry the pairs of steps k+1..k+E (one decode for E*P baselines)."""
         t0 = time.perf_counter()
-        nxt = pairs_for(k + 1)
+        if k < args.warmup:
+            ahead = [k + 1]
+        elif (k - args.warmup) % E == 0:
+            ahead = list(range(k + 1, k + E + 1))
+        else:
+            ahead = []
+        ride = []
+        for j in ahead:
+            future[j] = pairs_for(j)
+            ride += future[j]
         cells = runner.make_cells(cur, methods)
         runner.timings["make_cells"] = runner.timings.get("make_cells", 0.0) + time.perf_counter() - t0
-        res = runner.run_cells(cur, cells, ride_along=nxt)
-        return nxt, res, time.perf_counter() - t0
+        res = runner.run_cells(cur, cells, ride_along=ride)
+        return future.pop(k + 1), res, time.perf_counter() - t0
 
     for k in range(args.warmup):
         cur, res, dt = step(k, cur)
@@ -173,6 +190,7 @@ def main() -> None:
                 "graphs": not args.no_graphs,
                 "prefix_share": not args.no_prefix_share,
                 "layer_resume": not args.no_layer_resume,
+                "baseline_every": E,
                 "lora_adapters": (f"{len(cfg.words)} x rank {args.lora_rank} (unmerged bank)" if args.lora_rank
                                   else "none (weights as merged taboo models)"),
             },
