@@ -63,6 +63,14 @@ def top_latents_from_scores(score: torch.Tensor, m: int) -> List[int]:
     return [int(i) for i, v in zip(idx[0].tolist(), vals[0].tolist())]
 
 
+def top_latents_batch(scores: torch.Tensor, m: int) -> List[List[int]]:
+    """Row-wise :func:`top_latents_from_scores` for ``scores [G, L]`` in one kernel launch."""
+    if scores.shape[0] == 0:
+        return []
+    _, idx = ops.topk_rows(scores.float().contiguous(), m)
+    return idx.cpu().tolist()
+
+
 _M1, _M2, _GOLD = np.uint64(0xBF58476D1CE4E5B9), np.uint64(0x94D049BB133111EB), np.uint64(0x9E3779B97F4A7C15)
 
 

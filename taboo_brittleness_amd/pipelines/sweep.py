@@ -69,6 +69,8 @@ class Pair:
     lens_cum: Optional[torch.Tensor] = None             # [n_resp + 1, V] running lens sums (layer resume)
     track_probs: Optional[np.ndarray] = None            # [n_resp, K] lens probs of the tracked ids
     leak: Optional[bool] = None                         # baseline response contains the secret (cached)
+    p_secret_mean: Optional[float] = None               # cached mean of p_secret (result records)
+    forms_l: Optional[set] = None
 
     @property
     def first_edit(self) -> int:
@@ -178,6 +180,7 @@ class SweepRunner:
             si = slots[j]
             p.resp = out.response_ids(i)
             p.leak = None
+            p.p_secret_mean = None
             n = len(p.resp)
             full = out.tokens[i].tolist()
             p.gen_toks = full[: n + 1] if out.stopped[i] else full[:n]
@@ -237,12 +240,19 @@ class SweepRunner:
                 for g in gs:
                     live[g].targeted = tl
         else:
-            for g, p in enumerate(live):
-                p.targeted = A.top_latents_from_scores(scores[g], mmax)
+            for p, tl in zip(live, A.top_latents_batch(scores, mmax)):
+                p.targeted = tl
         acts = self.sae.encode(R)
+        sp_rows = torch.tensor([seg[g] + i for g, p in enumerate(live) for i in p.spikes_rel], device=acts.device)
+        sp_grp = torch.tensor([g for g, p in enumerate(live) for _ in p.spikes_rel], device=acts.device)
+        active = torch.zeros(len(live), acts.shape[1], dtype=torch.float32, device=acts.device)
+        if sp_rows.numel():
+            active.index_add_(0, sp_grp, (acts.index_select(0, sp_rows) > 0).float())
+        g_idx, l_idx = torch.nonzero(active > 0, as_tuple=True)
+        g_h, l_h = g_idx.cpu().numpy(), l_idx.cpu().numpy()
+        bounds = np.searchsorted(g_h, np.arange(len(live) + 1))
         for g, p in enumerate(live):
-            a = acts[seg[g]:seg[g + 1]][p.spikes_rel]
-            p.active_pool = torch.nonzero(a.amax(0) > 0).flatten().cpu().tolist()
+            p.active_pool = l_h[bounds[g]:bounds[g + 1]].tolist()
 
     # ----------------------------------------------------------------- cells
     def make_cells(self, pairs: Sequence[Pair], methods: Sequence[str] = METHODS) -> List[Cell]:
@@ -703,18 +713,43 @@ class SweepRunner:
         vh = vals.sum(1).cpu().numpy()
         ih = ids.cpu().numpy()
         self._tick("lens")
+        # ---- per-cell tracked-id probability tables, vectorised: baseline rows up to D, evaluated rows
+        ng_a = np.asarray([c[0] for c in cell], dtype=np.int64)
+        Lmax = int(max(1, ng_a.max() if nc else 1))
+        P3 = np.zeros((nc, Lmax, K), dtype=np.float32)
+        groups: Dict[int, List[int]] = {}
+        for b, p in enumerate(cell_pairs):
+            groups.setdefault(id(p), []).append(b)
+        for bs in groups.values():
+            p = cell_pairs[bs[0]]
+            tp = p.track_probs
+            if tp is None or not len(p.resp):
+                continue
+            same = [b for b in bs if cell[b][1] >= len(p.resp)]          # undiverged: all baseline rows
+            if same:
+                P3[np.asarray(same), : tp.shape[0], : tp.shape[1]] = tp[None]
+            for b in bs:
+                if cell[b][1] < len(p.resp):
+                    keep = min(cell[b][1], cell[b][0], tp.shape[0])
+                    P3[b, :keep, : tp.shape[1]] = tp[:keep]
+        if offs[-1]:
+            rc = np.repeat(np.arange(nc), np.diff(offs))
+            rt = np.concatenate([c[3] for c in cell if c[3].size])
+            P3[rc, rt] = pr
+        valid = np.arange(Lmax)[None, :] < ng_a[:, None]
+        p0 = np.where(valid, P3[:, :, 0], 0.0)
+        cnt = np.maximum(ng_a, 1)
+        ps_mean = p0.sum(1) / cnt
+        ps_final = P3[np.arange(nc), np.maximum(ng_a - 1, 0), 0]
+        ps_max = np.where(valid, P3[:, :, 0], -np.inf).max(1) if nc else np.zeros(0)
+        decoy = (np.where(valid[:, :, None], P3[:, :, 2:], 0.0).sum(1) / cnt[:, None]) if K > 2 else None
         results = []
         for b, (c, p) in enumerate(zip(batch, cell_pairs)):
             ng, d, resp, pos_c, sn, nll = cell[b]
-            Kp = len(p.track)
-            probs = np.zeros((ng, Kp), dtype=np.float32)
-            keep = min(d, ng, len(p.resp))
-            if keep:
-                probs[:keep] = p.track_probs[:keep, :Kp]
-            if pos_c.size:
-                probs[pos_c] = pr[offs[b]:offs[b + 1], :Kp]
             topk = ih[b].tolist() if ng > 0 and vh[b] > 0 else []
-            results.append(self._cell_result(c, p, ng, resp, probs, topk, nll, sn))
+            stats = (float(ps_mean[b]), float(ps_final[b]), float(ps_max[b])) if ng else (0.0, 0.0, 0.0)
+            dec = decoy[b, : len(p.track) - 2].tolist() if (decoy is not None and ng and len(p.track) > 2) else []
+            results.append(self._cell_record(c, p, ng, resp, stats, dec, topk, nll, sn))
         return results
 
     def _lens_base(self, cell_pairs: Sequence[Pair], Dc: Sequence[int], ngen: Sequence[int]) -> torch.Tensor:
@@ -832,6 +867,12 @@ class SweepRunner:
     def _cell_result(self, c: Cell, p: Pair, n_gen: int, resp: List[int], probs: np.ndarray, topk_ids: List[int],
                      nll_edit: float, nll_self: float) -> dict:
         ps = probs[:, 0] if probs.shape[0] else np.zeros(0, dtype=np.float32)
+        stats = (float(ps.mean()), float(ps[-1]), float(ps.max())) if ps.size else (0.0, 0.0, 0.0)
+        dec = [float(x) for x in probs[:, 2:].mean(0)] if probs.shape[0] else []
+        return self._cell_record(c, p, n_gen, resp, stats, dec, topk_ids, nll_edit, nll_self)
+
+    def _cell_record(self, c: Cell, p: Pair, n_gen: int, resp: List[int], stats: Tuple[float, float, float],
+                     decoy: List[float], topk_ids: List[int], nll_edit: float, nll_self: float) -> dict:
         dc = self._dec_cache
         guesses = []
         for t in topk_ids:
@@ -839,22 +880,23 @@ class SweepRunner:
             if g is None:
                 g = dc[t] = self.tok.decode([t]).strip()
             guesses.append(g)
-        if resp == p.resp:                  # unchanged response: the baseline's leak verdict
+        if resp is p.resp or resp == p.resp:     # unchanged response: the baseline's leak verdict
             if p.leak is None:
                 p.leak = contains_secret(self.tok.decode(p.resp), p.forms)
             leak = p.leak
         else:
             leak = contains_secret(self.tok.decode(resp), p.forms)
+        if p.p_secret_mean is None:
+            p.p_secret_mean = float(p.p_secret.mean()) if p.p_secret is not None and p.p_secret.size else 0.0
+            p.forms_l = {f.lower() for f in p.forms}
         return {
             "word": p.word, "prompt_idx": p.pidx, "method": c.method, "budget": c.budget, "trial": c.trial,
             "seed": c.seed, "n_gen": n_gen, "spikes": p.spikes_rel,
-            "p_secret_mean": float(ps.mean()) if ps.size else 0.0,
-            "p_secret_final": float(ps[-1]) if ps.size else 0.0,
-            "p_secret_max": float(ps.max()) if ps.size else 0.0,
-            "p_secret_mean_base": float(p.p_secret.mean()) if p.p_secret is not None and p.p_secret.size else 0.0,
+            "p_secret_mean": stats[0], "p_secret_final": stats[1], "p_secret_max": stats[2],
+            "p_secret_mean_base": p.p_secret_mean,
             "topk_ids": topk_ids, "guesses": guesses,
-            "secret_in_topk": any(g.lower() in {f.lower() for f in p.forms} for g in guesses),
-            "decoy_probs": [float(x) for x in probs[:, 2:].mean(0)] if probs.shape[0] else [],
+            "secret_in_topk": any(g.lower() in p.forms_l for g in guesses),
+            "decoy_probs": decoy,
             "leak": leak,
             "nll_edit": nll_edit, "nll_base": p.nll, "delta_nll": nll_edit - p.nll,
             "nll_self": nll_self,
