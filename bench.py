@@ -85,9 +85,10 @@ def main() -> None:
     cfg.experiment.max_new_tokens = args.max_new
     cfg.intervention.measure_nll = not args.no_nll
     P = args.pairs_per_step
+    E = max(e for e in range(1, max(1, args.baseline_every) + 1) if args.steps % e == 0)
 
     torch.manual_seed(0)
-    tag = f"{spec.name}_P{P}_new{args.max_new}"
+    tag = f"{spec.name}_P{P}_E{E}_new{args.max_new}"
     if on_gpu and not args.no_tuned_gemms:
         enable_tuned_gemms(tag, tune=args.tune_gemms)
     weights = random_gemma2(spec, device=dev, dtype=torch.bfloat16, seed=1234)
@@ -101,7 +102,6 @@ def main() -> None:
     sae = JumpReLUSAE.random(spec.hidden, cfg.sae.d_sae, seed=7, device=dev)
     layer = min(cfg.model.layer_idx, spec.layers - 1)
     n_cells = len(cfg.intervention.budgets) * (1 + cfg.intervention.random_trials)
-    E = max(e for e in range(1, max(1, args.baseline_every) + 1) if args.steps % e == 0)
     batch = P * n_cells + E * P
     runner = SweepRunner(cfg, model, tok, sae, batch=batch, device=dev, layer=layer,
                          use_graphs=not args.no_graphs, prefix_share=not args.no_prefix_share,
