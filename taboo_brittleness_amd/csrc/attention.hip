@@ -17,6 +17,8 @@
 //    transposed-read bank conflicts) and read with ds_read_b64_tr_b16 as the
 //    B operand (cdna_hip_programming.md T10).
 // Rows with pos < 0 (padding) produce zeros.
+#include <stdlib.h>
+
 #include "common.h"
 #include "api.h"
 
@@ -39,11 +41,15 @@ __device__ __forceinline__ v4i16 ds_read_tr16(const uint16_t* lds_ptr) {
 
 __device__ __forceinline__ bf16x8 as_bf16x8(const uint4& u) { return __builtin_bit_cast(bf16x8, u); }
 
-template <int HD, int G>
+// SPLIT = true: the 4 waves of a workgroup split one (query block, kv head) item's key range and merge
+// through LDS (long contexts).  SPLIT = false (block-table mode only): every wave owns its own item and
+// walks all of its keys — for short contexts (the sweep's teacher-forced tails: <= ~100 keys) where
+// a 4-way key split leaves waves idle and the merge costs more than it saves.
+template <int HD, int G, bool SPLIT = true>
 __global__ void __launch_bounds__(256) attn_cache_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
     uint16_t* __restrict__ out, const int32_t* __restrict__ pos, const int32_t* __restrict__ slot, int T, int Hq,
-    int Hkv, int S, float scale, float softcap, int window, const int32_t* __restrict__ blk) {
+    int Hkv, int S, float scale, float softcap, int window, const int32_t* __restrict__ blk, int nitems = 0) {
   constexpr int P = 16 / G;        // query positions per workgroup
   constexpr int KS = HD / 32;      // MFMA k-steps over head_dim
   constexpr int DT = HD / 16;      // 16-wide output dim tiles
@@ -57,9 +63,17 @@ __global__ void __launch_bounds__(256) attn_cache_kernel(
 
   // Row geometry: dense [B, T] layout (blk == nullptr) or a ragged block table blk[i] =
   // {first row, rows (<= P), cache slot} over packed rows (varlen prefill / teacher forcing).
-  const int kh = blockIdx.y;
+  int kh = blockIdx.y;
   int rbase, nvalid, cs;
-  if (blk != nullptr) {
+  if constexpr (!SPLIT) {
+    const int item = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (item >= nitems) return;                 // wave-uniform; no workgroup barrier in this variant
+    const int bi = item / Hkv;
+    kh = item % Hkv;
+    rbase = blk[3 * bi];
+    nvalid = blk[3 * bi + 1];
+    cs = blk[3 * bi + 2];
+  } else if (blk != nullptr) {
     rbase = blk[3 * blockIdx.x];
     nvalid = blk[3 * blockIdx.x + 1];
     cs = blk[3 * blockIdx.x + 2];
@@ -120,7 +134,7 @@ __global__ void __launch_bounds__(256) attn_cache_kernel(
   uint16_t* plds = plds_all + wid * 16 * PSTR;
   const float inv_cap = softcap > 0.f ? 1.f / softcap : 0.f;
 
-  for (int kb = kstart + wid * 32; kb <= kmax; kb += 4 * 32) {
+  for (int kb = kstart + (SPLIT ? wid * 32 : 0); kb <= kmax; kb += (SPLIT ? 4 * 32 : 32)) {
     // ---- stage V block (32 keys x HD) into this wave's LDS, coalesced 1 KB per instruction
     constexpr int VCH = HD / 8;                // 16-B chunks per key row
     constexpr int VIT = 32 * VCH / 64;         // instructions per lane
@@ -217,6 +231,28 @@ __global__ void __launch_bounds__(256) attn_cache_kernel(
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
 
+  if constexpr (!SPLIT) {
+    // own item: normalise in registers, transpose through this wave's staging LDS, 16-B stores
+    uint16_t* ob = vlds;                                  // [16][HD] bf16 <= 32 * VSTR halves
+    float inv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) inv[i] = l_r[i] > 0.f ? 1.f / l_r[i] : 0.f;
+#pragma unroll
+    for (int d = 0; d < DT; ++d)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ob[(4 * grp + i) * HD + d * 16 + col] = f2bf(o_acc[d][i] * inv[i]);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int e = lane; e < 16 * (HD / 8); e += 64) {
+      const int r = e / (HD / 8), c8 = (e % (HD / 8)) * 8;
+      const int t = r / G, h = kh * G + (r % G);
+      if (t < nvalid)
+        *reinterpret_cast<uint4*>(out + (((size_t)rbase + t) * Hq + h) * HD + c8) =
+            *reinterpret_cast<const uint4*>(ob + r * HD + c8);
+    }
+    return;
+  }
   // ---- merge the 4 waves: publish (m, l) and O (fp32, reusing the V staging area)
   __syncthreads();
   float* ofin = reinterpret_cast<float*>(smem);   // [4][16][HD] fp32 = 64 KB for HD=256
@@ -272,15 +308,28 @@ void launch_attn(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, uint
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
+  static const bool force_split = getenv("TB_ATTN_SPLIT") != nullptr && getenv("TB_ATTN_SPLIT")[0] == '1';
+  if (blk != nullptr && S <= 512 && !force_split) {
+    static bool attr_short = false;
+    if (!attr_short) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_cache_kernel<HD, G, false>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      attr_short = true;
+    }
+    const int nitems = nblk * Hkv;
+    hipLaunchKernelGGL((attn_cache_kernel<HD, G, false>), dim3((nitems + 3) / 4), dim3(256), lds, st, q, kc, vc, out,
+                       pos, slot, T, Hq, Hkv, S, scale, softcap, window, blk, nitems);
+    return;
+  }
   if (blk != nullptr) {
     dim3 grid(nblk, Hkv, 1);
     hipLaunchKernelGGL((attn_cache_kernel<HD, G>), grid, dim3(256), lds, st, q, kc, vc, out, pos, slot, T, Hq, Hkv,
-                       S, scale, softcap, window, blk);
+                       S, scale, softcap, window, blk, 0);
     return;
   }
   dim3 grid((T + P - 1) / P, Hkv, B);
   hipLaunchKernelGGL((attn_cache_kernel<HD, G>), grid, dim3(256), lds, st, q, kc, vc, out, pos, slot, T, Hq, Hkv, S,
-                     scale, softcap, window, (const int32_t*)nullptr);
+                     scale, softcap, window, (const int32_t*)nullptr, 0);
 }
 
 

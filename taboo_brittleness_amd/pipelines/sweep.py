@@ -128,6 +128,7 @@ class SweepRunner:
         self._dec_cache: Dict[int, str] = {}
         self.layer_resume = cfg.runtime.layer_resume if layer_resume is None else layer_resume
         self.overlap_ride = os.environ.get("TB_OVERLAP_RIDE", "1") == "1"
+        self.tf_streams = os.environ.get("TB_TF_STREAMS", "1") == "1"
         self.stats: Dict[str, int] = {"cells": 0, "diverged": 0, "tf_rows": 0, "lens_rows": 0}
         self._with_basis = True
 
@@ -833,32 +834,48 @@ class SweepRunner:
         rpb = 16 // max(1, m.lspec.heads // m.lspec.kv_heads)
         cap = 32768
         step = max(256, ((1 << 30) // (m.spec.vocab_size * 2)) // 256 * 256)     # 256-row multiples (GEMM tiles)
-        seqs = []
+        # chunks of whole cells (a cell never spans two chunks), so chunks are independent and
+        # alternate between two streams: one chunk's bandwidth-bound kernels (attention, norms, GeGLU,
+        # vocab head) overlap the other's GEMMs
+        chunks, cur, c_lo, c_rows = [], [], 0, 0
         for b, (f, E, r0) in enumerate(seg):
-            if E >= f:
-                seqs.append((r0, E - f + 1, b))
-        for c0 in range(0, M, cap):
-            c1 = min(M, c0 + cap)
-            Mc = c1 - c0
-            Mp = -(-Mc // 256) * 256
-            chunk = []
-            for (s0, Ln, b) in seqs:
-                a0, a1 = max(s0, c0), min(s0 + Ln, c1)
-                if a1 > a0:
-                    chunk.append((a0 - c0, a1 - a0, b))
-            blk = packed_blocks(chunk, rpb).to(dev)
-            cp = torch.full((Mp,), -1, dtype=torch.int32, device=dev)
-            cs = torch.zeros(Mp, dtype=torch.int32, device=dev)
-            hin = torch.zeros(Mp, H.shape[1], dtype=H.dtype, device=dev)
-            cp[:Mc], cs[:Mc], hin[:Mc] = pos_d[c0:c1], slot_d[c0:c1], H[c0:c1]
-            ws = self._nll_ws(min(cap, -(-M // 256) * 256)).rows(Mp)
-            x = m.forward_packed(None, cp, cs, blk, self.gen.cache, hooks, ws=ws, resume_after=self.layer,
-                                 h_in=hin)
-            for q0 in range(0, Mc, step):
-                q1 = min(Mc, q0 + step)
-                lg = m.logits(x[q0:q1])
-                ops.decode_head(lg, m.spec.final_softcap, tgt_d[c0 + q0:c0 + q1], nxt[c0 + q0:c0 + q1],
-                                ns[c0 + q0:c0 + q1], nt[c0 + q0:c0 + q1])
+            if E < f:
+                continue
+            Ln = E - f + 1
+            if cur and c_rows + Ln > cap:
+                chunks.append((c_lo, c_lo + c_rows, cur))
+                cur, c_lo, c_rows = [], r0, 0
+            if not cur:
+                c_lo = r0
+            cur.append((r0 - c_lo, Ln, b))
+            c_rows += Ln
+        if cur:
+            chunks.append((c_lo, c_lo + c_rows, cur))
+        main = torch.cuda.current_stream(dev) if dev.type == "cuda" else None
+        streams = [main] if main is None or len(chunks) < 2 or not self.tf_streams else [main, self._tf_stream()]
+        if len(streams) > 1:
+            streams[1].wait_stream(main)
+        ws_rows = min(cap, -(-M // 256) * 256)
+        for ci, (c0, c1, chunk) in enumerate(chunks):
+            st = streams[ci % len(streams)]
+            with (torch.cuda.stream(st) if st is not None else _nullctx()):
+                Mc = c1 - c0
+                Mp = -(-Mc // 256) * 256
+                blk = packed_blocks(chunk, rpb).to(dev)
+                cp = torch.full((Mp,), -1, dtype=torch.int32, device=dev)
+                cs = torch.zeros(Mp, dtype=torch.int32, device=dev)
+                hin = torch.zeros(Mp, H.shape[1], dtype=H.dtype, device=dev)
+                cp[:Mc], cs[:Mc], hin[:Mc] = pos_d[c0:c1], slot_d[c0:c1], H[c0:c1]
+                ws = self._nll_ws(ws_rows, key=ci % len(streams)).rows(Mp)
+                x = m.forward_packed(None, cp, cs, blk, self.gen.cache, hooks, ws=ws, resume_after=self.layer,
+                                     h_in=hin)
+                for q0 in range(0, Mc, step):
+                    q1 = min(Mc, q0 + step)
+                    lg = m.logits(x[q0:q1])
+                    ops.decode_head(lg, m.spec.final_softcap, tgt_d[c0 + q0:c0 + q1], nxt[c0 + q0:c0 + q1],
+                                    ns[c0 + q0:c0 + q1], nt[c0 + q0:c0 + q1])
+        if len(streams) > 1:
+            main.wait_stream(streams[1])
         res["nxt"] = nxt.cpu().numpy()
         res["nll_self"] = ns.cpu().numpy()
         res["nll_tgt"] = nt.cpu().numpy()
@@ -903,15 +920,22 @@ class SweepRunner:
             "response_ids": resp,
         }
 
-    def _nll_ws(self, M: int):
-        """Workspace for the ragged NLL pass, grown in 4096-row steps and sliced per chunk."""
-        ws = getattr(self, "_nll_wsp", None)
+    def _nll_ws(self, M: int, key: int = 0):
+        """Workspace for the ragged passes (one per stream ``key``), grown in 4096-row steps and sliced
+        per chunk."""
+        pool = self.__dict__.setdefault("_nll_wsp", {})
+        ws = pool.get(key)
         if ws is None or ws.M < M:
             from ..models.gemma2 import _Workspace
 
-            self._nll_wsp = None
-            ws = self._nll_wsp = _Workspace(self.m.lspec, -(-M // 4096) * 4096, self.dev, self.m.dtype)
+            pool.pop(key, None)
+            ws = pool[key] = _Workspace(self.m.lspec, -(-M // 4096) * 4096, self.dev, self.m.dtype)
         return ws
+
+    def _tf_stream(self):
+        if getattr(self, "_tf2", None) is None:
+            self._tf2 = torch.cuda.Stream(device=self.dev)
+        return self._tf2
 
     @torch.no_grad()
     def _nll_cells(self, cell_pairs: Sequence[Pair], plan_hook: EditHook, out, c0s: Sequence[int]) -> List[float]:
@@ -985,6 +1009,14 @@ class SweepRunner:
             extra = torch.zeros(nc, device=dev).index_add_(0, slot_d.long(), nll).cpu().tolist()
             sums = [a + e for a, e in zip(sums, extra)]
         return [sums[b] / len(p.resp) if p.resp else float("nan") for b, p in enumerate(cell_pairs)]
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
 
 
 def _cat_outputs(a, b):
