@@ -128,7 +128,7 @@ class SweepRunner:
         self._dec_cache: Dict[int, str] = {}
         self.layer_resume = cfg.runtime.layer_resume if layer_resume is None else layer_resume
         self.overlap_ride = os.environ.get("TB_OVERLAP_RIDE", "1") == "1"
-        self.tf_streams = os.environ.get("TB_TF_STREAMS", "1") == "1"
+        self.tf_streams = os.environ.get("TB_TF_STREAMS", "0") == "1"   # no measurable gain; opt-in
         self.stats: Dict[str, int] = {"cells": 0, "diverged": 0, "tf_rows": 0, "lens_rows": 0}
         self._with_basis = True
 
