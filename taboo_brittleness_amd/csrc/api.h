@@ -36,6 +36,7 @@ void tb_lens_colsum(const uint16_t* logits, const float* lse, const uint8_t* mas
 void tb_topk_rows(const float* x, float* vals, int32_t* idx, int R, int V, int K, hipStream_t st);
 void tb_xent_rows(const uint16_t* logits, const int32_t* tgt, float* nll, int R, int V, float cap, int emulate_bf16,
                   hipStream_t st);
+void tb_register_softcap_table(float cap, const uint16_t* tab);   // [32768] bf16 softcap of +bf16 bit patterns
 void tb_decode_head(const uint16_t* logits, const int32_t* tgt, int32_t* nxt, float* nll_self, float* nll_tgt, int R,
                     int V, float cap, hipStream_t st);
 // skinny.hip

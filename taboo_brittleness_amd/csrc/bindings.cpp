@@ -196,6 +196,13 @@ void xent_rows(torch::Tensor logits, torch::Tensor tgt, torch::Tensor nll, doubl
                cur_stream());
 }
 
+void register_softcap_table(torch::Tensor tab, double cap) {
+  CHECK_DEV(tab); CHECK_CONTIG(tab);
+  TORCH_CHECK(tab.scalar_type() == at::kBFloat16 && tab.numel() == 32768, "softcap table: 32768 bf16 entries");
+  c10::DeviceGuard g(tab.device());
+  tb_register_softcap_table((float)cap, reinterpret_cast<const uint16_t*>(tab.data_ptr()));
+}
+
 void decode_head(torch::Tensor logits, c10::optional<torch::Tensor> tgt, torch::Tensor nxt, torch::Tensor nll_self,
                  c10::optional<torch::Tensor> nll_tgt, double cap) {
   IN_BF16(logits); IN_I32(nxt); IN_F32(nll_self);
@@ -319,6 +326,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("topk_rows", &topk_rows);
   m.def("xent_rows", &xent_rows);
   m.def("decode_head", &decode_head);
+  m.def("register_softcap_table", &register_softcap_table);
   m.def("gemm_nt", &gemm_nt);
   m.def("gemm_skinny", &gemm_skinny);
   m.def("gemm_skinny_ok", &gemm_skinny_ok);

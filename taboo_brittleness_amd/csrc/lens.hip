@@ -40,6 +40,50 @@ __device__ __forceinline__ float softcap_bf16(float x, float cap) {
   return rbf(rbf(fast_tanh(rbf(x / cap))) * cap);
 }
 
+// ---- exact bf16 softcap by table ------------------------------------------------------------
+// softcap_bf16 is a pure function of its bf16 input bits and odd, so the 32768 results for the
+// non-negative bit patterns (built on the host with the reference op, registered per cap value)
+// make it one LDS lookup per element instead of ~25 VALU ops (the vocab-wide passes were
+// VALU-bound on it).  Every kernel that applies the emulated softcap copies the 64 KB table to LDS.
+constexpr int CTAB_N = 32768;
+
+__device__ __forceinline__ const uint16_t* stage_ctab(const uint16_t* tab, uint16_t* lds) {
+  if (tab == nullptr) return nullptr;
+  for (int i = threadIdx.x; i < CTAB_N / 8; i += blockDim.x)
+    reinterpret_cast<uint4*>(lds)[i] = reinterpret_cast<const uint4*>(tab)[i];
+  __syncthreads();
+  return lds;
+}
+
+__device__ __forceinline__ float ctab_get(const uint16_t* ct, uint32_t b) {
+  return __uint_as_float(((uint32_t)ct[b & 0x7fffu] | (b & 0x8000u)) << 16);
+}
+
+// 8 logits of a uint4 -> capped fp32 (table, emulated compute, fp32 tanh, or none)
+__device__ __forceinline__ void capped8(const uint4& v, float* f, const uint16_t* ct, float cap, int emu) {
+  if (ct != nullptr) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      f[2 * k] = ctab_get(ct, w[k] & 0xffffu);
+      f[2 * k + 1] = ctab_get(ct, w[k] >> 16);
+    }
+    return;
+  }
+  unpack8(v, f);
+  if (cap > 0.f) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = emu ? softcap_bf16(f[j], cap) : fast_tanh(f[j] / cap) * cap;
+  }
+}
+
+__device__ __forceinline__ float capped1(uint16_t b, const uint16_t* ct, float cap, int emu) {
+  if (ct != nullptr) return ctab_get(ct, b);
+  const float x = bf2f(b);
+  if (cap <= 0.f) return x;
+  return emu ? softcap_bf16(x, cap) : fast_tanh(x / cap) * cap;
+}
+
 struct ArgBest {
   float v;
   int i;
@@ -50,23 +94,23 @@ __device__ __forceinline__ ArgBest better(ArgBest a, ArgBest b) {
 }
 
 __global__ void __launch_bounds__(512) argmax_rows_kernel(const uint16_t* __restrict__ logits,
-                                                          int32_t* __restrict__ out, int V, float cap) {
+                                                          int32_t* __restrict__ out, int V, float cap,
+                                                          const uint16_t* __restrict__ tab) {
   __shared__ float sv[8];
   __shared__ int si[8];
+  extern __shared__ __attribute__((aligned(16))) uint16_t ctab_lds[];
+  const uint16_t* ct = stage_ctab(tab, ctab_lds);
   const uint16_t* row = logits + (size_t)blockIdx.x * V;
   ArgBest best{-INFINITY, 0x7fffffff};
   const int nv = V >> 3;
   for (int c = threadIdx.x; c < nv; c += blockDim.x) {
     float f[8];
-    unpack8(reinterpret_cast<const uint4*>(row)[c], f);
+    capped8(reinterpret_cast<const uint4*>(row)[c], f, ct, cap, 1);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float x = cap > 0.f ? softcap_bf16(f[j], cap) : f[j];
-      best = better(best, ArgBest{x, c * 8 + j});
-    }
+    for (int j = 0; j < 8; ++j) best = better(best, ArgBest{f[j], c * 8 + j});
   }
   for (int c = nv * 8 + threadIdx.x; c < V; c += blockDim.x) {
-    const float x = cap > 0.f ? softcap_bf16(bf2f(row[c]), cap) : bf2f(row[c]);
+    const float x = capped1(row[c], ct, cap, 1);
     best = better(best, ArgBest{x, c});
   }
 #pragma unroll
@@ -100,28 +144,27 @@ __device__ __forceinline__ void online_merge(float& m, float& s, float m2, float
 }
 
 __global__ void __launch_bounds__(512) row_lse_kernel(const uint16_t* __restrict__ logits, float* __restrict__ lse,
-                                                      int V, float cap, int emulate_bf16) {
+                                                      int V, float cap, int emulate_bf16,
+                                                      const uint16_t* __restrict__ tab) {
   __shared__ float sm[8], ss[8];
+  extern __shared__ __attribute__((aligned(16))) uint16_t ctab_lds[];
+  const uint16_t* ct = stage_ctab(tab, ctab_lds);
   const uint16_t* row = logits + (size_t)blockIdx.x * V;
   float m = -INFINITY, s = 0.f;
   const int nv = V >> 3;
   for (int c = threadIdx.x; c < nv; c += blockDim.x) {
     float f[8];
-    unpack8(reinterpret_cast<const uint4*>(row)[c], f);
+    capped8(reinterpret_cast<const uint4*>(row)[c], f, ct, cap, emulate_bf16);
     float lm = -INFINITY;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      if (cap > 0.f) f[j] = emulate_bf16 ? softcap_bf16(f[j], cap) : fast_tanh(f[j] / cap) * cap;
-      lm = fmaxf(lm, f[j]);
-    }
+    for (int j = 0; j < 8; ++j) lm = fmaxf(lm, f[j]);
     float ls = 0.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) ls += __expf(f[j] - lm);
     online_merge(m, s, lm, ls);
   }
   for (int c = nv * 8 + threadIdx.x; c < V; c += blockDim.x) {
-    float x = bf2f(row[c]);
-    if (cap > 0.f) x = emulate_bf16 ? softcap_bf16(x, cap) : fast_tanh(x / cap) * cap;
+    const float x = capped1(row[c], ct, cap, emulate_bf16);
     if (m == -INFINITY) { m = x; s = 1.f; } else online_add(m, s, x);
   }
 #pragma unroll
@@ -263,7 +306,8 @@ __global__ void __launch_bounds__(256) topk_rows_kernel(const float* __restrict_
 
 __global__ void __launch_bounds__(512) xent_rows_kernel(const uint16_t* __restrict__ logits,
                                                         const int32_t* __restrict__ tgt, float* __restrict__ nll,
-                                                        int V, float cap, int emulate_bf16) {
+                                                        int V, float cap, int emulate_bf16,
+                                                        const uint16_t* __restrict__ tab) {
   __shared__ float sm[8], ss[8];
   const int r = blockIdx.x;
   const int t = tgt[r];
@@ -271,26 +315,24 @@ __global__ void __launch_bounds__(512) xent_rows_kernel(const uint16_t* __restri
     if (threadIdx.x == 0) nll[r] = 0.f;
     return;
   }
+  extern __shared__ __attribute__((aligned(16))) uint16_t ctab_lds[];
+  const uint16_t* ct = stage_ctab(tab, ctab_lds);
   const uint16_t* row = logits + (size_t)r * V;
   float m = -INFINITY, s = 0.f;
   const int nv = V >> 3;
   for (int c = threadIdx.x; c < nv; c += blockDim.x) {
     float f[8];
-    unpack8(reinterpret_cast<const uint4*>(row)[c], f);
+    capped8(reinterpret_cast<const uint4*>(row)[c], f, ct, cap, emulate_bf16);
     float lm = -INFINITY;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      if (cap > 0.f) f[j] = emulate_bf16 ? softcap_bf16(f[j], cap) : fast_tanh(f[j] / cap) * cap;
-      lm = fmaxf(lm, f[j]);
-    }
+    for (int j = 0; j < 8; ++j) lm = fmaxf(lm, f[j]);
     float ls = 0.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) ls += __expf(f[j] - lm);
     online_merge(m, s, lm, ls);
   }
   for (int c = nv * 8 + threadIdx.x; c < V; c += blockDim.x) {
-    float x = bf2f(row[c]);
-    if (cap > 0.f) x = emulate_bf16 ? softcap_bf16(x, cap) : fast_tanh(x / cap) * cap;
+    const float x = capped1(row[c], ct, cap, emulate_bf16);
     if (m == -INFINITY) { m = x; s = 1.f; } else online_add(m, s, x);
   }
 #pragma unroll
@@ -304,8 +346,7 @@ __global__ void __launch_bounds__(512) xent_rows_kernel(const uint16_t* __restri
   if (threadIdx.x == 0) {
     float M = sm[0], Ssum = ss[0];
     for (int w = 1; w < (int)(blockDim.x >> 6); ++w) online_merge(M, Ssum, sm[w], ss[w]);
-    float zt = bf2f(row[t]);
-    if (cap > 0.f) zt = emulate_bf16 ? softcap_bf16(zt, cap) : fast_tanh(zt / cap) * cap;
+    const float zt = capped1(row[t], ct, cap, emulate_bf16);
     nll[r] = (M + __logf(Ssum)) - zt;
   }
 }
@@ -313,9 +354,11 @@ __global__ void __launch_bounds__(512) xent_rows_kernel(const uint16_t* __restri
 __global__ void __launch_bounds__(512) decode_head_kernel(const uint16_t* __restrict__ logits,
                                                           const int32_t* __restrict__ tgt, int32_t* __restrict__ nxt,
                                                           float* __restrict__ nll_self, float* __restrict__ nll_tgt,
-                                                          int V, float cap) {
+                                                          int V, float cap, const uint16_t* __restrict__ tab) {
   __shared__ float sm[8], ss[8], sv[8];
   __shared__ int si[8];
+  extern __shared__ __attribute__((aligned(16))) uint16_t ctab_lds[];
+  const uint16_t* ct = stage_ctab(tab, ctab_lds);
   const int r = blockIdx.x;
   const uint16_t* row = logits + (size_t)r * V;
   float m = -INFINITY, s = 0.f;
@@ -323,11 +366,10 @@ __global__ void __launch_bounds__(512) decode_head_kernel(const uint16_t* __rest
   const int nv = V >> 3;
   for (int c = threadIdx.x; c < nv; c += blockDim.x) {
     float f[8];
-    unpack8(reinterpret_cast<const uint4*>(row)[c], f);
+    capped8(reinterpret_cast<const uint4*>(row)[c], f, ct, cap, 1);
     float lm = -INFINITY;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      if (cap > 0.f) f[j] = softcap_bf16(f[j], cap);
       lm = fmaxf(lm, f[j]);
       best = better(best, ArgBest{f[j], c * 8 + j});
     }
@@ -337,7 +379,7 @@ __global__ void __launch_bounds__(512) decode_head_kernel(const uint16_t* __rest
     online_merge(m, s, lm, ls);
   }
   for (int c = nv * 8 + threadIdx.x; c < V; c += blockDim.x) {
-    const float x = cap > 0.f ? softcap_bf16(bf2f(row[c]), cap) : bf2f(row[c]);
+    const float x = capped1(row[c], ct, cap, 1);
     best = better(best, ArgBest{x, c});
     if (m == -INFINITY) { m = x; s = 1.f; } else online_add(m, s, x);
   }
@@ -364,28 +406,74 @@ __global__ void __launch_bounds__(512) decode_head_kernel(const uint16_t* __rest
     if (nll_tgt != nullptr) {
       const int t = tgt[r];
       float zt = 0.f;
-      if (t >= 0 && t < V) zt = cap > 0.f ? softcap_bf16(bf2f(row[t]), cap) : bf2f(row[t]);
+      if (t >= 0 && t < V) zt = capped1(row[t], ct, cap, 1);
       nll_tgt[r] = (t >= 0 && t < V) ? lse - zt : 0.f;
     }
   }
 }
 
+// softcap tables registered from the host, keyed by (device, cap bits)
+struct CapTab {
+  int dev;
+  uint32_t capbits;
+  const uint16_t* ptr;
+};
+CapTab g_tabs[16];
+int g_ntabs = 0;
+
+const uint16_t* find_tab(float cap, int emulate) {
+  if (!(cap > 0.f) || !emulate) return nullptr;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  const uint32_t cb = __builtin_bit_cast(uint32_t, cap);
+  for (int i = 0; i < g_ntabs; ++i)
+    if (g_tabs[i].dev == dev && g_tabs[i].capbits == cb) return g_tabs[i].ptr;
+  return nullptr;
+}
+
+size_t tab_lds(const void* kernel, const uint16_t* tab, bool& attr_done) {
+  if (tab == nullptr) return 0;
+  if (!attr_done) {   // > 64 KB of LDS needs the opt-in; first call is never inside a graph capture
+    (void)hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, CTAB_N * 2 + 256);
+    attr_done = true;
+  }
+  return CTAB_N * 2;
+}
+
 }  // namespace
+
+void tb_register_softcap_table(float cap, const uint16_t* tab) {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  const uint32_t cb = __builtin_bit_cast(uint32_t, cap);
+  for (int i = 0; i < g_ntabs; ++i)
+    if (g_tabs[i].dev == dev && g_tabs[i].capbits == cb) { g_tabs[i].ptr = tab; return; }
+  if (g_ntabs < 16) g_tabs[g_ntabs++] = CapTab{dev, cb, tab};
+}
 
 void tb_decode_head(const uint16_t* logits, const int32_t* tgt, int32_t* nxt, float* nll_self, float* nll_tgt, int R,
                     int V, float cap, hipStream_t st) {
   if (R <= 0) return;
-  hipLaunchKernelGGL(decode_head_kernel, dim3(R), dim3(512), 0, st, logits, tgt, nxt, nll_self, nll_tgt, V, cap);
+  const uint16_t* tab = find_tab(cap, 1);
+  static bool attr_decode_head_kernel = false;
+  hipLaunchKernelGGL(decode_head_kernel, dim3(R), dim3(512), tab_lds(reinterpret_cast<const void*>(decode_head_kernel), tab, attr_decode_head_kernel), st, logits, tgt, nxt,
+                     nll_self, nll_tgt, V, cap, tab);
 }
 
 void tb_argmax_rows(const uint16_t* logits, int32_t* out, int R, int V, float cap, hipStream_t st) {
   if (R <= 0) return;
-  hipLaunchKernelGGL(argmax_rows_kernel, dim3(R), dim3(512), 0, st, logits, out, V, cap);
+  const uint16_t* tab = find_tab(cap, 1);
+  static bool attr_argmax_rows_kernel = false;
+  hipLaunchKernelGGL(argmax_rows_kernel, dim3(R), dim3(512), tab_lds(reinterpret_cast<const void*>(argmax_rows_kernel), tab, attr_argmax_rows_kernel), st, logits, out, V, cap,
+                     tab);
 }
 
 void tb_row_lse(const uint16_t* logits, float* lse, int R, int V, float cap, int emulate_bf16, hipStream_t st) {
   if (R <= 0) return;
-  hipLaunchKernelGGL(row_lse_kernel, dim3(R), dim3(512), 0, st, logits, lse, V, cap, emulate_bf16);
+  const uint16_t* tab = find_tab(cap, emulate_bf16);
+  static bool attr_row_lse_kernel = false;
+  hipLaunchKernelGGL(row_lse_kernel, dim3(R), dim3(512), tab_lds(reinterpret_cast<const void*>(row_lse_kernel), tab, attr_row_lse_kernel), st, logits, lse, V, cap,
+                     emulate_bf16, tab);
 }
 
 void tb_gather_probs(const uint16_t* logits, const float* lse, const int32_t* ids, float* out, int R, int K, int V,
@@ -416,5 +504,8 @@ void tb_topk_rows(const float* x, float* vals, int32_t* idx, int R, int V, int K
 void tb_xent_rows(const uint16_t* logits, const int32_t* tgt, float* nll, int R, int V, float cap, int emulate_bf16,
                   hipStream_t st) {
   if (R <= 0) return;
-  hipLaunchKernelGGL(xent_rows_kernel, dim3(R), dim3(512), 0, st, logits, tgt, nll, V, cap, emulate_bf16);
+  const uint16_t* tab = find_tab(cap, emulate_bf16);
+  static bool attr_xent_rows_kernel = false;
+  hipLaunchKernelGGL(xent_rows_kernel, dim3(R), dim3(512), tab_lds(reinterpret_cast<const void*>(xent_rows_kernel), tab, attr_xent_rows_kernel), st, logits, tgt, nll, V,
+                     cap, emulate_bf16, tab);
 }

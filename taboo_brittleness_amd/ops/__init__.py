@@ -28,6 +28,22 @@ def _out(out: Optional[torch.Tensor], shape, dtype, device) -> torch.Tensor:
     return out
 
 
+_CAP_TABLES = {}
+
+
+def _softcap_table(cap: float, device) -> None:
+    """Register the exact bf16 softcap table for ``cap`` on ``device`` (built once with the reference
+    op, so the GPU lookup reproduces it bit for bit); used by every emulated-softcap vocab kernel."""
+    key = (float(cap), device.index if device.index is not None else torch.cuda.current_device())
+    if key in _CAP_TABLES or not (cap > 0):
+        return
+    bits = torch.arange(32768, dtype=torch.int32).to(torch.int16)
+    x = bits.view(BF16)
+    tab = ref.softcap_bf16(x, float(cap)).to(BF16).contiguous().to(device)
+    _k().register_softcap_table(tab, float(cap))
+    _CAP_TABLES[key] = tab        # keep alive: kernels (and captured graphs) hold its pointer
+
+
 SKINNY_MAX_M = int(os.environ.get("TB_SKINNY_MAX_M", "0"))   # v1 kernel loses to hipBLASLt: opt-in
 
 
@@ -143,6 +159,7 @@ def geglu(gu, out=None):
 
 def argmax_rows(logits, cap=0.0, out=None):
     if logits.is_cuda:
+        _softcap_table(cap, logits.device)
         out = _out(out, logits.shape[:-1], torch.int32, logits.device)
         _k().argmax_rows(logits, out, float(cap))
         return out
@@ -155,6 +172,8 @@ def argmax_rows(logits, cap=0.0, out=None):
 
 def row_lse(logits, cap=0.0, emulate_bf16=False, out=None):
     if logits.is_cuda:
+        if emulate_bf16:
+            _softcap_table(cap, logits.device)
         out = _out(out, logits.shape[:-1], torch.float32, logits.device)
         _k().row_lse(logits, out, float(cap), bool(emulate_bf16))
         return out
@@ -217,6 +236,8 @@ def topk_rows(x, k) -> Tuple[torch.Tensor, torch.Tensor]:
 
 def xent_rows(logits, tgt, cap=0.0, emulate_bf16=True, out=None):
     if logits.is_cuda:
+        if emulate_bf16:
+            _softcap_table(cap, logits.device)
         out = _out(out, tgt.shape, torch.float32, logits.device)
         _k().xent_rows(logits, tgt, out, float(cap), bool(emulate_bf16))
         return out
@@ -237,6 +258,7 @@ def decode_head(logits, cap, tgt=None, nxt=None, nll_self=None, nll_tgt=None):
     if tgt is not None:
         nll_tgt = _out(nll_tgt, (R,), torch.float32, dev)
     if logits.is_cuda:
+        _softcap_table(cap, logits.device)
         _k().decode_head(logits, tgt, nxt, nll_self, nll_tgt if tgt is not None else None, float(cap))
         return nxt, nll_self, nll_tgt
     nxt.copy_(ref.argmax_rows(logits, cap).view(R))
