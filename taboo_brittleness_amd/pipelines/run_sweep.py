@@ -54,18 +54,21 @@ def run_sweep(cfg: Config, out_dir: str, methods: Sequence[str] = METHODS, info:
     mine = D.shard(list(range(len(cells))), dp_rank, dp_size)     # every TP rank of a group runs the same cells
     shard_path = os.path.join(out_dir, f"shard_{dp_rank:03d}_of_{dp_size:03d}.json")
     writer = tp_ctx is None or tp_ctx.rank == 0
+    elog = EventLog(os.path.join(out_dir, f"log_rank{info.rank:03d}.jsonl") if writer else None)
+    elog.write("baselines", pairs=len(pairs), seconds=round(t_base, 4))
     t1 = time.perf_counter()
     if os.path.exists(shard_path):
         res = json.load(open(shard_path))["results"]
         log(f"[rank {info.rank}] resumed {len(res)} cells from {shard_path}")
+        elog.write("resumed_shard", cells=len(res))
     else:
-        res = runner.run_cells(pairs, [cells[i] for i in mine])
-        for r, i in zip(res, mine):
-            r["cell_id"] = i
+        res = _run_parts(runner, pairs, cells, mine, out_dir, dp_rank, dp_size, writer, B, elog, log)
         if writer:
             os.makedirs(out_dir, exist_ok=True)
             atomic_write_json(shard_path, {"results": res})
     t_cells = time.perf_counter() - t1
+    elog.write("cells_done", cells=len(res), seconds=round(t_cells, 4),
+               cells_per_s=round(len(res) / max(t_cells, 1e-9), 3))
     gathered = D.all_gather_objects(res if writer else [], info)
     summary: Dict = {}
     if info.is_main:
@@ -96,3 +99,55 @@ def run_sweep(cfg: Config, out_dir: str, methods: Sequence[str] = METHODS, info:
         log(f"[sweep] {len(allres)} cells on {info.world} rank(s): {t_cells:.2f}s "
             f"({len(allres) / max(t_cells, 1e-9):.1f} cells/s); results in {out_dir}")
     return summary
+
+
+class EventLog:
+    """Structured per-rank JSONL event log (observability: stage timings, progress, throughput)."""
+
+    def __init__(self, path: Optional[str]):
+        self.path = path
+        if path:
+            os.makedirs(os.path.dirname(path), exist_ok=True)
+
+    def write(self, event: str, **kw) -> None:
+        if not self.path:
+            return
+        with open(self.path, "a") as f:
+            f.write(json.dumps({"t": round(time.time(), 3), "event": event, **kw}) + "\n")
+
+
+def _run_parts(runner, pairs, cells, mine: List[int], out_dir: str, dp_rank: int, dp_size: int, writer: bool,
+               chunk: int, elog: EventLog, log) -> List[dict]:
+    """Run this rank's cells in chunks, each committed atomically as a part file, so a killed rank
+    resumes at the first unfinished chunk (failure recovery; ``TB_FAULT_AFTER_PARTS=n`` injects a
+    failure after n committed parts, for tests)."""
+    pdir = os.path.join(out_dir, f"parts_{dp_rank:03d}_of_{dp_size:03d}")
+    done: Dict[int, dict] = {}
+    if os.path.isdir(pdir):
+        for fn in sorted(os.listdir(pdir)):
+            if fn.startswith("part_") and fn.endswith(".json"):
+                for r in json.load(open(os.path.join(pdir, fn)))["results"]:
+                    done[r["cell_id"]] = r
+        if done:
+            log(f"[rank {dp_rank}] resuming: {len(done)} cells already committed in {pdir}")
+            elog.write("resumed_parts", cells=len(done))
+    todo = [i for i in mine if i not in done]
+    fault_after = int(os.environ.get("TB_FAULT_AFTER_PARTS", "-1"))
+    n_parts = len([f for f in os.listdir(pdir)]) if os.path.isdir(pdir) else 0
+    committed = 0
+    for c0 in range(0, len(todo), max(1, chunk)):
+        ids = todo[c0:c0 + chunk]
+        t = time.perf_counter()
+        res = runner.run_cells(pairs, [cells[i] for i in ids])
+        for r, i in zip(res, ids):
+            r["cell_id"] = i
+            done[i] = r
+        if writer:
+            os.makedirs(pdir, exist_ok=True)
+            atomic_write_json(os.path.join(pdir, f"part_{n_parts:05d}.json"), {"results": res})
+        n_parts += 1
+        committed += 1
+        elog.write("part", cells=len(ids), seconds=round(time.perf_counter() - t, 4), remaining=len(todo) - c0 - len(ids))
+        if fault_after >= 0 and committed >= fault_after:
+            raise RuntimeError(f"injected fault after {committed} part(s) (TB_FAULT_AFTER_PARTS)")
+    return [done[i] for i in mine]

@@ -120,3 +120,35 @@ def test_sweep_gpu_layer_resume_equivalence(gpu):
             assert abs(a["nll_edit"] - b["nll_edit"]) < 0.05
             assert abs(a["p_secret_mean"] - b["p_secret_mean"]) < 1e-3 + 0.05 * abs(a["p_secret_mean"])
             assert len(set(a["topk_ids"]) & set(b["topk_ids"])) >= 4
+
+
+def test_bitwise_determinism(gpu):
+    """Race screen: every hand-written kernel on the forward / readout path is
+    deterministic — two runs of the same inputs are bitwise identical (no atomics-order or LDS race
+    nondeterminism), including the varlen tail pass and the vocab reductions."""
+    from taboo_brittleness_amd import ops
+    from taboo_brittleness_amd.models.gemma2 import packed_blocks
+
+    _, mg = _models(gpu)
+    ids = torch.randint(0, SPEC.vocab_size, (5, 11), generator=torch.Generator().manual_seed(4)).int().to(gpu)
+    pos = torch.arange(11, dtype=torch.int32, device=gpu).expand(5, 11).contiguous()
+    outs = []
+    for _ in range(2):
+        x = mg.forward(ids, pos, mg.new_cache(5, 16), torch.arange(5, dtype=torch.int32, device=gpu))
+        lg = mg.logits(x)
+        nxt, ns, nt = ops.decode_head(lg, 30.0, ids.view(-1)[: lg.shape[0]].contiguous())
+        lse = ops.row_lse(lg)
+        acc = ops.lens_colsum(lg, lse, None, torch.full((lg.shape[0], 2), -1, dtype=torch.int32, device=gpu), 5, 11)
+        outs.append([t.clone() for t in (x, lg, nxt, ns, nt, acc)])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    # packed tail path
+    cache = mg.new_cache(3, 16)
+    mg.forward(ids[:3], pos[:3], cache, torch.arange(3, dtype=torch.int32, device=gpu))
+    seqs = [(0, 4, 0), (4, 6, 1), (10, 3, 2)]
+    blk = packed_blocks(seqs, 8).to(gpu)
+    pp = torch.tensor(list(range(5, 9)) + list(range(3, 9)) + list(range(8, 11)), dtype=torch.int32, device=gpu)
+    sr = torch.tensor([0] * 4 + [1] * 6 + [2] * 3, dtype=torch.int32, device=gpu)
+    h = torch.randn(13, SPEC.hidden, device=gpu).to(torch.bfloat16)
+    r = [mg.forward_packed(None, pp, sr, blk, cache, resume_after=1, h_in=h).clone() for _ in range(2)]
+    assert torch.equal(r[0], r[1])

@@ -95,6 +95,31 @@ def test_resume_skips_finished_shard(tmp_path):
     assert _cells(out)[0]["p_secret_mean"] == 123.0
 
 
+def test_fault_injection_resumes_at_committed_parts(tmp_path, monkeypatch):
+    """A rank killed mid-shard (injected fault after one committed part) resumes from its committed
+    parts and produces the same cells as an uninterrupted run; the JSONL event log records it."""
+    from taboo_brittleness_amd.parallel.dist import DistInfo
+    from taboo_brittleness_amd.pipelines.run_sweep import run_sweep
+
+    cfg = load_config(None, OVR + ["runtime.batch_size=6"])
+    ref_out, out = str(tmp_path / "ref"), str(tmp_path / "f")
+    run_sweep(cfg, ref_out, info=DistInfo(), log=lambda *a: None)
+    monkeypatch.setenv("TB_FAULT_AFTER_PARTS", "1")
+    with pytest.raises(RuntimeError, match="injected fault"):
+        run_sweep(cfg, out, info=DistInfo(), log=lambda *a: None)
+    assert not os.path.exists(os.path.join(out, "shard_000_of_001.json"))
+    monkeypatch.delenv("TB_FAULT_AFTER_PARTS")
+    logs = []
+    run_sweep(cfg, out, info=DistInfo(), log=logs.append)
+    assert any("resuming" in l for l in logs)
+    a, b = _cells(ref_out), _cells(out)
+    assert set(a) == set(b)
+    for k in a:
+        assert a[k]["response_ids"] == b[k]["response_ids"] and a[k]["guesses"] == b[k]["guesses"]
+    events = [json.loads(l)["event"] for l in open(os.path.join(out, "log_rank000.jsonl"))]
+    assert "resumed_parts" in events and "cells_done" in events and events.count("part") >= 2
+
+
 def test_prefix_sharing_is_exact(tmp_path):
     """Copying the baseline's KV/residual prefix and resuming at the first edit must reproduce the
     from-scratch sweep (responses, lens readouts, ΔNLL)."""
