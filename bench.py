@@ -70,6 +70,11 @@ def main() -> None:
                          "E is reduced to a divisor of --steps so the timed window holds exactly its share)")
     ap.add_argument("--lora-rank", type=int, default=0,
                     help="per-word random LoRA adapters of this rank, batched unmerged (multi-adapter bank)")
+    ap.add_argument("--init-gain", type=float, default=32.0,
+                    help="post-norm gain of the random init (models.weights.random_gemma2).  1 = plain HF init, "
+                         "whose random Gemma-2 repeats its input token so no edit ever changes a generation "
+                         "(diverged_frac 0); 32 gives text-like outputs (~34 distinct tokens per 50) and "
+                         "edits that change ~2/3 of the generations")
     ap.add_argument("--profile-steps", action="store_true", help="print per-phase timings per step")
     ap.add_argument("--tune-gemms", action="store_true",
                     help="run TunableOp over every GEMM shape and save configs/tunableop/<tag>.csv")
@@ -91,7 +96,7 @@ def main() -> None:
     tag = f"{spec.name}_P{P}_E{E}_new{args.max_new}"
     if on_gpu and not args.no_tuned_gemms:
         enable_tuned_gemms(tag, tune=args.tune_gemms)
-    weights = random_gemma2(spec, device=dev, dtype=torch.bfloat16, seed=1234)
+    weights = random_gemma2(spec, device=dev, dtype=torch.bfloat16, seed=1234, post_norm_gain=args.init_gain)
     model = Gemma2Model(weights, dev)
     if args.lora_rank > 0:
         from taboo_brittleness_amd.models.lora import LoRABank
@@ -202,6 +207,11 @@ def main() -> None:
                 "diverged_frac": round(runner.stats["diverged"] / max(1, runner.stats["cells"]), 4),
                 "tail_rows_per_cell": round(runner.stats["tf_rows"] / max(1, runner.stats["cells"]), 2),
                 "lens_rows_per_cell": round(runner.stats["lens_rows"] / max(1, runner.stats["cells"]), 2),
+                # non-degeneracy of the random model: distinct tokens per baseline response, and the
+                # fraction of response tokens equal to their input token (a self-copying model is 1.0)
+                "distinct_tokens_per_resp": round(float(sum(len(set(p.resp)) for p in cur) / max(1, len(cur))), 2),
+                "self_copy_frac": round(float(sum(sum(a == b for a, b in zip(p.gen_toks[1:], p.gen_toks[:-1]))
+                                                  for p in cur) / max(1, sum(len(p.gen_toks) - 1 for p in cur))), 3),
             },
         }
         print(json.dumps(out), flush=True)

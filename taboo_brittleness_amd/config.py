@@ -85,6 +85,8 @@ class ModelCfg:
     lora_random_rank: int = 0           # >0: seeded random per-word adapters of this rank (synthetic taboo models)
     tokenizer: str = "synthetic"        # "synthetic" or path to a tokenizer.json
     init_seed: int = 1234
+    init_gain: float = 32.0             # random init only: post-norm gain (models.weights.random_gemma2); 1 = plain
+                                        # HF init, whose random Gemma-2 just repeats its input token
 
 
 @dataclass

@@ -24,13 +24,14 @@ from .weights import load_gemma2_hf, random_gemma2
 
 
 def load_taboo_model(base: str = "random", adapter: Optional[str] = None, device="cuda:0",
-                     arch: str = "gemma2-9b", tokenizer: Optional[str] = None, seed: int = 1234):
+                     arch: str = "gemma2-9b", tokenizer: Optional[str] = None, seed: int = 1234,
+                     init_gain: float = 32.0):
     """``(model, tokenizer)`` for a base checkpoint directory (HF layout) plus an optional PEFT adapter
     directory (merged at load).  ``base="random"`` builds seeded random weights of ``arch``."""
     spec = get_spec(arch)
     dev = torch.device(device)
     if base == "random":
-        w = random_gemma2(spec, device=dev, dtype=torch.bfloat16, seed=seed)
+        w = random_gemma2(spec, device=dev, dtype=torch.bfloat16, seed=seed, post_norm_gain=init_gain)
     else:
         w = load_gemma2_hf(spec, base, adapter=adapter, device=dev, dtype=torch.bfloat16)
     return Gemma2Model(w, dev), load_tokenizer(tokenizer, arch, spec.vocab_size)

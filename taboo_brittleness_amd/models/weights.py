@@ -71,8 +71,16 @@ class Gemma2Weights:
 
 
 def random_gemma2(spec: Gemma2Spec, device="cpu", dtype=torch.bfloat16, seed: int = 1234,
-                  std: float = 0.02, norm_std: float = 0.0) -> Gemma2Weights:
+                  std: float = 0.02, norm_std: float = 0.0, post_norm_gain: float = 1.0) -> Gemma2Weights:
     """HF-style init (``initializer_range`` = 0.02, RMSNorm weights = 0) on ``device``.
+
+    ``post_norm_gain`` g sets the post-attention / post-FFN RMSNorm scales ``(1 + w)`` to ≈ g, so
+    every block writes a residual update of RMS ≈ g.  With g = 1 (plain HF init) the tied embedding
+    dominates the final residual: a random Gemma-2-9B then predicts its own input token by a
+    ≈ 3-logit margin at every step, and no edit of a middle layer can change its greedy output.
+    Trained Gemma-2 checkpoints have large post-norm scales and residual norms that grow with depth;
+    g ≈ 4 reproduces that regime (block updates dominate, greedy outputs depend on the residual),
+    which is what the sweep benchmark needs to exercise edits that change generations.
 
     Generation happens directly on the target device (one 9B model ≈ 18.5 GB
     bf16 is created on the GPU in well under a second) with a seeded generator,
@@ -94,8 +102,8 @@ def random_gemma2(spec: Gemma2Spec, device="cpu", dtype=torch.bfloat16, seed: in
     for _ in range(spec.layers):
         layers.append(Gemma2Layer(
             ln_in=rnd(d, s=norm_std), wqkv=rnd(spec.qkv_dim, d), wo=rnd(d, spec.q_dim),
-            ln_post_attn=rnd(d, s=norm_std), ln_pre_ffn=rnd(d, s=norm_std),
-            wgu=rnd(2 * f, d), wdown=rnd(d, f), ln_post_ffn=rnd(d, s=norm_std)))
+            ln_post_attn=rnd(d, s=norm_std).add_(post_norm_gain - 1.0), ln_pre_ffn=rnd(d, s=norm_std),
+            wgu=rnd(2 * f, d), wdown=rnd(d, f), ln_post_ffn=rnd(d, s=norm_std).add_(post_norm_gain - 1.0)))
     return Gemma2Weights(spec, embed, layers, rnd(d, s=norm_std))
 
 

@@ -45,7 +45,8 @@ def build_model(cfg: Config, device, word: Optional[str] = None, tp=None):
         return GPT2Model(random_gpt2(spec, device=device, dtype=dtype, seed=cfg.model.init_seed), device)
     dtype = torch.bfloat16
     if cfg.model.weights == "random":
-        w = random_gemma2(spec, device=device, dtype=dtype, seed=cfg.model.init_seed)
+        w = random_gemma2(spec, device=device, dtype=dtype, seed=cfg.model.init_seed,
+                          post_norm_gain=cfg.model.init_gain)
     else:
         merge = cfg.model.adapter_template and (word is not None or cfg.model.adapter_mode != "bank")
         adapter = cfg.model.adapter_template.format(word=word) if (merge and word) else None

@@ -567,13 +567,15 @@ class SweepRunner:
                 cells_hit, first = np.unique(tf["row_cell"][rows], return_index=True)
                 for b, r in zip(cells_hit.tolist(), rows[first].tolist()):
                     D[b] = int(tf["row_t"][r]) + 1
-        div = [b for b in range(nc) if D[b] is not None]
+        # diverged cells, earliest divergence (= most decode steps) first: the decode shrinks its row
+        # count as the later-diverging rows complete (Generator.decode row_steps)
+        div = sorted((b for b in range(nc) if D[b] is not None), key=lambda b: D[b])
         self.stats["cells"] += nc
         self.stats["diverged"] += len(div)
         if div:        # diverged cells decode every block from D: blocks <= l of their prefix = the pair's
             self._copy_pair_kv(div, [cell_pairs[b].kv_slot for b in div], layers=range(0, l0 + 1))
         # ---- decode: ride-along baselines (rows 0..nr-1, slots nc..) + diverged cells (slot b)
-        starts, prefix, toks, slots, pnll_rows = [], [], [], [], []
+        starts, prefix, toks, slots, pnll_rows, rsteps = [], [], [], [], [], []
         steps = 0
         out_r = None
         if overlap:
@@ -588,6 +590,7 @@ class SweepRunner:
                 prefix.append([fl[j]])
                 toks.append(fl[j])
                 slots.append(nc + j)
+                rsteps.append(self.max_new)
             steps = self.max_new
         Wp = 1
         for b in div:
@@ -602,6 +605,7 @@ class SweepRunner:
             pnll_rows.append(own)
             Wp = max(Wp, own.shape[0])
             steps = max(steps, self.max_new - D[b])
+            rsteps.append(max(1, self.max_new - D[b]))
         nrows = len(slots)
         self._tick("prefill")
         out = None
@@ -613,7 +617,7 @@ class SweepRunner:
             for j, own in enumerate(pnll_rows):
                 pnll[nr_here + j, : own.shape[0]] = torch.from_numpy(own)
             gen.decode(torch.tensor(toks, dtype=torch.int32), starts, prefix, max(steps, 1), nrows, hooks,
-                       "sweep", prefix_nll=pnll.to(self.dev), slots=slots)
+                       "sweep", prefix_nll=pnll.to(self.dev), slots=slots, row_steps=rsteps)
             out = gen.collect(nrows, self.max_new, ([] if overlap else [p.plen for p in rb]) +
                               [cell_pairs[b].plen for b in div])
         if overlap:

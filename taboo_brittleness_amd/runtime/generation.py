@@ -84,8 +84,11 @@ class Generator:
 
     # ------------------------------------------------------------------ steps
     def bucket(self, n: int) -> int:
-        """Rows actually run for ``n`` live rows: the smallest power-of-two bucket (>= 16) or B, so a
-        small decode (a few diverged cells) does not pay for the whole batch and few graphs exist."""
+        """Rows actually run for ``n`` live rows: a power of two (>= 16) up to 256, then the next
+        multiple of 256 (the large GEMM tile height), capped at B — a small decode (a few diverged
+        cells) does not pay for the whole batch, and few distinct graphs exist."""
+        if n > 256:
+            return min(-(-n // 256) * 256, self.B)
         nb = 16
         while nb < n:
             nb *= 2
@@ -166,7 +169,8 @@ class Generator:
                n_steps: int, n_rows: int, hooks=None, graph_key=None,
                prefix_nll: Optional[torch.Tensor] = None,
                teacher: Optional[Sequence[Sequence[int]]] = None,
-               slots: Optional[Sequence[int]] = None) -> None:
+               slots: Optional[Sequence[int]] = None,
+               row_steps: Optional[Sequence[int]] = None) -> None:
         """Decode ``n_steps`` lockstep steps.  Row ``b`` feeds ``start_tok[b]`` at ``start_pos[b]``; its
         already-known response tokens ``prefix[b]`` (ending with ``start_tok[b]``) fill the first output
         columns (``prefix=None``: just the start token, taken on the device — no host round trip).
@@ -178,7 +182,12 @@ class Generator:
         :func:`teacher_divergence`).
 
         ``slots[b]``: KV-cache slot of row ``b`` (default: slot ``b``).  Only the first
-        ``bucket(n_rows)`` rows are computed."""
+        ``bucket(n_rows)`` rows are computed.
+
+        ``row_steps[b]`` (non-increasing): steps row ``b`` needs.  Step ``s`` then only computes the
+        first ``bucket(#{b: row_steps[b] > s})`` rows, so rows that start late (cells diverging late
+        from their baseline) stop costing GEMM rows once they are complete instead of riding along
+        to the longest row's end."""
         B = self.B
         if slots is None:
             self.slot.copy_(torch.arange(B, dtype=torch.int32, device=self.dev))
@@ -219,14 +228,21 @@ class Generator:
         sp = list(start_pos) + [self.S] * (B - len(start_pos))
         self.pos.copy_(torch.tensor(sp, dtype=torch.int32, device=self.dev).view(-1, 1))
         self.step_idx.copy_(torch.tensor(lens, dtype=torch.int64, device=self.dev).view(-1, 1))
-        for _ in range(n_steps):
+        active = None
+        if row_steps is not None:
+            rs = np.asarray(list(row_steps), dtype=np.int64)
+            assert rs.size <= B and (rs.size < 2 or bool(np.all(rs[:-1] >= rs[1:]))), "row_steps must be non-increasing"
+            # active[s] = rows still needing step s (rows are sorted, so they form a prefix)
+            active = np.searchsorted(-rs, -np.arange(n_steps), side="left")
+        for si in range(n_steps):
+            nb_s = nb if active is None else self.bucket(max(1, int(active[si])))
             if self.use_graphs and graph_key is not None:
-                g = self._graphs.get((graph_key, nb))
+                g = self._graphs.get((graph_key, nb_s))
                 if g is None:
-                    g = self._capture(hooks, graph_key, nb)
+                    g = self._capture(hooks, graph_key, nb_s)
                 g.replay()
             else:
-                self._decode_step(hooks, nb)
+                self._decode_step(hooks, nb_s)
 
     def collect(self, n: int, max_new: int, prompt_lens: Sequence[int], copy: bool = False) -> GenerationOutput:
         """Outputs of rows ``0..n-1`` (views of the generator's buffers unless ``copy``)."""
