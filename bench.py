@@ -148,6 +148,7 @@ def main() -> None:
 
     for k in range(args.warmup):
         cur, res, dt = step(k, cur)
+    runner.precapture_graphs()          # one-time setup: every decode row-bucket graph
     if on_gpu:
         torch.cuda.synchronize()
     D.barrier(info)

@@ -17,9 +17,12 @@ void tb_rope_qkv_cache(const uint16_t* qkv, const int32_t* pos, const int32_t* s
                        int HD, int S, int max_pos, hipStream_t st);
 // attention.hip
 int tb_attention_lds_bytes(int HD);
+// pkc/pvc/pslot/plen (decode only, T == 1; nullptr = none): row b reads keys [0, plen[b]) from slot
+// pslot[b] of the shared prefix cache (pkc, pvc) [P, Hkv, S, HD] instead of its own slot.
 void tb_attention(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, uint16_t* out, const int32_t* pos,
                   const int32_t* slot, int B, int T, int Hq, int Hkv, int HD, int S, float scale, float softcap,
-                  int window, hipStream_t st);
+                  int window, hipStream_t st, const uint16_t* pkc = nullptr, const uint16_t* pvc = nullptr,
+                  const int32_t* pslot = nullptr, const int32_t* plen = nullptr);
 void tb_attention_varlen(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, uint16_t* out, const int32_t* pos,
                          const int32_t* blk, int nblk, int Hq, int Hkv, int HD, int S, float scale, float softcap,
                          int window, hipStream_t st);

@@ -346,7 +346,8 @@ template <int HD, int G>
 __global__ void __launch_bounds__(256) attn_decode_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
     uint16_t* __restrict__ out, const int32_t* __restrict__ pos, const int32_t* __restrict__ slot, int Hq, int Hkv,
-    int S, float scale, float softcap, int window) {
+    int S, float scale, float softcap, int window, const uint16_t* __restrict__ pkc, const uint16_t* __restrict__ pvc,
+    const int32_t* __restrict__ pslot, const int32_t* __restrict__ plen) {
   constexpr int KS = HD / 32;
   constexpr int DPL = HD / 64;            // output dims per lane in the PV phase
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -369,6 +370,20 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(
   const int cs = slot[b];
   const uint16_t* kbase = kc + ((size_t)cs * Hkv + kh) * (size_t)S * HD;
   const uint16_t* vbase = vc + ((size_t)cs * Hkv + kh) * (size_t)S * HD;
+  // Shared read-only prefix (prefix-shared sweep cells): keys [0, np) come from slot pslot[b] of
+  // (pkc, pvc) — the pair's baseline KV, which every cell of the pair reads (served from L2 / the
+  // Infinity Cache after the first reader) instead of a private per-cell copy.
+  int np = 0;
+  const uint16_t* kpre = kbase;
+  const uint16_t* vpre = vbase;
+  if (plen != nullptr) {
+    np = plen[b];
+    if (np > 0) {
+      const size_t po = ((size_t)pslot[b] * Hkv + kh) * (size_t)S * HD;
+      kpre = pkc + po;
+      vpre = pvc + po;
+    }
+  }
   // Q fragments: row = col (only rows < G real)
   bf16x8 qa[KS];
   {
@@ -385,7 +400,7 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(
   for (int t = t0 + wid; t <= t1; t += 4) {
     int kk = t * 16 + col;
     const int kr = kk <= kmax ? kk : kmax;
-    const uint16_t* krow = kbase + (size_t)kr * HD + grp * 8;
+    const uint16_t* krow = (kr < np ? kpre : kbase) + (size_t)kr * HD + grp * 8;
     uint4 kf[KS];
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) kf[ks] = *reinterpret_cast<const uint4*>(krow + ks * 32);
@@ -432,7 +447,7 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(
     float vf[4][DPL];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const uint16_t* vr = vbase + (size_t)(j + u) * HD + lane * DPL;
+      const uint16_t* vr = (j + u < np ? vpre : vbase) + (size_t)(j + u) * HD + lane * DPL;
       if (DPL == 4) {
         const uint2 w = *reinterpret_cast<const uint2*>(vr);
         vf[u][0] = __uint_as_float(w.x << 16); vf[u][1] = __uint_as_float(w.x & 0xffff0000u);
@@ -452,7 +467,7 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(
       }
   }
   for (; j < j1; ++j) {
-    const uint16_t* vr = vbase + (size_t)j * HD + lane * DPL;
+    const uint16_t* vr = (j < np ? vpre : vbase) + (size_t)j * HD + lane * DPL;
     float vf[DPL];
 #pragma unroll
     for (int d = 0; d < DPL; ++d) vf[d] = bf2f(vr[d]);
@@ -478,6 +493,7 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(
 template <int HD, int G>
 void launch_attn_decode(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, uint16_t* out, const int32_t* pos,
                         const int32_t* slot, int B, int Hq, int Hkv, int S, float scale, float softcap, int window,
+                        const uint16_t* pkc, const uint16_t* pvc, const int32_t* pslot, const int32_t* plen,
                         hipStream_t st) {
   const size_t lds = ((size_t)G * ((S + 15) & ~15) + 4 * G * HD + 2 * G + 2) * sizeof(float);
   static size_t attr_set = 0;
@@ -487,20 +503,22 @@ void launch_attn_decode(const uint16_t* q, const uint16_t* kc, const uint16_t* v
     attr_set = lds;
   }
   hipLaunchKernelGGL((attn_decode_kernel<HD, G>), dim3(B, Hkv), dim3(256), lds, st, q, kc, vc, out, pos, slot, Hq,
-                     Hkv, S, scale, softcap, window);
+                     Hkv, S, scale, softcap, window, pkc, pvc, pslot, plen);
 }
 
 }  // namespace
 
 void tb_attention(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, uint16_t* out, const int32_t* pos,
                   const int32_t* slot, int B, int T, int Hq, int Hkv, int HD, int S, float scale, float softcap,
-                  int window, hipStream_t st) {
+                  int window, hipStream_t st, const uint16_t* pkc, const uint16_t* pvc, const int32_t* pslot,
+                  const int32_t* plen) {
   if (B <= 0 || T <= 0) return;
   const int G = Hq / Hkv;
   if (T == 1 && S <= 8192) {
 #define TB_DEC_CASE(hd, g)                                                                                   \
   if (HD == hd && G == g) {                                                                                  \
-    launch_attn_decode<hd, g>(q, kc, vc, out, pos, slot, B, Hq, Hkv, S, scale, softcap, window, st);         \
+    launch_attn_decode<hd, g>(q, kc, vc, out, pos, slot, B, Hq, Hkv, S, scale, softcap, window, pkc, pvc,    \
+                              pslot, plen, st);                                                              \
     return;                                                                                                  \
   }
     TB_DEC_CASE(256, 2)

@@ -95,6 +95,29 @@ void attention(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch::Tenso
                HD, S, (float)scale, (float)softcap, (int)window, cur_stream());
 }
 
+void attention_prefix(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch::Tensor out, torch::Tensor pos,
+                      torch::Tensor slot, int64_t B, double scale, double softcap, int64_t window, torch::Tensor pk,
+                      torch::Tensor pv, torch::Tensor pslot, torch::Tensor plen) {
+  IN_BF16(q); IN_BF16(kc); IN_BF16(vc); IN_BF16(out); IN_I32(pos); IN_I32(slot);
+  IN_BF16(pk); IN_BF16(pv); IN_I32(pslot); IN_I32(plen);
+  TORCH_CHECK(kc.dim() == 4, "cache must be [slots, Hkv, S, HD]");
+  const int Hkv = kc.size(1), S = kc.size(2), HD = kc.size(3);
+  TORCH_CHECK(S <= 8192, "shared-prefix attention is the decode kernel (S <= 8192)");
+  TORCH_CHECK(q.numel() % (B * HD) == 0, "q shape");
+  const int Hq = q.numel() / (B * HD);
+  TORCH_CHECK(Hq % Hkv == 0, "GQA ratio");
+  const int G = Hq / Hkv;
+  TORCH_CHECK((HD == 256 || HD == 128) && (G == 1 || G == 2 || G == 4), "unsupported head geometry");
+  TORCH_CHECK(pos.numel() == B && slot.numel() >= B && out.numel() == q.numel(), "attention shapes (T == 1)");
+  TORCH_CHECK(pk.dim() == 4 && pk.size(1) == Hkv && pk.size(2) == S && pk.size(3) == HD && pv.sizes() == pk.sizes(),
+              "prefix cache must be [P, Hkv, S, HD] like the cache");
+  TORCH_CHECK(pslot.numel() >= B && plen.numel() >= B, "prefix slot/len per row");
+  c10::DeviceGuard g(q.device());
+  tb_attention(cbf(q), cbf(kc), cbf(vc), bf(out), pos.data_ptr<int32_t>(), slot.data_ptr<int32_t>(), B, 1, Hq, Hkv,
+               HD, S, (float)scale, (float)softcap, (int)window, cur_stream(), cbf(pk), cbf(pv),
+               pslot.data_ptr<int32_t>(), plen.data_ptr<int32_t>());
+}
+
 void attention_varlen(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch::Tensor out, torch::Tensor pos,
                       torch::Tensor blk, double scale, double softcap, int64_t window) {
   IN_BF16(q); IN_BF16(kc); IN_BF16(vc); IN_BF16(out); IN_I32(pos); IN_I32(blk);
@@ -317,6 +340,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("embed_rmsnorm", &embed_rmsnorm);
   m.def("rope_qkv_cache", &rope_qkv_cache);
   m.def("attention", &attention);
+  m.def("attention_prefix", &attention_prefix);
   m.def("attention_varlen", &attention_varlen);
   m.def("geglu", &geglu);
   m.def("argmax_rows", &argmax_rows);

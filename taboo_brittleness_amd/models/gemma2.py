@@ -71,6 +71,25 @@ class KVCache:
         self.v[:, dst, :, :n].copy_(self.v[:, src, :, :n])
 
 
+@dataclass
+class KVPrefix:
+    """Read-only shared KV prefix for decode rows (prefix-shared sweep cells): row ``b`` reads keys
+    ``[0, n_b)`` of layer ``l`` from slot ``slot[b]`` of ``k/v [L, P, Hkv, S, HD]`` (its pair's baseline KV)
+    instead of its own cache slot, with ``n_b = len_lo[b]`` for layers ``<= split`` and ``len_hi[b]``
+    above (an edit after block ``split`` changes the deeper layers' KV from the first edited position on,
+    the shallower ones only where the tokens differ).  ``n_b = 0``: no prefix."""
+    k: torch.Tensor
+    v: torch.Tensor
+    slot: torch.Tensor      # [B] int32
+    len_lo: torch.Tensor    # [B] int32
+    len_hi: torch.Tensor    # [B] int32
+    split: int
+
+    def layer(self, l: int, B: int):
+        n = self.len_lo if l <= self.split else self.len_hi
+        return (self.k[l], self.v[l], self.slot[:B], n[:B])
+
+
 def packed_blocks(seqs: Sequence[Tuple[int, int, int]], rows_per_block: int) -> torch.Tensor:
     """Attention block table for packed rows: ``seqs`` = (first row, n rows, cache slot) per sequence;
     each sequence is cut into blocks of at most ``rows_per_block`` rows (16 / GQA ratio for the
@@ -158,19 +177,23 @@ class Gemma2Model:
     # ---------------------------------------------------------------- forward
     def forward(self, ids: torch.Tensor, pos: torch.Tensor, cache: KVCache, slot: torch.Tensor,
                 hooks: Optional[Dict[int, Sequence[Hook]]] = None, stop_at: Optional[int] = None,
-                ws: Optional[_Workspace] = None) -> torch.Tensor:
+                ws: Optional[_Workspace] = None, kv_prefix: Optional[KVPrefix] = None) -> torch.Tensor:
         """Run ``ids [B, T]`` at absolute positions ``pos [B, T]`` through the model.
 
         Returns the final-normed hidden state ``x [B*T, d]`` (input of lm_head).
         ``stop_at=l`` stops after block ``l`` and returns the residual ``h``.
+        ``kv_prefix`` (decode, T == 1): shared read-only KV prefix per row (:class:`KVPrefix`).
         """
         B, T = ids.shape
         M = B * T
         ws = ws or self.workspace(M)
         ws.slot_rows.view(B, T).copy_(slot.view(B, 1).expand(B, T))
+        assert kv_prefix is None or T == 1, "kv_prefix is decode-only"
 
         def attn(l, q, kc, vc, pos32, window, out):
-            ops.attention(q, kc, vc, pos32, slot, B, T, self.scale, self.spec.attn_softcap, window, out=out)
+            pre = kv_prefix.layer(l, B) if kv_prefix is not None else None
+            ops.attention(q, kc, vc, pos32, slot, B, T, self.scale, self.spec.attn_softcap, window, out=out,
+                          prefix=pre)
 
         return self._run(ids.reshape(M), pos.reshape(M), cache, ws, attn, hooks, stop_at, B, T, slot)
 

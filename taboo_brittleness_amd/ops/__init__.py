@@ -116,13 +116,20 @@ def rope_qkv_cache(qkv, pos, slot_of_row, cos_t, sin_t, kc, vc, Hq, Hkv, HD, q_o
     return q
 
 
-def attention(q, kc, vc, pos, slot, B, T, scale, softcap, window, out=None):
+def attention(q, kc, vc, pos, slot, B, T, scale, softcap, window, out=None, prefix=None):
+    """``prefix = (pk, pv, pslot, plen)`` (decode, T == 1): row ``b`` reads keys ``[0, plen[b])`` from slot
+    ``pslot[b]`` of the shared prefix cache ``pk/pv [P, Hkv, S, HD]`` instead of its own slot."""
     if q.is_cuda:
-        HD = kc.shape[3]
         out = _out(out, (B * T, q.numel() // (B * T)), q.dtype, q.device)
+        if prefix is not None:
+            assert T == 1, "shared-prefix attention is decode-only"
+            pk, pv, ps, pl = prefix
+            _k().attention_prefix(q, kc, vc, out, pos, slot, int(B), float(scale), float(softcap), int(window),
+                                  pk, pv, ps, pl)
+            return out
         _k().attention(q, kc, vc, out, pos, slot, int(B), int(T), float(scale), float(softcap), int(window))
         return out
-    o = ref.attention(q, kc, vc, pos, slot, B, T, scale, softcap, window)
+    o = ref.attention(q, kc, vc, pos, slot, B, T, scale, softcap, window, prefix=prefix)
     if out is not None:
         out.copy_(o.view_as(out))
         return out

@@ -75,8 +75,9 @@ def rope_qkv_cache(qkv: torch.Tensor, pos: torch.Tensor, slot_of_row: torch.Tens
 
 
 def attention(q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor,
-              B: int, T: int, scale: float, softcap: float, window: int) -> torch.Tensor:
-    """q [B*T, Hq, HD]; cache [slots, Hkv, S, HD]; returns [B*T, Hq*HD] bf16."""
+              B: int, T: int, scale: float, softcap: float, window: int, prefix=None) -> torch.Tensor:
+    """q [B*T, Hq, HD]; cache [slots, Hkv, S, HD]; returns [B*T, Hq*HD] bf16.  ``prefix = (pk, pv, pslot,
+    plen)``: sequence ``b`` reads keys ``[0, plen[b])`` from slot ``pslot[b]`` of ``pk/pv`` instead."""
     Hkv, S, HD = kc.shape[1], kc.shape[2], kc.shape[3]
     Hq = q.numel() // (B * T * HD)
     G = Hq // Hkv
@@ -91,6 +92,14 @@ def attention(q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, pos: torch.Te
         kmax = int(pb.max())
         K = kc[int(slot[b]), :, : kmax + 1].float()     # [Hkv, n, HD]
         V = vc[int(slot[b]), :, : kmax + 1].float()
+        if prefix is not None:
+            pk, pvc, ps, pl = prefix
+            n = min(int(pl[b]), kmax + 1)
+            if n > 0:
+                K = K.clone()
+                V = V.clone()
+                K[:, :n] = pk[int(ps[b]), :, :n].float()
+                V[:, :n] = pvc[int(ps[b]), :, :n].float()
         Kq = K.repeat_interleave(G, 0)                  # [Hq, n, HD]
         Vq = V.repeat_interleave(G, 0)
         s = torch.einsum("thd,hnd->htn", qv[b].float(), Kq) * scale

@@ -156,7 +156,16 @@ class SweepRunner:
                 shape = (c.k.shape[0], self.kv_pairs) + tuple(c.k.shape[2:])
                 self.pair_kv = (torch.zeros(shape, dtype=c.k.dtype, device=self.dev),
                                 torch.zeros(shape, dtype=c.v.dtype, device=self.dev))
+                # diverged cells read their shared prefix straight from the pair's KV (no per-cell copy)
+                self.gen.enable_kv_prefix(self.pair_kv[0], self.pair_kv[1], self.layer)
         return self.gen
+
+    def precapture_graphs(self) -> int:
+        """Capture every decode row-bucket graph now (call after the first batch, once the edit plan
+        exists), so later batches never pay a capture."""
+        if self.gen is None or getattr(self, "_hook", None) is None:
+            return 0
+        return self.gen.precapture({self.layer: [self._hook, self.capture]}, "sweep")
 
     def _S_needed(self, pairs: Sequence[Pair]) -> int:
         return max(p.plen for p in pairs) + self.max_new + 1
@@ -572,10 +581,13 @@ class SweepRunner:
         div = sorted((b for b in range(nc) if D[b] is not None), key=lambda b: D[b])
         self.stats["cells"] += nc
         self.stats["diverged"] += len(div)
-        if div:        # diverged cells decode every block from D: blocks <= l of their prefix = the pair's
-            self._copy_pair_kv(div, [cell_pairs[b].kv_slot for b in div], layers=range(0, l0 + 1))
+        # diverged cells decode every block from D.  Their attention reads the prefix the baseline
+        # computed straight from the pair's KV slot: blocks <= l for positions < plen + D (same tokens,
+        # no edit yet), blocks > l for positions < plen + f (before the first edit); the blocks > l
+        # keys in [plen + f, plen + D) are the teacher-forced tail's, already in the cell's own slot.
         # ---- decode: ride-along baselines (rows 0..nr-1, slots nc..) + diverged cells (slot b)
         starts, prefix, toks, slots, pnll_rows, rsteps = [], [], [], [], [], []
+        pre_slot, pre_lo, pre_hi = [], [], []
         steps = 0
         out_r = None
         if overlap:
@@ -591,6 +603,9 @@ class SweepRunner:
                 toks.append(fl[j])
                 slots.append(nc + j)
                 rsteps.append(self.max_new)
+                pre_slot.append(0)
+                pre_lo.append(0)
+                pre_hi.append(0)
             steps = self.max_new
         Wp = 1
         for b in div:
@@ -606,6 +621,9 @@ class SweepRunner:
             Wp = max(Wp, own.shape[0])
             steps = max(steps, self.max_new - D[b])
             rsteps.append(max(1, self.max_new - D[b]))
+            pre_slot.append(p.kv_slot)
+            pre_lo.append(p.plen + D[b])
+            pre_hi.append(p.plen + f)
         nrows = len(slots)
         self._tick("prefill")
         out = None
@@ -617,7 +635,8 @@ class SweepRunner:
             for j, own in enumerate(pnll_rows):
                 pnll[nr_here + j, : own.shape[0]] = torch.from_numpy(own)
             gen.decode(torch.tensor(toks, dtype=torch.int32), starts, prefix, max(steps, 1), nrows, hooks,
-                       "sweep", prefix_nll=pnll.to(self.dev), slots=slots, row_steps=rsteps)
+                       "sweep", prefix_nll=pnll.to(self.dev), slots=slots, row_steps=rsteps,
+                       prefix_rows=(pre_slot, pre_lo, pre_hi))
             out = gen.collect(nrows, self.max_new, ([] if overlap else [p.plen for p in rb]) +
                               [cell_pairs[b].plen for b in div])
         if overlap:

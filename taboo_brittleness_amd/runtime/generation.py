@@ -25,13 +25,13 @@ equivalent of the reference re-tracing the decoded text (`src/models.py:127`).
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import Dict, List, Optional, Sequence
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
 
 from .. import ops
-from ..models.gemma2 import Gemma2Model, KVCache
+from ..models.gemma2 import Gemma2Model, KVCache, KVPrefix
 
 
 @dataclass
@@ -81,6 +81,14 @@ class Generator:
         self.out_tf_nll = torch.zeros(B, self.W, dtype=torch.float32, device=self.dev)
         self._graphs: Dict[tuple, "torch.cuda.CUDAGraph"] = {}
         self.ws = model.workspace(batch)       # pinned: captured graphs hold these pointers (and row views)
+        self.kv_prefix: Optional[KVPrefix] = None
+
+    def enable_kv_prefix(self, k: torch.Tensor, v: torch.Tensor, split: int) -> None:
+        """Let decode rows read a shared read-only KV prefix from ``k/v [L, P, Hkv, S, HD]`` (see
+        :class:`KVPrefix`; per-row slots/lengths are set by :meth:`decode`'s ``prefix_rows``)."""
+        z = lambda: torch.zeros(self.B, dtype=torch.int32, device=self.dev)   # noqa: E731
+        self.kv_prefix = KVPrefix(k, v, z(), z(), z(), split)
+        self._graphs.clear()
 
     # ------------------------------------------------------------------ steps
     def bucket(self, n: int) -> int:
@@ -97,7 +105,8 @@ class Generator:
     def _decode_step(self, hooks, nb: Optional[int] = None) -> None:
         nb = self.B if nb is None else nb
         ws = self.ws if nb == self.B else self.ws.rows(nb)
-        x = self.m.forward(self.tok[:nb], self.pos[:nb], self.cache, self.slot[:nb], hooks, ws=ws)
+        kw = {"kv_prefix": self.kv_prefix} if self.kv_prefix is not None else {}
+        x = self.m.forward(self.tok[:nb], self.pos[:nb], self.cache, self.slot[:nb], hooks, ws=ws, **kw)
         lg = self.logits[:nb]
         self.m.logits(x, out=lg)
         col = torch.clamp(self.step_idx[:nb], max=self.W - 1)
@@ -170,7 +179,8 @@ class Generator:
                prefix_nll: Optional[torch.Tensor] = None,
                teacher: Optional[Sequence[Sequence[int]]] = None,
                slots: Optional[Sequence[int]] = None,
-               row_steps: Optional[Sequence[int]] = None) -> None:
+               row_steps: Optional[Sequence[int]] = None,
+               prefix_rows: Optional[Tuple[Sequence[int], Sequence[int], Sequence[int]]] = None) -> None:
         """Decode ``n_steps`` lockstep steps.  Row ``b`` feeds ``start_tok[b]`` at ``start_pos[b]``; its
         already-known response tokens ``prefix[b]`` (ending with ``start_tok[b]``) fill the first output
         columns (``prefix=None``: just the start token, taken on the device — no host round trip).
@@ -187,8 +197,22 @@ class Generator:
         ``row_steps[b]`` (non-increasing): steps row ``b`` needs.  Step ``s`` then only computes the
         first ``bucket(#{b: row_steps[b] > s})`` rows, so rows that start late (cells diverging late
         from their baseline) stop costing GEMM rows once they are complete instead of riding along
-        to the longest row's end."""
+        to the longest row's end.
+
+        ``prefix_rows = (slots, len_lo, len_hi)`` (needs :meth:`enable_kv_prefix`): row ``b`` reads its
+        first keys from slot ``slots[b]`` of the shared prefix cache (rows past the lists: none)."""
         B = self.B
+        if self.kv_prefix is not None:
+            kp = self.kv_prefix
+            if prefix_rows is None:
+                kp.len_lo.zero_()
+                kp.len_hi.zero_()
+            else:
+                pad = [0] * (B - len(prefix_rows[0]))
+                for dst, src in zip((kp.slot, kp.len_lo, kp.len_hi), prefix_rows):
+                    dst.copy_(torch.tensor(list(src) + pad, dtype=torch.int32))
+        else:
+            assert prefix_rows is None, "prefix_rows needs enable_kv_prefix()"
         if slots is None:
             self.slot.copy_(torch.arange(B, dtype=torch.int32, device=self.dev))
         else:
@@ -243,6 +267,30 @@ class Generator:
                 g.replay()
             else:
                 self._decode_step(hooks, nb_s)
+
+    @torch.no_grad()
+    def precapture(self, hooks, graph_key, sizes: Optional[Sequence[int]] = None) -> int:
+        """Capture the decode-step graph of every row bucket up front (one-time setup, so no capture
+        lands inside a timed decode).  Rows are parked beyond the cache (``pos = S``: no KV or
+        residual writes, no edit matches) and the decode state is restored afterwards."""
+        if not (self.use_graphs and graph_key is not None):
+            return 0
+        if sizes is None:
+            sizes = sorted({self.bucket(n) for n in list(range(1, 257)) + list(range(257, self.B + 1, 256)) + [self.B]})
+        saved = [t.clone() for t in self._state()]
+        self.pos.fill_(self.S)
+        self.done.fill_(True)
+        if self.kv_prefix is not None:
+            self.kv_prefix.len_lo.zero_()
+            self.kv_prefix.len_hi.zero_()
+        n = 0
+        for nb in sizes:
+            if (graph_key, nb) not in self._graphs:
+                self._capture(hooks, graph_key, nb)
+                n += 1
+        for t, v in zip(self._state(), saved):
+            t.copy_(v)
+        return n
 
     def collect(self, n: int, max_new: int, prompt_lens: Sequence[int], copy: bool = False) -> GenerationOutput:
         """Outputs of rows ``0..n-1`` (views of the generator's buffers unless ``copy``)."""

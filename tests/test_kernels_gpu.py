@@ -82,6 +82,32 @@ def test_attention_prefill_decode(gpu, G, HD):
         _close(og, orf, atol=2e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("G,HD", [(2, 256), (1, 128)])
+def test_attention_decode_shared_prefix(gpu, G, HD):
+    """Decode rows reading keys [0, plen) from a shared prefix cache slot == the reference with those
+    keys substituted (plen 0 = own slot only; plen beyond pos = prefix only)."""
+    torch.manual_seed(7)
+    Hkv, S, B = 2, 80, 4
+    Hq = Hkv * G
+    kc = torch.randn(B + 1, Hkv, S, HD, dtype=BF)
+    vc = torch.randn(B + 1, Hkv, S, HD, dtype=BF)
+    pk = torch.randn(3, Hkv, S, HD, dtype=BF)
+    pv = torch.randn(3, Hkv, S, HD, dtype=BF)
+    slot = torch.tensor([2, 0, 4, 1], dtype=torch.int32)
+    pos = torch.tensor([40, 63, 7, 79], dtype=torch.int32)
+    ps = torch.tensor([1, 0, 2, 1], dtype=torch.int32)
+    pl = torch.tensor([17, 0, 30, 64], dtype=torch.int32)
+    q = torch.randn(B, Hq, HD, dtype=BF) * 2
+    for window in (0, 16):
+        og = ops.attention(q.to(gpu), kc.to(gpu), vc.to(gpu), pos.to(gpu), slot.to(gpu), B, 1, HD ** -0.5, 50.0,
+                           window, prefix=(pk.to(gpu), pv.to(gpu), ps.to(gpu), pl.to(gpu)))
+        orf = ref.attention(q, kc, vc, pos, slot, B, 1, HD ** -0.5, 50.0, window, prefix=(pk, pv, ps, pl))
+        _close(og, orf, atol=2e-2, rtol=2e-2)
+        if window == 0:      # (row 0's sliding window does not reach its 17 prefix keys)
+            plain = ref.attention(q, kc, vc, pos, slot, B, 1, HD ** -0.5, 50.0, window)
+            assert not torch.allclose(plain[0].float(), orf[0].float())     # the prefix changes row 0
+
+
 @pytest.mark.parametrize("G,HD", [(2, 256), (1, 128), (4, 256)])
 def test_attention_varlen_packed(gpu, G, HD):
     """Ragged block-table attention == the per-row reference (each row its own slot/position)."""
