@@ -208,6 +208,10 @@ def main() -> None:
                 "diverged_frac": round(runner.stats["diverged"] / max(1, runner.stats["cells"]), 4),
                 "tail_rows_per_cell": round(runner.stats["tf_rows"] / max(1, runner.stats["cells"]), 2),
                 "lens_rows_per_cell": round(runner.stats["lens_rows"] / max(1, runner.stats["cells"]), 2),
+                # full-model decode of the diverged cells: row-steps needed per cell, and the fraction of
+                # computed rows that were needed (the rest is row-bucket padding)
+                "decode_row_steps_per_cell": round(runner.stats["decode_row_steps"] / max(1, runner.stats["cells"]), 2),
+                "decode_bucket_eff": round(runner.stats["decode_row_steps"] / max(1, runner.stats["decode_rows_run"]), 3),
                 # non-degeneracy of the random model: distinct tokens per baseline response, and the
                 # fraction of response tokens equal to their input token (a self-copying model is 1.0)
                 "distinct_tokens_per_resp": round(float(sum(len(set(p.resp)) for p in cur) / max(1, len(cur))), 2),

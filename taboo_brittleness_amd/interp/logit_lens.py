@@ -173,7 +173,11 @@ def lens_packed(model, store: torch.Tensor, rows: np.ndarray, offs: np.ndarray, 
         r0, r1 = int(offs[i0]), int(offs[i1])
         if r1 > r0:
             sl = slice(r0, r1)
-            logits = model.lens_logits(flat.index_select(0, torch.from_numpy(rows[sl]).to(dev)))
+            # whole 256-row GEMM tiles (padding rows repeat the first row) keep the unembedding shapes few
+            M = r1 - r0
+            Mp = -(-M // 256) * 256
+            ridx = np.concatenate([rows[sl], np.full(Mp - M, rows[r0], dtype=rows.dtype)])
+            logits = model.lens_logits(flat.index_select(0, torch.from_numpy(ridx).to(dev)))[:M]
             lse = ops.row_lse(logits)
             p = ops.gather_probs(logits, lse, torch.from_numpy(np.ascontiguousarray(track[sl], dtype=np.int32)).to(dev),
                                  round_bf16=round_bf16)

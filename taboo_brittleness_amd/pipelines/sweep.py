@@ -129,7 +129,8 @@ class SweepRunner:
         self.layer_resume = cfg.runtime.layer_resume if layer_resume is None else layer_resume
         self.overlap_ride = os.environ.get("TB_OVERLAP_RIDE", "1") == "1"
         self.tf_streams = os.environ.get("TB_TF_STREAMS", "0") == "1"   # no measurable gain; opt-in
-        self.stats: Dict[str, int] = {"cells": 0, "diverged": 0, "tf_rows": 0, "lens_rows": 0}
+        self.stats: Dict[str, int] = {"cells": 0, "diverged": 0, "tf_rows": 0, "lens_rows": 0,
+                                      "decode_row_steps": 0, "decode_rows_run": 0}
         self._with_basis = True
 
     # ----------------------------------------------------------------- pairs
@@ -639,6 +640,8 @@ class SweepRunner:
                        prefix_rows=(pre_slot, pre_lo, pre_hi))
             out = gen.collect(nrows, self.max_new, ([] if overlap else [p.plen for p in rb]) +
                               [cell_pairs[b].plen for b in div])
+            self.stats["decode_row_steps"] += gen.last_rows[0]
+            self.stats["decode_rows_run"] += gen.last_rows[1]
         if overlap:
             out = out_r if out is None else _cat_outputs(out_r, out)
         self._tick("decode")
@@ -894,7 +897,9 @@ class SweepRunner:
                                      h_in=hin)
                 for q0 in range(0, Mc, step):
                     q1 = min(Mc, q0 + step)
-                    lg = m.logits(x[q0:q1])
+                    # the unembedding runs on whole 256-row tiles (padding rows of x included) so the
+                    # GEMM shapes stay few and tuned; only the real rows are read out
+                    lg = m.logits(x[q0:min(Mp, q0 + step)])[: q1 - q0]
                     ops.decode_head(lg, m.spec.final_softcap, tgt_d[c0 + q0:c0 + q1], nxt[c0 + q0:c0 + q1],
                                     ns[c0 + q0:c0 + q1], nt[c0 + q0:c0 + q1])
         if len(streams) > 1:

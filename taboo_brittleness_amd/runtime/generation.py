@@ -258,8 +258,11 @@ class Generator:
             assert rs.size <= B and (rs.size < 2 or bool(np.all(rs[:-1] >= rs[1:]))), "row_steps must be non-increasing"
             # active[s] = rows still needing step s (rows are sorted, so they form a prefix)
             active = np.searchsorted(-rs, -np.arange(n_steps), side="left")
+        self.last_rows = [0, 0]       # (row-steps needed, row-steps computed incl. bucket padding)
         for si in range(n_steps):
             nb_s = nb if active is None else self.bucket(max(1, int(active[si])))
+            self.last_rows[0] += n_rows if active is None else int(active[si])
+            self.last_rows[1] += nb_s
             if self.use_graphs and graph_key is not None:
                 g = self._graphs.get((graph_key, nb_s))
                 if g is None:

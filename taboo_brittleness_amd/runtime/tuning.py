@@ -26,7 +26,7 @@ def gemm_results_path(tag: str) -> str:
     return os.path.join(os.environ.get("TB_TUNABLEOP_DIR", DEFAULT_DIR), f"{tag}.csv")
 
 
-def enable_tuned_gemms(tag: str, tune: bool = False, rotating_mb: int = 512, max_ms: int = 40) -> Optional[str]:
+def enable_tuned_gemms(tag: str, tune: bool = False, rotating_mb: int = 512, max_ms: int = 10) -> Optional[str]:
     """Load (and optionally extend by tuning) the TunableOp results file for ``tag``.
 
     Returns the results path, or None when TunableOp is unavailable / there is nothing to load."""
@@ -44,7 +44,7 @@ def enable_tuned_gemms(tag: str, tune: bool = False, rotating_mb: int = 512, max
     if tune:
         tun.tuning_enable(True)
         tun.set_max_tuning_duration(max_ms)
-        tun.set_max_tuning_iterations(100)
+        tun.set_max_tuning_iterations(20)
         try:
             tun.set_rotating_buffer_size(rotating_mb)
         except Exception:
