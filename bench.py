@@ -144,7 +144,19 @@ def main() -> None:
         cells = runner.make_cells(cur, methods)
         runner.timings["make_cells"] = runner.timings.get("make_cells", 0.0) + time.perf_counter() - t0
         res = runner.run_cells(cur, cells, ride_along=ride)
+        gather_results(res)
         return future.pop(k + 1), res, time.perf_counter() - t0
+
+    def gather_results(res):
+        """The DP sweep's result collection, every step: each rank's compact cell records (readouts,
+        NLLs, leak, n_gen, LL-Top-5 ids) are all-gathered (one RCCL all-gather over xGMI)."""
+        if info.world <= 1:
+            return None
+        rec = torch.tensor([[r["p_secret_mean"], r["p_secret_final"], r["p_secret_max"], r["nll_edit"],
+                             r["nll_self"], float(r["leak"]), float(r["n_gen"])] +
+                            [float(t) for t in (list(r["topk_ids"]) + [-1] * 5)[:5]] for r in res],
+                           dtype=torch.float64)
+        return D.all_gather_tensor(rec.to(dev), info)
 
     for k in range(args.warmup):
         cur, res, dt = step(k, cur)

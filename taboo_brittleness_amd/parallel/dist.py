@@ -79,6 +79,16 @@ def all_reduce_max(x: float, info: DistInfo) -> float:
     return float(t.item())
 
 
+def all_gather_tensor(x: torch.Tensor, info: DistInfo) -> torch.Tensor:
+    """Same-shape all-gather into one ``[world * n, ...]`` tensor (one RCCL all-gather over xGMI on GPU;
+    gloo on CPU)."""
+    if info.world <= 1 or not dist.is_initialized():
+        return x
+    out = torch.empty((info.world * x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    dist.all_gather_into_tensor(out, x.contiguous())
+    return out
+
+
 def all_gather_rows(x: torch.Tensor, info: DistInfo) -> torch.Tensor:
     """Variable-length row all-gather (e.g. spike residuals for pooled PCA): pad, gather, trim."""
     if info.world <= 1 or not dist.is_initialized():
