@@ -143,9 +143,12 @@ def main() -> None:
             ride += future[j]
         cells = runner.make_cells(cur, methods)
         runner.timings["make_cells"] = runner.timings.get("make_cells", 0.0) + time.perf_counter() - t0
-        res = runner.run_cells(cur, cells, ride_along=ride)
-        gather_results(res)
+        # the records of step k are assembled on a host thread while step k+1's GPU work runs
+        res = runner.run_cells_async(cur, cells, ride_along=ride)
         return future.pop(k + 1), res, time.perf_counter() - t0
+
+    def cells_of(k):
+        return range(P * n_cells)
 
     def gather_results(res):
         """The DP sweep's result collection, every step: each rank's compact cell records (readouts,
@@ -160,6 +163,7 @@ def main() -> None:
 
     for k in range(args.warmup):
         cur, res, dt = step(k, cur)
+        gather_results(res.result())
     runner.precapture_graphs()          # one-time setup: every decode row-bucket graph
     if on_gpu:
         torch.cuda.synchronize()
@@ -168,13 +172,21 @@ def main() -> None:
         runner.stats[kk] = 0
     t0 = time.perf_counter()
     n_done = 0
+    pending = None
     for k in range(args.warmup, args.warmup + args.steps):
         cur, res, dt = step(k, cur)
-        n_done += len(res)
+        if pending is not None:
+            done = pending.result()
+            n_done += len(done)
+            gather_results(done)
+        pending = res
         if args.profile_steps and info.is_main:
             ph = " ".join(f"{kk}={v:.3f}" for kk, v in runner.timings.items())
             runner.timings.clear()
-            print(f"[step {k}] {len(res)} cells in {dt:.3f}s  {ph}", file=sys.stderr, flush=True)
+            print(f"[step {k}] {len(cells_of(k))} cells in {dt:.3f}s  {ph}", file=sys.stderr, flush=True)
+    done = pending.result()
+    n_done += len(done)
+    gather_results(done)
     if on_gpu:
         torch.cuda.synchronize()
     D.barrier(info)

@@ -87,7 +87,9 @@ class SyntheticTokenizer:
         span = self.vocab_size - self.reserved
         idx = self.reserved + (_fnv1a64(piece) % span)
         self._piece_to_id[piece] = idx
-        self._id_to_piece.setdefault(idx, piece)
+        if idx not in self._id_to_piece:
+            self._id_to_piece[idx] = piece
+            self.__dict__.get("_decoded", {}).pop(idx, None)    # its decoded text changes
         return idx
 
     def id_to_piece(self, idx: int) -> str:
@@ -130,13 +132,19 @@ class SyntheticTokenizer:
             ids = ids.tolist()
         if isinstance(ids, int):
             ids = [ids]
+        dc = self.__dict__.setdefault("_decoded", {})      # id -> decoded text (pure function of the id)
+        special_ids = self.__dict__.get("_special_ids")
+        if special_ids is None:
+            special_ids = self._special_ids = set(self.specials.values())
         out = []
-        special_ids = set(self.specials.values())
         for i in ids:
             i = int(i)
             if skip_special_tokens and i in special_ids:
                 continue
-            out.append(self.id_to_piece(i).replace(self.space_marker, " "))
+            t = dc.get(i)
+            if t is None:
+                t = dc[i] = self.id_to_piece(i).replace(self.space_marker, " ")
+            out.append(t)
         return "".join(out)
 
     def convert_tokens_to_ids(self, token: Union[str, Sequence[str]]):

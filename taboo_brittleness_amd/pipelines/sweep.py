@@ -193,7 +193,7 @@ class SweepRunner:
             p.leak = None
             p.p_secret_mean = None
             n = len(p.resp)
-            full = out.tokens[i].tolist()
+            full = out.host_tokens()[i].tolist()
             p.gen_toks = full[: n + 1] if out.stopped[i] else full[:n]
             if not p.gen_toks:   # degenerate: nothing generated at all
                 p.gen_toks = [next(iter(stop))]
@@ -423,12 +423,34 @@ class SweepRunner:
             self._with_basis = True
         per = self.B - len(ride)
         assert per > 0 or not cells, "batch too small for the ride-along baselines"
-        results: List[dict] = []
+        parts = []
         batches = [list(cells[i:i + per]) for i in range(0, len(cells), per)] or [[]]
         for bi, batch in enumerate(batches):
             rb = ride if bi == 0 else []
-            results += self._run_batch(pairs, batch, rb, measure_nll, bases)
-        return results
+            parts.append(self._run_batch(pairs, batch, rb, measure_nll, bases))
+        if getattr(self, "_defer", False):
+            return _Deferred(parts)
+        return [r for part in parts for r in part]
+
+    def run_cells_async(self, pairs: List[Pair], cells: Sequence[Cell], measure_nll: Optional[bool] = None,
+                        ride_along: Sequence[Pair] = ()) -> "_Deferred":
+        """:meth:`run_cells` whose per-cell result records are assembled on a host worker thread: the
+        GPU work (and everything later batches depend on: baselines, spikes, scores, KV) is done when
+        this returns, so the caller can launch the next batch while the records of this one are built.
+        ``.result()`` returns the records."""
+        self._defer = True
+        try:
+            out = self.run_cells(pairs, cells, measure_nll, ride_along)
+        finally:
+            self._defer = False
+        return out if isinstance(out, _Deferred) else _Deferred([out])
+
+    def _records_pool(self):
+        if getattr(self, "_pool", None) is None:
+            from concurrent.futures import ThreadPoolExecutor
+
+            self._pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="tb-records")
+        return self._pool
 
     def _tick(self, name: str) -> None:
         if not self.phase_timing:
@@ -740,6 +762,13 @@ class SweepRunner:
         vh = vals.sum(1).cpu().numpy()
         ih = ids.cpu().numpy()
         self._tick("lens")
+        if getattr(self, "_defer", False):
+            return self._records_pool().submit(self._resume_records, batch, cell_pairs, cell, offs, pr, vh, ih, K)
+        return self._resume_records(batch, cell_pairs, cell, offs, pr, vh, ih, K)
+
+    def _resume_records(self, batch, cell_pairs, cell, offs, pr, vh, ih, K) -> List[dict]:
+        """Host half of :meth:`_resume_readout`: per-cell readout statistics and result records."""
+        nc = len(cell_pairs)
         # ---- per-cell tracked-id probability tables, vectorised: baseline rows up to D, evaluated rows
         ng_a = np.asarray([c[0] for c in cell], dtype=np.int64)
         Lmax = int(max(1, ng_a.max() if nc else 1))
@@ -1037,6 +1066,19 @@ class SweepRunner:
             extra = torch.zeros(nc, device=dev).index_add_(0, slot_d.long(), nll).cpu().tolist()
             sums = [a + e for a, e in zip(sums, extra)]
         return [sums[b] / len(p.resp) if p.resp else float("nan") for b, p in enumerate(cell_pairs)]
+
+
+class _Deferred:
+    """Result records of :meth:`SweepRunner.run_cells_async` (lists and/or futures, in cell order)."""
+
+    def __init__(self, parts):
+        self.parts = parts
+
+    def result(self) -> List[dict]:
+        out: List[dict] = []
+        for p in self.parts:
+            out += p.result() if hasattr(p, "result") else p
+        return out
 
 
 class _nullctx:

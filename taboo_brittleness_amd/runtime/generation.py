@@ -43,8 +43,14 @@ class GenerationOutput:
     tok_nll: Optional[torch.Tensor] = None   # [n, max_new] NLL of each generated token under the (edited) model
     tf_nll: Optional[torch.Tensor] = None    # [n, max_new] NLL of the teacher's token at each column
 
+    def host_tokens(self) -> np.ndarray:
+        host = self.__dict__.get("_host")
+        if host is None:              # one D2H copy for all rows (tokens are final once collected)
+            host = self._host = self.tokens.cpu().numpy()
+        return host
+
     def response_ids(self, b: int) -> List[int]:
-        return self.tokens[b, : self.n_gen[b]].tolist()
+        return self.host_tokens()[b, : self.n_gen[b]].tolist()
 
 
 class Generator:
