@@ -187,6 +187,8 @@ class SweepRunner:
         nll = out.tok_nll.float().cpu().numpy()
         stop = set(int(x) for x in self.gen.stop_ids.tolist())
         slots = list(rows) if slots is None else list(slots)
+        kv_dst: List[int] = []
+        kv_src: List[int] = []
         for j, (p, i) in enumerate(zip(chunk, rows)):
             si = slots[j]
             p.resp = out.response_ids(i)
@@ -213,10 +215,15 @@ class SweepRunner:
                 self._kv_owner[p.kv_slot] = id(p)
                 self._kv_pair[p.kv_slot] = p
                 p.lens_cum = lr.cum[i] if lr.cum is not None else None
-                c = self.gen.cache
-                for l in range(c.k.shape[0]):
-                    self.pair_kv[0][l, p.kv_slot].copy_(c.k[l, si])
-                    self.pair_kv[1][l, p.kv_slot].copy_(c.v[l, si])
+                kv_dst.append(p.kv_slot)
+                kv_src.append(si)
+        if kv_dst:       # every layer's K/V of the finished baselines -> their pair-KV slots (2 gathers)
+            c = self.gen.cache
+            last = dict(zip(kv_dst, kv_src))           # a ring slot reused within one call: last owner wins
+            dst = torch.tensor(list(last.keys()), device=self.dev)
+            src = torch.tensor(list(last.values()), device=self.dev)
+            self.pair_kv[0].index_copy_(1, dst, c.k.index_select(1, src))
+            self.pair_kv[1].index_copy_(1, dst, c.v.index_select(1, src))
 
     def _readout(self, chunk, n_gen, resp_ids, track, seqs=None, keep_cum=False):
         excl = [reference_exclusions(self.tok, r) for r in resp_ids] if self.exclusion == "reference" else None
