@@ -57,7 +57,7 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--arch", default="gemma2-9b")
-    ap.add_argument("--pairs-per-step", type=int, default=60)
+    ap.add_argument("--pairs-per-step", type=int, default=90)
     ap.add_argument("--max-new", type=int, default=50)
     ap.add_argument("--no-nll", action="store_true")
     ap.add_argument("--no-graphs", action="store_true")
@@ -238,6 +238,7 @@ def main() -> None:
                 "decode_bucket_eff": round(runner.stats["decode_row_steps"] / max(1, runner.stats["decode_rows_run"]), 3),
                 # non-degeneracy of the random model: distinct tokens per baseline response, and the
                 # fraction of response tokens equal to their input token (a self-copying model is 1.0)
+                "peak_mem_gb": round(torch.cuda.max_memory_reserved(dev) / 1e9, 1) if on_gpu else None,
                 "distinct_tokens_per_resp": round(float(sum(len(set(p.resp)) for p in cur) / max(1, len(cur))), 2),
                 "self_copy_frac": round(float(sum(sum(a == b for a, b in zip(p.gen_toks[1:], p.gen_toks[:-1]))
                                                   for p in cur) / max(1, sum(len(p.gen_toks) - 1 for p in cur))), 3),

@@ -23,9 +23,12 @@ void tb_attention(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, uin
                   const int32_t* slot, int B, int T, int Hq, int Hkv, int HD, int S, float scale, float softcap,
                   int window, hipStream_t st, const uint16_t* pkc = nullptr, const uint16_t* pvc = nullptr,
                   const int32_t* pslot = nullptr, const int32_t* plen = nullptr);
+// blk [nblk, bw]: (first row, rows, slot) (bw = 3) or + (prefix slot, prefix length) (bw = 5, keys below the
+// prefix length read from that slot of pkc/pvc).
 void tb_attention_varlen(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, uint16_t* out, const int32_t* pos,
                          const int32_t* blk, int nblk, int Hq, int Hkv, int HD, int S, float scale, float softcap,
-                         int window, hipStream_t st);
+                         int window, hipStream_t st, int bw = 3, const uint16_t* pkc = nullptr,
+                         const uint16_t* pvc = nullptr);
 // elementwise.hip
 void tb_geglu(const uint16_t* gu, uint16_t* out, int M, int F, hipStream_t st);
 // lens.hip

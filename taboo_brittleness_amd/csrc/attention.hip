@@ -49,7 +49,8 @@ template <int HD, int G, bool SPLIT = true>
 __global__ void __launch_bounds__(256) attn_cache_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
     uint16_t* __restrict__ out, const int32_t* __restrict__ pos, const int32_t* __restrict__ slot, int T, int Hq,
-    int Hkv, int S, float scale, float softcap, int window, const int32_t* __restrict__ blk, int nitems = 0) {
+    int Hkv, int S, float scale, float softcap, int window, const int32_t* __restrict__ blk, int nitems = 0,
+    int bw = 3, const uint16_t* __restrict__ pkc = nullptr, const uint16_t* __restrict__ pvc = nullptr) {
   constexpr int P = 16 / G;        // query positions per workgroup
   constexpr int KS = HD / 32;      // MFMA k-steps over head_dim
   constexpr int DT = HD / 16;      // 16-wide output dim tiles
@@ -63,20 +64,24 @@ __global__ void __launch_bounds__(256) attn_cache_kernel(
 
   // Row geometry: dense [B, T] layout (blk == nullptr) or a ragged block table blk[i] =
   // {first row, rows (<= P), cache slot} over packed rows (varlen prefill / teacher forcing).
+  // bw = 5: blk[i] also holds (prefix slot, prefix length): keys [0, plen) are read from that slot of
+  // the shared prefix cache (pkc, pvc) — the pair's baseline KV — instead of the row's own slot.
   int kh = blockIdx.y;
-  int rbase, nvalid, cs;
+  int rbase, nvalid, cs, ps = 0, np = 0;
   if constexpr (!SPLIT) {
     const int item = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (item >= nitems) return;                 // wave-uniform; no workgroup barrier in this variant
     const int bi = item / Hkv;
     kh = item % Hkv;
-    rbase = blk[3 * bi];
-    nvalid = blk[3 * bi + 1];
-    cs = blk[3 * bi + 2];
+    rbase = blk[bw * bi];
+    nvalid = blk[bw * bi + 1];
+    cs = blk[bw * bi + 2];
+    if (bw == 5) { ps = blk[bw * bi + 3]; np = blk[bw * bi + 4]; }
   } else if (blk != nullptr) {
-    rbase = blk[3 * blockIdx.x];
-    nvalid = blk[3 * blockIdx.x + 1];
-    cs = blk[3 * blockIdx.x + 2];
+    rbase = blk[bw * blockIdx.x];
+    nvalid = blk[bw * blockIdx.x + 1];
+    cs = blk[bw * blockIdx.x + 2];
+    if (bw == 5) { ps = blk[bw * blockIdx.x + 3]; np = blk[bw * blockIdx.x + 4]; }
   } else {
     const int b = blockIdx.z, t0 = blockIdx.x * P;
     rbase = b * T + t0;
@@ -87,6 +92,12 @@ __global__ void __launch_bounds__(256) attn_cache_kernel(
   const int grp = lane >> 4, col = lane & 15;
   const uint16_t* kbase = kc + ((size_t)cs * Hkv + kh) * (size_t)S * HD;
   const uint16_t* vbase = vc + ((size_t)cs * Hkv + kh) * (size_t)S * HD;
+  const uint16_t* kpre = kbase;
+  const uint16_t* vpre = vbase;
+  if (np > 0) {
+    kpre = pkc + ((size_t)ps * Hkv + kh) * (size_t)S * HD;
+    vpre = pvc + ((size_t)ps * Hkv + kh) * (size_t)S * HD;
+  }
 
   // --- query rows: A-layout row = col; C-layout rows = 4*grp + i
   auto row_pos = [&](int r) -> int {
@@ -144,7 +155,7 @@ __global__ void __launch_bounds__(256) attn_cache_kernel(
       const int c = it * 64 + lane, key = c / VCH, ch = c % VCH;
       int kk = kb + key;
       kk = kk < S ? kk : S - 1;
-      vreg[it] = *reinterpret_cast<const uint4*>(vbase + (size_t)kk * HD + ch * 8);
+      vreg[it] = *reinterpret_cast<const uint4*>((kk < np ? vpre : vbase) + (size_t)kk * HD + ch * 8);
     }
     // ---- S = Q K^T for two 16-key tiles
     f32x4 sacc[2];
@@ -152,7 +163,7 @@ __global__ void __launch_bounds__(256) attn_cache_kernel(
     for (int tt = 0; tt < 2; ++tt) {
       int kk = kb + tt * 16 + col;
       kk = kk < S ? kk : S - 1;
-      const uint16_t* krow = kbase + (size_t)kk * HD + grp * 8;
+      const uint16_t* krow = (kk < np ? kpre : kbase) + (size_t)kk * HD + grp * 8;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
@@ -299,7 +310,8 @@ __global__ void __launch_bounds__(256) attn_cache_kernel(
 template <int HD, int G>
 void launch_attn(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, uint16_t* out, const int32_t* pos,
                  const int32_t* slot, int B, int T, int Hq, int Hkv, int S, float scale, float softcap, int window,
-                 hipStream_t st, const int32_t* blk = nullptr, int nblk = 0) {
+                 hipStream_t st, const int32_t* blk = nullptr, int nblk = 0, int bw = 3,
+                 const uint16_t* pkc = nullptr, const uint16_t* pvc = nullptr) {
   constexpr int P = 16 / G;
   const size_t lds = (size_t)tb_attention_lds_bytes(HD);
   static bool attr_set = false;   // > 64 KB dynamic LDS needs the opt-in (first call is never captured)
@@ -318,13 +330,13 @@ void launch_attn(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, uint
     }
     const int nitems = nblk * Hkv;
     hipLaunchKernelGGL((attn_cache_kernel<HD, G, false>), dim3((nitems + 3) / 4), dim3(256), lds, st, q, kc, vc, out,
-                       pos, slot, T, Hq, Hkv, S, scale, softcap, window, blk, nitems);
+                       pos, slot, T, Hq, Hkv, S, scale, softcap, window, blk, nitems, bw, pkc, pvc);
     return;
   }
   if (blk != nullptr) {
     dim3 grid(nblk, Hkv, 1);
     hipLaunchKernelGGL((attn_cache_kernel<HD, G>), grid, dim3(256), lds, st, q, kc, vc, out, pos, slot, T, Hq, Hkv,
-                       S, scale, softcap, window, blk, 0);
+                       S, scale, softcap, window, blk, 0, bw, pkc, pvc);
     return;
   }
   dim3 grid((T + P - 1) / P, Hkv, B);
@@ -545,12 +557,13 @@ void tb_attention(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, uin
 
 void tb_attention_varlen(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, uint16_t* out, const int32_t* pos,
                          const int32_t* blk, int nblk, int Hq, int Hkv, int HD, int S, float scale, float softcap,
-                         int window, hipStream_t st) {
+                         int window, hipStream_t st, int bw, const uint16_t* pkc, const uint16_t* pvc) {
   if (nblk <= 0) return;
   const int G = Hq / Hkv;
 #define TB_VL_CASE(hd, g)                                                                                    \
   if (HD == hd && G == g) {                                                                                  \
-    launch_attn<hd, g>(q, kc, vc, out, pos, nullptr, 0, 0, Hq, Hkv, S, scale, softcap, window, st, blk, nblk); \
+    launch_attn<hd, g>(q, kc, vc, out, pos, nullptr, 0, 0, Hq, Hkv, S, scale, softcap, window, st, blk, nblk,  \
+                       bw, pkc, pvc);                                                                        \
     return;                                                                                                  \
   }
   TB_VL_CASE(256, 2)

@@ -135,6 +135,29 @@ void attention_varlen(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch
                       blk.size(0), Hq, Hkv, HD, S, (float)scale, (float)softcap, (int)window, cur_stream());
 }
 
+// Varlen attention whose blocks read keys [0, plen) from a shared prefix cache slot:
+// blk [nblk, 5] = (row0, nrows, slot, prefix slot, prefix length).
+void attention_varlen_prefix(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch::Tensor out, torch::Tensor pos,
+                             torch::Tensor blk, double scale, double softcap, int64_t window, torch::Tensor pk,
+                             torch::Tensor pv) {
+  IN_BF16(q); IN_BF16(kc); IN_BF16(vc); IN_BF16(out); IN_I32(pos); IN_I32(blk); IN_BF16(pk); IN_BF16(pv);
+  TORCH_CHECK(kc.dim() == 4, "cache must be [slots, Hkv, S, HD]");
+  const int Hkv = kc.size(1), S = kc.size(2), HD = kc.size(3);
+  const int M = pos.numel();
+  TORCH_CHECK(q.numel() % ((int64_t)M * HD) == 0 && out.numel() == q.numel(), "q/out shape");
+  const int Hq = q.numel() / ((int64_t)M * HD);
+  TORCH_CHECK(Hq % Hkv == 0 && (HD == 256 || HD == 128), "unsupported head geometry");
+  const int G = Hq / Hkv;
+  TORCH_CHECK(G == 1 || G == 2 || G == 4, "unsupported GQA ratio");
+  TORCH_CHECK(blk.dim() == 2 && blk.size(1) == 5, "blk must be [nblk, 5] = (row0, nrows, slot, pslot, plen)");
+  TORCH_CHECK(pk.dim() == 4 && pk.size(1) == Hkv && pk.size(2) == S && pk.size(3) == HD && pv.sizes() == pk.sizes(),
+              "prefix cache must be [P, Hkv, S, HD] like the cache");
+  c10::DeviceGuard g(q.device());
+  tb_attention_varlen(cbf(q), cbf(kc), cbf(vc), bf(out), pos.data_ptr<int32_t>(), blk.data_ptr<int32_t>(),
+                      blk.size(0), Hq, Hkv, HD, S, (float)scale, (float)softcap, (int)window, cur_stream(), 5,
+                      cbf(pk), cbf(pv));
+}
+
 void geglu(torch::Tensor gu, torch::Tensor out) {
   IN_BF16(gu); IN_BF16(out);
   const int F2 = gu.size(-1), M = gu.numel() / F2;
@@ -342,6 +365,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attention", &attention);
   m.def("attention_prefix", &attention_prefix);
   m.def("attention_varlen", &attention_varlen);
+  m.def("attention_varlen_prefix", &attention_varlen_prefix);
   m.def("geglu", &geglu);
   m.def("argmax_rows", &argmax_rows);
   m.def("row_lse", &row_lse);

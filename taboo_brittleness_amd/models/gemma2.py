@@ -90,15 +90,18 @@ class KVPrefix:
         return (self.k[l], self.v[l], self.slot[:B], n[:B])
 
 
-def packed_blocks(seqs: Sequence[Tuple[int, int, int]], rows_per_block: int) -> torch.Tensor:
-    """Attention block table for packed rows: ``seqs`` = (first row, n rows, cache slot) per sequence;
-    each sequence is cut into blocks of at most ``rows_per_block`` rows (16 / GQA ratio for the
-    MFMA kernel).  Returns int32 ``[nblk, 3]`` (CPU)."""
+def packed_blocks(seqs: Sequence[Tuple[int, ...]], rows_per_block: int) -> torch.Tensor:
+    """Attention block table for packed rows: ``seqs`` = (first row, n rows, cache slot) per sequence,
+    optionally + (prefix slot, prefix length) — keys below that length are read from the shared prefix
+    cache (:func:`ops.attention_varlen` ``prefix_kv``); each sequence is cut into blocks of at most
+    ``rows_per_block`` rows (16 / GQA ratio for the MFMA kernel).  Returns int32 ``[nblk, 3|5]`` (CPU)."""
     out = []
-    for r0, n, sl in seqs:
+    w = len(seqs[0]) if seqs else 3
+    for sq in seqs:
+        r0, n = sq[0], sq[1]
         for i in range(0, n, rows_per_block):
-            out.append((r0 + i, min(rows_per_block, n - i), sl))
-    return torch.tensor(out or [(0, 0, 0)], dtype=torch.int32).view(-1, 3)
+            out.append((r0 + i, min(rows_per_block, n - i)) + tuple(sq[2:]))
+    return torch.tensor(out or [(0, 0, 0) + (0,) * (w - 3)], dtype=torch.int32).view(-1, w)
 
 
 class _Workspace:
@@ -200,7 +203,8 @@ class Gemma2Model:
     def forward_packed(self, ids: Optional[torch.Tensor], pos: torch.Tensor, slot_rows: torch.Tensor,
                        blk: torch.Tensor, cache: KVCache, hooks: Optional[Dict[int, Sequence[Hook]]] = None,
                        stop_at: Optional[int] = None, ws: Optional[_Workspace] = None,
-                       resume_after: Optional[int] = None, h_in: Optional[torch.Tensor] = None) -> torch.Tensor:
+                       resume_after: Optional[int] = None, h_in: Optional[torch.Tensor] = None,
+                       prefix_kv: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
         """Ragged forward over packed rows ``ids [M]`` (no padding between sequences): row ``i`` sits at
         position ``pos[i]`` of cache slot ``slot_rows[i]``; ``blk`` is the attention block table
         (:func:`packed_blocks`).  Hooks see every row as its own length-1 sequence (``ctx.B = M``,
@@ -209,14 +213,19 @@ class Gemma2Model:
         ``resume_after=l, h_in [M, d]``: start from the residual stream *after* block ``l`` (its hooks
         run first, then blocks ``l+1..``; ``ids`` unused).  Blocks ``<= l`` — and their KV — are not
         touched: the caller guarantees they equal what a full forward of these tokens would produce
-        (the exact layer-resume of prefix-shared sweep cells)."""
+        (the exact layer-resume of prefix-shared sweep cells).
+
+        ``prefix_kv = (k, v)`` (``[L, P, Hkv, S, HD]``) with a 5-column ``blk``: each block reads its keys
+        below its prefix length from its prefix slot of ``k/v`` (no copy into the row's own slot)."""
         M = pos.numel()
         ws = ws or self.workspace(M)
         ws.slot_rows.copy_(slot_rows.view(M))
         sr = ws.slot_rows
 
         def attn(l, q, kc, vc, pos32, window, out):
-            ops.attention_varlen(q, kc, vc, pos32, sr, blk, self.scale, self.spec.attn_softcap, window, out=out)
+            pre = (prefix_kv[0][l], prefix_kv[1][l]) if prefix_kv is not None else None
+            ops.attention_varlen(q, kc, vc, pos32, sr, blk, self.scale, self.spec.attn_softcap, window, out=out,
+                                 prefix_kv=pre)
 
         if resume_after is not None:
             return self._run(None, pos.reshape(M), cache, ws, attn, hooks, stop_at, M, 1, sr,

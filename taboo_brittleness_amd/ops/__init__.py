@@ -136,16 +136,30 @@ def attention(q, kc, vc, pos, slot, B, T, scale, softcap, window, out=None, pref
     return o
 
 
-def attention_varlen(q, kc, vc, pos, slot_rows, blk, scale, softcap, window, out=None):
+def attention_varlen(q, kc, vc, pos, slot_rows, blk, scale, softcap, window, out=None, prefix_kv=None):
     """Attention over packed rows ``q [M, Hq, HD]``: row ``i`` reads cache slot ``slot_rows[i]`` up to
     ``pos[i]``.  ``blk [nblk, 3] = (first row, rows, slot)`` groups consecutive rows of one sequence
-    (<= 16 / GQA-ratio rows each) for the MFMA kernel; the CPU path only needs ``slot_rows``."""
+    (<= 16 / GQA-ratio rows each) for the MFMA kernel; the CPU path only needs ``slot_rows``.
+    ``prefix_kv = (pk, pv)`` with ``blk [nblk, 5]`` (+ prefix slot, prefix length): a block's keys below
+    its prefix length come from that slot of the shared prefix cache ``pk/pv [P, Hkv, S, HD]``."""
     M = pos.numel()
     if q.is_cuda:
         out = _out(out, (M, q.numel() // M), q.dtype, q.device)
+        if prefix_kv is not None:
+            _k().attention_varlen_prefix(q, kc, vc, out, pos, blk, float(scale), float(softcap), int(window),
+                                         prefix_kv[0], prefix_kv[1])
+            return out
         _k().attention_varlen(q, kc, vc, out, pos, blk, float(scale), float(softcap), int(window))
         return out
-    o = ref.attention(q, kc, vc, pos, slot_rows, M, 1, scale, softcap, window)
+    pre = None
+    if prefix_kv is not None:
+        ps = torch.zeros(M, dtype=torch.long)
+        pl = torch.zeros(M, dtype=torch.long)
+        for r0, n, _, s_, l_ in blk.cpu().long().tolist():
+            ps[r0:r0 + n] = s_
+            pl[r0:r0 + n] = l_
+        pre = (prefix_kv[0], prefix_kv[1], ps, pl)
+    o = ref.attention(q, kc, vc, pos, slot_rows, M, 1, scale, softcap, window, prefix=pre)
     if out is not None:
         out.copy_(o.view_as(out))
         return out

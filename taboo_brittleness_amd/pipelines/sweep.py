@@ -129,6 +129,7 @@ class SweepRunner:
         self.layer_resume = cfg.runtime.layer_resume if layer_resume is None else layer_resume
         self.overlap_ride = os.environ.get("TB_OVERLAP_RIDE", "1") == "1"
         self.tf_streams = os.environ.get("TB_TF_STREAMS", "0") == "1"   # no measurable gain; opt-in
+        self.tf_prefix = os.environ.get("TB_TF_PREFIX", "1") == "1"
         self.stats: Dict[str, int] = {"cells": 0, "diverged": 0, "tf_rows": 0, "lens_rows": 0,
                                       "decode_row_steps": 0, "decode_rows_run": 0}
         self._with_basis = True
@@ -594,7 +595,10 @@ class SweepRunner:
                 first = gen.prefill([p.ids for p in rb], list(range(nc, nc + nr)), hooks, out_rows=list(range(nr)))
                 gen.decode(first, [p.plen for p in rb], None, self.max_new, nr, hooks, "sweep",
                            slots=list(range(nc, nc + nr)))
-        self._copy_pair_kv(range(nc), [p.kv_slot for p in cell_pairs], layers=range(l0 + 1, L))
+        # blocks > l read the pair's baseline KV below the first edit in place (no per-cell copy), or copy
+        # it into each cell's slot first (TB_TF_PREFIX=0, A/B switch)
+        if not self.tf_prefix:
+            self._copy_pair_kv(range(nc), [p.kv_slot for p in cell_pairs], layers=range(l0 + 1, L))
         self._tick("kv_copy")
         tf = self._tf_pass(cell_pairs, hooks)
         self._tick("tf_pass")
@@ -909,7 +913,8 @@ class SweepRunner:
                 cur, c_lo, c_rows = [], r0, 0
             if not cur:
                 c_lo = r0
-            cur.append((r0 - c_lo, Ln, b))
+            cur.append((r0 - c_lo, Ln, b, cell_pairs[b].kv_slot, int(plen_a[b] + f)) if self.tf_prefix
+                       else (r0 - c_lo, Ln, b))
             c_rows += Ln
         if cur:
             chunks.append((c_lo, c_lo + c_rows, cur))
@@ -930,7 +935,7 @@ class SweepRunner:
                 cp[:Mc], cs[:Mc], hin[:Mc] = pos_d[c0:c1], slot_d[c0:c1], H[c0:c1]
                 ws = self._nll_ws(ws_rows, key=ci % len(streams)).rows(Mp)
                 x = m.forward_packed(None, cp, cs, blk, self.gen.cache, hooks, ws=ws, resume_after=self.layer,
-                                     h_in=hin)
+                                     h_in=hin, prefix_kv=self.pair_kv if self.tf_prefix else None)
                 for q0 in range(0, Mc, step):
                     q1 = min(Mc, q0 + step)
                     # the unembedding runs on whole 256-row tiles (padding rows of x included) so the

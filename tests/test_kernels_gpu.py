@@ -136,6 +136,38 @@ def test_attention_varlen_packed(gpu, G, HD):
         _close(og, orf, atol=2e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("G,HD", [(2, 256), (1, 128)])
+def test_attention_varlen_shared_prefix(gpu, G, HD):
+    """Packed blocks whose keys below a per-block prefix length come from a shared prefix-cache slot
+    (5-column block table) == the reference with those keys substituted."""
+    from taboo_brittleness_amd.models.gemma2 import packed_blocks
+
+    torch.manual_seed(15)
+    Hkv, S = 2, 96
+    Hq = Hkv * G
+    kc = torch.randn(5, Hkv, S, HD, dtype=BF)
+    vc = torch.randn(5, Hkv, S, HD, dtype=BF)
+    pk = torch.randn(3, Hkv, S, HD, dtype=BF)
+    pv = torch.randn(3, Hkv, S, HD, dtype=BF)
+    spec_ = [(3, 10, 23, 1, 12), (0, 40, 1, 0, 0), (4, 5, 13, 2, 9), (1, 70, 26, 1, 75)]   # + (pslot, plen)
+    pos, slot_rows, seqs = [], [], []
+    for sl, p0, n, ps, pl in spec_:
+        seqs.append((len(pos), n, sl, ps, pl))
+        pos += list(range(p0, p0 + n))
+        slot_rows += [sl] * n
+    M = len(pos)
+    pos_t = torch.tensor(pos, dtype=torch.int32)
+    sr = torch.tensor(slot_rows, dtype=torch.int32)
+    blk = packed_blocks(seqs, 16 // G)
+    assert blk.shape[1] == 5
+    q = torch.randn(M, Hq, HD, dtype=BF) * 2
+    for window in (0, 16):
+        og = ops.attention_varlen(q.to(gpu), kc.to(gpu), vc.to(gpu), pos_t.to(gpu), sr.to(gpu), blk.to(gpu),
+                                  HD ** -0.5, 50.0, window, prefix_kv=(pk.to(gpu), pv.to(gpu)))
+        orf = ops.attention_varlen(q, kc, vc, pos_t, sr, blk, HD ** -0.5, 50.0, window, prefix_kv=(pk, pv))
+        _close(og, orf, atol=2e-2, rtol=2e-2)
+
+
 def test_decode_head(gpu):
     torch.manual_seed(13)
     R, V = 6, 4099 * 8 + 5
