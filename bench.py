@@ -70,6 +70,10 @@ def main() -> None:
                          "E is reduced to a divisor of --steps so the timed window holds exactly its share)")
     ap.add_argument("--lora-rank", type=int, default=0,
                     help="per-word random LoRA adapters of this rank, batched unmerged (multi-adapter bank)")
+    ap.add_argument("--carry-rows", type=int, default=0,
+                    help="decode-tail carry-over: once fewer diverged cells than this still decode, they continue in "
+                         "the next step's decode (spare KV slots; warmup and the last timed step drain); 0 = off. "
+                         "768 measured +1.6%% at +31 GB (profiles/bench_r1_carry_ab.log), so off by default")
     ap.add_argument("--init-gain", type=float, default=32.0,
                     help="post-norm gain of the random init (models.weights.random_gemma2).  1 = plain HF init, "
                          "whose random Gemma-2 repeats its input token so no edit ever changes a generation "
@@ -107,10 +111,12 @@ def main() -> None:
     sae = JumpReLUSAE.random(spec.hidden, cfg.sae.d_sae, seed=7, device=dev)
     layer = min(cfg.model.layer_idx, spec.layers - 1)
     n_cells = len(cfg.intervention.budgets) * (1 + cfg.intervention.random_trials)
-    batch = P * n_cells + E * P
+    C = max(0, args.carry_rows) if not args.no_layer_resume else 0
+    batch = P * n_cells + E * P + C
     runner = SweepRunner(cfg, model, tok, sae, batch=batch, device=dev, layer=layer,
                          use_graphs=not args.no_graphs, prefix_share=not args.no_prefix_share,
-                         kv_pairs=(E + 2) * P + 2, layer_resume=not args.no_layer_resume)
+                         kv_pairs=(E + 3) * P + 2, layer_resume=not args.no_layer_resume)
+    runner.carry_rows = C
     templates = runner.build_pairs(cfg.words, cfg.prompts)
     methods = ("sae_targeted", "sae_random")
 
@@ -143,8 +149,10 @@ def main() -> None:
             ride += future[j]
         cells = runner.make_cells(cur, methods)
         runner.timings["make_cells"] = runner.timings.get("make_cells", 0.0) + time.perf_counter() - t0
-        # the records of step k are assembled on a host thread while step k+1's GPU work runs
-        res = runner.run_cells_async(cur, cells, ride_along=ride)
+        # the records of step k are assembled on a host thread while step k+1's GPU work runs; decode
+        # tails carry into the next step except out of warmup and out of the last timed step
+        drain = k < args.warmup or k == args.warmup + args.steps - 1
+        res = runner.run_cells_async(cur, cells, ride_along=ride, drain=drain)
         return future.pop(k + 1), res, time.perf_counter() - t0
 
     def cells_of(k):
@@ -221,6 +229,7 @@ def main() -> None:
                 "prefix_share": not args.no_prefix_share,
                 "layer_resume": not args.no_layer_resume,
                 "baseline_every": E,
+                "carry_rows": C,
                 "lora_adapters": (f"{len(cfg.words)} x rank {args.lora_rank} (unmerged bank)" if args.lora_rank
                                   else "none (weights as merged taboo models)"),
             },
@@ -236,6 +245,7 @@ def main() -> None:
                 # computed rows that were needed (the rest is row-bucket padding)
                 "decode_row_steps_per_cell": round(runner.stats["decode_row_steps"] / max(1, runner.stats["cells"]), 2),
                 "decode_bucket_eff": round(runner.stats["decode_row_steps"] / max(1, runner.stats["decode_rows_run"]), 3),
+                "carried_cells_per_step": round(runner.stats["carried"] / max(1, args.steps), 1),
                 # non-degeneracy of the random model: distinct tokens per baseline response, and the
                 # fraction of response tokens equal to their input token (a self-copying model is 1.0)
                 "peak_mem_gb": round(torch.cuda.max_memory_reserved(dev) / 1e9, 1) if on_gpu else None,
@@ -245,6 +255,10 @@ def main() -> None:
             },
         }
         print(json.dumps(out), flush=True)
+    marks = os.environ.get("TB_PHASE_MARKS")
+    if marks and info.is_main:
+        with open(marks, "w") as f:
+            json.dump(getattr(runner, "phase_marks", []), f)
     if args.tune_gemms:
         flush_tuned_gemms()
     D.destroy(info)

@@ -101,6 +101,24 @@ class Cell:
         return "sae" if self.method.startswith("sae") else "proj"
 
 
+@dataclass
+class _Carry:
+    """A diverged cell whose decode continues in the next batch (decode-tail carry-over): its KV,
+    capture-store row and edit-plan row live in the runner's carry region at ``slot``."""
+    cell: Cell
+    pair: Pair
+    d: int                       # divergence point D
+    nll: float                   # teacher-forced edit NLL of the baseline hint (already complete)
+    slot: int
+    tok: int                     # next token to feed, at position ``pos``
+    pos: int
+    prefix: List[int]            # response tokens so far (ends with ``tok``)
+    prefix_nll: np.ndarray       # their NLLs
+    steps: int                   # decode steps still needed
+    pre: Tuple[int, int, int]    # (pair KV slot, len_lo, len_hi) of the shared prefix
+    plan_row: Tuple[np.ndarray, int, np.ndarray, int]   # host (spikes, kind, idx, cnt) of the slot
+
+
 class SweepRunner:
     def __init__(self, cfg, model, tok, sae, batch: int, device, layer: Optional[int] = None,
                  max_new: Optional[int] = None, use_graphs: bool = True, exclusion: str = "reference",
@@ -131,7 +149,15 @@ class SweepRunner:
         self.tf_streams = os.environ.get("TB_TF_STREAMS", "0") == "1"   # no measurable gain; opt-in
         self.tf_prefix = os.environ.get("TB_TF_PREFIX", "1") == "1"
         self.stats: Dict[str, int] = {"cells": 0, "diverged": 0, "tf_rows": 0, "lens_rows": 0,
-                                      "decode_row_steps": 0, "decode_rows_run": 0}
+                                      "decode_row_steps": 0, "decode_rows_run": 0, "carried": 0}
+        # decode-tail carry-over (opt-in; needs ``batch`` to include ``carry_rows`` spare slots): once fewer
+        # than ``carry_rows`` diverged cells still decode, the rest continue in the next batch's decode
+        # (merged with its new rows) instead of running a long small-batch tail.  Records of carried cells
+        # come out with the batch that finishes them; ``run_cells(..., drain=True)`` carries nothing.
+        self.carry_rows = 0
+        self._carry: List[_Carry] = []
+        self._drain = True
+        self._drain_batch = True
         self._with_basis = True
 
     # ----------------------------------------------------------------- pairs
@@ -351,10 +377,16 @@ class SweepRunner:
                     kd[ci] = 2
                     brow.append(np.arange(ci * rmax, ci * rmax + r))
                     bval.append(U.float().cpu())
+        for cr in self._carry:                  # carried cells keep editing at their carry-region slots
+            cs_, ck_, ci_, cc_ = cr.plan_row
+            sp[cr.slot] = cs_
+            kd[cr.slot] = ck_
+            ix[cr.slot] = ci_
+            cn[cr.slot] = cc_
         basis = None
         if brow:
             basis = (np.concatenate(brow), torch.cat(bval, 0))
-        return {"spikes": sp, "kind": kd, "idx": ix, "cnt": cn, "basis": basis, "rows": B * rmax}
+        return {"spikes": sp, "kind": kd, "idx": ix, "cnt": cn, "basis": basis, "rows": B * rmax, "rmax": rmax}
 
     def _load_plan(self, plan: dict) -> EditHook:
         """Upload into the persistent plan (fixed tensors, so a captured decode graph stays valid)."""
@@ -414,10 +446,12 @@ class SweepRunner:
     # -------------------------------------------------------------------- run
     @torch.no_grad()
     def run_cells(self, pairs: List[Pair], cells: Sequence[Cell], measure_nll: Optional[bool] = None,
-                  ride_along: Sequence[Pair] = ()) -> List[dict]:
+                  ride_along: Sequence[Pair] = (), drain: bool = True) -> List[dict]:
         """Run edited cells; ``ride_along`` pairs get their *baseline* generated in the same batch
-        (unedited rows), which pipelines the next cells' baselines behind the current ones."""
+        (unedited rows), which pipelines the next cells' baselines behind the current ones.
+        ``drain=False`` (with ``carry_rows``) lets the last batch's decode tail carry into the next call."""
         measure_nll = self.iv.measure_nll if measure_nll is None else measure_nll
+        self._drain = drain
         ride = list(ride_along)
         if not cells and not ride:
             return []
@@ -435,20 +469,21 @@ class SweepRunner:
         batches = [list(cells[i:i + per]) for i in range(0, len(cells), per)] or [[]]
         for bi, batch in enumerate(batches):
             rb = ride if bi == 0 else []
+            self._drain_batch = drain or bi + 1 < len(batches)
             parts.append(self._run_batch(pairs, batch, rb, measure_nll, bases))
         if getattr(self, "_defer", False):
             return _Deferred(parts)
         return [r for part in parts for r in part]
 
     def run_cells_async(self, pairs: List[Pair], cells: Sequence[Cell], measure_nll: Optional[bool] = None,
-                        ride_along: Sequence[Pair] = ()) -> "_Deferred":
+                        ride_along: Sequence[Pair] = (), drain: bool = True) -> "_Deferred":
         """:meth:`run_cells` whose per-cell result records are assembled on a host worker thread: the
         GPU work (and everything later batches depend on: baselines, spikes, scores, KV) is done when
         this returns, so the caller can launch the next batch while the records of this one are built.
         ``.result()`` returns the records."""
         self._defer = True
         try:
-            out = self.run_cells(pairs, cells, measure_nll, ride_along)
+            out = self.run_cells(pairs, cells, measure_nll, ride_along, drain)
         finally:
             self._defer = False
         return out if isinstance(out, _Deferred) else _Deferred([out])
@@ -470,6 +505,8 @@ class SweepRunner:
         if last is not None and name != "start":
             self.timings[name] = self.timings.get(name, 0.0) + (now - last)
         self._t_last = now
+        # phase boundaries on the monotonic clock rocprofv3 stamps kernels with (tools/phase_kernels.py)
+        self.__dict__.setdefault("phase_marks", []).append((name, time.monotonic_ns()))
 
     def _resumable(self, cell_pairs: Sequence[Pair]) -> bool:
         return self.layer_resume and self.prefix_share and bool(cell_pairs) and all(
@@ -488,6 +525,7 @@ class SweepRunner:
         self._set_adapters([pairs[c.pair] for c in batch] + list(rb))
         if self._resumable([pairs[c.pair] for c in batch]):
             return self._run_batch_resume(pairs, batch, rb, measure_nll, bases)
+        assert not self._carry, "carried cells need the layer-resume path (drain before switching)"
         gen = self.gen
         self._tick("start")
         nc = len(batch)
@@ -619,14 +657,31 @@ class SweepRunner:
         # computed straight from the pair's KV slot: blocks <= l for positions < plen + D (same tokens,
         # no edit yet), blocks > l for positions < plen + f (before the first edit); the blocks > l
         # keys in [plen + f, plen + D) are the teacher-forced tail's, already in the cell's own slot.
-        # ---- decode: ride-along baselines (rows 0..nr-1, slots nc..) + diverged cells (slot b)
+        # ---- per-cell teacher-forced numbers (complete for every cell): edit NLL, and the self NLL of
+        # cells whose tokens never left the baseline's
+        seg = tf["seg"]
+        ns_cs = np.concatenate([[0.0], np.cumsum(tf["nll_self"], dtype=np.float64)])
+        nt_cs = np.concatenate([[0.0], np.cumsum(tf["nll_tgt"], dtype=np.float64)])
+        nll_c, sn_c = [float("nan")] * nc, [float("nan")] * nc
+        for b, p in enumerate(cell_pairs):
+            f, E, r0 = seg[b]
+            n = len(p.resp)
+            if not n:
+                continue
+            ntail = max(0, n - 1 - f)
+            base_self = float(p.tok_nll[: min(f + 1, n)].sum())
+            if measure_nll:
+                nll_c[b] = (base_self + float(nt_cs[r0 + ntail] - nt_cs[r0])) / n
+            sn_c[b] = (base_self + float(ns_cs[r0 + ntail] - ns_cs[r0])) / n
+        # ---- decode: ride-along baselines (rows 0..nr-1, slots nc..) + diverged cells (slot b) + cells
+        # carried over from the previous batch (carry-region slots), longest remaining decode first
         starts, prefix, toks, slots, pnll_rows, rsteps = [], [], [], [], [], []
         pre_slot, pre_lo, pre_hi = [], [], []
         steps = 0
         out_r = None
         if overlap:
             torch.cuda.current_stream(self.dev).wait_stream(side)
-            out_r = gen.collect(nr, self.max_new, [p.plen for p in rb], copy=bool(div))
+            out_r = gen.collect(nr, self.max_new, [p.plen for p in rb], copy=bool(div) or bool(self._carry))
             self._tick("ride_decode_join")
         elif nr:
             first = gen.prefill([p.ids for p in rb], list(range(nc, nc + nr)), hooks, out_rows=list(range(nr)))
@@ -637,44 +692,71 @@ class SweepRunner:
                 toks.append(fl[j])
                 slots.append(nc + j)
                 rsteps.append(self.max_new)
+                pnll_rows.append(None)
                 pre_slot.append(0)
                 pre_lo.append(0)
                 pre_hi.append(0)
             steps = self.max_new
-        Wp = 1
-        for b in div:
-            p = cell_pairs[b]
-            f, E, r0 = tf["seg"][b]
-            e = int(tf["nxt"][r0 + D[b] - 1 - f])
-            starts.append(p.plen + D[b])
-            prefix.append(list(p.gen_toks[: D[b]]) + [e])
-            toks.append(e)
-            slots.append(b)
-            own = np.concatenate([p.tok_nll[: f + 1], tf["nll_self"][r0: r0 + D[b] - f]]).astype(np.float32)
-            pnll_rows.append(own)
-            Wp = max(Wp, own.shape[0])
-            steps = max(steps, self.max_new - D[b])
-            rsteps.append(max(1, self.max_new - D[b]))
-            pre_slot.append(p.kv_slot)
-            pre_lo.append(p.plen + D[b])
-            pre_hi.append(p.plen + f)
+        n_ride_rows = len(slots)
+        crow = [(max(1, self.max_new - D[b]), 0, b) for b in div] + \
+               [(cr.steps, 1, i) for i, cr in enumerate(self._carry)]
+        crow.sort(key=lambda t: -t[0])                       # stable: new rows before carried on ties
+        carry_in = self._carry
+        self._carry = []
+        row_src = []                                         # per cell decode row: ("new", b) | ("carry", _Carry)
+        for st, kind, i in crow:
+            if kind == 0:
+                b = i
+                p = cell_pairs[b]
+                f, E, r0 = seg[b]
+                e = int(tf["nxt"][r0 + D[b] - 1 - f])
+                starts.append(p.plen + D[b])
+                prefix.append(list(p.gen_toks[: D[b]]) + [e])
+                toks.append(e)
+                slots.append(b)
+                pnll_rows.append(np.concatenate([p.tok_nll[: f + 1], tf["nll_self"][r0: r0 + D[b] - f]]).astype(np.float32))
+                pre_slot.append(p.kv_slot)
+                pre_lo.append(p.plen + D[b])
+                pre_hi.append(p.plen + f)
+                row_src.append(("new", b))
+            else:
+                cr = carry_in[i]
+                starts.append(cr.pos)
+                prefix.append(cr.prefix)
+                toks.append(cr.tok)
+                slots.append(cr.slot)
+                pnll_rows.append(cr.prefix_nll)
+                pre_slot.append(cr.pre[0])
+                pre_lo.append(cr.pre[1])
+                pre_hi.append(cr.pre[2])
+                row_src.append(("carry", cr))
+            rsteps.append(st)
+            steps = max(steps, st)
         nrows = len(slots)
         self._tick("prefill")
         out = None
+        ran = steps
+        carry_move = None
         if nrows:
             nr_here = 0 if overlap else nr
+            Wp = max([1] + [len(x) for x in pnll_rows if x is not None])
             pnll = torch.zeros(nrows, Wp)
             if nr_here:
                 pnll[:nr, :1] = gen.out_nll[:nr, :1].cpu()
             for j, own in enumerate(pnll_rows):
-                pnll[nr_here + j, : own.shape[0]] = torch.from_numpy(own)
-            gen.decode(torch.tensor(toks, dtype=torch.int32), starts, prefix, max(steps, 1), nrows, hooks,
-                       "sweep", prefix_nll=pnll.to(self.dev), slots=slots, row_steps=rsteps,
-                       prefix_rows=(pre_slot, pre_lo, pre_hi))
+                if own is not None:
+                    pnll[j, : own.shape[0]] = torch.from_numpy(np.asarray(own, dtype=np.float32))
+            carry_ok = (self.carry_rows > 0 and not self._drain_batch and n_ride_rows == 0)
+            ran = gen.decode(torch.tensor(toks, dtype=torch.int32), starts, prefix, max(steps, 1), nrows, hooks,
+                             "sweep", prefix_nll=pnll.to(self.dev), slots=slots, row_steps=rsteps,
+                             prefix_rows=(pre_slot, pre_lo, pre_hi),
+                             stop_below=self.carry_rows if carry_ok else 0,
+                             min_steps=max([cr.steps for cr in carry_in] + [0]))
             out = gen.collect(nrows, self.max_new, ([] if overlap else [p.plen for p in rb]) +
-                              [cell_pairs[b].plen for b in div])
+                              [(cell_pairs[src[1]].plen if src[0] == "new" else src[1].pair.plen) for src in row_src])
             self.stats["decode_row_steps"] += gen.last_rows[0]
             self.stats["decode_rows_run"] += gen.last_rows[1]
+            carry_move = self._carry_out(plan, cell_pairs, batch, D, seg, nll_c, row_src, rsteps, ran, n_ride_rows)
         if overlap:
             out = out_r if out is None else _cat_outputs(out_r, out)
         self._tick("decode")
@@ -689,10 +771,94 @@ class SweepRunner:
             self._score_pairs(rb)
             self._tick("baseline_scores")
         self._tick("baseline_lens+finalize")
-        # ---- cells: responses, reused + partial lens
-        results = self._resume_readout(batch, cell_pairs, tf, D, div, out, nr, measure_nll)
+        # ---- cells: responses, reused + partial lens.  Readout entries: every cell of this batch except
+        # the ones carried on, then the carried cells of earlier batches that finished here
+        carried_now = {id(cr.cell) for cr in self._carry}
+        drow = {}
+        fin_carry = []
+        for j, src in enumerate(row_src):
+            if src[0] == "new":
+                drow[src[1]] = nr + j
+            elif id(src[1].cell) not in carried_now:
+                fin_carry.append((src[1], nr + j))
+        entries = []
+        for b, (c, p) in enumerate(zip(batch, cell_pairs)):
+            if id(c) in carried_now:
+                continue
+            if D[b] is None:
+                entries.append((c, p, b, None, nll_c[b], sn_c[b], None))
+            else:
+                entries.append((c, p, b, D[b], nll_c[b], None, drow[b]))
+        for cr, j in fin_carry:
+            entries.append((cr.cell, cr.pair, cr.slot, cr.d, cr.nll, None, j))
+        results = self._resume_readout(entries, out) if entries else []
+        if carry_move is not None:      # after the readout has read the finished carried cells' store rows
+            carry_move()
         self._tick("results")
         return results
+
+    def _carry_out(self, plan, cell_pairs, batch, D, seg, nll_c, row_src, rsteps, ran, n_ride_rows):
+        """After an early-stopped decode: record the still-unfinished cell rows as carried and return the
+        move of their data to the carry region (KV of every layer, capture-store row, adapter id,
+        projection basis rows) — to run once this batch's readout has read the store rows of the
+        carried cells that finished here (the region slots get reused)."""
+        gen = self.gen
+        unf = [j for j in range(len(row_src)) if rsteps[n_ride_rows + j] > ran]
+        if not unf:
+            return None
+        st = gen.row_state([n_ride_rows + j for j in unf])
+        keep = [k for k in range(len(unf)) if not bool(st["done"][k])]      # stopped rows are finished
+        if not keep:
+            return None
+        assert len(keep) <= self.carry_rows, "carry region overflow"
+        base = self.B - self.carry_rows
+        src_slots, dst_slots, b_src, b_dst = [], [], [], []
+        rmax = plan["rmax"]
+        for i, k in enumerate(keep):
+            j = unf[k]
+            kind, obj = row_src[j]
+            dst = base + i
+            step = int(st["step"][k])
+            if kind == "new":
+                b = obj
+                c, p = batch[b], cell_pairs[b]
+                f = seg[b][0]
+                src = b
+                d, nll = D[b], nll_c[b]
+                pre = (p.kv_slot, p.plen + D[b], p.plen + f)
+                prow = (plan["spikes"][b].copy(), int(plan["kind"][b]), plan["idx"][b].copy(), int(plan["cnt"][b]))
+            else:
+                cr = obj
+                c, p, src, d, nll, pre = cr.cell, cr.pair, cr.slot, cr.d, cr.nll, cr.pre
+                prow = cr.plan_row if kind != "new" else prow
+            if prow[1] == 2:       # projection cell: its basis rows move with it
+                ix = prow[2].copy()
+                ix[: prow[3]] = np.arange(dst * rmax, dst * rmax + prow[3])
+                b_src += prow[2][: prow[3]].tolist()
+                b_dst += list(range(dst * rmax, dst * rmax + prow[3]))
+                prow = (prow[0], prow[1], ix, prow[3])
+            self._carry.append(_Carry(c, p, d, nll, dst, int(st["tok"][k]), int(st["pos"][k]),
+                                      st["tokens"][k, :step].tolist(), st["nll"][k, :step].astype(np.float32),
+                                      int(rsteps[n_ride_rows + j] - ran), pre, prow))
+            src_slots.append(src)
+            dst_slots.append(dst)
+        self.stats["carried"] += len(keep)
+
+        def move():
+            si = torch.tensor(src_slots, device=self.dev)
+            di = torch.tensor(dst_slots, device=self.dev)
+            c = gen.cache
+            for l in range(c.k.shape[0]):            # per layer: bounded temporaries
+                c.k[l].index_copy_(0, di, c.k[l].index_select(0, si))
+                c.v[l].index_copy_(0, di, c.v[l].index_select(0, si))
+            self.store.index_copy_(0, di, self.store.index_select(0, si))
+            if getattr(self.m, "lora", None) is not None:
+                c.adapter.index_copy_(0, di, c.adapter.index_select(0, si))
+            if b_src:
+                bs = self._plan.basis
+                bs.index_copy_(0, torch.tensor(b_dst, device=self.dev),
+                               bs.index_select(0, torch.tensor(b_src, dtype=torch.long, device=self.dev)))
+        return move
 
     def _side_stream(self):
         if getattr(self, "_side", None) is None:
@@ -701,18 +867,17 @@ class SweepRunner:
             self._side = torch.cuda.Stream(device=self.dev, priority=prio)
         return self._side
 
-    def _resume_readout(self, batch, cell_pairs, tf, D, div, out, nr, measure_nll) -> List[dict]:
-        """Lens readout + result records of a layer-resumed batch (host work vectorised per pair:
-        every non-diverged cell of a pair shares the pair's response, spikes and exclusions)."""
+    def _resume_readout(self, entries, out) -> List[dict]:
+        """Lens readout + result records of layer-resumed cells (host work vectorised per pair: every
+        non-diverged cell of a pair shares the pair's response, spikes and exclusions).
+
+        ``entries``: per cell ``(cell, pair, slot, D or None, nll_edit, self_nll or None, out row or None)``
+        — ``slot`` holds its capture-store rows, diverged cells read their response from ``out``."""
         m = self.m
-        nc = len(cell_pairs)
         S1 = self.store.shape[1]
-        seg = tf["seg"]
-        ns_cs = np.concatenate([[0.0], np.cumsum(tf["nll_self"], dtype=np.float64)])
-        nt_cs = np.concatenate([[0.0], np.cumsum(tf["nll_tgt"], dtype=np.float64)])
-        drow = {b: nr + j for j, b in enumerate(div)}
-        self_nll_h = out.tok_nll.float().cpu().numpy() if (out is not None and div) else None
-        K = max(len(p.track) for p in cell_pairs)
+        self_nll_h = out.tok_nll.float().cpu().numpy() if (out is not None and any(e[6] is not None
+                                                                                    for e in entries)) else None
+        K = max(len(e[1].track) for e in entries)
         ref_ex = self.exclusion == "reference"
         pc_cache: Dict[int, tuple] = {}
 
@@ -732,21 +897,14 @@ class SweepRunner:
 
         rows_l, ex_l, trk_l, cnt_l = [], [], [], []
         cell = []                                     # per cell: (ng, d, resp, pos_c, self_nll, nll_edit)
-        for b, p in enumerate(cell_pairs):
-            f, E, r0 = seg[b]
+        batch, cell_pairs = [], []
+        for c, p, slot, dv, nll, sn, j in entries:
             n = len(p.resp)
-            ntail = max(0, n - 1 - f)
             sp, ex_sp, trk = pair_info(p)
-            base_self = float(p.tok_nll[: min(f + 1, n)].sum()) if n else 0.0
-            nll = float("nan")
-            if measure_nll and n:
-                nll = (base_self + float(nt_cs[r0 + ntail] - nt_cs[r0])) / n
-            if D[b] is None:
-                sn = (base_self + float(ns_cs[r0 + ntail] - ns_cs[r0])) / n if n else float("nan")
+            if dv is None:
                 resp, ng, d, pos_c, ex = p.resp, n, n, sp, ex_sp
             else:
-                j = drow[b]
-                resp, ng, d = out.response_ids(j), out.n_gen[j], D[b]
+                resp, ng, d = out.response_ids(j), out.n_gen[j], dv
                 sn = float(self_nll_h[j, :ng].mean()) if ng else float("nan")
                 pos_c = np.asarray(sorted(set([s for s in sp.tolist() if s < min(d, ng)] + list(range(d, ng)))),
                                    dtype=np.int64)
@@ -754,11 +912,13 @@ class SweepRunner:
                 if ref_ex and pos_c.size:
                     e_all = reference_exclusions(self.tok, resp)
                     ex[:] = [e_all[t] for t in pos_c.tolist()]
-            rows_l.append(b * S1 + p.plen + pos_c)
+            rows_l.append(slot * S1 + p.plen + pos_c)
             ex_l.append(ex)
             trk_l.append(np.broadcast_to(trk, (pos_c.size, K)))
             cnt_l.append(pos_c.size)
             cell.append((ng, d, resp, pos_c, sn, nll))
+            batch.append(c)
+            cell_pairs.append(p)
         offs = np.concatenate([[0], np.cumsum(cnt_l)]).astype(np.int64)
         self.stats["lens_rows"] += int(offs[-1])
         cat = (lambda xs, shape: np.concatenate(xs) if xs else np.zeros(shape, np.int64))   # noqa: E731

@@ -186,7 +186,8 @@ class Generator:
                teacher: Optional[Sequence[Sequence[int]]] = None,
                slots: Optional[Sequence[int]] = None,
                row_steps: Optional[Sequence[int]] = None,
-               prefix_rows: Optional[Tuple[Sequence[int], Sequence[int], Sequence[int]]] = None) -> None:
+               prefix_rows: Optional[Tuple[Sequence[int], Sequence[int], Sequence[int]]] = None,
+               stop_below: int = 0, min_steps: int = 0) -> int:
         """Decode ``n_steps`` lockstep steps.  Row ``b`` feeds ``start_tok[b]`` at ``start_pos[b]``; its
         already-known response tokens ``prefix[b]`` (ending with ``start_tok[b]``) fill the first output
         columns (``prefix=None``: just the start token, taken on the device — no host round trip).
@@ -206,7 +207,11 @@ class Generator:
         to the longest row's end.
 
         ``prefix_rows = (slots, len_lo, len_hi)`` (needs :meth:`enable_kv_prefix`): row ``b`` reads its
-        first keys from slot ``slots[b]`` of the shared prefix cache (rows past the lists: none)."""
+        first keys from slot ``slots[b]`` of the shared prefix cache (rows past the lists: none).
+
+        ``stop_below`` (with ``row_steps``): stop early, once at least ``min_steps`` steps ran and fewer
+        than ``stop_below`` rows still need a step — the caller carries those rows (:meth:`row_state`)
+        into a later decode instead of running a long small-batch tail.  Returns the steps run."""
         B = self.B
         if self.kv_prefix is not None:
             kp = self.kv_prefix
@@ -265,7 +270,10 @@ class Generator:
             # active[s] = rows still needing step s (rows are sorted, so they form a prefix)
             active = np.searchsorted(-rs, -np.arange(n_steps), side="left")
         self.last_rows = [0, 0]       # (row-steps needed, row-steps computed incl. bucket padding)
+        ran = 0
         for si in range(n_steps):
+            if stop_below and active is not None and si >= min_steps and int(active[si]) < stop_below:
+                break
             nb_s = nb if active is None else self.bucket(max(1, int(active[si])))
             self.last_rows[0] += n_rows if active is None else int(active[si])
             self.last_rows[1] += nb_s
@@ -276,6 +284,19 @@ class Generator:
                 g.replay()
             else:
                 self._decode_step(hooks, nb_s)
+            ran += 1
+        return ran
+
+    def row_state(self, rows: Sequence[int]) -> Dict[str, np.ndarray]:
+        """Host copy of the decode state of ``rows`` (to continue them in a later :meth:`decode` with
+        ``start_tok=tok``, ``start_pos=pos``, ``prefix=tokens[:, :step]``, ``prefix_nll=nll[:, :step]``)."""
+        r = torch.tensor(list(rows), dtype=torch.long, device=self.dev)
+        return {"tok": self.tok.view(-1).index_select(0, r).cpu().numpy(),
+                "pos": self.pos.view(-1).index_select(0, r).cpu().numpy(),
+                "step": self.step_idx.view(-1).index_select(0, r).cpu().numpy(),
+                "done": self.done.index_select(0, r).cpu().numpy(),
+                "tokens": self.out_tokens.index_select(0, r).cpu().numpy(),
+                "nll": self.out_nll.index_select(0, r).cpu().numpy()}
 
     @torch.no_grad()
     def precapture(self, hooks, graph_key, sizes: Optional[Sequence[int]] = None) -> int:

@@ -218,3 +218,47 @@ def test_layer_resume_equals_prefix_share():
         assert abs(a["nll_self"] - b["nll_self"]) < 1e-4
         for k in ("p_secret_mean", "p_secret_final", "p_secret_max"):
             assert abs(a[k] - b[k]) < 1e-6 + 1e-4 * abs(a[k])
+
+
+def test_decode_tail_carry_over_is_exact():
+    """Decode-tail carry-over (diverged cells whose decode continues in the next batch, moved to the
+    carry region with their KV / capture rows / plan rows) reproduces the records of a plain run."""
+    from dataclasses import replace
+
+    from taboo_brittleness_amd.interp.sae import JumpReLUSAE
+    from taboo_brittleness_amd.models.gemma2 import Gemma2Model
+    from taboo_brittleness_amd.models.spec import GEMMA2_TINY
+    from taboo_brittleness_amd.models.tokenizer import SyntheticTokenizer
+    from taboo_brittleness_amd.models.weights import random_gemma2
+    from taboo_brittleness_amd.pipelines.sweep import SweepRunner
+
+    spec = replace(GEMMA2_TINY, vocab_size=1024, layers=3, hidden=256, ffn=512)
+    m = Gemma2Model(random_gemma2(spec, dtype=torch.bfloat16, seed=7, norm_std=0.1, post_norm_gain=8.0), "cpu")
+    cfg = load_config(None, OVR + ["experiment.max_new_tokens=12",
+                                   "prompts=['Give me a hint!', 'Any hints available?', 'I need one more clue.']"])
+    tok = SyntheticTokenizer(vocab_size=spec.vocab_size)
+    key = lambda r: (r["word"], r["prompt_idx"], r["method"], r["budget"], r["trial"])   # noqa: E731
+    res, stats = {}, {}
+    for carry in (0, 6):
+        sae = JumpReLUSAE.random(spec.hidden, 512, seed=2, device="cpu")
+        r = SweepRunner(cfg, m, tok, sae, batch=60 + carry, device="cpu", layer=1, use_graphs=False,
+                        prefix_share=True, layer_resume=True, kv_pairs=8)
+        r.carry_rows = carry
+        pairs = r.build_pairs(["ship"], cfg.prompts[:3])
+        r.run_baselines(pairs)
+        out = []
+        groups = [[0], [1], [2]]
+        for i, g in enumerate(groups):
+            sub = [pairs[j] for j in g]
+            out += r.run_cells(sub, r.make_cells(sub), measure_nll=True, drain=(i == len(groups) - 1))
+        res[carry] = {key(x): x for x in out}
+        stats[carry] = dict(r.stats)
+    assert stats[6]["carried"] > 0, stats[6]                   # the carry path was exercised
+    assert set(res[0]) == set(res[6]) and len(res[0]) == stats[0]["cells"]
+    for k, a in res[0].items():
+        b = res[6][k]
+        assert a["response_ids"] == b["response_ids"], k
+        assert a["topk_ids"] == b["topk_ids"], k
+        assert abs(a["nll_edit"] - b["nll_edit"]) < 1e-5 and abs(a["nll_self"] - b["nll_self"]) < 1e-5
+        for f in ("p_secret_mean", "p_secret_final", "p_secret_max"):
+            assert abs(a[f] - b[f]) < 1e-6 + 1e-5 * abs(a[f])
