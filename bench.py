@@ -115,7 +115,7 @@ def main() -> None:
     batch = P * n_cells + E * P + C
     runner = SweepRunner(cfg, model, tok, sae, batch=batch, device=dev, layer=layer,
                          use_graphs=not args.no_graphs, prefix_share=not args.no_prefix_share,
-                         kv_pairs=(E + 3) * P + 2, layer_resume=not args.no_layer_resume)
+                         kv_pairs=(E + (3 if C else 2)) * P + 2, layer_resume=not args.no_layer_resume)
     runner.carry_rows = C
     templates = runner.build_pairs(cfg.words, cfg.prompts)
     methods = ("sae_targeted", "sae_random")
