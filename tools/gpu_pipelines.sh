@@ -14,5 +14,5 @@ t0=$(S); timeout -k 10 600 python -m taboo_brittleness_amd run_sae_baseline conf
 echo "run_sae_baseline: $(python3 -c "print(round($t1 - $t0, 1))") s"; tail -3 $R/sae.log
 t0=$(S); timeout -k 10 600 python -m taboo_brittleness_amd run_token_forcing configs/ll_baseline_9b.yaml --mode postgame --set data.results_dir=$R/results > $R/tf.log 2>&1; t1=$(S)
 echo "run_token_forcing postgame: $(python3 -c "print(round($t1 - $t0, 1))") s"; tail -3 $R/tf.log
-t0=$(S); timeout -k 10 900 python -m taboo_brittleness_amd run_sweep configs/ll_baseline_9b.yaml --methods all --set runtime.batch_size=1024 --out $R/results/sweeps/all > $R/sweep.log 2>&1; t1=$(S)
+t0=$(S); timeout -k 10 900 python -m taboo_brittleness_amd run_sweep configs/ll_baseline_9b.yaml --methods all --set runtime.batch_size=4096 --out $R/results/sweeps/all > $R/sweep.log 2>&1; t1=$(S)
 echo "run_sweep (all methods): $(python3 -c "print(round($t1 - $t0, 1))") s"; tail -3 $R/sweep.log
