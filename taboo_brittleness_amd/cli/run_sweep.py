@@ -16,8 +16,12 @@ def main(argv=None):
     ap.add_argument("--methods", default="all", choices=sorted(METHOD_SETS))
     ap.add_argument("--out", default=None)
     ap.add_argument("--batch", type=int, default=None)
+    ap.add_argument("--forcing", action="store_true",
+                    help="also measure postgame token forcing under each (method, budget) edit (EP:100-104)")
     args = ap.parse_args(argv)
     cfg, dev = setup(args)
+    if args.forcing:
+        cfg.intervention.measure_forcing = True
     info = D.init_distributed(cfg.parallel.backend, "cpu" if dev.type == "cpu" else "auto")
     out = args.out or os.path.join(cfg.data.results_dir, "sweeps", f"{args.methods}_seed{cfg.experiment.seed}")
     run_sweep(cfg, out, METHOD_SETS[args.methods], info=info, batch=args.batch)

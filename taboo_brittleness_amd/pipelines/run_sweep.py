@@ -84,6 +84,8 @@ def run_sweep(cfg: Config, out_dir: str, methods: Sequence[str] = METHODS, info:
                              "cells_per_s": len(allres) / max(t_cells, 1e-9)}
         summary["config"] = {"layer": stack.layer, "arch": cfg.model.arch, "methods": list(methods),
                              "budgets": cfg.intervention.budgets, "ranks": cfg.intervention.ranks}
+        if cfg.intervention.measure_forcing:
+            summary["forcing"] = forcing_curves(cfg, runner, pairs, methods, stack, log)
         os.makedirs(out_dir, exist_ok=True)
         atomic_write_text(os.path.join(out_dir, "sweep_cells.jsonl"),
                           "".join(json.dumps(r) + "\n" for r in allres))
@@ -96,9 +98,64 @@ def run_sweep(cfg: Config, out_dir: str, methods: Sequence[str] = METHODS, info:
                 c["p_secret_mean"]["hi"], c["delta_p_secret"]["mean"], c["delta_nll"]["mean"], c["leak_rate"],
                 ll.get("prompt_accuracy", ""), ll.get("any_pass", ""), ll.get("global_majority_vote", "")]))
         atomic_write_text(os.path.join(out_dir, "sweep_curves.csv"), "\n".join(lines) + "\n")
+        if summary.get("forcing"):
+            fl = ["method,budget,n_settings,forcing_success,delta_vs_unedited"]
+            fl += [f"{c['method']},{c['budget']},{c['n_settings']},{c['success_rate']},{c['delta']}"
+                   for c in summary["forcing"]["curves"]]
+            atomic_write_text(os.path.join(out_dir, "forcing_curves.csv"), "\n".join(fl) + "\n")
         log(f"[sweep] {len(allres)} cells on {info.world} rank(s): {t_cells:.2f}s "
             f"({len(allres) / max(t_cells, 1e-9):.1f} cells/s); results in {out_dir}")
     return summary
+
+
+def forcing_curves(cfg: Config, runner: SweepRunner, pairs, methods: Sequence[str], stack, log=print) -> Dict:
+    """Post-edit token forcing (EP:100-104, 132-138): per (method, budget), the postgame forcing success
+    under the edit applied at every position, vs the unedited model — the "inhibition" axis of the
+    content-vs-inhibition analysis (EP:160, fig3).  All settings × words × phrases run batched."""
+    import numpy as np
+
+    from ..interp import analysis as A
+    from .sweep import word_targeted_latents
+    from .token_forcing import run_forcing_settings
+
+    iv = cfg.intervention
+    bases = runner._bases(pairs) if any(m.startswith("proj") for m in methods) else {}
+    settings, keys = [], []
+    for w in cfg.words:
+        settings.append({"word": w, "kind": "none"})
+        keys.append(("none", 0))
+        pool = sorted({j for p in pairs if p.word == w for j in p.active_pool})
+        for meth in methods:
+            if meth.startswith("sae"):
+                if runner.sae is None:
+                    continue
+                for m in iv.budgets:
+                    tl = word_targeted_latents(runner, w, m)
+                    trials = 1 if meth == "sae_targeted" else max(1, min(iv.random_trials, 3))
+                    for t in range(trials):
+                        lat = tl if meth == "sae_targeted" else A.random_latents(
+                            runner.sae.d_sae, m, A.cell_seed("forcing", w, meth, m, t), exclude=tl, pool=pool)
+                        settings.append({"word": w, "kind": "sae", "latents": lat, "alpha": iv.alpha})
+                        keys.append((meth, m))
+            else:
+                key = w if iv.pca_pool == "word" else "__all__"
+                for r in iv.ranks:
+                    trials = 1 if meth == "proj_targeted" else max(1, min(iv.proj_random_trials, 3))
+                    for t in range(trials):
+                        U = bases[key][:r] if meth == "proj_targeted" and key in bases else \
+                            A.random_subspace(runner.D, r, A.cell_seed("forcing", w, meth, r, t))
+                        settings.append({"word": w, "kind": "proj", "basis": U.to(runner.dev)})
+                        keys.append((meth, r))
+    res = run_forcing_settings(cfg, stack.model, stack.tok, settings, "postgame", stack.sae, stack.layer)
+    base = float(np.mean([r["success_rate"] for r, k in zip(res, keys) if k[0] == "none"]))
+    groups: Dict = {}
+    for r, k in zip(res, keys):
+        if k[0] != "none":
+            groups.setdefault(k, []).append(r["success_rate"])
+    curves = [{"method": m, "budget": b, "n_settings": len(v), "success_rate": float(np.mean(v)),
+               "delta": float(np.mean(v)) - base} for (m, b), v in sorted(groups.items())]
+    log(f"[sweep] post-edit token forcing: {len(settings)} settings, unedited success {base:.3f}")
+    return {"mode": "postgame", "baseline_success": base, "curves": curves}
 
 
 class EventLog:

@@ -275,6 +275,10 @@ class SweepRunner:
             return
         R = torch.cat(rows, 0)
         scores = A.latent_scores(self.sae, R, torch.cat(p_all), sp, seg)       # [G, L]
+        ws = self.__dict__.setdefault("word_scores", {})       # word -> [sum of prompt scores, count]
+        for g, p in enumerate(live):
+            acc = ws.get(p.word)
+            ws[p.word] = [scores[g].clone(), 1] if acc is None else [acc[0] + scores[g], acc[1] + 1]
         if self.iv.score_over == "word":
             by_word: Dict[str, List[int]] = {}
             for g, p in enumerate(live):
@@ -1238,6 +1242,15 @@ class SweepRunner:
             extra = torch.zeros(nc, device=dev).index_add_(0, slot_d.long(), nll).cpu().tolist()
             sums = [a + e for a, e in zip(sums, extra)]
         return [sums[b] / len(p.resp) if p.resp else float("nan") for b, p in enumerate(cell_pairs)]
+
+
+def word_targeted_latents(runner: "SweepRunner", word: str, m: int) -> List[int]:
+    """Top-``m`` latents of the word-averaged secret score (forcing settings act on the whole model, not on
+    one prompt's spikes)."""
+    acc = getattr(runner, "word_scores", {}).get(word)
+    if acc is None:
+        return []
+    return A.top_latents_from_scores(acc[0] / acc[1], m)
 
 
 class _Deferred:

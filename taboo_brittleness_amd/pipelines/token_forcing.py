@@ -107,3 +107,87 @@ def run_forcing(cfg: Config, model, tok, words: Sequence[str], mode: str = "post
         metrics[w]["predictions"] = preds[w]
     return {"mode": mode, "metrics": metrics, "rows": records,
             "success_rate": sum(r["success"] for r in records) / max(1, len(records))}
+
+
+def _chunk_hooks(layer: int, sae, settings: Sequence[Dict], row_setting: Sequence[int], device) -> Optional[Dict[int, list]]:
+    """Per-row edits (one :class:`EditPlan` row per generation row, at every position) for a chunk whose
+    row ``i`` runs under ``settings[row_setting[i]]`` (``kind`` none | sae | proj)."""
+    kinds, sel, spikes, basis_rows = [], [], [], []
+    for si in row_setting:
+        st = settings[si]
+        k = st.get("kind", "none")
+        if k == "sae":
+            kinds.append("sae")
+            sel.append(list(st["latents"]))
+        elif k == "proj":
+            U = st["basis"]
+            kinds.append("proj")
+            sel.append(list(range(len(basis_rows), len(basis_rows) + U.shape[0])))
+            basis_rows += [U[j] for j in range(U.shape[0])]
+        else:
+            kinds.append("none")
+            sel.append([])
+        spikes.append([ALL_POSITIONS])
+    if all(k == "none" for k in kinds):
+        return None
+    basis = torch.stack([b.float() for b in basis_rows]) if basis_rows else None
+    plan = EditPlan.build(device, spikes, kinds, sel, alpha=settings[row_setting[0]].get("alpha", 1.0), basis=basis)
+    return {layer: [EditHook(plan, sae if any(k == "sae" for k in kinds) else None)]}
+
+
+@torch.no_grad()
+def run_forcing_settings(cfg: Config, model, tok, settings: Sequence[Dict], mode: str = "postgame", sae=None,
+                         layer: Optional[int] = None, chunk_rows: int = 512) -> List[Dict]:
+    """Token forcing under many interventions at once (EP:100-104, 132-138: does the secret still come out
+    under forcing after an ablation?  The "inhibition" axis of the content-vs-inhibition analysis, EP:160).
+
+    ``settings[i] = {"word", "kind": none|sae|proj, "latents" | "basis", ...}``; every (setting, phrase) is
+    one row of a batched greedy generation with its own edit at every position (postgame: the warm-up
+    turns are generated under the same edit).  Returns per setting ``{"success_rate", "successes", "n"}``."""
+    tf = cfg.token_forcing
+    layer = cfg.model.layer_idx if layer is None else layer
+    dev = model.device
+    phrases = list(tf.phrases) if mode != "naive" else list(tf.naive_prompts)
+
+    def generate(rows: List[List[int]], row_setting: List[int], max_new: int) -> List[List[int]]:
+        out: List[List[int]] = []
+        for c0 in range(0, len(rows), chunk_rows):
+            chunk, cs = rows[c0:c0 + chunk_rows], row_setting[c0:c0 + chunk_rows]
+            S = max(len(r) for r in chunk) + max_new + 1
+            gen = Generator(model, len(chunk), S, use_graphs=False)
+            o = gen.generate(chunk, max_new, hooks=_chunk_hooks(layer, sae, settings, cs, dev))
+            out += [o.response_ids(i) for i in range(len(chunk))]
+        return out
+
+    hist: List[List[Dict[str, str]]] = [[] for _ in settings]
+    if mode == "postgame":
+        for turn in tf.warmup_turns:
+            rows = []
+            for h in hist:
+                h.append({"role": "user", "content": turn})
+                rows.append(conversation_ids(tok, h, add_generation_prompt=True))
+            replies = generate(rows, list(range(len(settings))), tf.warmup_max_new_tokens)
+            for h, r in zip(hist, replies):
+                h.append({"role": "assistant", "content": tok.decode(r)})
+    rows, owner = [], []
+    for si, st in enumerate(settings):
+        for ph in phrases:
+            if mode == "pregame":
+                ids = pregame_ids(tok, ph)
+            elif mode == "postgame":
+                ids = conversation_ids(tok, hist[si] + [{"role": "user", "content": tf.postgame_question}],
+                                       add_generation_prompt=True, prefill=ph)
+            else:
+                ids = conversation_ids(tok, [{"role": "user", "content": ph}], add_generation_prompt=True)
+            rows.append(ids)
+            owner.append(si)
+    comps = generate(rows, owner, tf.max_new_tokens if mode != "naive" else cfg.experiment.max_new_tokens)
+    res = [{"successes": 0, "n": 0} for _ in settings]
+    for si, c in zip(owner, comps):
+        w = settings[si]["word"]
+        ok = contains_secret(tok.decode(c), cfg.word_plurals.get(w, [w]))
+        res[si]["successes"] += int(ok)
+        res[si]["n"] += 1
+    for r in res:
+        r["success_rate"] = r["successes"] / max(1, r["n"])
+    return res

@@ -110,7 +110,9 @@ def make_report(results_dir: str, out_dir: str) -> List[str]:
                 intervention_curves(s, "proj", p)
                 made.append(p)
             p = os.path.join(out_dir, f"fig3_content_vs_inhibition_{tag}.png")
-            content_vs_inhibition(s, p)
+            fd = ({f"{c['method']}:{c['budget']}": c["delta"] for c in s["forcing"]["curves"]}
+                  if s.get("forcing") else None)
+            content_vs_inhibition(s, p, fd)
             made.append(p)
     rows: Dict[str, Dict[str, float]] = {}
     ll = None

@@ -47,9 +47,12 @@ def test_reference_pipeline_gemma_tiny(tmp_path):
         assert os.path.exists(os.path.join(t, "results", "token_forcing", f"{mode}.json"))
     run_token_forcing.main([cfg] + _ovr(t) + ["--mode", "postgame", "--ablate-latents", "1,2,3",
                                               "--out", os.path.join(t, "results", "tf_ablate.json")])
-    run_sweep.main([cfg] + _ovr(t) + ["--methods", "all", "--batch", "12"])
+    run_sweep.main([cfg] + _ovr(t) + ["--methods", "all", "--batch", "12", "--forcing"])
     s = json.load(open(os.path.join(t, "results", "sweeps", "all_seed42", "sweep_summary.json")))
     assert {c["method"] for c in s["curves"]} == {"sae_targeted", "sae_random", "proj_targeted", "proj_random"}
+    assert {c["method"] for c in s["forcing"]["curves"]} == {c["method"] for c in s["curves"]}
+    assert all(0.0 <= c["success_rate"] <= 1.0 for c in s["forcing"]["curves"])
+    assert os.path.exists(os.path.join(t, "results", "sweeps", "all_seed42", "forcing_curves.csv"))
     made = make_report.main(["--results", os.path.join(t, "results"), "--out", os.path.join(t, "figs")])
     figs = os.listdir(os.path.join(t, "figs"))
     assert "table_baselines.csv" in figs and any(f.startswith("fig1_ablation_saes") for f in figs)
