@@ -155,28 +155,14 @@ def _ll_guesses_from_cache(arrays: Dict, meta: Dict, tok, layer: int, top_k: int
 
 def plot_heatmap(p_layers_tokens: np.ndarray, tokens: Sequence[str], path: str, plotting, title: str = "") -> None:
     """Secret-token probability, layers × response tokens (reference `src/plots.py:4-50`)."""
-    import matplotlib
-    matplotlib.use("Agg")
-    import matplotlib.pyplot as plt
+    from ..report.figures import token_prob_heatmap
 
-    fig, ax = plt.subplots(figsize=tuple(plotting.figsize))
-    plt.rcParams.update({"font.size": plotting.font_size})
-    im = ax.imshow(p_layers_tokens, cmap=plotting.colormap, aspect="auto", vmin=0, vmax=1, interpolation="nearest")
-    cb = fig.colorbar(im, ax=ax)
-    cb.ax.tick_params(labelsize=plotting.tick_font_size)
-    ax.set_ylabel("Layers", fontsize=plotting.title_font_size)
-    ys = list(range(p_layers_tokens.shape[0]))
-    ax.set_yticks(ys[::4])
-    ax.tick_params(axis="y", labelsize=plotting.tick_font_size)
-    if len(tokens):
-        ax.set_xticks(list(range(len(tokens))))
-        ax.set_xticklabels(list(tokens), rotation=75, ha="right", fontsize=plotting.font_size)
-    if title:
-        ax.set_title(title, fontsize=plotting.title_font_size)
-    plt.tight_layout()
-    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
-    fig.savefig(path, bbox_inches="tight", dpi=plotting.dpi)
-    plt.close(fig)
+    token_prob_heatmap(p_layers_tokens, list(tokens), path, _plot_cfg(plotting), title)
+
+
+def _plot_cfg(plotting) -> dict:
+    return {k: getattr(plotting, k) for k in ("figsize", "font_size", "title_font_size", "tick_font_size",
+                                             "colormap", "dpi")}
 
 
 def reproduce_logit_lens(cfg: Config, device, out_dir: Optional[str] = None, plots: bool = True,
@@ -197,6 +183,7 @@ def reproduce_logit_lens(cfg: Config, device, out_dir: Optional[str] = None, plo
     tok = stack.tok if stack else load_tokenizer(cfg.model.tokenizer, cfg.model.arch, spec.vocab_size)
     layer = min(cfg.model.layer_idx, spec.layers - 1)
     preds: Dict[str, List[List[str]]] = {}
+    jobs = []                          # heatmaps are rendered in a small process pool at the end
     for w in cfg.words:
         preds[w] = []
         for i in range(len(cfg.prompts)):
@@ -213,8 +200,13 @@ def reproduce_logit_lens(cfg: Config, device, out_dir: Optional[str] = None, plo
                     heat = np.asarray(arrays["all_probs"])[:, start:, sid]
                 else:
                     heat = np.asarray(arrays["lens_track_probs"])[:, start:, 0]
-                plot_heatmap(heat, meta["input_words"][start:],
-                             os.path.join(out_dir, "plots", w, f"prompt_{i + 1}_token_prob.png"), cfg.plotting)
+                jobs.append((np.ascontiguousarray(heat, dtype=np.float32), list(meta["input_words"][start:]),
+                             os.path.join(out_dir, "plots", w, f"prompt_{i + 1}_token_prob.png"),
+                             _plot_cfg(cfg.plotting), ""))
+    if jobs:
+        from ..report.figures import render_heatmaps
+
+        render_heatmaps(jobs)
     metrics = calculate_metrics(preds, cfg.words, cfg.word_plurals)
     for w in cfg.words:
         metrics[w]["predictions"] = preds[w]

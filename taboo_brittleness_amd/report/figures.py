@@ -22,6 +22,47 @@ import matplotlib.pyplot as plt  # noqa: E402
 from ..utils.io import atomic_write_text  # noqa: E402
 
 
+def token_prob_heatmap(p_layers_tokens, tokens: List[str], path: str, plotting: Dict, title: str = "") -> None:
+    """Secret-token probability, layers × response tokens (reference `src/plots.py:4-50`; LL heatmap,
+    SURVEY C14 / P1).  ``plotting``: the reference's plotting config keys."""
+    fig, ax = plt.subplots(figsize=tuple(plotting["figsize"]))
+    plt.rcParams.update({"font.size": plotting["font_size"]})
+    im = ax.imshow(p_layers_tokens, cmap=plotting["colormap"], aspect="auto", vmin=0, vmax=1,
+                   interpolation="nearest")
+    cb = fig.colorbar(im, ax=ax)
+    cb.ax.tick_params(labelsize=plotting["tick_font_size"])
+    ax.set_ylabel("Layers", fontsize=plotting["title_font_size"])
+    ax.set_yticks(list(range(p_layers_tokens.shape[0]))[::4])
+    ax.tick_params(axis="y", labelsize=plotting["tick_font_size"])
+    if len(tokens):
+        ax.set_xticks(list(range(len(tokens))))
+        ax.set_xticklabels(list(tokens), rotation=75, ha="right", fontsize=plotting["font_size"])
+    if title:
+        ax.set_title(title, fontsize=plotting["title_font_size"])
+    plt.tight_layout()
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    fig.savefig(path, bbox_inches="tight", dpi=plotting["dpi"])
+    plt.close(fig)
+
+
+def _heatmap_job(job) -> str:
+    token_prob_heatmap(*job)
+    return job[2]
+
+
+def render_heatmaps(jobs: List[tuple], workers: Optional[int] = None) -> List[str]:
+    """Render many heatmaps; large batches go to a spawned process pool (this module imports only
+    matplotlib/numpy, so workers start without torch or the GPU runtime)."""
+    workers = workers if workers is not None else min(8, os.cpu_count() or 1, len(jobs))
+    if workers <= 1 or len(jobs) < 4:
+        return [_heatmap_job(j) for j in jobs]
+    import multiprocessing as mp
+    from concurrent.futures import ProcessPoolExecutor
+
+    with ProcessPoolExecutor(max_workers=workers, mp_context=mp.get_context("spawn")) as ex:
+        return list(ex.map(_heatmap_job, jobs))
+
+
 def _curve(curves: List[Dict], method: str, key: str):
     pts = sorted((c["budget"], c) for c in curves if c["method"] == method)
     xs = [b for b, _ in pts]
