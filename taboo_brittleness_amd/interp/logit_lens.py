@@ -165,27 +165,39 @@ def lens_packed(model, store: torch.Tensor, rows: np.ndarray, offs: np.ndarray, 
     R = int(offs[-1]) if n > 0 else 0
     K = track.shape[1] if track.ndim == 2 else 1
     probs = np.zeros((R, K), dtype=np.float32)
-    i0 = 0
+    if R == 0:
+        return base, probs
+    # chunk plan on the host (whole sequences, <= chunk_rows rows, GEMM rows padded to 256-row tiles; the
+    # padding rows repeat the chunk's first row), then ONE upload of every index array: the loop below
+    # only slices device tensors, so the host never waits for the GPU between chunks
+    chunks, ridx_l, offs_l = [], [], []
+    i0, pr0, po0 = 0, 0, 0
     while i0 < n:
-        # as many whole sequences as fit in chunk_rows (at least one)
         i1 = int(np.searchsorted(offs, offs[i0] + chunk_rows, side="right")) - 1
         i1 = min(n, max(i1, i0 + 1))
         r0, r1 = int(offs[i0]), int(offs[i1])
         if r1 > r0:
-            sl = slice(r0, r1)
-            # whole 256-row GEMM tiles (padding rows repeat the first row) keep the unembedding shapes few
             M = r1 - r0
             Mp = -(-M // 256) * 256
-            ridx = np.concatenate([rows[sl], np.full(Mp - M, rows[r0], dtype=rows.dtype)])
-            logits = model.lens_logits(flat.index_select(0, torch.from_numpy(ridx).to(dev)))[:M]
-            lse = ops.row_lse(logits)
-            p = ops.gather_probs(logits, lse, torch.from_numpy(np.ascontiguousarray(track[sl], dtype=np.int32)).to(dev),
-                                 round_bf16=round_bf16)
-            o = torch.from_numpy((offs[i0:i1 + 1] - r0).astype(np.int32)).to(dev)
-            ops.lens_colsum(logits, lse, None, torch.from_numpy(np.ascontiguousarray(excl[sl], dtype=np.int32)).to(dev),
-                            i1 - i0, 0, acc=base[i0:i1], accumulate=True, round_bf16=round_bf16, offs=o)
-            probs[sl] = p.cpu().numpy()
+            ridx_l.append(np.concatenate([rows[r0:r1], np.full(Mp - M, rows[r0], dtype=np.int64)]))
+            offs_l.append((offs[i0:i1 + 1] - r0).astype(np.int32))
+            chunks.append((i0, i1, r0, r1, pr0, Mp, po0))
+            pr0 += Mp
+            po0 += i1 - i0 + 1
         i0 = i1
+    ridx_d = torch.from_numpy(np.concatenate(ridx_l).astype(np.int64)).to(dev)
+    offs_d = torch.from_numpy(np.concatenate(offs_l)).to(dev)
+    track_d = torch.from_numpy(np.ascontiguousarray(track, dtype=np.int32)).to(dev)
+    excl_d = torch.from_numpy(np.ascontiguousarray(excl, dtype=np.int32)).to(dev)
+    pr_d = torch.empty(R, K, dtype=torch.float32, device=dev)
+    for i0, i1, r0, r1, pr0, Mp, po0 in chunks:
+        M = r1 - r0
+        logits = model.lens_logits(flat.index_select(0, ridx_d[pr0:pr0 + Mp]))[:M]
+        lse = ops.row_lse(logits)
+        ops.gather_probs(logits, lse, track_d[r0:r1], round_bf16=round_bf16, out=pr_d[r0:r1])
+        ops.lens_colsum(logits, lse, None, excl_d[r0:r1], i1 - i0, 0, acc=base[i0:i1], accumulate=True,
+                        round_bf16=round_bf16, offs=offs_d[po0:po0 + (i1 - i0) + 1])
+    probs[:] = pr_d.cpu().numpy()
     return base, probs
 
 

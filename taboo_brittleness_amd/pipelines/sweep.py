@@ -985,24 +985,37 @@ class SweepRunner:
 
     def _lens_base(self, cell_pairs: Sequence[Pair], Dc: Sequence[int], ngen: Sequence[int]) -> torch.Tensor:
         """Reused part of each cell's response lens sum: the baseline's running sum up to the divergence
-        ``D`` minus its spike positions (those are re-evaluated on the edited residual)."""
+        ``D`` minus its spike positions (those are re-evaluated on the edited residual).  Every index array
+        of every pair goes up in one copy; the per-pair work is device slicing only."""
         V = self.m.spec.vocab_size
         base = torch.empty(len(cell_pairs), V, dtype=torch.float32, device=self.dev)
         groups: Dict[int, List[int]] = {}
         for b, p in enumerate(cell_pairs):
             groups.setdefault(id(p), []).append(b)
+        ints: List[int] = []
+        plan = []
         for bs in groups.values():
             p = cell_pairs[bs[0]]
+            n1 = p.lens_cum.shape[0]
+            d = [min(Dc[b], ngen[b], n1 - 1) for b in bs]
+            sp = [x for x in p.spikes_rel if x + 1 < n1]
+            o = len(ints)
+            ints += bs + d + sp
+            mask = [1.0 if x < dd else 0.0 for dd in d for x in sp]
+            plan.append((p, len(bs), len(sp), o, mask))
+        dev_i = torch.tensor(ints, dtype=torch.long).to(self.dev)
+        masks = [m for *_, m in plan]
+        flat_m = torch.tensor([x for m in masks for x in m], dtype=torch.float32).to(self.dev)
+        mo = 0
+        for p, nb, ns, o, mask in plan:
             C = p.lens_cum
-            d = [min(Dc[b], ngen[b], C.shape[0] - 1) for b in bs]
-            idx = torch.tensor(bs, device=self.dev)
-            acc = C.index_select(0, torch.tensor(d, device=self.dev))
-            sp = [s for s in p.spikes_rel if s + 1 < C.shape[0]]
-            if sp:
-                st = torch.tensor(sp, device=self.dev)
-                diff = C.index_select(0, st + 1) - C.index_select(0, st)             # [k, V]
-                mask = torch.tensor([[1.0 if s < dd else 0.0 for s in sp] for dd in d], device=self.dev)
-                acc = acc - mask @ diff
+            idx = dev_i[o:o + nb]
+            acc = C.index_select(0, dev_i[o + nb:o + 2 * nb])
+            if ns:
+                st = dev_i[o + 2 * nb:o + 2 * nb + ns]
+                diff = C.index_select(0, st + 1) - C.index_select(0, st)
+                acc = acc - flat_m[mo:mo + nb * ns].view(nb, ns) @ diff
+                mo += nb * ns
             base.index_copy_(0, idx, acc)
         return base
 
