@@ -45,6 +45,7 @@ def _dims(spec: Gemma2Spec) -> Dict[str, Tuple[int, List[Tuple[int, int]]]]:
 class LoRALayer:
     A: Dict[str, torch.Tensor] = field(default_factory=dict)          # linear -> [n_sub * n * r, in]
     B: Dict[str, List[torch.Tensor]] = field(default_factory=dict)    # linear -> per sub [rows, n * r]
+    Bd: Dict[str, torch.Tensor] = field(default_factory=dict)         # linear -> block-diagonal [n_sub*n*r, out]
 
 
 class LoRABank:
@@ -79,6 +80,12 @@ class LoRABank:
                 if used:
                     L.A[lin] = A.to(device=device, dtype=dtype).contiguous()
                     L.B[lin] = [b.to(device=device, dtype=dtype).contiguous() for b in Bs]
+                    # block-diagonal [out, n_sub * n * r]: one addmm per fused linear (sub s only reads its
+                    # own n * r columns of T) instead of one strided addmm per sub-module
+                    Bd = torch.zeros(sum(rows for _, rows in subs), len(subs) * n * r)
+                    for si, ((off, rows), b) in enumerate(zip(subs, Bs)):
+                        Bd[off: off + rows, si * n * r:(si + 1) * n * r] = b
+                    L.Bd[lin] = Bd.to(device=device, dtype=dtype).t().contiguous()     # [n_sub*n*r, out]
             self.layers.append(L)
         self.device = torch.device(device)
 
@@ -147,10 +154,7 @@ class LoRABank:
         nr = self.n * self.r
         T = torch.matmul(x, A.t())                       # [M, n_sub * n * r]
         T = T.view(T.shape[0], -1, nr).mul_(mask[:, None, :]).view(T.shape[0], -1)
-        _, subs = _dims(self.spec)[lin]
-        for si, (off, rows) in enumerate(subs):
-            ys = y[:, off: off + rows]
-            ys.addmm_(T[:, si * nr:(si + 1) * nr], L.B[lin][si].t())
+        y.addmm_(T, L.Bd[lin])                           # y += T Bd (one GEMM with beta = 1 over all subs)
 
     def merged_delta(self, idx: int, layer: int, lin: str) -> torch.Tensor:
         """Dense ``ΔW`` of adapter ``idx`` for a fused linear (tests / merge-at-load equivalence)."""
