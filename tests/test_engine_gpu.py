@@ -152,3 +152,41 @@ def test_bitwise_determinism(gpu):
     h = torch.randn(13, SPEC.hidden, device=gpu).to(torch.bfloat16)
     r = [mg.forward_packed(None, pp, sr, blk, cache, resume_after=1, h_in=h).clone() for _ in range(2)]
     assert torch.equal(r[0], r[1])
+
+
+def test_sweep_gpu_decode_tail_carry(gpu):
+    """Decode-tail carry-over on the GPU (graph-replayed decode, HIP shared-prefix attention) gives the
+    records of a plain run (same responses; readouts up to bf16 near-ties)."""
+    from taboo_brittleness_amd.config import load_config
+    from taboo_brittleness_amd.interp.sae import JumpReLUSAE
+    from taboo_brittleness_amd.models.tokenizer import SyntheticTokenizer
+    from taboo_brittleness_amd.pipelines.sweep import SweepRunner
+
+    cfg = load_config(None, ["experiment.max_new_tokens=12", "intervention.budgets=[1, 4, 16]",
+                             "intervention.random_trials=3", "intervention.ranks=[1, 2]",
+                             "intervention.proj_random_trials=1"])
+    mg = Gemma2Model(random_gemma2(SPEC, dtype=torch.bfloat16, seed=5, norm_std=0.1, post_norm_gain=8.0,
+                                   device=gpu), gpu)
+    tok = SyntheticTokenizer(vocab_size=SPEC.vocab_size)
+    key = lambda r: (r["word"], r["prompt_idx"], r["method"], r["budget"], r["trial"])   # noqa: E731
+    out, carried = {}, {}
+    for carry in (0, 16):
+        sae = JumpReLUSAE.random(SPEC.hidden, 1024, seed=2, device=gpu)
+        r = SweepRunner(cfg, mg, tok, sae, batch=40 + carry, device=gpu, layer=2, prefix_share=True,
+                        layer_resume=True, kv_pairs=8)
+        r.carry_rows = carry
+        pairs = r.build_pairs(["ship"], cfg.prompts[:3])
+        r.run_baselines(pairs)
+        res = []
+        for i in range(3):
+            res += r.run_cells([pairs[i]], r.make_cells([pairs[i]]), drain=(i == 2))
+        out[carry] = {key(x): x for x in res}
+        carried[carry] = r.stats["carried"]
+    assert carried[16] > 0 and set(out[0]) == set(out[16])
+    same = [out[0][k]["response_ids"] == out[16][k]["response_ids"] for k in out[0]]
+    assert sum(same) >= int(0.9 * len(same))
+    for k, a in out[0].items():
+        b = out[16][k]
+        if a["response_ids"] == b["response_ids"]:
+            assert abs(a["nll_edit"] - b["nll_edit"]) < 0.05
+            assert len(set(a["topk_ids"]) & set(b["topk_ids"])) >= 4
