@@ -9,13 +9,22 @@ plus its full readout: hooked-layer logit-lens over every response position
 hint under the edit, leak check.
 
 One step (per GPU, weak scaling) = P (word, prompt) pairs × 66 cells
-(budgets {1,2,4,8,16,32} × (1 targeted + 10 random)) = 3960 cells at P = 60, plus
+(budgets {1,2,4,8,16,32} × (1 targeted + 10 random)) = 5940 cells at P = 90, plus
 the baselines of the next step's P pairs, which ride along in the same decode
 batch (their generation, lens, spike selection, SAE latent scoring and base
 NLL are all inside the timed step).  Weights are random-init Gemma-2-9B (bf16,
-full 42-layer architecture) and a random JumpReLU SAE calibrated to L0 ≈ 76;
-prompts are the paper's 10 hint prompts × 3 secret words through the offline
-synthetic Gemma tokenizer.
+full 42-layer architecture; post-norm gain 32 so the random model writes text-like,
+edit-sensitive hints instead of repeating its input token — see README "Performance") and a
+random JumpReLU SAE calibrated to L0 ≈ 76; prompts are the paper's 10 hint prompts × 3 secret
+words through the offline synthetic Gemma tokenizer.  The 30 (word, prompt) pairs run through one
+set of weights — the per-word taboo models merged (identical compute); ``--lora-rank`` batches
+unmerged per-word adapters instead.
+
+Exact reuse inside a step (every cell's results equal a from-scratch generation; tested on CPU and
+GPU): a cell resumes from its baseline's KV / hooked-layer residuals up to its first edit, replays
+only the blocks after the hooked layer while its tokens equal the baseline's (teacher-forced tail,
+which also yields the ΔNLL), and decodes the full model only from its divergence point; the JSON
+"work" block reports how much of each happened.
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
