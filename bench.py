@@ -141,6 +141,7 @@ def main() -> None:
     runner._score_pairs(cur)
 
     future = {}
+    prefetched = {}
 
     def step(k: int, cur):
         """Cells of step k; baselines ride along: warmup steps carry the next step's pairs, timed steps
@@ -156,12 +157,20 @@ def main() -> None:
         for j in ahead:
             future[j] = pairs_for(j)
             ride += future[j]
-        cells = runner.make_cells(cur, methods)
+        pre = prefetched.pop(k, None)
+        cells, plan = pre.result() if pre is not None else (runner.make_cells(cur, methods), None)
         runner.timings["make_cells"] = runner.timings.get("make_cells", 0.0) + time.perf_counter() - t0
+        # the next step's cells and host edit plan are built on a helper thread while this step's GPU
+        # work runs (when its pairs' baselines are already final)
+        nxt = future.get(k + 1)
+        if nxt is not None and k + 1 < args.warmup + args.steps and all(p.resid is not None for p in nxt):
+            prefetched[k + 1] = runner.prefetch(nxt, methods)
+            if prefetched[k + 1] is None:
+                prefetched.pop(k + 1)
         # the records of step k are assembled on a host thread while step k+1's GPU work runs; decode
         # tails carry into the next step except out of warmup and out of the last timed step
         drain = k < args.warmup or k == args.warmup + args.steps - 1
-        res = runner.run_cells_async(cur, cells, ride_along=ride, drain=drain)
+        res = runner.run_cells_async(cur, cells, ride_along=ride, drain=drain, plan=plan)
         return future.pop(k + 1), res, time.perf_counter() - t0
 
     def cells_of(k):

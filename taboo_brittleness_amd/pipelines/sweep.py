@@ -334,7 +334,8 @@ class SweepRunner:
             groups.setdefault(key, []).append(p.resid[p.spikes_rel].float())
         return {k: A.secret_subspace(torch.cat(v, 0), rmax) for k, v in groups.items()}
 
-    def _plan_for(self, cells: Sequence[Cell], pairs: Sequence[Pair], bases: Dict[str, torch.Tensor]):
+    def _plan_for(self, cells: Sequence[Cell], pairs: Sequence[Pair], bases: Dict[str, torch.Tensor],
+                  with_carry: bool = True):
         """Host-side plan of a batch: int arrays (one row per cell, cell ``i`` = row/slot ``i``) plus the
         projection basis rows to upload (row ``i * rmax + j`` = j-th direction of proj cell ``i``)."""
         K = self.iv.spikes_k
@@ -384,16 +385,39 @@ class SweepRunner:
                     kd[ci] = 2
                     brow.append(np.arange(ci * rmax, ci * rmax + r))
                     bval.append(U.float().cpu())
-        for cr in self._carry:                  # carried cells keep editing at their carry-region slots
-            cs_, ck_, ci_, cc_ = cr.plan_row
-            sp[cr.slot] = cs_
-            kd[cr.slot] = ck_
-            ix[cr.slot] = ci_
-            cn[cr.slot] = cc_
         basis = None
         if brow:
             basis = (np.concatenate(brow), torch.cat(bval, 0))
-        return {"spikes": sp, "kind": kd, "idx": ix, "cnt": cn, "basis": basis, "rows": B * rmax, "rmax": rmax}
+        plan = {"spikes": sp, "kind": kd, "idx": ix, "cnt": cn, "basis": basis, "rows": B * rmax, "rmax": rmax}
+        return self._plan_add_carry(plan) if with_carry else plan
+
+    def _plan_add_carry(self, plan: dict) -> dict:
+        for cr in self._carry:                  # carried cells keep editing at their carry-region slots
+            cs_, ck_, ci_, cc_ = cr.plan_row
+            plan["spikes"][cr.slot] = cs_
+            plan["kind"][cr.slot] = ck_
+            plan["idx"][cr.slot] = ci_
+            plan["cnt"][cr.slot] = cc_
+        return plan
+
+    def prefetch(self, pairs: Sequence[Pair], methods: Sequence[str] = METHODS):
+        """Build a future step's cells and host edit plan on a helper thread (pure host work: cell
+        enumeration, seeded random latent sets, plan arrays) while the GPU runs the current step.
+        Needs the pairs' baselines (spikes, targeted latents) to be final.  Pass the result to
+        :meth:`run_cells` / :meth:`run_cells_async` as ``prefetched``; ``None`` if it cannot apply."""
+        if any(not m.startswith("sae") for m in methods) or not pairs or any(p.resid is None for p in pairs):
+            return None
+        if getattr(self, "_prefetch_pool", None) is None:
+            from concurrent.futures import ThreadPoolExecutor
+
+            self._prefetch_pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="tb-prefetch")
+
+        def work():
+            cells = self.make_cells(pairs, methods)
+            if len(cells) > self.B:
+                return cells, None
+            return cells, self._plan_for(cells, pairs, {}, with_carry=False)
+        return self._prefetch_pool.submit(work)
 
     def _load_plan(self, plan: dict) -> EditHook:
         """Upload into the persistent plan (fixed tensors, so a captured decode graph stays valid)."""
@@ -453,12 +477,14 @@ class SweepRunner:
     # -------------------------------------------------------------------- run
     @torch.no_grad()
     def run_cells(self, pairs: List[Pair], cells: Sequence[Cell], measure_nll: Optional[bool] = None,
-                  ride_along: Sequence[Pair] = (), drain: bool = True) -> List[dict]:
+                  ride_along: Sequence[Pair] = (), drain: bool = True, plan: Optional[dict] = None) -> List[dict]:
         """Run edited cells; ``ride_along`` pairs get their *baseline* generated in the same batch
         (unedited rows), which pipelines the next cells' baselines behind the current ones.
-        ``drain=False`` (with ``carry_rows``) lets the last batch's decode tail carry into the next call."""
+        ``drain=False`` (with ``carry_rows``) lets the last batch's decode tail carry into the next call.
+        ``plan``: the host edit plan of ``cells`` from :meth:`prefetch` (single-batch calls only)."""
         measure_nll = self.iv.measure_nll if measure_nll is None else measure_nll
         self._drain = drain
+        self._pre_plan = plan
         ride = list(ride_along)
         if not cells and not ride:
             return []
@@ -474,23 +500,26 @@ class SweepRunner:
         assert per > 0 or not cells, "batch too small for the ride-along baselines"
         parts = []
         batches = [list(cells[i:i + per]) for i in range(0, len(cells), per)] or [[]]
+        if len(batches) > 1 or len(cells) + len(ride) > self.B:
+            self._pre_plan = None
         for bi, batch in enumerate(batches):
             rb = ride if bi == 0 else []
             self._drain_batch = drain or bi + 1 < len(batches)
             parts.append(self._run_batch(pairs, batch, rb, measure_nll, bases))
+        self._pre_plan = None
         if getattr(self, "_defer", False):
             return _Deferred(parts)
         return [r for part in parts for r in part]
 
     def run_cells_async(self, pairs: List[Pair], cells: Sequence[Cell], measure_nll: Optional[bool] = None,
-                        ride_along: Sequence[Pair] = (), drain: bool = True) -> "_Deferred":
+                        ride_along: Sequence[Pair] = (), drain: bool = True, plan: Optional[dict] = None) -> "_Deferred":
         """:meth:`run_cells` whose per-cell result records are assembled on a host worker thread: the
         GPU work (and everything later batches depend on: baselines, spikes, scores, KV) is done when
         this returns, so the caller can launch the next batch while the records of this one are built.
         ``.result()`` returns the records."""
         self._defer = True
         try:
-            out = self.run_cells(pairs, cells, measure_nll, ride_along, drain)
+            out = self.run_cells(pairs, cells, measure_nll, ride_along, drain, plan)
         finally:
             self._defer = False
         return out if isinstance(out, _Deferred) else _Deferred([out])
@@ -624,7 +653,8 @@ class SweepRunner:
         rb = list(rb)
         nr = len(rb)
         l0, L = self.layer, m.spec.layers
-        plan = self._plan_for(batch, pairs, bases)
+        pre = getattr(self, "_pre_plan", None)
+        plan = self._plan_add_carry(pre) if pre is not None else self._plan_for(batch, pairs, bases)
         self._tick("plan_host")
         hook = self._load_plan(plan)
         hooks = {self.layer: [hook, self.capture]}
@@ -1103,12 +1133,16 @@ class SweepRunner:
         if len(streams) > 1:
             streams[1].wait_stream(main)
         ws_rows = min(cap, -(-M // 256) * 256)
+        # every chunk's attention block table in one upload (no host sync between chunks)
+        tabs = [packed_blocks(chunk, rpb) for (_, _, chunk) in chunks]
+        tab_off = np.concatenate([[0], np.cumsum([t.shape[0] for t in tabs])]).astype(np.int64)
+        tab_d = torch.cat(tabs, 0).to(dev) if tabs else None
         for ci, (c0, c1, chunk) in enumerate(chunks):
             st = streams[ci % len(streams)]
             with (torch.cuda.stream(st) if st is not None else _nullctx()):
                 Mc = c1 - c0
                 Mp = -(-Mc // 256) * 256
-                blk = packed_blocks(chunk, rpb).to(dev)
+                blk = tab_d[int(tab_off[ci]):int(tab_off[ci + 1])]
                 cp = torch.full((Mp,), -1, dtype=torch.int32, device=dev)
                 cs = torch.zeros(Mp, dtype=torch.int32, device=dev)
                 hin = torch.zeros(Mp, H.shape[1], dtype=H.dtype, device=dev)
