@@ -39,7 +39,7 @@ import torch
 from .. import ops
 from ..interp import analysis as A
 from ..interp.edits import CaptureHook, EditHook, EditPlan
-from ..interp.logit_lens import lens_packed, lens_readout, reference_exclusions
+from ..interp.logit_lens import _excl_id, lens_packed, lens_readout, reference_exclusions
 from ..interp.prompts import contains_secret, hint_prompt_ids
 from ..models.tokenizer import secret_token_id
 from ..runtime.generation import Generator
@@ -943,12 +943,14 @@ class SweepRunner:
             else:
                 resp, ng, d = out.response_ids(j), out.n_gen[j], dv
                 sn = float(self_nll_h[j, :ng].mean()) if ng else float("nan")
-                pos_c = np.asarray(sorted(set([s for s in sp.tolist() if s < min(d, ng)] + list(range(d, ng)))),
-                                   dtype=np.int64)
+                # spikes before the divergence (all < d) then every position from d: already sorted
+                pos_c = np.concatenate([sp[sp < min(d, ng)], np.arange(d, ng, dtype=np.int64)])
                 ex = np.full((pos_c.size, 2), -1, dtype=np.int64)
                 if ref_ex and pos_c.size:
-                    e_all = reference_exclusions(self.tok, resp)
-                    ex[:] = [e_all[t] for t in pos_c.tolist()]
+                    cur = np.fromiter((_excl_id(self.tok, t) for t in resp), dtype=np.int64, count=len(resp))
+                    ex[:, 0] = cur[pos_c]
+                    prev = pos_c - 1
+                    ex[:, 1] = np.where(prev >= 0, cur[np.maximum(prev, 0)], -1)
             rows_l.append(slot * S1 + p.plen + pos_c)
             ex_l.append(ex)
             trk_l.append(np.broadcast_to(trk, (pos_c.size, K)))

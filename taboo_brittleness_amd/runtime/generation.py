@@ -327,18 +327,16 @@ class Generator:
         toks = self.out_tokens[:n, :max_new]
         if copy:
             toks = toks.clone()
-        host = toks.cpu()
-        stop = set(int(s) for s in self.stop_ids.tolist())
-        n_gen, stopped = [], []
-        for b in range(n):
-            row = host[b].tolist()
-            k = next((i for i, t in enumerate(row) if t in stop), None)
-            n_gen.append(len(row) if k is None else k)
-            stopped.append(k is not None)
+        host = toks.cpu().numpy()
+        is_stop = np.isin(host, self.stop_ids.cpu().numpy())          # first stop token per row, vectorised
+        hit = is_stop.any(1)
+        first = np.where(hit, is_stop.argmax(1), host.shape[1])
         nll, tf = self.out_nll[:n, :max_new], self.out_tf_nll[:n, :max_new]
         if copy:
             nll, tf = nll.clone(), tf.clone()
-        return GenerationOutput(list(prompt_lens), toks, n_gen, stopped, nll, tf)
+        out = GenerationOutput(list(prompt_lens), toks, first.tolist(), hit.tolist(), nll, tf)
+        out._host = host                                                # reused by response_ids()
+        return out
 
     # -------------------------------------------------------------- generate
     @torch.no_grad()
