@@ -52,6 +52,19 @@ def _excl_id(tok, t: int) -> int:
     return v
 
 
+def excl_table(tok, vocab_size: int) -> np.ndarray:
+    """``table[id] = convert_tokens_to_ids(decode([id]))`` for every id (built once per tokenizer), so the
+    reference's per-position exclusions of a whole batch are one array gather."""
+    tab = getattr(tok, "_tb_excl_table", None)
+    if tab is None or tab.shape[0] < vocab_size:
+        tab = np.fromiter((_excl_id(tok, t) for t in range(vocab_size)), dtype=np.int64, count=vocab_size)
+        try:
+            tok._tb_excl_table = tab
+        except AttributeError:
+            pass
+    return tab
+
+
 def reference_exclusions(tok, ids: Sequence[int]) -> List[Tuple[int, int]]:
     """Per response position: (id of current token, id of previous token or -1) as the reference
     computes them via ``convert_tokens_to_ids(decoded_string)`` (`src/01_reproduce_logit_lens.py:56-69`).

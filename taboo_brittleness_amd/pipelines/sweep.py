@@ -39,7 +39,7 @@ import torch
 from .. import ops
 from ..interp import analysis as A
 from ..interp.edits import CaptureHook, EditHook, EditPlan
-from ..interp.logit_lens import _excl_id, lens_packed, lens_readout, reference_exclusions
+from ..interp.logit_lens import excl_table, lens_packed, lens_readout, reference_exclusions
 from ..interp.prompts import contains_secret, hint_prompt_ids
 from ..models.tokenizer import secret_token_id
 from ..runtime.generation import Generator
@@ -916,6 +916,7 @@ class SweepRunner:
                                                                                     for e in entries)) else None
         K = max(len(e[1].track) for e in entries)
         ref_ex = self.exclusion == "reference"
+        etab = excl_table(self.tok, self.m.spec.vocab_size) if ref_ex else None
         pc_cache: Dict[int, tuple] = {}
 
         def pair_info(p: Pair):
@@ -947,7 +948,7 @@ class SweepRunner:
                 pos_c = np.concatenate([sp[sp < min(d, ng)], np.arange(d, ng, dtype=np.int64)])
                 ex = np.full((pos_c.size, 2), -1, dtype=np.int64)
                 if ref_ex and pos_c.size:
-                    cur = np.fromiter((_excl_id(self.tok, t) for t in resp), dtype=np.int64, count=len(resp))
+                    cur = etab[np.asarray(resp, dtype=np.int64)]
                     ex[:, 0] = cur[pos_c]
                     prev = pos_c - 1
                     ex[:, 1] = np.where(prev >= 0, cur[np.maximum(prev, 0)], -1)
