@@ -124,7 +124,7 @@ def forcing_curves(cfg: Config, runner: SweepRunner, pairs, methods: Sequence[st
     for w in cfg.words:
         settings.append({"word": w, "kind": "none"})
         keys.append(("none", 0))
-        pool = sorted({j for p in pairs if p.word == w for j in p.active_pool})
+        pool = np.unique(np.concatenate([np.zeros(0, dtype=np.int64)] + [p.active_pool for p in pairs if p.word == w]))
         for meth in methods:
             if meth.startswith("sae"):
                 if runner.sae is None:

@@ -62,7 +62,7 @@ class Pair:
     resid: Optional[torch.Tensor] = None   # [n_resp, D] hooked-layer residuals (device)
     nll: float = float("nan")
     targeted: List[int] = field(default_factory=list)
-    active_pool: List[int] = field(default_factory=list)
+    active_pool: np.ndarray = field(default_factory=lambda: np.zeros(0, dtype=np.int64))  # sorted, unique
     gen_toks: List[int] = field(default_factory=list)   # generated tokens incl. the stop token (if any)
     tok_nll: Optional[np.ndarray] = None                # per generated token NLL under the unedited model
     kv_slot: int = -1                                   # slot in the runner's pair-KV store
@@ -304,7 +304,7 @@ class SweepRunner:
         g_h, l_h = g_idx.cpu().numpy(), l_idx.cpu().numpy()
         bounds = np.searchsorted(g_h, np.arange(len(live) + 1))
         for g, p in enumerate(live):
-            p.active_pool = l_h[bounds[g]:bounds[g + 1]].tolist()
+            p.active_pool = l_h[bounds[g]:bounds[g + 1]].astype(np.int64)
 
     # ----------------------------------------------------------------- cells
     def make_cells(self, pairs: Sequence[Pair], methods: Sequence[str] = METHODS) -> List[Cell]:
@@ -413,10 +413,14 @@ class SweepRunner:
             self._prefetch_pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="tb-prefetch")
 
         def work():
+            t0 = time.perf_counter()
             cells = self.make_cells(pairs, methods)
-            if len(cells) > self.B:
-                return cells, None
-            return cells, self._plan_for(cells, pairs, {}, with_carry=False)
+            t1 = time.perf_counter()
+            out = (cells, None) if len(cells) > self.B else (cells, self._plan_for(cells, pairs, {}, with_carry=False))
+            t2 = time.perf_counter()
+            self.timings["prefetch_cells"] = self.timings.get("prefetch_cells", 0.0) + t1 - t0
+            self.timings["prefetch_plan"] = self.timings.get("prefetch_plan", 0.0) + t2 - t1
+            return out
         return self._prefetch_pool.submit(work)
 
     def _load_plan(self, plan: dict) -> EditHook:

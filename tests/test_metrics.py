@@ -81,3 +81,34 @@ def test_bootstrap_ci():
     g = grouped_bootstrap_ci([1, 1, 2, 2, 3, 3], [0, 0, 1, 1, 2, 2], seed=1)
     assert g["lo"] <= 2.0 <= g["hi"]
     assert bootstrap_ci([], seed=0)["n"] == 0
+
+
+def test_random_latents_batch_sampling():
+    """Random controls (EP:128): size, distinct, drawn from the pool minus exclusions, seed-deterministic,
+    uniform over the pool; small pools take the exhaustive ranking, short pools fill from all latents."""
+    import numpy as np
+
+    from taboo_brittleness_amd.interp.analysis import random_latents_batch
+
+    rng = np.random.default_rng(0)
+    pool = np.sort(rng.choice(16384, 600, replace=False)).astype(np.int64)
+    budgets = [1, 2, 4, 8, 16, 32] * 50
+    seeds = list(range(1000, 1000 + len(budgets)))
+    ex = [pool[: b].tolist() for b in budgets]
+    got = random_latents_batch(16384, budgets, seeds, ex, pool=pool)
+    counts = np.zeros(16384)
+    for g, b, e in zip(got, budgets, ex):
+        assert len(g) == b and len(set(g)) == b
+        assert set(g) <= set(pool.tolist()) and not (set(g) & set(e))
+        counts[g] += 1
+    assert got == random_latents_batch(16384, budgets, seeds, ex, pool=pool.tolist())
+    # uniformity: every pool latent outside the most-excluded head is equally likely (chi-square, loose)
+    tail = counts[pool[32:]]
+    exp = tail.mean()
+    chi2 = float(((tail - exp) ** 2 / exp).sum())
+    assert chi2 < 1.5 * tail.size
+    # small pool: exhaustive ranking; short pool: filled from the whole dictionary
+    small = random_latents_batch(16384, [8, 8], [1, 2], [[], [5]], pool=list(range(20)))
+    assert all(len(set(s)) == 8 and set(s) <= set(range(20)) for s in small) and 5 not in small[1]
+    short = random_latents_batch(16384, [8], [3], [[0]], pool=[0, 1, 2])
+    assert len(set(short[0])) == 8 and {1, 2} <= set(short[0]) and 0 not in short[0]
