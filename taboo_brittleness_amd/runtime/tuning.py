@@ -51,6 +51,9 @@ def enable_tuned_gemms(tag: str, tune: bool = False, rotating_mb: int = 512, max
             pass
     else:
         tun.tuning_enable(False)
+        # read-only use: with one process per GPU every rank shares this file, so none rewrites it at exit
+        if hasattr(tun, "write_file_on_exit"):
+            tun.write_file_on_exit(False)
     if os.path.exists(path):
         tun.read_file(path)
     return path
