@@ -155,6 +155,7 @@ class ParallelCfg:
     dp: int = 1
     tp: int = 1
     backend: str = "auto"               # auto -> nccl (RCCL) on GPU, gloo on CPU
+    tp_allreduce: str = "rccl"          # rccl | p2p (one-shot xGMI peer all-reduce, parallel/p2p.py)
 
 
 @dataclass

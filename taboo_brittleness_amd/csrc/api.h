@@ -59,3 +59,15 @@ void tb_sae_decode_sparse(const float* acts, const uint16_t* Wdec, const float* 
                           float* out_f32, int M, int L, int D, hipStream_t st);
 void tb_latent_score(const float* acts, const float* p, const uint8_t* spike, const int32_t* seg, float* out,
                      float* spike_mean, float* corr, int G, int L, hipStream_t st);
+// p2p.hip
+int tb_p2p_header_bytes();
+int tb_p2p_max_ranks();
+void* tb_p2p_alloc(size_t bytes, int uncached);
+int tb_p2p_free(void* p);
+int tb_p2p_get_handle(void* p, void* handle_out);
+int tb_p2p_handle_size();
+void* tb_p2p_open_handle(const void* handle);
+int tb_p2p_close_handle(void* p);
+int tb_p2p_allreduce(void* const* bases, int rank, int world, const void* in, void* out, size_t nbytes, int is_bf16,
+                     int blocks, int spin_max, int barriers, hipStream_t st);
+uint32_t tb_p2p_read_error(void* own_base);

@@ -354,6 +354,53 @@ void latent_score(torch::Tensor acts, torch::Tensor p, torch::Tensor spike, torc
 
 int64_t attention_lds_bytes(int64_t hd) { return tb_attention_lds_bytes((int)hd); }
 
+// ---- one-shot P2P all-reduce (p2p.hip): regions are raw device pointers passed as int64
+int64_t p2p_alloc(int64_t bytes, bool uncached) {
+  void* p = tb_p2p_alloc((size_t)bytes, uncached ? 1 : 0);
+  TORCH_CHECK(p != nullptr, "p2p_alloc: device allocation of ", bytes, " bytes failed");
+  return reinterpret_cast<int64_t>(p);
+}
+
+void p2p_free(int64_t p) { TORCH_CHECK(tb_p2p_free(reinterpret_cast<void*>(p)) == 0, "p2p_free failed"); }
+
+py::bytes p2p_get_handle(int64_t p) {
+  std::string h((size_t)tb_p2p_handle_size(), '\0');
+  const int e = tb_p2p_get_handle(reinterpret_cast<void*>(p), &h[0]);
+  TORCH_CHECK(e == 0, "hipIpcGetMemHandle failed (hipError ", e, ")");
+  return py::bytes(h);
+}
+
+int64_t p2p_open_handle(py::bytes handle) {
+  std::string h = handle;
+  TORCH_CHECK((int)h.size() == tb_p2p_handle_size(), "p2p_open_handle: bad handle size");
+  void* p = tb_p2p_open_handle(h.data());
+  TORCH_CHECK(p != nullptr, "hipIpcOpenMemHandle failed");
+  return reinterpret_cast<int64_t>(p);
+}
+
+void p2p_close_handle(int64_t p) { TORCH_CHECK(tb_p2p_close_handle(reinterpret_cast<void*>(p)) == 0, "p2p_close failed"); }
+
+void p2p_allreduce(std::vector<int64_t> bases, int64_t rank, torch::Tensor in, torch::Tensor out, int64_t blocks,
+                   int64_t spin_max, bool barriers) {
+  CHECK_DEV(in); CHECK_CONTIG(in); CHECK_DEV(out); CHECK_CONTIG(out);
+  const bool is_bf16 = in.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(is_bf16 || in.scalar_type() == at::kFloat, "p2p_allreduce: bf16 or fp32");
+  TORCH_CHECK(out.scalar_type() == in.scalar_type() && out.numel() == in.numel(), "p2p_allreduce: out mismatch");
+  const int world = (int)bases.size();
+  TORCH_CHECK(world >= 1 && world <= tb_p2p_max_ranks() && rank >= 0 && rank < world, "p2p_allreduce: ranks");
+  std::vector<void*> b(world);
+  for (int r = 0; r < world; ++r) b[r] = reinterpret_cast<void*>(bases[r]);
+  c10::DeviceGuard g(in.device());
+  const size_t nbytes = (size_t)in.numel() * in.element_size();
+  const int e = tb_p2p_allreduce(b.data(), (int)rank, world, in.data_ptr(), out.data_ptr(), nbytes, is_bf16 ? 1 : 0,
+                                 (int)blocks, (int)spin_max, barriers ? 1 : 0, cur_stream());
+  TORCH_CHECK(e == 0, "p2p_allreduce launch failed (", e, ")");
+}
+
+int64_t p2p_read_error(int64_t own) { return (int64_t)tb_p2p_read_error(reinterpret_cast<void*>(own)); }
+int64_t p2p_header_bytes() { return tb_p2p_header_bytes(); }
+int64_t p2p_max_ranks() { return tb_p2p_max_ranks(); }
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -382,4 +429,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sae_decode_sparse", &sae_decode_sparse);
   m.def("latent_score", &latent_score);
   m.def("attention_lds_bytes", &attention_lds_bytes);
+  m.def("p2p_alloc", &p2p_alloc);
+  m.def("p2p_free", &p2p_free);
+  m.def("p2p_get_handle", &p2p_get_handle);
+  m.def("p2p_open_handle", &p2p_open_handle);
+  m.def("p2p_close_handle", &p2p_close_handle);
+  m.def("p2p_allreduce", &p2p_allreduce);
+  m.def("p2p_read_error", &p2p_read_error);
+  m.def("p2p_header_bytes", &p2p_header_bytes);
+  m.def("p2p_max_ranks", &p2p_max_ranks);
 }

@@ -1,0 +1,128 @@
+"""One-shot peer-to-peer all-reduce over xGMI (``csrc/p2p.hip``).
+
+TP's all-reduces are small (2 × ``[M, 3584]`` bf16 per block), so they are latency-bound.  On the
+MI355X's point-to-point xGMI fabric every GPU is one hop from each of its 7 peers; a ring pays
+2(N-1) dependent hops over one link each, a one-shot reduce pays one: every rank stages its input in
+an IPC-exported region, a barrier of release/acquire flags says "all staged", and each rank reads
+the N inputs straight out of the peers' HBM (N-1 links in parallel) and sums them in rank order —
+the result is bit-identical on every rank, which TP's replicated readouts rely on.
+
+The IPC handles are exchanged once through the process group (RCCL or gloo); afterwards no
+collective library is involved.  Messages larger than the staging area fall back to RCCL.
+
+The reference has no collectives at all (SURVEY §2.4 "Collective / NCCL call sites: none").
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+
+def _ext():
+    from ..ops._ext import kernels
+
+    return kernels()
+
+
+class P2PAllReduce:
+    """Per-process state of the one-shot all-reduce for one (TP) group.
+
+    ``max_bytes`` sizes each rank's staging area (a decode step of a few hundred rows is ≈1-3 MB;
+    prefill chunks above the size use RCCL).  ``blocks`` workgroups each own a grid-stride share of
+    16-byte vectors and a private pair of barrier slots; ``spin_max`` bounds every wait (a missing
+    peer sets the error word instead of hanging the GPU — :meth:`check` raises on it).
+    """
+
+    def __init__(self, group=None, device: Optional[torch.device] = None, max_bytes: int = 8 << 20,
+                 blocks: int = 64, spin_max: int = 1 << 22, uncached: bool = True):
+        ext = _ext()
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        if self.world > int(ext.p2p_max_ranks()):
+            raise ValueError(f"p2p all-reduce supports at most {ext.p2p_max_ranks()} ranks")
+        self.device = device or torch.device("cuda", torch.cuda.current_device())
+        self.max_bytes = int(max_bytes)
+        self.blocks = int(blocks)
+        self.spin_max = int(spin_max)
+        with torch.cuda.device(self.device):
+            self.own = int(ext.p2p_alloc(int(ext.p2p_header_bytes()) + self.max_bytes, uncached))
+            handle = ext.p2p_get_handle(self.own)
+        handles: List[bytes] = [b""] * self.world
+        if self.world > 1:
+            dist.all_gather_object(handles, handle, group=group)
+        else:
+            handles = [handle]
+        self.opened: List[int] = []
+        bases = []
+        with torch.cuda.device(self.device):
+            for r, h in enumerate(handles):
+                if r == self.rank:
+                    bases.append(self.own)
+                else:
+                    p = int(ext.p2p_open_handle(h))
+                    self.opened.append(p)
+                    bases.append(p)
+        self.bases = bases
+        self.calls = 0
+        self.fallbacks = 0
+
+    def supports(self, t: torch.Tensor) -> bool:
+        nbytes = t.numel() * t.element_size()
+        align = 16 if t.dtype == torch.bfloat16 else 32
+        return (t.is_cuda and t.dtype in (torch.bfloat16, torch.float32) and nbytes <= self.max_bytes
+                and nbytes % align == 0 and t.is_contiguous())
+
+    def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
+        """In-place sum over the group (stream-ordered on the current stream)."""
+        if self.world == 1:
+            return t
+        if not self.supports(t):
+            self.fallbacks += 1
+            dist.all_reduce(t, group=self.group)
+            return t
+        _ext().p2p_allreduce(self.bases, self.rank, t, t, self.blocks, self.spin_max, True)
+        self.calls += 1
+        return t
+
+    def check(self) -> None:
+        """Raise if any barrier wait of this rank timed out since the last check (synchronises)."""
+        torch.cuda.synchronize(self.device)
+        err = int(_ext().p2p_read_error(self.own))
+        if err:
+            raise RuntimeError(f"p2p all-reduce rank {self.rank}: barrier timed out waiting for ranks "
+                               f"{[r for r in range(32) if err >> r & 1]}")
+
+    def close(self) -> None:
+        if not self.bases:
+            return
+        ext = _ext()
+        torch.cuda.synchronize(self.device)
+        for p in self.opened:
+            ext.p2p_close_handle(p)
+        ext.p2p_free(self.own)
+        self.bases, self.opened = [], []
+
+
+def reduce_local(inputs: List[torch.Tensor], blocks: int = 64) -> torch.Tensor:
+    """Single-process check of the reduction math: ``inputs`` (same shape, on one GPU) are staged into
+    per-"rank" regions and summed by the kernel with its barriers off.  Returns rank 0's output."""
+    ext = _ext()
+    n = len(inputs)
+    nbytes = inputs[0].numel() * inputs[0].element_size()
+    hdr = int(ext.p2p_header_bytes())
+    bases = [int(ext.p2p_alloc(hdr + nbytes, True)) for _ in range(n)]
+    try:
+        out = torch.empty_like(inputs[0])
+        for r, x in enumerate(inputs):
+            # stage rank r's input: its own call with barriers off writes the staging area (the output
+            # of these calls is discarded; only the final rank-0 call below is returned)
+            ext.p2p_allreduce(bases[:r + 1], r, x.contiguous(), torch.empty_like(x), blocks, 1, False)
+        ext.p2p_allreduce(bases, 0, inputs[0].contiguous(), out, blocks, 1, False)
+        torch.cuda.synchronize()
+        return out
+    finally:
+        for b in bases:
+            ext.p2p_free(b)

@@ -35,10 +35,13 @@ class TPContext:
     size: int
     rank: int
     group: Optional[object] = None      # torch.distributed ProcessGroup (None = world / single process)
+    p2p: Optional[object] = None        # parallel.p2p.P2PAllReduce: one-shot xGMI all-reduce for GPU tensors
 
     def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
         if self.size > 1:
-            if t.dtype == torch.bfloat16 and not t.is_cuda:
+            if self.p2p is not None and t.is_cuda:
+                self.p2p.all_reduce_(t)          # falls back to RCCL itself for oversized messages
+            elif t.dtype == torch.bfloat16 and not t.is_cuda:
                 # gloo has no bf16 sum: reduce in fp32 and round once (same single rounding as RCCL bf16 2-way)
                 f = t.float()
                 dist.all_reduce(f, group=self.group)
@@ -48,8 +51,11 @@ class TPContext:
         return t
 
 
-def make_groups(world: int, rank: int, tp: int):
-    """Create every TP group (all ranks must call this) and return (TPContext, dp_rank, dp_size)."""
+def make_groups(world: int, rank: int, tp: int, allreduce: str = "rccl", device: Optional[torch.device] = None):
+    """Create every TP group (all ranks must call this) and return (TPContext, dp_rank, dp_size).
+
+    ``allreduce="p2p"`` gives each GPU group the one-shot peer all-reduce (``parallel/p2p.py``)
+    instead of RCCL's ring for the per-block activations."""
     assert world % tp == 0, f"world {world} not divisible by tp {tp}"
     dp = world // tp
     mine = None
@@ -58,6 +64,10 @@ def make_groups(world: int, rank: int, tp: int):
         grp = dist.new_group(ranks) if (tp > 1 and dist.is_initialized()) else None
         if rank in ranks:
             mine = TPContext(tp, rank - g * tp, grp)
+    if allreduce == "p2p" and tp > 1 and device is not None and device.type == "cuda":
+        from .p2p import P2PAllReduce
+
+        mine.p2p = P2PAllReduce(group=mine.group, device=device)
     return mine, rank // tp, dp
 
 

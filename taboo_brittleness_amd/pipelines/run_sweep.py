@@ -34,7 +34,8 @@ def run_sweep(cfg: Config, out_dir: str, methods: Sequence[str] = METHODS, info:
     if cfg.parallel.tp > 1:
         from ..parallel.tp import make_groups
 
-        tp_ctx, dp_rank, dp_size = make_groups(info.world, info.rank, cfg.parallel.tp)
+        tp_ctx, dp_rank, dp_size = make_groups(info.world, info.rank, cfg.parallel.tp,
+                                                 cfg.parallel.tp_allreduce, info.device)
     stack = build_stack(cfg, info.device, tp=tp_ctx)
     model, tok, sae = stack.model, stack.tok, stack.sae
     B = batch or cfg.runtime.batch_size

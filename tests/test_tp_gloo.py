@@ -20,7 +20,7 @@ def _port():
     return p
 
 
-def _run(tp_ctx):
+def _run(tp_ctx, device="cpu"):
     from taboo_brittleness_amd.models.gemma2 import Gemma2Model
     from taboo_brittleness_amd.models.weights import random_gemma2
     from taboo_brittleness_amd.parallel.tp import shard_weights
@@ -29,10 +29,12 @@ def _run(tp_ctx):
     w = random_gemma2(SPEC, dtype=torch.bfloat16, seed=11, norm_std=0.1)
     if tp_ctx is not None:
         w = shard_weights(w, tp_ctx)
-    m = Gemma2Model(w, "cpu", tp=tp_ctx)
-    ids = torch.randint(0, SPEC.vocab_size, (2, 7), generator=torch.Generator().manual_seed(0)).int()
-    pos = torch.arange(7, dtype=torch.int32).expand(2, 7).contiguous()
-    x = m.forward(ids, pos, m.new_cache(2, 8), torch.arange(2, dtype=torch.int32))
+    if device != "cpu":
+        w = w.to(device)
+    m = Gemma2Model(w, device, tp=tp_ctx)
+    ids = torch.randint(0, SPEC.vocab_size, (2, 7), generator=torch.Generator().manual_seed(0)).int().to(device)
+    pos = torch.arange(7, dtype=torch.int32).expand(2, 7).contiguous().to(device)
+    x = m.forward(ids, pos, m.new_cache(2, 8), torch.arange(2, dtype=torch.int32, device=device))
     logits = m.logits(x).float()
     gen = Generator(m, 2, 16, use_graphs=False, stop_ids=(10_000,))
     out = gen.generate([[2, 5, 9, 11], [2, 7, 8]], 5)
