@@ -133,12 +133,18 @@ def random_latents_batch(d_sae: int, budgets: Sequence[int], seeds: Sequence[int
     if pool is not None and len(pool):
         pl = np.unique(np.asarray(pool if isinstance(pool, np.ndarray) else list(pool), dtype=np.int64))
         N = pl.size
-        if N <= 4 * mmax:
-            out = _ranked_pool(sd, pl, mmax, excludes)
-        else:
-            R = 2 * mmax + 8
+        # every decision below is per row (its own budget), so a cell's set never depends on which
+        # other cells share the batch: small pool for this budget -> exhaustive ranking; otherwise
+        # the first 2*m+8 stream draws, falling back to the ranking if they leave the row short
+        ranked = N <= 4 * bud
+        redo_rows = np.nonzero(ranked)[0]
+        stream_rows = np.nonzero(~ranked)[0]
+        if stream_rows.size:
+            sr = stream_rows
+            rlen = 2 * bud[sr] + 8
+            R = int(rlen.max())
             with np.errstate(over="ignore"):
-                v = pl[(_keys(sd, np.arange(R, dtype=np.int64), 3) % np.uint64(N)).astype(np.int64)]
+                v = pl[(_keys(sd[sr], np.arange(R, dtype=np.int64), 3) % np.uint64(N)).astype(np.int64)]
             # first occurrence of each value within its row (stable sort keeps draw order among repeats)
             o = np.argsort(v, axis=1, kind="stable")
             vs = np.take_along_axis(v, o, 1)
@@ -146,21 +152,22 @@ def random_latents_batch(d_sae: int, budgets: Sequence[int], seeds: Sequence[int
             first_s[:, 1:] = vs[:, 1:] != vs[:, :-1]
             ok = np.empty_like(first_s)
             np.put_along_axis(ok, o, first_s, 1)
-            ex_rows = [np.full(len(ex), i, dtype=np.int64) for i, ex in enumerate(excludes) if len(ex)]
+            ok &= np.arange(R, dtype=np.int64)[None, :] < rlen[:, None]
+            ex_rows = [np.full(len(excludes[i]), k, dtype=np.int64) for k, i in enumerate(sr) if len(excludes[i])]
             if ex_rows:
                 ex_key = np.concatenate(ex_rows) * d_sae + np.concatenate(
-                    [np.asarray(list(ex), dtype=np.int64) for ex in excludes if len(ex)])
-                ok &= ~np.isin(np.arange(n, dtype=np.int64)[:, None] * d_sae + v, ex_key)
+                    [np.asarray(list(excludes[i]), dtype=np.int64) for i in sr if len(excludes[i])])
+                ok &= ~np.isin(np.arange(sr.size, dtype=np.int64)[:, None] * d_sae + v, ex_key)
             rank = np.cumsum(ok, axis=1)
-            keep = ok & (rank <= bud[:, None])
-            short = rank[:, -1] < bud
-            for i in range(n):
-                out[i] = v[i][keep[i]].tolist()
-            if short.any():
-                rows = np.nonzero(short)[0]
-                redo = _ranked_pool(sd[rows], pl, mmax, [excludes[i] for i in rows])
-                for i, r in zip(rows.tolist(), redo):
-                    out[i] = r
+            keep = ok & (rank <= bud[sr][:, None])
+            short = rank[:, -1] < bud[sr]
+            for k, i in enumerate(sr.tolist()):
+                out[i] = v[k][keep[k]].tolist()
+            redo_rows = np.concatenate([redo_rows, sr[short]])
+        if redo_rows.size:
+            redo = _ranked_pool(sd[redo_rows], pl, int(bud[redo_rows].max()), [excludes[i] for i in redo_rows])
+            for i, r in zip(redo_rows.tolist(), redo):
+                out[i] = r
         for i in range(n):
             del out[i][int(bud[i]):]
     for i in range(n):
