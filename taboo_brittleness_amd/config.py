@@ -120,6 +120,7 @@ class SAECfg:
     d_sae: int = 16384
     apply_b_dec_to_input: bool = False
     dtype: str = "bfloat16"             # compute dtype of the HIP path
+    html_id: str = "gemma-2-9b-it"      # Neuronpedia model id for latent dashboards (v0 ``sae.html_id``)
 
 
 @dataclass

@@ -155,6 +155,10 @@ def make_report(results_dir: str, out_dir: str) -> List[str]:
                   if s.get("forcing") else None)
             content_vs_inhibition(s, p, fd)
             made.append(p)
+            if s.get("baselines"):
+                from .dashboards import write_latent_dashboard
+
+                made.append(write_latent_dashboard(s, os.path.join(out_dir, f"latent_dashboard_{tag}.html")))
     rows: Dict[str, Dict[str, float]] = {}
     ll = None
     for root, _, files in os.walk(results_dir):

@@ -57,6 +57,8 @@ def test_reference_pipeline_gemma_tiny(tmp_path):
     figs = os.listdir(os.path.join(t, "figs"))
     assert "table_baselines.csv" in figs and any(f.startswith("fig1_ablation_saes") for f in figs)
     assert any(f.startswith("fig2_lowrank") for f in figs)
+    dash = open(os.path.join(t, "figs", "latent_dashboard_all_seed42.html")).read()
+    assert "2-gemmascope-res-16k" in dash and "<h2>ship</h2>" in dash
 
 
 def test_gpt2_cpu_plumbing_config(tmp_path):

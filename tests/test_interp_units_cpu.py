@@ -237,3 +237,21 @@ def test_pair_cache_roundtrip_and_resume(tmp_path):
     assert sorted(os.listdir(os.path.dirname(npz))) == ["prompt_01.json", "prompt_01.npz"]
     tio.atomic_write_json(str(tmp_path / "r.json"), {"a": np.int64(3), "b": np.float32(0.5), "c": np.arange(2)})
     assert json.load(open(tmp_path / "r.json")) == {"a": 3, "b": 0.5, "c": [0, 1]}
+
+
+# ----------------------------------------------------------------------------- latent dashboards (G9)
+def test_latent_dashboard_offline_html(tmp_path):
+    from taboo_brittleness_amd.config import Config
+    from taboo_brittleness_amd.report.dashboards import neuronpedia_url, targeted_latent_counts, write_latent_dashboard
+
+    assert Config().sae.html_id == "gemma-2-9b-it"
+    assert neuronpedia_url(5404) == "https://www.neuronpedia.org/gemma-2-9b-it/31-gemmascope-res-16k/5404"
+    assert neuronpedia_url(7, layer=20, embed=True).split("?")[1].startswith("embed=true")
+    summary = {"config": {"layer": 31}, "baselines": [
+        {"word": "ship", "targeted_latents": [5404, 11, 12]}, {"word": "ship", "targeted_latents": [5404, 13]},
+        {"word": "moon", "targeted_latents": [13740]}]}
+    c = targeted_latent_counts(summary["baselines"])
+    assert c["ship"][5404] == 2 and c["moon"][13740] == 1
+    page = open(write_latent_dashboard(summary, str(tmp_path / "d.html"))).read()
+    assert "<h2>moon</h2>" in page and "<h2>ship</h2>" in page
+    assert page.count("<iframe") == 2 and "31-gemmascope-res-16k/5404" in page
