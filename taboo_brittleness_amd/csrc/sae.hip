@@ -20,7 +20,8 @@
 
 namespace {
 
-constexpr int GBM = 128, GBN = 128, GBK = 32, GLDS = 40;   // padded LDS row (bf16 elements)
+constexpr int GBM = 128, GBN = 128, GBK = 64, GLDS = 72;   // padded LDS row (bf16 elements)
+constexpr int GCPR = GBK / 8;                               // 16-B chunks per tile row
 
 __device__ __forceinline__ bf16x8 as_bf16x8(const uint4& u) { return __builtin_bit_cast(bf16x8, u); }
 
@@ -42,24 +43,26 @@ __global__ void __launch_bounds__(256) gemm_nt_kernel(const uint16_t* __restrict
   const int wm = wid >> 1, wn = wid & 1;
   const int grp = lane >> 4, col = lane & 15;
 
-  // staging assignment: A 128 rows x 4 chunks(16B) = 512 chunks; W 128 x 4 = 512 chunks (2 + 2 per thread)
-  const int a_row = tid >> 2, a_ch = tid & 3;
-  const int w_row0 = tid >> 2, w_ch = tid & 3;     // rows w_row0 and w_row0 + 64
-  auto load_tile = [&](int k0, uint4& ra, uint4& ra1, uint4& rw0, uint4& rw1) {
-    const int ar = m0 + a_row, ar1 = ar + 64;
-    ra = (ar < M) ? *reinterpret_cast<const uint4*>(A + (size_t)ar * K + k0 + a_ch * 8) : make_uint4(0, 0, 0, 0);
-    ra1 = (ar1 < M) ? *reinterpret_cast<const uint4*>(A + (size_t)ar1 * K + k0 + a_ch * 8) : make_uint4(0, 0, 0, 0);
-    const int wr0 = n0 + w_row0, wr1 = n0 + w_row0 + 64;
-    rw0 = (wr0 < N) ? *reinterpret_cast<const uint4*>(W + (size_t)wr0 * K + k0 + w_ch * 8) : make_uint4(0, 0, 0, 0);
-    rw1 = (wr1 < N) ? *reinterpret_cast<const uint4*>(W + (size_t)wr1 * K + k0 + w_ch * 8) : make_uint4(0, 0, 0, 0);
+  // staging: each operand tile is 128 rows x 8 chunks (16 B) = 1024 chunks, 4 per thread; chunks past K
+  // (K % 64 == 32) are zero-filled, so any K % 32 == 0 works
+  auto load_tile = [&](int k0, uint4 (&ra)[4], uint4 (&rw)[4]) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int id = tid + c * 256, row = id / GCPR, kk = k0 + (id % GCPR) * 8;
+      const int ar = m0 + row, wr = n0 + row;
+      ra[c] = (ar < M && kk < K) ? *reinterpret_cast<const uint4*>(A + (size_t)ar * K + kk) : make_uint4(0, 0, 0, 0);
+      rw[c] = (wr < N && kk < K) ? *reinterpret_cast<const uint4*>(W + (size_t)wr * K + kk) : make_uint4(0, 0, 0, 0);
+    }
   };
-  auto store_tile = [&](int buf, const uint4& ra, const uint4& ra1, const uint4& rw0, const uint4& rw1) {
+  auto store_tile = [&](int buf, const uint4 (&ra)[4], const uint4 (&rw)[4]) {
     uint16_t* la = lds[buf];
     uint16_t* lw = lds[buf] + GBM * GLDS;
-    *reinterpret_cast<uint4*>(la + a_row * GLDS + a_ch * 8) = ra;
-    *reinterpret_cast<uint4*>(la + (a_row + 64) * GLDS + a_ch * 8) = ra1;
-    *reinterpret_cast<uint4*>(lw + w_row0 * GLDS + w_ch * 8) = rw0;
-    *reinterpret_cast<uint4*>(lw + (w_row0 + 64) * GLDS + w_ch * 8) = rw1;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int id = tid + c * 256, off = (id / GCPR) * GLDS + (id % GCPR) * 8;
+      *reinterpret_cast<uint4*>(la + off) = ra[c];
+      *reinterpret_cast<uint4*>(lw + off) = rw[c];
+    }
   };
 
   f32x4 acc[4][4];
@@ -68,28 +71,32 @@ __global__ void __launch_bounds__(256) gemm_nt_kernel(const uint16_t* __restrict
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  uint4 ra, ra1, rw0, rw1;
-  load_tile(0, ra, ra1, rw0, rw1);
-  store_tile(0, ra, ra1, rw0, rw1);
+  uint4 ra[4], rw[4];
+  load_tile(0, ra, rw);
+  store_tile(0, ra, rw);
   __syncthreads();
-  const int nk = K / GBK;
+  const int nk = (K + GBK - 1) / GBK;
   int cur = 0;
   for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) load_tile((kt + 1) * GBK, ra, ra1, rw0, rw1);
+    if (kt + 1 < nk) load_tile((kt + 1) * GBK, ra, rw);
     const uint16_t* la = lds[cur];
     const uint16_t* lw = lds[cur] + GBM * GLDS;
-    bf16x8 af[4], bfr[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      af[i] = as_bf16x8(*reinterpret_cast<const uint4*>(la + (wm * 64 + i * 16 + col) * GLDS + grp * 8));
+    for (int ks = 0; ks < GBK / 32; ++ks) {
+      bf16x8 af[4], bfr[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      bfr[j] = as_bf16x8(*reinterpret_cast<const uint4*>(lw + (wn * 64 + j * 16 + col) * GLDS + grp * 8));
+      for (int i = 0; i < 4; ++i)
+        af[i] = as_bf16x8(*reinterpret_cast<const uint4*>(la + (wm * 64 + i * 16 + col) * GLDS + ks * 32 + grp * 8));
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+      for (int j = 0; j < 4; ++j)
+        bfr[j] = as_bf16x8(*reinterpret_cast<const uint4*>(lw + (wn * 64 + j * 16 + col) * GLDS + ks * 32 + grp * 8));
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    if (kt + 1 < nk) store_tile(cur ^ 1, ra, ra1, rw0, rw1);
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) store_tile(cur ^ 1, ra, rw);
     __syncthreads();
     cur ^= 1;
   }

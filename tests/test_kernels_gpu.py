@@ -248,7 +248,7 @@ def test_vocab_readouts(gpu):
     _close(ops.xent_rows(g, tgt.to(gpu), 30.0, True), ref.xent_rows(lg, tgt, 30.0, True), atol=2e-3, rtol=1e-4)
 
 
-@pytest.mark.parametrize("M,N,K", [(1, 128, 64), (70, 384, 3584), (257, 16384, 512)])
+@pytest.mark.parametrize("M,N,K", [(1, 128, 64), (33, 200, 96), (70, 384, 3584), (257, 16384, 512)])
 def test_gemm_nt_epilogues(gpu, M, N, K):
     torch.manual_seed(5)
     A = torch.randn(M, K, dtype=BF)
