@@ -8,6 +8,8 @@
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <c10/core/DeviceGuard.h>
 
+#include <cstdlib>
+
 #include "api.h"
 
 namespace {
@@ -26,6 +28,18 @@ hipStream_t cur_stream() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUD
 #define IN_F32(t) CHECK_DEV(t); CHECK_CONTIG(t); CHECK_F32(t)
 #define IN_I32(t) CHECK_DEV(t); CHECK_CONTIG(t); CHECK_I32(t)
 #define IN_U8(t) CHECK_DEV(t); CHECK_CONTIG(t); CHECK_U8(t)
+
+// TB_DEBUG_CHECKS=1: extra device-syncing argument checks (index ranges); never inside a stream capture.
+bool debug_checks() {
+  static const bool on = [] {
+    const char* e = std::getenv("TB_DEBUG_CHECKS");
+    return e != nullptr && e[0] == '1';
+  }();
+  if (!on) return false;
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(cur_stream(), &st) != hipSuccess) return false;
+  return st == hipStreamCaptureStatusNone;
+}
 
 inline uint16_t* bf(torch::Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
 inline const uint16_t* cbf(const torch::Tensor& t) { return reinterpret_cast<const uint16_t*>(t.data_ptr()); }
@@ -285,6 +299,11 @@ void gemm_nt(torch::Tensor A, torch::Tensor W, torch::Tensor C, c10::optional<to
   const int K = A.size(-1), M = A.numel() / K, N = W.size(0);
   TORCH_CHECK(W.size(1) == K && K % 32 == 0, "gemm_nt: K must match and be a multiple of 32");
   TORCH_CHECK(C.numel() == (int64_t)M * N, "gemm_nt: C shape");
+  TORCH_CHECK(epi >= 0 && epi <= 2, "gemm_nt: epi must be 0, 1 or 2");
+  if (epi == 2) {
+    TORCH_CHECK(!bias.has_value() || !bias->defined() || bias->numel() == N, "gemm_nt: bias numel must be N");
+    TORCH_CHECK(!thr.has_value() || !thr->defined() || thr->numel() == N, "gemm_nt: thr numel must be N");
+  }
   if (epi == 0) {
     TORCH_CHECK(C.scalar_type() == at::kBFloat16, "epi 0 writes bf16");
   } else {
@@ -305,8 +324,16 @@ void lowrank_edit(torch::Tensor h, c10::optional<torch::Tensor> x_next, torch::T
   TORCH_CHECK(f32 || E.scalar_type() == at::kBFloat16, "table dtype");
   const int D = h.size(-1), M = h.numel() / D;
   TORCH_CHECK(E.size(1) == D && Dm.size(1) == D && apply.numel() == M && cnt.numel() == M, "lowrank shapes");
+  TORCH_CHECK(D % 8 == 0 && D <= 256 * 8 * 4, "lowrank_edit: need D % 8 == 0 and D <= 8192");
   const int mmax = idx.numel() / M;
   TORCH_CHECK(mmax >= 1 && mmax <= 256, "lowrank mmax");
+  TORCH_CHECK(!bias.has_value() || !bias->defined() || bias->numel() == E.size(0), "lowrank_edit: bias numel");
+  TORCH_CHECK(!thr.has_value() || !thr->defined() || thr->numel() == E.size(0), "lowrank_edit: thr numel");
+  TORCH_CHECK(!pre_bias.has_value() || !pre_bias->defined() || pre_bias->numel() == D, "lowrank_edit: pre_bias");
+  if (debug_checks() && idx.numel() > 0) {   // device sync: debug builds / tests only
+    TORCH_CHECK(idx.min().item<int32_t>() >= 0 && idx.max().item<int32_t>() < std::min(E.size(0), Dm.size(0)),
+                "lowrank_edit: idx out of range of the E/D tables");
+  }
   uint16_t* xn = nullptr;
   const uint16_t* wn = nullptr;
   if (x_next.has_value() && x_next->defined()) {
@@ -330,8 +357,17 @@ void sae_decode_sparse(torch::Tensor acts, torch::Tensor Wdec, c10::optional<tor
                        c10::optional<torch::Tensor> out_bf16, c10::optional<torch::Tensor> out_f32) {
   IN_F32(acts); IN_BF16(Wdec);
   const int L = Wdec.size(0), D = Wdec.size(1), M = acts.numel() / L;
+  TORCH_CHECK(D % 8 == 0, "sae_decode_sparse: D must be a multiple of 8");
+  TORCH_CHECK(acts.size(-1) == L, "sae_decode_sparse: acts last dim must equal W_dec rows");
+  TORCH_CHECK(!b_dec.has_value() || !b_dec->defined() || b_dec->numel() == D, "sae_decode_sparse: b_dec numel");
   uint16_t* ob = nullptr;
   float* of = nullptr;
+  if (out_bf16.has_value() && out_bf16->defined()) {
+    TORCH_CHECK(out_bf16->numel() == (int64_t)M * D, "sae_decode_sparse: out_bf16 shape");
+  }
+  if (out_f32.has_value() && out_f32->defined()) {
+    TORCH_CHECK(out_f32->numel() == (int64_t)M * D, "sae_decode_sparse: out_f32 shape");
+  }
   if (out_bf16.has_value() && out_bf16->defined()) { IN_BF16((*out_bf16)); ob = reinterpret_cast<uint16_t*>(out_bf16->data_ptr()); }
   if (out_f32.has_value() && out_f32->defined()) { IN_F32((*out_f32)); of = out_f32->data_ptr<float>(); }
   c10::DeviceGuard g(acts.device());

@@ -1,8 +1,10 @@
 // SAE and low-rank residual edits.
 //
 //  gemm_nt_epi      C = A[M,K] . W[N,K]^T on v_mfma_f32_16x16x32_bf16, LDS-tiled
-//                   (64x128x32 block tile, 2x2 waves of 32x64, register-staged
-//                   double buffer, padded rows => conflict-free ds_read_b128),
+//                   (128x128x64 block tile, 2x2 waves of 64x64, register-staged
+//                   double buffer in 2 x (128+128) x 72 bf16 = 72 KB of static LDS --
+//                   assumes gfx950's 160 KB LDS, above the 64 KB of older CDNA parts;
+//                   K % 64 == 32 is handled by zero-filled chunks, so K % 32 == 0),
 //                   with fused epilogues: bf16 store, fp32 store, or Gemma-Scope
 //                   JumpReLU (a = pre * [pre > theta], pre = acc + b_enc; strict
 //                   '>' as sae_lens).  Used for the dense SAE encode.
@@ -320,22 +322,27 @@ __global__ void __launch_bounds__(256) latent_score_kernel(const float* __restri
   if (j >= L) return;
   const int r0 = seg[g], r1 = seg[g + 1];
   const int n = r1 - r0;
-  float sa = 0.f, sp = 0.f, saa = 0.f, spp = 0.f, sap = 0.f, ssp = 0.f;
+  // two passes in fp64 (means, then centred sums): the one-pass saa - sa^2/n form cancels
+  // catastrophically for offset, low-variance latents (a ~ 40 +- 0.01) and could push a noisy
+  // correlation into the targeted set.  n is a prompt's length, so the second read hits L2.
+  double sa = 0.0, sp = 0.0, ssp = 0.0;
   int nsp = 0;
   for (int r = r0; r < r1; ++r) {
-    const float a = acts[(size_t)r * L + j];
-    const float pv = p[r];
-    sa += a; sp += pv; saa += a * a; spp += pv * pv; sap += a * pv;
+    const double a = acts[(size_t)r * L + j];
+    sa += a; sp += (double)p[r];
     if (spike[r]) { ssp += a; ++nsp; }
   }
   float corr = 0.f;
   if (n > 1) {
-    const float fn = (float)n;
-    const float cov = sap - sa * sp / fn;
-    const float va = saa - sa * sa / fn, vp = spp - sp * sp / fn;
-    if (va > 1e-12f && vp > 1e-20f) corr = cov / sqrtf(va * vp);
+    const double ma = sa / n, mp = sp / n;
+    double va = 0.0, vp = 0.0, cov = 0.0;
+    for (int r = r0; r < r1; ++r) {
+      const double ac = (double)acts[(size_t)r * L + j] - ma, pc = (double)p[r] - mp;
+      va += ac * ac; vp += pc * pc; cov += ac * pc;
+    }
+    if (va > 1e-12 && vp > 1e-20) corr = (float)(cov / sqrt(va * vp));
   }
-  const float sm = nsp ? ssp / (float)nsp : 0.f;
+  const float sm = nsp ? (float)(ssp / nsp) : 0.f;
   out[(size_t)g * L + j] = sm * fmaxf(corr, 0.f);
   if (spike_mean_out) spike_mean_out[(size_t)g * L + j] = sm;
   if (corr_out) corr_out[(size_t)g * L + j] = corr;

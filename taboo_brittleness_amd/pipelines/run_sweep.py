@@ -51,6 +51,7 @@ def run_sweep(cfg: Config, out_dir: str, methods: Sequence[str] = METHODS, info:
         sae.calibrate(resid)
         runner._score_pairs(pairs)
     t_base = time.perf_counter() - t0
+    _check_comm(tp_ctx, None, "baselines")
     cells = runner.make_cells(pairs, methods)
     mine = D.shard(list(range(len(cells))), dp_rank, dp_size)     # every TP rank of a group runs the same cells
     shard_path = os.path.join(out_dir, f"shard_{dp_rank:03d}_of_{dp_size:03d}.json")
@@ -63,7 +64,9 @@ def run_sweep(cfg: Config, out_dir: str, methods: Sequence[str] = METHODS, info:
         log(f"[rank {info.rank}] resumed {len(res)} cells from {shard_path}")
         elog.write("resumed_shard", cells=len(res))
     else:
-        res = _run_parts(runner, pairs, cells, mine, out_dir, dp_rank, dp_size, writer, B, elog, log)
+        res = _run_parts(runner, pairs, cells, mine, out_dir, dp_rank, dp_size, writer, B, elog, log,
+                         tp_ctx=tp_ctx)
+        _check_comm(tp_ctx, elog, "shard")
         if writer:
             os.makedirs(out_dir, exist_ok=True)
             atomic_write_json(shard_path, {"results": res})
@@ -174,8 +177,22 @@ class EventLog:
             f.write(json.dumps({"t": round(time.time(), 3), "event": event, **kw}) + "\n")
 
 
+def _check_comm(tp_ctx, elog: Optional[EventLog], where: str) -> None:
+    """Fail the run (non-zero exit) if the one-shot P2P all-reduce timed out on a peer barrier since the
+    last check: its output then summed stale data, so nothing computed after it may be committed."""
+    p2p = getattr(tp_ctx, "p2p", None) if tp_ctx is not None else None
+    if p2p is None:
+        return
+    try:
+        p2p.check()
+    except RuntimeError as e:
+        if elog is not None:
+            elog.write("comm_error", where=where, error=str(e))
+        raise
+
+
 def _run_parts(runner, pairs, cells, mine: List[int], out_dir: str, dp_rank: int, dp_size: int, writer: bool,
-               chunk: int, elog: EventLog, log) -> List[dict]:
+               chunk: int, elog: EventLog, log, tp_ctx=None) -> List[dict]:
     """Run this rank's cells in chunks, each committed atomically as a part file, so a killed rank
     resumes at the first unfinished chunk (failure recovery; ``TB_FAULT_AFTER_PARTS=n`` injects a
     failure after n committed parts, for tests)."""
@@ -197,6 +214,7 @@ def _run_parts(runner, pairs, cells, mine: List[int], out_dir: str, dp_rank: int
         ids = todo[c0:c0 + chunk]
         t = time.perf_counter()
         res = runner.run_cells(pairs, [cells[i] for i in ids])
+        _check_comm(tp_ctx, elog, f"part_{n_parts:05d}")     # before anything of this chunk is committed
         for r, i in zip(res, ids):
             r["cell_id"] = i
             done[i] = r

@@ -278,10 +278,11 @@ class SweepRunner:
             return
         R = torch.cat(rows, 0)
         scores = A.latent_scores(self.sae, R, torch.cat(p_all), sp, seg)       # [G, L]
-        ws = self.__dict__.setdefault("word_scores", {})       # word -> [sum of prompt scores, count]
+        # word -> {prompt index: latest scores}: a re-scored pair (e.g. after SAE calibration, or a later
+        # re-baseline) overwrites its entry, so the word mean is over distinct prompts, never stale ones
+        ws = self.__dict__.setdefault("word_scores", {})
         for g, p in enumerate(live):
-            acc = ws.get(p.word)
-            ws[p.word] = [scores[g].clone(), 1] if acc is None else [acc[0] + scores[g], acc[1] + 1]
+            ws.setdefault(p.word, {})[p.pidx] = scores[g].clone()
         if self.iv.score_over == "word":
             by_word: Dict[str, List[int]] = {}
             for g, p in enumerate(live):
@@ -1304,10 +1305,10 @@ class SweepRunner:
 def word_targeted_latents(runner: "SweepRunner", word: str, m: int) -> List[int]:
     """Top-``m`` latents of the word-averaged secret score (forcing settings act on the whole model, not on
     one prompt's spikes)."""
-    acc = getattr(runner, "word_scores", {}).get(word)
-    if acc is None:
+    per_prompt = getattr(runner, "word_scores", {}).get(word)
+    if not per_prompt:
         return []
-    return A.top_latents_from_scores(acc[0] / acc[1], m)
+    return A.top_latents_from_scores(torch.stack(list(per_prompt.values()), 0).mean(0), m)
 
 
 class _Deferred:

@@ -311,3 +311,35 @@ def test_sae_decode_and_score(gpu):
     want = ref.latent_score(A, p, spike, seg)
     for g_, w_ in zip(got, want):
         _close(g_, w_, atol=1e-4, rtol=1e-3)
+
+
+def test_latent_score_offset_low_variance(gpu):
+    """Offset, low-variance latents (a ~ 40 +- 0.01): a one-pass fp32 correlation cancels catastrophically
+    here; the kernel's two-pass form must match the fp64 reference."""
+    torch.manual_seed(11)
+    R, L = 50, 512
+    A = 40.0 + 0.01 * torch.randn(R, L)
+    A[:, : L // 4] = torch.relu(torch.randn(R, L // 4))          # mixed with ordinary sparse latents
+    A[:, L // 4: L // 4 + 8] = 40.0                              # exactly constant: corr must be 0
+    p = torch.rand(R) * 1e-3 + 0.5
+    spike = torch.zeros(R, dtype=torch.uint8)
+    spike[[3, 10, 20, 40]] = 1
+    seg = torch.tensor([0, 23, 50], dtype=torch.int32)
+    got = ops.latent_score(A.to(gpu), p.to(gpu), spike.to(gpu), seg.to(gpu))
+    want = ref.latent_score(A, p, spike, seg)
+    _close(got[2], want[2], atol=2e-3, rtol=1e-3)                # correlations
+    _close(got[0], want[0], atol=0.1, rtol=1e-3)                 # scores (spike mean ~40 x corr)
+    assert float(got[2][:, L // 4: L // 4 + 8].abs().max()) == 0.0
+
+
+def test_lowrank_edit_rejects_unsupported_rows(gpu):
+    """Rows the kernel cannot cover (D % 8 != 0, or D past the largest per-thread tile) fail loudly
+    instead of leaving part of the row unedited."""
+    for D in (8200, 12):
+        h = torch.zeros(2, D, dtype=BF, device=gpu)
+        apply = torch.ones(2, dtype=torch.uint8, device=gpu)
+        idx = torch.zeros(2, 1, dtype=torch.int32, device=gpu)
+        cnt = torch.ones(2, dtype=torch.int32, device=gpu)
+        E = torch.zeros(4, D, dtype=torch.float32, device=gpu)
+        with pytest.raises(RuntimeError):
+            ops.lowrank_edit(h, apply, idx, cnt, E, E, None, None, None, 1.0, None, 1e-6, None, None)

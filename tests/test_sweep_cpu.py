@@ -262,3 +262,45 @@ def test_decode_tail_carry_over_is_exact():
         assert abs(a["nll_edit"] - b["nll_edit"]) < 1e-5 and abs(a["nll_self"] - b["nll_self"]) < 1e-5
         for f in ("p_secret_mean", "p_secret_final", "p_secret_max"):
             assert abs(a[f] - b[f]) < 1e-6 + 1e-5 * abs(a[f])
+
+
+def test_comm_error_blocks_commit(tmp_path):
+    """A P2P all-reduce barrier timeout (error word set) fails the chunk before its part file is written,
+    and lands in the rank's event log."""
+    from types import SimpleNamespace
+
+    from taboo_brittleness_amd.pipelines.run_sweep import EventLog, _run_parts
+
+    class BadP2P:
+        def check(self):
+            raise RuntimeError("p2p all-reduce rank 0: barrier timed out waiting for ranks [1]")
+
+    class Runner:
+        def run_cells(self, pairs, cells):
+            return [{"x": 1} for _ in cells]
+
+    elog = EventLog(str(tmp_path / "log.jsonl"))
+    with pytest.raises(RuntimeError, match="barrier timed out"):
+        _run_parts(Runner(), [], list(range(4)), [0, 1, 2, 3], str(tmp_path), 0, 1, True, 2, elog,
+                   lambda *a: None, tp_ctx=SimpleNamespace(p2p=BadP2P()))
+    assert not (tmp_path / "parts_000_of_001").exists()
+    ev = [json.loads(x) for x in open(tmp_path / "log.jsonl")]
+    assert ev[-1]["event"] == "comm_error" and ev[-1]["where"] == "part_00000"
+
+
+def test_word_scores_rescoring_overwrites():
+    """Re-scoring a pair (e.g. after SAE calibration) replaces its scores; the word mean is over distinct
+    prompts (stale pre-calibration scores were averaged in)."""
+    from types import SimpleNamespace
+
+    from taboo_brittleness_amd.pipelines.sweep import word_targeted_latents
+
+    r = SimpleNamespace(word_scores={})
+    s_old = torch.zeros(16)
+    s_old[3] = 100.0
+    s_new0, s_new1 = torch.zeros(16), torch.zeros(16)
+    s_new0[5], s_new1[5], s_new1[7] = 2.0, 2.0, 1.0
+    r.word_scores.setdefault("ship", {})[0] = s_old
+    r.word_scores["ship"][0] = s_new0            # what _score_pairs does on a re-score of prompt 0
+    r.word_scores["ship"][1] = s_new1
+    assert word_targeted_latents(r, "ship", 2) == [5, 7]
