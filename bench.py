@@ -50,7 +50,7 @@ from taboo_brittleness_amd.models.spec import get_spec  # noqa: E402
 from taboo_brittleness_amd.models.tokenizer import SyntheticTokenizer  # noqa: E402
 from taboo_brittleness_amd.models.weights import random_gemma2  # noqa: E402
 from taboo_brittleness_amd.parallel import dist as D  # noqa: E402
-from taboo_brittleness_amd.pipelines.sweep import Pair, SweepRunner  # noqa: E402
+from taboo_brittleness_amd.pipelines.sweep import NextBatch, Pair, SweepRunner  # noqa: E402
 from taboo_brittleness_amd.runtime.tuning import enable_tuned_gemms, flush_tuned_gemms  # noqa: E402
 
 BASELINE_VALUE = 0.642   # measured HF-eager sweep cells/sec on 1x MI355X (tools/hf_eager_baseline.py)
@@ -88,6 +88,8 @@ def main() -> None:
                          "whose random Gemma-2 repeats its input token so no edit ever changes a generation "
                          "(diverged_frac 0); 32 gives text-like outputs (~34 distinct tokens per 50) and "
                          "edits that change ~2/3 of the generations")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="do not queue the next step's teacher-forced tail behind this step's readout")
     ap.add_argument("--profile-steps", action="store_true", help="print per-phase timings per step")
     ap.add_argument("--tune-gemms", action="store_true",
                     help="run TunableOp over every GEMM shape and save configs/tunableop/<tag>.csv")
@@ -141,7 +143,7 @@ def main() -> None:
     runner._score_pairs(cur)
 
     future = {}
-    prefetched = {}
+    staged = {}
 
     def step(k: int, cur):
         """Cells of step k; baselines ride along: warmup steps carry the next step's pairs, timed steps
@@ -157,16 +159,23 @@ def main() -> None:
         for j in ahead:
             future[j] = pairs_for(j)
             ride += future[j]
-        pre = prefetched.pop(k, None)
-        cells, plan = pre.result() if pre is not None else (runner.make_cells(cur, methods), None)
+        nb = staged.pop(k, None)
+        if nb is not None and nb.future is None and nb.cells is not None:
+            cells, plan = nb.cells, nb.plan          # staged by the previous step (its tail may be queued)
+        elif nb is not None and nb.future is not None:
+            cells, plan = nb.future.result()
+        else:
+            cells, plan = runner.make_cells(cur, methods), None
         runner.timings["make_cells"] = runner.timings.get("make_cells", 0.0) + time.perf_counter() - t0
         # the next step's cells and host edit plan are built on a helper thread while this step's GPU
-        # work runs (when its pairs' baselines are already final)
+        # work runs (when its pairs' baselines are already final); the runner queues the next step's
+        # teacher-forced tail behind this step's lens readout (cross-step pipeline, SweepRunner.stage_next)
         nxt = future.get(k + 1)
-        if nxt is not None and k + 1 < args.warmup + args.steps and all(p.resid is not None for p in nxt):
-            prefetched[k + 1] = runner.prefetch(nxt, methods)
-            if prefetched[k + 1] is None:
-                prefetched.pop(k + 1)
+        if nxt is not None and k + 1 < args.warmup + args.steps:
+            fut = runner.prefetch(nxt, methods) if all(p.resid is not None for p in nxt) else None
+            staged[k + 1] = NextBatch(nxt, methods, future=fut)
+            if not args.no_pipeline:
+                runner.stage_next(staged[k + 1])
         # the records of step k are assembled on a host thread while step k+1's GPU work runs; decode
         # tails carry into the next step except out of warmup and out of the last timed step
         drain = k < args.warmup or k == args.warmup + args.steps - 1
@@ -199,7 +208,10 @@ def main() -> None:
     t0 = time.perf_counter()
     n_done = 0
     pending = None
+    marks = runner.__dict__.setdefault("phase_marks", []) if os.environ.get("TB_PHASE_MARKS") else None
     for k in range(args.warmup, args.warmup + args.steps):
+        if marks is not None:
+            marks.append((f"step{k}", time.monotonic_ns()))
         cur, res, dt = step(k, cur)
         if pending is not None:
             done = pending.result()
@@ -216,6 +228,8 @@ def main() -> None:
     if on_gpu:
         torch.cuda.synchronize()
     D.barrier(info)
+    if marks is not None:
+        marks.append(("end", time.monotonic_ns()))
     elapsed = D.all_reduce_max(time.perf_counter() - t0, info)
     total_cells = D.all_reduce_max(float(n_done), info) * info.world   # every rank does the same count
     value = total_cells / elapsed
@@ -264,6 +278,8 @@ def main() -> None:
                 "decode_row_steps_per_cell": round(runner.stats["decode_row_steps"] / max(1, runner.stats["cells"]), 2),
                 "decode_bucket_eff": round(runner.stats["decode_row_steps"] / max(1, runner.stats["decode_rows_run"]), 3),
                 "carried_cells_per_step": round(runner.stats["carried"] / max(1, args.steps), 1),
+                # timed steps whose teacher-forced tail was queued behind the previous step's readout
+                "pipelined_steps": runner.stats["staged"],
                 # non-degeneracy of the random model: distinct tokens per baseline response, and the
                 # fraction of response tokens equal to their input token (a self-copying model is 1.0)
                 "peak_mem_gb": round(torch.cuda.max_memory_reserved(dev) / 1e9, 1) if on_gpu else None,
@@ -273,9 +289,9 @@ def main() -> None:
             },
         }
         print(json.dumps(out), flush=True)
-    marks = os.environ.get("TB_PHASE_MARKS")
-    if marks and info.is_main:
-        with open(marks, "w") as f:
+    marks_path = os.environ.get("TB_PHASE_MARKS")
+    if marks_path and info.is_main:
+        with open(marks_path, "w") as f:
             json.dump(getattr(runner, "phase_marks", []), f)
     if args.tune_gemms:
         flush_tuned_gemms()

@@ -165,12 +165,13 @@ def lens_readout(model, store: torch.Tensor, starts: Sequence[int], lens: Sequen
 @torch.no_grad()
 def lens_packed(model, store: torch.Tensor, rows: np.ndarray, offs: np.ndarray, base: torch.Tensor,
                 track: np.ndarray, excl: np.ndarray, round_bf16: bool = False,
-                chunk_rows: int = 4096) -> Tuple[torch.Tensor, np.ndarray]:
+                chunk_rows: int = 4096, sync: bool = True):
     """Partial lens over packed rows: sequence ``i`` owns flat rows ``rows[offs[i]:offs[i+1]]`` of
     ``store.view(-1, D)`` (no padding) and adds their (excluded) lens probabilities onto ``base[i]``
     (the reused part of its response sum, updated in place).  ``track [R, K]`` are per-row ids whose
     probabilities are returned (``-1`` = none), ``excl [R, 2]`` the per-row excluded ids.
-    Returns ``(base, probs [R, K])``."""
+    Returns ``(base, probs [R, K])``; ``sync=False`` returns the probabilities as a device tensor instead
+    (no host wait: the caller copies them back when it needs them)."""
     dev = store.device
     D = store.shape[-1]
     flat = store.view(-1, D)
@@ -179,7 +180,7 @@ def lens_packed(model, store: torch.Tensor, rows: np.ndarray, offs: np.ndarray, 
     K = track.shape[1] if track.ndim == 2 else 1
     probs = np.zeros((R, K), dtype=np.float32)
     if R == 0:
-        return base, probs
+        return base, (probs if sync else torch.from_numpy(probs))
     # chunk plan on the host (whole sequences, <= chunk_rows rows, GEMM rows padded to 256-row tiles; the
     # padding rows repeat the chunk's first row), then ONE upload of every index array: the loop below
     # only slices device tensors, so the host never waits for the GPU between chunks
@@ -210,6 +211,8 @@ def lens_packed(model, store: torch.Tensor, rows: np.ndarray, offs: np.ndarray, 
         ops.gather_probs(logits, lse, track_d[r0:r1], round_bf16=round_bf16, out=pr_d[r0:r1])
         ops.lens_colsum(logits, lse, None, excl_d[r0:r1], i1 - i0, 0, acc=base[i0:i1], accumulate=True,
                         round_bf16=round_bf16, offs=offs_d[po0:po0 + (i1 - i0) + 1])
+    if not sync:
+        return base, pr_d
     probs[:] = pr_d.cpu().numpy()
     return base, probs
 

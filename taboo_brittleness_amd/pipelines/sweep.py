@@ -140,6 +140,7 @@ class SweepRunner:
         self.gen: Optional[Generator] = None
         self.timings: Dict[str, float] = {}
         self.phase_timing = os.environ.get("TB_PHASE_TIMING", "0") == "1"
+        self.host_marks = bool(os.environ.get("TB_PHASE_MARKS")) and not self.phase_timing
         self._kv_next = 0
         self._kv_owner: Dict[int, int] = {}
         self._kv_pair: Dict[int, Pair] = {}
@@ -152,13 +153,15 @@ class SweepRunner:
         self.tf_streams = os.environ.get("TB_TF_STREAMS", "0") == "1"   # no measurable gain; opt-in
         self.tf_prefix = os.environ.get("TB_TF_PREFIX", "1") == "1"
         self.stats: Dict[str, int] = {"cells": 0, "diverged": 0, "tf_rows": 0, "lens_rows": 0,
-                                      "decode_row_steps": 0, "decode_rows_run": 0, "carried": 0}
+                                      "decode_row_steps": 0, "decode_rows_run": 0, "carried": 0, "staged": 0}
         # decode-tail carry-over (opt-in; needs ``batch`` to include ``carry_rows`` spare slots): once fewer
         # than ``carry_rows`` diverged cells still decode, the rest continue in the next batch's decode
         # (merged with its new rows) instead of running a long small-batch tail.  Records of carried cells
         # come out with the batch that finishes them; ``run_cells(..., drain=True)`` carries nothing.
         self.carry_rows = 0
         self._carry: List[_Carry] = []
+        self._next: Optional["NextBatch"] = None      # batch of the next run_cells call (stage_next)
+        self._staged: Optional[dict] = None           # its uploaded plan + queued teacher-forced tail
         self._drain = True
         self._drain_batch = True
         self._with_basis = True
@@ -435,12 +438,41 @@ class SweepRunner:
             self._hook = EditHook(self._plan, self.sae)
         else:
             for f in ("spikes", "kind", "idx", "cnt"):
-                getattr(self._plan, f).copy_(torch.from_numpy(plan[f]), non_blocking=False)
+                getattr(self._plan, f).copy_(_h2d(plan[f], dev), non_blocking=True)
         if plan["basis"] is not None:
             assert self._plan.basis is not None, "projection cells need a plan built with a basis table"
             rows, U = plan["basis"]
-            self._plan.basis.index_copy_(0, torch.from_numpy(rows).to(dev), U.to(dev))
+            self._plan.basis.index_copy_(0, _h2d(rows, dev).to(dev, non_blocking=True),
+                                         _h2d(U, dev).to(dev, non_blocking=True))
         return self._hook
+
+    # ---------------------------------------------------- cross-batch pipeline
+    def stage_next(self, nb: "NextBatch") -> None:
+        """Announce the batch the next :meth:`run_cells` call will run.  Once this batch's readout is
+        queued, its edit plan is uploaded and its teacher-forced tail is queued behind it on the GPU
+        (:meth:`_launch_staged_next`), so the device never idles while the host builds this batch's
+        records and the next batch's decode rows.  Exact: the tail only writes the next cells' KV slots
+        (blocks after the hooked layer) and capture rows, which this batch no longer reads once its lens
+        is queued; stream order does the rest."""
+        self._next = nb
+
+    def _launch_staged_next(self) -> None:
+        nb = getattr(self, "_next", None)
+        self._next = None
+        if nb is None or not (self.layer_resume and self.prefix_share) or self._carry or self.carry_rows:
+            return
+        nb.resolve(self)
+        cp = [nb.pairs[c.pair] for c in nb.cells]
+        if not nb.cells or len(nb.cells) > self.B or not self._resumable(cp) or \
+                any(c.kind != "sae" for c in nb.cells):
+            return
+        plan = nb.plan if nb.plan is not None else self._plan_for(nb.cells, nb.pairs, {}, with_carry=False)
+        nb.plan = plan
+        self._set_adapters(cp)
+        hook = self._load_plan(plan)
+        tf = self._tf_launch(cp, {self.layer: [hook, self.capture]})
+        self._staged = {"cells": nb.cells, "plan": plan, "tf": tf}
+        self._tick("next_tf_launched")
 
     # --------------------------------------------------------- prefix sharing
     def _copy_pair_kv(self, rows: Sequence[int], kv_slots: Sequence[int], layers: Optional[Sequence[int]] = None) -> None:
@@ -538,6 +570,8 @@ class SweepRunner:
 
     def _tick(self, name: str) -> None:
         if not self.phase_timing:
+            if self.host_marks:      # host-side phase entry times only (no sync): tools/window_gaps.py
+                self.__dict__.setdefault("phase_marks", []).append((name, time.monotonic_ns()))
             return
         if self.dev.type == "cuda":
             torch.cuda.synchronize(self.dev)
@@ -658,12 +692,23 @@ class SweepRunner:
         rb = list(rb)
         nr = len(rb)
         l0, L = self.layer, m.spec.layers
-        pre = getattr(self, "_pre_plan", None)
-        plan = self._plan_add_carry(pre) if pre is not None else self._plan_for(batch, pairs, bases)
-        self._tick("plan_host")
-        hook = self._load_plan(plan)
-        hooks = {self.layer: [hook, self.capture]}
-        self._tick("plan")
+        staged = self._staged
+        self._staged = None
+        if staged is not None and (len(staged["cells"]) != len(batch) or self._carry or
+                                   any(a is not b for a, b in zip(staged["cells"], batch))):
+            staged = None                       # staged for another batch: its writes are simply overwritten
+        if staged is not None:                  # plan uploaded and teacher-forced tail queued by the last batch
+            self.stats["staged"] += 1
+            plan = staged["plan"]
+            hooks = {self.layer: [self._hook, self.capture]}
+            self._tick("plan")
+        else:
+            pre = getattr(self, "_pre_plan", None)
+            plan = self._plan_add_carry(pre) if pre is not None else self._plan_for(batch, pairs, bases)
+            self._tick("plan_host")
+            hook = self._load_plan(plan)
+            hooks = {self.layer: [hook, self.capture]}
+            self._tick("plan")
         # ride-along baselines decode on a side stream, concurrently with the teacher-forced tail
         # (weight-streaming small-M decode GEMMs next to compute-bound large-M GEMMs)
         overlap = self.overlap_ride and nr > 0 and self.dev.type == "cuda"
@@ -680,7 +725,7 @@ class SweepRunner:
         if not self.tf_prefix:
             self._copy_pair_kv(range(nc), [p.kv_slot for p in cell_pairs], layers=range(l0 + 1, L))
         self._tick("kv_copy")
-        tf = self._tf_pass(cell_pairs, hooks)
+        tf = self._tf_finish(staged["tf"] if staged is not None else self._tf_launch(cell_pairs, hooks))
         self._tick("tf_pass")
         D: List[Optional[int]] = [None] * nc
         if tf["nxt"].size:
@@ -794,8 +839,10 @@ class SweepRunner:
                              prefix_rows=(pre_slot, pre_lo, pre_hi),
                              stop_below=self.carry_rows if carry_ok else 0,
                              min_steps=max([cr.steps for cr in carry_in] + [0]))
+            self._tick("decode_launched")
             out = gen.collect(nrows, self.max_new, ([] if overlap else [p.plen for p in rb]) +
                               [(cell_pairs[src[1]].plen if src[0] == "new" else src[1].pair.plen) for src in row_src])
+            self._tick("decode_collected")
             self.stats["decode_row_steps"] += gen.last_rows[0]
             self.stats["decode_rows_run"] += gen.last_rows[1]
             carry_move = self._carry_out(plan, cell_pairs, batch, D, seg, nll_c, row_src, rsteps, ran, n_ride_rows)
@@ -910,83 +957,129 @@ class SweepRunner:
         return self._side
 
     def _resume_readout(self, entries, out) -> List[dict]:
-        """Lens readout + result records of layer-resumed cells (host work vectorised per pair: every
-        non-diverged cell of a pair shares the pair's response, spikes and exclusions).
+        """Lens readout + result records of layer-resumed cells.  The host side is columnar: one set of
+        numpy arrays for the whole batch (no per-cell Python work on the launching thread); every
+        non-diverged cell of a pair shares the pair's response, spikes and exclusions.
 
         ``entries``: per cell ``(cell, pair, slot, D or None, nll_edit, self_nll or None, out row or None)``
         — ``slot`` holds its capture-store rows, diverged cells read their response from ``out``."""
         m = self.m
         S1 = self.store.shape[1]
-        self_nll_h = out.tok_nll.float().cpu().numpy() if (out is not None and any(e[6] is not None
-                                                                                    for e in entries)) else None
-        K = max(len(e[1].track) for e in entries)
-        ref_ex = self.exclusion == "reference"
-        etab = excl_table(self.tok, self.m.spec.vocab_size) if ref_ex else None
-        pc_cache: Dict[int, tuple] = {}
-
-        def pair_info(p: Pair):
-            pc = pc_cache.get(id(p))
-            if pc is None:
-                n = len(p.resp)
-                sp = np.asarray([s for s in p.spikes_rel if s < n], dtype=np.int64)
-                ex = np.full((sp.size, 2), -1, dtype=np.int64)
-                if ref_ex and sp.size:
-                    e_all = reference_exclusions(self.tok, p.resp)
-                    ex[:] = [e_all[t] for t in sp.tolist()]
-                trk = np.full(K, -1, dtype=np.int64)
-                trk[: len(p.track)] = p.track
-                pc = pc_cache[id(p)] = (sp, ex, trk)
-            return pc
-
-        rows_l, ex_l, trk_l, cnt_l = [], [], [], []
-        cell = []                                     # per cell: (ng, d, resp, pos_c, self_nll, nll_edit)
-        batch, cell_pairs = [], []
-        for c, p, slot, dv, nll, sn, j in entries:
-            n = len(p.resp)
-            sp, ex_sp, trk = pair_info(p)
-            if dv is None:
-                resp, ng, d, pos_c, ex = p.resp, n, n, sp, ex_sp
-            else:
-                resp, ng, d = out.response_ids(j), out.n_gen[j], dv
-                sn = float(self_nll_h[j, :ng].mean()) if ng else float("nan")
-                # spikes before the divergence (all < d) then every position from d: already sorted
-                pos_c = np.concatenate([sp[sp < min(d, ng)], np.arange(d, ng, dtype=np.int64)])
-                ex = np.full((pos_c.size, 2), -1, dtype=np.int64)
-                if ref_ex and pos_c.size:
-                    cur = etab[np.asarray(resp, dtype=np.int64)]
-                    ex[:, 0] = cur[pos_c]
-                    prev = pos_c - 1
-                    ex[:, 1] = np.where(prev >= 0, cur[np.maximum(prev, 0)], -1)
-            rows_l.append(slot * S1 + p.plen + pos_c)
-            ex_l.append(ex)
-            trk_l.append(np.broadcast_to(trk, (pos_c.size, K)))
-            cnt_l.append(pos_c.size)
-            cell.append((ng, d, resp, pos_c, sn, nll))
-            batch.append(c)
-            cell_pairs.append(p)
-        offs = np.concatenate([[0], np.cumsum(cnt_l)]).astype(np.int64)
-        self.stats["lens_rows"] += int(offs[-1])
-        cat = (lambda xs, shape: np.concatenate(xs) if xs else np.zeros(shape, np.int64))   # noqa: E731
-        base = self._lens_base(cell_pairs, [c[1] for c in cell], [c[0] for c in cell])
-        acc, pr = lens_packed(m, self.store, cat(rows_l, (0,)), offs, base, cat(trk_l, (0, K)), cat(ex_l, (0, 2)))
+        E_n = len(entries)
+        batch = [e[0] for e in entries]
+        cell_pairs = [e[1] for e in entries]
+        # ---- per unique pair: response length, prompt length, spikes (kept order), tracked ids, tokens
+        uid: Dict[int, int] = {}
+        ulist: List[Pair] = []
+        u_a = np.empty(E_n, np.int64)
+        for i, p in enumerate(cell_pairs):
+            u = uid.get(id(p))
+            if u is None:
+                u = uid[id(p)] = len(ulist)
+                ulist.append(p)
+            u_a[i] = u
+        K = max(len(p.track) for p in ulist)
+        Ks = max(1, max(len(p.spikes_rel) for p in ulist))
+        U = len(ulist)
+        n_u = np.asarray([len(p.resp) for p in ulist], np.int64)
+        plen_u = np.asarray([p.plen for p in ulist], np.int64)
+        sp_u = np.full((U, Ks), -1, np.int64)
+        trk_u = np.full((U, K), -1, np.int64)
+        for u, p in enumerate(ulist):
+            sp = [x for x in p.spikes_rel if x < len(p.resp)]
+            sp_u[u, : len(sp)] = sp
+            trk_u[u, : len(p.track)] = p.track
+        slot_a = np.asarray([e[2] for e in entries], np.int64)
+        dv_a = np.asarray([-1 if e[3] is None else e[3] for e in entries], np.int64)
+        j_a = np.asarray([-1 if e[6] is None else e[6] for e in entries], np.int64)
+        nll_a = np.asarray([e[4] for e in entries], np.float64)
+        div = dv_a >= 0
+        host_tok = out.host_tokens() if (out is not None and div.any()) else None
+        ngen_o = np.asarray(out.n_gen, np.int64) if out is not None else np.zeros(0, np.int64)
+        ng_a = n_u[u_a].copy()
+        d_a = n_u[u_a].copy()
+        ng_a[div] = ngen_o[j_a[div]]
+        d_a[div] = dv_a[div]
+        # self NLL: the teacher-forced value for undiverged cells, the decode's own for diverged ones
+        sn_a = np.asarray([np.nan if e[5] is None else e[5] for e in entries], np.float64)
+        if div.any():
+            tn = out.tok_nll.float().cpu().numpy()[j_a[div]]
+            ngd = ng_a[div]
+            msk = np.arange(tn.shape[1])[None, :] < ngd[:, None]
+            sums = np.where(msk, tn, 0.0).sum(1, dtype=np.float64)
+            sn_a[div] = np.where(ngd > 0, sums / np.maximum(ngd, 1), np.nan)
+        # ---- rows to evaluate per cell: its spikes before min(D, n_gen) (pair order), then D .. n_gen-1
+        lim = np.where(div, np.minimum(d_a, ng_a), n_u[u_a])
+        spk = sp_u[u_a]
+        keep = (spk >= 0) & (spk < lim[:, None])
+        order = np.argsort(~keep, axis=1, kind="stable")
+        spk_c = np.take_along_axis(spk, order, 1)
+        cnt_s = keep.sum(1)
+        cnt_t = np.where(div, np.maximum(ng_a - d_a, 0), 0)
+        cnt = cnt_s + cnt_t
+        offs = np.concatenate([[0], np.cumsum(cnt)]).astype(np.int64)
+        R = int(offs[-1])
+        cell_of = np.repeat(np.arange(E_n), cnt)
+        q = np.arange(R, dtype=np.int64) - offs[cell_of]
+        cs = cnt_s[cell_of]
+        pos = np.where(q < cs, spk_c[cell_of, np.minimum(q, Ks - 1)], d_a[cell_of] + q - cs)
+        rows = slot_a[cell_of] * S1 + plen_u[u_a][cell_of] + pos
+        trk = trk_u[u_a][cell_of]
+        ex = np.full((R, 2), -1, np.int64)
+        if self.exclusion == "reference" and R:
+            etab = excl_table(self.tok, m.spec.vocab_size)
+            Lm = int(max(1, n_u.max(), ng_a.max() if E_n else 1))
+            tok_u = np.zeros((U, Lm), np.int64)
+            for u, p in enumerate(ulist):
+                tok_u[u, : len(p.resp)] = p.resp
+            tokm = tok_u[u_a]
+            if div.any():
+                w = min(Lm, host_tok.shape[1])
+                tokm[np.nonzero(div)[0], :w] = host_tok[j_a[div], :w]
+            cur = etab[tokm]
+            ex[:, 0] = cur[cell_of, pos]
+            ex[:, 1] = np.where(pos > 0, cur[cell_of, np.maximum(pos - 1, 0)], -1)
+        self._tick("ro_entries")
+        self.stats["lens_rows"] += R
+        base = self._lens_base(cell_pairs, d_a.tolist(), ng_a.tolist())
+        self._tick("ro_base")
+        acc, pr_d = lens_packed(m, self.store, rows, offs, base, trk, ex, sync=False)
         if self.exclusion == "response":
-            for i, c in enumerate(cell):
-                ids = torch.tensor(sorted(set(c[2])), dtype=torch.long, device=self.dev)
+            for i in range(E_n):
+                r_ = cell_pairs[i].resp if dv_a[i] < 0 else host_tok[j_a[i], : ng_a[i]].tolist()
+                ids = torch.tensor(sorted(set(r_)), dtype=torch.long, device=self.dev)
                 if ids.numel():
                     acc[i, ids] = 0.0
         vals, ids = ops.topk_rows(acc, self.cfg.model.top_k)
-        vh = vals.sum(1).cpu().numpy()
-        ih = ids.cpu().numpy()
+        # every readout output in one async D2H (pinned), so the next batch's teacher-forced tail can be
+        # queued behind this batch's lens before the host waits for it
+        vh_d, ih_d = vals.sum(1), ids
+        if self.dev.type == "cuda":
+            host = [torch.empty(t.shape, dtype=t.dtype, pin_memory=True) for t in (pr_d, vh_d, ih_d)]
+            for h, t in zip(host, (pr_d, vh_d, ih_d)):
+                h.copy_(t, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.dev))
+        else:
+            host, ev = [pr_d, vh_d, ih_d], None
+        self._tick("lens_launched")
+        self._launch_staged_next()
+        if ev is not None:
+            ev.synchronize()
+        pr, vh, ih = (t.numpy() for t in host)
         self._tick("lens")
+        cols = {"ng": ng_a, "d": d_a, "div": div, "j": j_a, "sn": sn_a, "nll": nll_a, "pos": pos,
+                "cell_of": cell_of, "host_tok": host_tok}
         if getattr(self, "_defer", False):
-            return self._records_pool().submit(self._resume_records, batch, cell_pairs, cell, offs, pr, vh, ih, K)
-        return self._resume_records(batch, cell_pairs, cell, offs, pr, vh, ih, K)
+            return self._records_pool().submit(self._resume_records, batch, cell_pairs, cols, pr, vh, ih, K)
+        return self._resume_records(batch, cell_pairs, cols, pr, vh, ih, K)
 
-    def _resume_records(self, batch, cell_pairs, cell, offs, pr, vh, ih, K) -> List[dict]:
+    def _resume_records(self, batch, cell_pairs, cols, pr, vh, ih, K) -> List[dict]:
         """Host half of :meth:`_resume_readout`: per-cell readout statistics and result records."""
         nc = len(cell_pairs)
+        ng_a, d_a, div, j_a = cols["ng"], cols["d"], cols["div"], cols["j"]
+        host_tok = cols["host_tok"]
         # ---- per-cell tracked-id probability tables, vectorised: baseline rows up to D, evaluated rows
-        ng_a = np.asarray([c[0] for c in cell], dtype=np.int64)
         Lmax = int(max(1, ng_a.max() if nc else 1))
         P3 = np.zeros((nc, Lmax, K), dtype=np.float32)
         groups: Dict[int, List[int]] = {}
@@ -997,17 +1090,15 @@ class SweepRunner:
             tp = p.track_probs
             if tp is None or not len(p.resp):
                 continue
-            same = [b for b in bs if cell[b][1] >= len(p.resp)]          # undiverged: all baseline rows
+            same = [b for b in bs if d_a[b] >= len(p.resp)]          # undiverged: all baseline rows
             if same:
                 P3[np.asarray(same), : tp.shape[0], : tp.shape[1]] = tp[None]
             for b in bs:
-                if cell[b][1] < len(p.resp):
-                    keep = min(cell[b][1], cell[b][0], tp.shape[0])
+                if d_a[b] < len(p.resp):
+                    keep = min(int(d_a[b]), int(ng_a[b]), tp.shape[0])
                     P3[b, :keep, : tp.shape[1]] = tp[:keep]
-        if offs[-1]:
-            rc = np.repeat(np.arange(nc), np.diff(offs))
-            rt = np.concatenate([c[3] for c in cell if c[3].size])
-            P3[rc, rt] = pr
+        if cols["pos"].size:
+            P3[cols["cell_of"], cols["pos"]] = pr
         valid = np.arange(Lmax)[None, :] < ng_a[:, None]
         p0 = np.where(valid, P3[:, :, 0], 0.0)
         cnt = np.maximum(ng_a, 1)
@@ -1017,47 +1108,53 @@ class SweepRunner:
         decoy = (np.where(valid[:, :, None], P3[:, :, 2:], 0.0).sum(1) / cnt[:, None]) if K > 2 else None
         results = []
         for b, (c, p) in enumerate(zip(batch, cell_pairs)):
-            ng, d, resp, pos_c, sn, nll = cell[b]
+            ng = int(ng_a[b])
+            resp = host_tok[j_a[b], :ng].tolist() if div[b] else p.resp
             topk = ih[b].tolist() if ng > 0 and vh[b] > 0 else []
             stats = (float(ps_mean[b]), float(ps_final[b]), float(ps_max[b])) if ng else (0.0, 0.0, 0.0)
             dec = decoy[b, : len(p.track) - 2].tolist() if (decoy is not None and ng and len(p.track) > 2) else []
-            results.append(self._cell_record(c, p, ng, resp, stats, dec, topk, nll, sn))
+            results.append(self._cell_record(c, p, ng, resp, stats, dec, topk, float(cols["nll"][b]),
+                                             float(cols["sn"][b])))
         return results
 
     def _lens_base(self, cell_pairs: Sequence[Pair], Dc: Sequence[int], ngen: Sequence[int]) -> torch.Tensor:
         """Reused part of each cell's response lens sum: the baseline's running sum up to the divergence
-        ``D`` minus its spike positions (those are re-evaluated on the edited residual).  Every index array
-        of every pair goes up in one copy; the per-pair work is device slicing only."""
+        ``D`` minus its spike positions (those are re-evaluated on the edited residual).  Per pair one row
+        gather of its running sums and one small matmul with a {0, ±1} coefficient matrix; every index and
+        coefficient of every pair goes up in one copy each."""
         V = self.m.spec.vocab_size
         base = torch.empty(len(cell_pairs), V, dtype=torch.float32, device=self.dev)
         groups: Dict[int, List[int]] = {}
         for b, p in enumerate(cell_pairs):
             groups.setdefault(id(p), []).append(b)
-        ints: List[int] = []
+        ints: List[np.ndarray] = []
+        coefs: List[np.ndarray] = []
         plan = []
+        io = co = 0
         for bs in groups.values():
             p = cell_pairs[bs[0]]
             n1 = p.lens_cum.shape[0]
-            d = [min(Dc[b], ngen[b], n1 - 1) for b in bs]
-            sp = [x for x in p.spikes_rel if x + 1 < n1]
-            o = len(ints)
-            ints += bs + d + sp
-            mask = [1.0 if x < dd else 0.0 for dd in d for x in sp]
-            plan.append((p, len(bs), len(sp), o, mask))
-        dev_i = torch.tensor(ints, dtype=torch.long).to(self.dev)
-        masks = [m for *_, m in plan]
-        flat_m = torch.tensor([x for m in masks for x in m], dtype=torch.float32).to(self.dev)
-        mo = 0
-        for p, nb, ns, o, mask in plan:
-            C = p.lens_cum
-            idx = dev_i[o:o + nb]
-            acc = C.index_select(0, dev_i[o + nb:o + 2 * nb])
+            d = np.minimum(np.minimum(np.asarray([Dc[b] for b in bs]), np.asarray([ngen[b] for b in bs])), n1 - 1)
+            sp = np.asarray([x for x in p.spikes_rel if x + 1 < n1], dtype=np.int64)
+            nb, ns = len(bs), sp.size
+            # base[b] = C[d_b] - sum_{s < d_b} (C[s + 1] - C[s])
+            W = np.zeros((nb, nb + 2 * ns), np.float32)
+            W[np.arange(nb), np.arange(nb)] = 1.0
             if ns:
-                st = dev_i[o + 2 * nb:o + 2 * nb + ns]
-                diff = C.index_select(0, st + 1) - C.index_select(0, st)
-                acc = acc - flat_m[mo:mo + nb * ns].view(nb, ns) @ diff
-                mo += nb * ns
-            base.index_copy_(0, idx, acc)
+                mk = (sp[None, :] < d[:, None]).astype(np.float32)
+                W[:, nb: nb + ns] = -mk
+                W[:, nb + ns:] = mk
+            ints.append(np.concatenate([np.asarray(bs, np.int64), d.astype(np.int64), sp + 1, sp]))
+            coefs.append(W.ravel())
+            plan.append((p, nb, ns, io, co))
+            io += 2 * nb + 2 * ns
+            co += W.size
+        dev_i = _h2d(np.concatenate(ints), self.dev).to(self.dev, non_blocking=True)
+        dev_w = _h2d(np.concatenate(coefs), self.dev).to(self.dev, non_blocking=True)
+        for p, nb, ns, o, c in plan:
+            rows = p.lens_cum.index_select(0, dev_i[o + nb: o + 2 * nb + 2 * ns])
+            acc = dev_w[c: c + nb * (nb + 2 * ns)].view(nb, nb + 2 * ns) @ rows if ns else rows
+            base.index_copy_(0, dev_i[o: o + nb], acc)
         return base
 
     @torch.no_grad()
@@ -1065,6 +1162,24 @@ class SweepRunner:
         """Blocks after the hooked layer over response positions ``f..E`` of every cell (packed rows,
         fed the baseline residuals; edit + capture hooks at the hooked layer).  Returns per-row greedy
         token, its NLL and the NLL of the baseline's next token, and per cell ``(f, E, first row)``."""
+        return self._tf_finish(self._tf_launch(cell_pairs, hooks))
+
+    def _tf_finish(self, res: dict) -> dict:
+        """Host side of a launched teacher-forced tail: wait for its one D2H copy, split it."""
+        pend = res.pop("_pending", None)
+        if pend is not None:
+            host, ev, M = pend
+            if ev is not None:
+                ev.synchronize()
+            res["nxt"] = host[0, :M].view(torch.int32).numpy()
+            res["nll_self"] = host[1, :M].numpy()
+            res["nll_tgt"] = host[2, :M].numpy()
+        return res
+
+    @torch.no_grad()
+    def _tf_launch(self, cell_pairs: Sequence[Pair], hooks) -> dict:
+        """Enqueue the teacher-forced tail (no host sync): host index arrays, the packed forward, the vocab
+        head, and one async D2H copy of its per-row outputs; :meth:`_tf_finish` waits for it."""
         from ..models.gemma2 import packed_blocks
 
         m = self.m
@@ -1103,6 +1218,7 @@ class SweepRunner:
         tgt = gtab[up_a[rb_], t_ + 1].astype(np.int32)
         src = base_a[rb_] + t_
         self.stats["tf_rows"] += M
+        self._tick("tf_host_prep")
         res = {"seg": seg, "nxt": np.zeros(0, np.int32), "nll_self": np.zeros(0, np.float32),
                "nll_tgt": np.zeros(0, np.float32), "row_cell": rb_, "row_t": t_, "tgt": tgt}
         if M == 0:
@@ -1112,9 +1228,8 @@ class SweepRunner:
         pos_d = torch.from_numpy(pos).to(dev)
         slot_d = torch.from_numpy(slot).to(dev)
         tgt_d = torch.from_numpy(tgt).to(dev)
-        nxt = torch.empty(M, dtype=torch.int32, device=dev)
-        ns = torch.empty(M, dtype=torch.float32, device=dev)
-        nt = torch.empty(M, dtype=torch.float32, device=dev)
+        outs = torch.empty(3, M, dtype=torch.float32, device=dev)      # [greedy id bits, NLL self, NLL target]
+        nxt, ns, nt = outs[0].view(torch.int32), outs[1], outs[2]
         rpb = 16 // max(1, m.lspec.heads // m.lspec.kv_heads)
         cap = 32768
         step = max(256, ((1 << 30) // (m.spec.vocab_size * 2)) // 256 * 256)     # 256-row multiples (GEMM tiles)
@@ -1167,9 +1282,15 @@ class SweepRunner:
                                     ns[c0 + q0:c0 + q1], nt[c0 + q0:c0 + q1])
         if len(streams) > 1:
             main.wait_stream(streams[1])
-        res["nxt"] = nxt.cpu().numpy()
-        res["nll_self"] = ns.cpu().numpy()
-        res["nll_tgt"] = nt.cpu().numpy()
+        if dev.type == "cuda":
+            host = torch.empty(3, M, dtype=torch.float32, pin_memory=True)
+            host.copy_(outs, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(dev))
+        else:
+            host, ev = outs, None
+        res["_pending"] = (host, ev, M)
+        self._tick("tf_launched")
         return res
 
     def _cell_result(self, c: Cell, p: Pair, n_gen: int, resp: List[int], probs: np.ndarray, topk_ids: List[int],
@@ -1309,6 +1430,28 @@ def word_targeted_latents(runner: "SweepRunner", word: str, m: int) -> List[int]
     if not per_prompt:
         return []
     return A.top_latents_from_scores(torch.stack(list(per_prompt.values()), 0).mean(0), m)
+
+
+class NextBatch:
+    """The next :meth:`SweepRunner.run_cells` batch, for :meth:`SweepRunner.stage_next`: its pairs, and
+    either its ``(cells, plan)`` prefetch future, or ``cells`` (``plan`` built when staged).  Run the
+    next call with ``nb.cells`` (the same list object) so the staged work is used."""
+
+    def __init__(self, pairs, methods=METHODS, cells=None, plan=None, future=None):
+        self.pairs, self.methods, self.cells, self.plan, self.future = pairs, methods, cells, plan, future
+
+    def resolve(self, runner) -> None:
+        if self.future is not None:
+            self.cells, self.plan = self.future.result()
+            self.future = None
+        if self.cells is None:
+            self.cells = runner.make_cells(self.pairs, self.methods)
+
+
+def _h2d(a, dev):
+    """Host array -> pinned CPU tensor for a non-blocking upload (plain tensor on CPU devices)."""
+    t = a if isinstance(a, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(a))
+    return t.pin_memory() if dev.type == "cuda" else t
 
 
 class _Deferred:

@@ -304,3 +304,53 @@ def test_word_scores_rescoring_overwrites():
     r.word_scores["ship"][0] = s_new0            # what _score_pairs does on a re-score of prompt 0
     r.word_scores["ship"][1] = s_new1
     assert word_targeted_latents(r, "ship", 2) == [5, 7]
+
+
+def test_cross_batch_pipeline_is_exact():
+    """Queueing the next batch's teacher-forced tail behind this batch's readout (stage_next) gives the
+    same records as running the batches one after the other."""
+    from dataclasses import replace
+
+    from taboo_brittleness_amd.interp.sae import JumpReLUSAE
+    from taboo_brittleness_amd.models.gemma2 import Gemma2Model
+    from taboo_brittleness_amd.models.spec import GEMMA2_TINY
+    from taboo_brittleness_amd.models.tokenizer import SyntheticTokenizer
+    from taboo_brittleness_amd.models.weights import random_gemma2
+    from taboo_brittleness_amd.pipelines.sweep import NextBatch, SweepRunner
+
+    spec = replace(GEMMA2_TINY, vocab_size=1024, layers=3, hidden=256, ffn=512)
+    m = Gemma2Model(random_gemma2(spec, dtype=torch.bfloat16, seed=7, norm_std=0.1, post_norm_gain=8.0), "cpu")
+    cfg = load_config(None, OVR + ["experiment.max_new_tokens=12",
+                                   "prompts=['Give me a hint!', 'Any hints available?', 'I need one more clue.']"])
+    tok = SyntheticTokenizer(vocab_size=spec.vocab_size)
+    key = lambda r: (r["word"], r["prompt_idx"], r["method"], r["budget"], r["trial"])   # noqa: E731
+    res, staged_used = {}, {}
+    methods = ("sae_targeted", "sae_random")
+    for pipe in (False, True):
+        sae = JumpReLUSAE.random(spec.hidden, 512, seed=2, device="cpu")
+        r = SweepRunner(cfg, m, tok, sae, batch=30, device="cpu", layer=1, use_graphs=False,
+                        prefix_share=True, layer_resume=True, kv_pairs=8)
+        pairs = r.build_pairs(["ship"], cfg.prompts[:3])
+        r.run_baselines(pairs)
+        subs = [[pairs[0]], [pairs[1]], [pairs[2]]]
+        cells = [r.make_cells(subs[0], methods), None, None]
+        out = []
+        for i, sub in enumerate(subs):
+            if pipe and i + 1 < len(subs):
+                nb = NextBatch(subs[i + 1], methods)
+                r.stage_next(nb)
+            got = r.run_cells(sub, cells[i], measure_nll=True)
+            out += got
+            if i + 1 < len(subs):
+                cells[i + 1] = nb.cells if pipe else r.make_cells(subs[i + 1], methods)
+        res[pipe] = {key(x): x for x in out}
+        staged_used[pipe] = r.stats["staged"]
+    assert staged_used[True] == 2                                # both later batches were staged
+    assert set(res[False]) == set(res[True])
+    for k, a in res[False].items():
+        b = res[True][k]
+        assert a["response_ids"] == b["response_ids"], k
+        assert a["topk_ids"] == b["topk_ids"], k
+        assert abs(a["nll_edit"] - b["nll_edit"]) < 1e-6 and abs(a["nll_self"] - b["nll_self"]) < 1e-6
+        for f in ("p_secret_mean", "p_secret_final", "p_secret_max"):
+            assert abs(a[f] - b[f]) < 1e-7 + 1e-6 * abs(a[f])
