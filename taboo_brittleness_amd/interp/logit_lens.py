@@ -199,10 +199,14 @@ def lens_packed(model, store: torch.Tensor, rows: np.ndarray, offs: np.ndarray, 
             pr0 += Mp
             po0 += i1 - i0 + 1
         i0 = i1
-    ridx_d = torch.from_numpy(np.concatenate(ridx_l).astype(np.int64)).to(dev)
-    offs_d = torch.from_numpy(np.concatenate(offs_l)).to(dev)
-    track_d = torch.from_numpy(np.ascontiguousarray(track, dtype=np.int32)).to(dev)
-    excl_d = torch.from_numpy(np.ascontiguousarray(excl, dtype=np.int32)).to(dev)
+    def up(a):    # pinned + non-blocking on GPU: no stream drain while earlier work is queued
+        t = torch.from_numpy(np.ascontiguousarray(a))
+        return t.pin_memory().to(dev, non_blocking=True) if dev.type == "cuda" else t
+
+    ridx_d = up(np.concatenate(ridx_l).astype(np.int64))
+    offs_d = up(np.concatenate(offs_l))
+    track_d = up(np.asarray(track, dtype=np.int32))
+    excl_d = up(np.asarray(excl, dtype=np.int32))
     pr_d = torch.empty(R, K, dtype=torch.float32, device=dev)
     for i0, i1, r0, r1, pr0, Mp, po0 in chunks:
         M = r1 - r0

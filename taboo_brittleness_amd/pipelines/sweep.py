@@ -727,98 +727,126 @@ class SweepRunner:
         self._tick("kv_copy")
         tf = self._tf_finish(staged["tf"] if staged is not None else self._tf_launch(cell_pairs, hooks))
         self._tick("tf_pass")
-        D: List[Optional[int]] = [None] * nc
+        # ---- divergence point D of every cell: first tail row whose greedy token leaves the baseline's
+        D_a = np.full(nc, -1, np.int64)
         if tf["nxt"].size:
             mism = (tf["nxt"] != tf["tgt"]) & (tf["tgt"] >= 0)
             rows = np.nonzero(mism)[0]
             if rows.size:
                 cells_hit, first = np.unique(tf["row_cell"][rows], return_index=True)
-                for b, r in zip(cells_hit.tolist(), rows[first].tolist()):
-                    D[b] = int(tf["row_t"][r]) + 1
+                D_a[cells_hit] = tf["row_t"][rows[first]] + 1
+        D: List[Optional[int]] = [None if d < 0 else int(d) for d in D_a.tolist()]
         # diverged cells, earliest divergence (= most decode steps) first: the decode shrinks its row
         # count as the later-diverging rows complete (Generator.decode row_steps)
-        div = sorted((b for b in range(nc) if D[b] is not None), key=lambda b: D[b])
+        div_a = np.nonzero(D_a >= 0)[0]
+        div_a = div_a[np.argsort(D_a[div_a], kind="stable")]
+        div = div_a.tolist()
         self.stats["cells"] += nc
         self.stats["diverged"] += len(div)
         # diverged cells decode every block from D.  Their attention reads the prefix the baseline
         # computed straight from the pair's KV slot: blocks <= l for positions < plen + D (same tokens,
         # no edit yet), blocks > l for positions < plen + f (before the first edit); the blocks > l
         # keys in [plen + f, plen + D) are the teacher-forced tail's, already in the cell's own slot.
-        # ---- per-cell teacher-forced numbers (complete for every cell): edit NLL, and the self NLL of
-        # cells whose tokens never left the baseline's
+        # ---- per-cell teacher-forced numbers (complete for every cell, vectorised): edit NLL, and the
+        # self NLL of cells whose tokens never left the baseline's
         seg = tf["seg"]
+        upairs, up = tf["upairs"], tf["up"]
+        f_a, r0_a = tf["f"], tf["r0"]
+        U = len(upairs)
+        Gm = max([1] + [len(q.gen_toks) for q in upairs])
+        ntab = np.zeros((max(U, 1), Gm + 1), np.float64)     # per pair: cumulative baseline token NLLs
+        for u, q in enumerate(upairs):
+            ntab[u, 1: len(q.tok_nll) + 1] = np.cumsum(q.tok_nll, dtype=np.float64)
+        n_a = np.asarray([len(q.resp) for q in upairs], np.int64)[up] if nc else np.zeros(0, np.int64)
         ns_cs = np.concatenate([[0.0], np.cumsum(tf["nll_self"], dtype=np.float64)])
         nt_cs = np.concatenate([[0.0], np.cumsum(tf["nll_tgt"], dtype=np.float64)])
-        nll_c, sn_c = [float("nan")] * nc, [float("nan")] * nc
-        for b, p in enumerate(cell_pairs):
-            f, E, r0 = seg[b]
-            n = len(p.resp)
-            if not n:
-                continue
-            ntail = max(0, n - 1 - f)
-            base_self = float(p.tok_nll[: min(f + 1, n)].sum())
-            if measure_nll:
-                nll_c[b] = (base_self + float(nt_cs[r0 + ntail] - nt_cs[r0])) / n
-            sn_c[b] = (base_self + float(ns_cs[r0 + ntail] - ns_cs[r0])) / n
-        # ---- decode: ride-along baselines (rows 0..nr-1, slots nc..) + diverged cells (slot b) + cells
+        ntail = np.maximum(0, n_a - 1 - f_a)
+        base_self = ntab[up, np.minimum(f_a + 1, n_a)] if nc else np.zeros(0)
+        inv_n = np.where(n_a > 0, 1.0 / np.maximum(n_a, 1), np.nan)
+        sn_v = (base_self + ns_cs[r0_a + ntail] - ns_cs[r0_a]) * inv_n
+        nll_v = (base_self + nt_cs[r0_a + ntail] - nt_cs[r0_a]) * inv_n if measure_nll else np.full(nc, np.nan)
+        nll_c, sn_c = nll_v.tolist(), sn_v.tolist()
+        # ---- decode rows: ride-along baselines (slots nc..), then the diverged cells (slot b) and cells
         # carried over from the previous batch (carry-region slots), longest remaining decode first
-        starts, prefix, toks, slots, pnll_rows, rsteps = [], [], [], [], [], []
-        pre_slot, pre_lo, pre_hi = [], [], []
-        steps = 0
         out_r = None
+        R_start, R_tok, R_slot, R_steps, R_ps, R_lo, R_hi, R_pref, R_nll = [], [], [], [], [], [], [], [], []
         if overlap:
             torch.cuda.current_stream(self.dev).wait_stream(side)
             out_r = gen.collect(nr, self.max_new, [p.plen for p in rb], copy=bool(div) or bool(self._carry))
             self._tick("ride_decode_join")
         elif nr:
             first = gen.prefill([p.ids for p in rb], list(range(nc, nc + nr)), hooks, out_rows=list(range(nr)))
-            fl = first.tolist()
-            for j, p in enumerate(rb):
-                starts.append(p.plen)
-                prefix.append([fl[j]])
-                toks.append(fl[j])
-                slots.append(nc + j)
-                rsteps.append(self.max_new)
-                pnll_rows.append(None)
-                pre_slot.append(0)
-                pre_lo.append(0)
-                pre_hi.append(0)
-            steps = self.max_new
-        n_ride_rows = len(slots)
-        crow = [(max(1, self.max_new - D[b]), 0, b) for b in div] + \
-               [(cr.steps, 1, i) for i, cr in enumerate(self._carry)]
-        crow.sort(key=lambda t: -t[0])                       # stable: new rows before carried on ties
+            fl = np.asarray(first.tolist(), np.int64)
+            z = np.zeros(nr, np.int64)
+            R_start.append(np.asarray([p.plen for p in rb], np.int64))
+            R_tok.append(fl)
+            R_slot.append(np.arange(nc, nc + nr, dtype=np.int64))
+            R_steps.append(np.full(nr, self.max_new, np.int64))
+            R_ps.append(z)
+            R_lo.append(z)
+            R_hi.append(z)
+            R_pref.append([[int(t)] for t in fl.tolist()])
+            R_nll.append(None)                  # their first NLL comes from the prefill (out_nll[:, 0])
+        n_ride_rows = nr if (nr and not overlap) else 0
+        # new diverged rows, vectorised over cells
+        nd = div_a.size
+        ud = up[div_a] if nd else np.zeros(0, np.int64)
+        Dd, fd, rd = D_a[div_a], f_a[div_a], r0_a[div_a]
+        plen_u = np.asarray([q.plen for q in upairs], np.int64)
+        kv_u = np.asarray([q.kv_slot for q in upairs], np.int64)
+        e_d = tf["nxt"][rd + Dd - 1 - fd].astype(np.int64) if nd else np.zeros(0, np.int64)
+        Wn = int(Dd.max()) + 1 if nd else 1
+        col = np.arange(Wn)[None, :]
+        gt = tf["gtab"]
+        pref_d = np.where(col < Dd[:, None], gt[ud][:, :Wn] if gt.shape[1] >= Wn else
+                          np.pad(gt[ud], ((0, 0), (0, Wn - gt.shape[1])))[:, :Wn], self.gen.pad_id)
+        pref_d = np.where(col == Dd[:, None], e_d[:, None], pref_d)
+        nllm_d = np.zeros((nd, Wn), np.float32)
+        if nd:
+            tokn = np.zeros((U, Gm), np.float32)
+            for u, q in enumerate(upairs):
+                tokn[u, : len(q.tok_nll)] = q.tok_nll
+            cmat = np.broadcast_to(col, (nd, Wn))
+            base_part = tokn[ud][:, :Wn] if Gm >= Wn else np.pad(tokn[ud], ((0, 0), (0, Wn - Gm)))
+            tail_idx = np.clip(rd[:, None] + cmat - fd[:, None] - 1, 0, max(0, tf["nll_self"].size - 1))
+            tail_part = tf["nll_self"][tail_idx] if tf["nll_self"].size else np.zeros((nd, Wn), np.float32)
+            nllm_d = np.where(cmat <= fd[:, None], base_part, np.where(cmat <= Dd[:, None], tail_part, 0.0))
+        steps_d = np.maximum(1, self.max_new - Dd)
         carry_in = self._carry
         self._carry = []
-        row_src = []                                         # per cell decode row: ("new", b) | ("carry", _Carry)
-        for st, kind, i in crow:
-            if kind == 0:
-                b = i
-                p = cell_pairs[b]
-                f, E, r0 = seg[b]
-                e = int(tf["nxt"][r0 + D[b] - 1 - f])
-                starts.append(p.plen + D[b])
-                prefix.append(list(p.gen_toks[: D[b]]) + [e])
-                toks.append(e)
-                slots.append(b)
-                pnll_rows.append(np.concatenate([p.tok_nll[: f + 1], tf["nll_self"][r0: r0 + D[b] - f]]).astype(np.float32))
-                pre_slot.append(p.kv_slot)
-                pre_lo.append(p.plen + D[b])
-                pre_hi.append(p.plen + f)
-                row_src.append(("new", b))
-            else:
-                cr = carry_in[i]
-                starts.append(cr.pos)
-                prefix.append(cr.prefix)
-                toks.append(cr.tok)
-                slots.append(cr.slot)
-                pnll_rows.append(cr.prefix_nll)
-                pre_slot.append(cr.pre[0])
-                pre_lo.append(cr.pre[1])
-                pre_hi.append(cr.pre[2])
-                row_src.append(("carry", cr))
-            rsteps.append(st)
-            steps = max(steps, st)
+        # merge with carried rows: stable by remaining steps, new rows before carried ones on ties
+        c_steps = np.asarray([cr.steps for cr in carry_in], np.int64)
+        allsteps = np.concatenate([steps_d, c_steps])
+        order = np.argsort(-allsteps, kind="stable")
+        row_src = [("new", int(div_a[i])) if i < nd else ("carry", carry_in[i - nd]) for i in order.tolist()]
+        cat = lambda a, b: np.concatenate([a, np.asarray(b, np.int64)])[order]   # noqa: E731
+        R_start.append(cat(plen_u[ud] + Dd, [cr.pos for cr in carry_in]))
+        R_tok.append(cat(e_d, [cr.tok for cr in carry_in]))
+        R_slot.append(cat(div_a, [cr.slot for cr in carry_in]))
+        R_steps.append(allsteps[order])
+        R_ps.append(cat(kv_u[ud], [cr.pre[0] for cr in carry_in]))
+        R_lo.append(cat(plen_u[ud] + Dd, [cr.pre[1] for cr in carry_in]))
+        R_hi.append(cat(plen_u[ud] + fd, [cr.pre[2] for cr in carry_in]))
+        if carry_in:
+            Wc = max([Wn] + [len(cr.prefix) for cr in carry_in])
+            pm = np.full((nd + len(carry_in), Wc), self.gen.pad_id, np.int64)
+            nm = np.zeros((nd + len(carry_in), Wc), np.float32)
+            pm[:nd, :Wn], nm[:nd, :Wn] = pref_d, nllm_d
+            for i, cr in enumerate(carry_in):
+                pm[nd + i, : len(cr.prefix)] = cr.prefix
+                nm[nd + i, : len(cr.prefix_nll)] = cr.prefix_nll
+            lens_all = np.concatenate([Dd + 1, [len(cr.prefix) for cr in carry_in]])
+            R_pref.append((pm[order], lens_all[order]))
+            R_nll.append(nm[order])
+        else:
+            R_pref.append((pref_d, Dd + 1))
+            R_nll.append(nllm_d)
+        starts = np.concatenate(R_start) if R_start else np.zeros(0, np.int64)
+        toks = np.concatenate(R_tok) if R_tok else np.zeros(0, np.int64)
+        slots = np.concatenate(R_slot) if R_slot else np.zeros(0, np.int64)
+        rsteps = np.concatenate(R_steps) if R_steps else np.zeros(0, np.int64)
+        pre_slot, pre_lo, pre_hi = (np.concatenate(x) for x in (R_ps, R_lo, R_hi))
+        steps = int(rsteps.max()) if rsteps.size else 0
         nrows = len(slots)
         self._tick("prefill")
         out = None
@@ -826,16 +854,24 @@ class SweepRunner:
         carry_move = None
         if nrows:
             nr_here = 0 if overlap else nr
-            Wp = max([1] + [len(x) for x in pnll_rows if x is not None])
-            pnll = torch.zeros(nrows, Wp)
+            pm, lens_c = R_pref[-1]
+            nm = R_nll[-1]
+            Wp = max(1, pm.shape[1])
+            pref_all = np.full((nrows, Wp), self.gen.pad_id, np.int64)
+            lens_all = np.ones(nrows, np.int64)
+            pref_all[nr_here:, : pm.shape[1]] = pm
+            lens_all[nr_here:] = lens_c
             if nr_here:
-                pnll[:nr, :1] = gen.out_nll[:nr, :1].cpu()
-            for j, own in enumerate(pnll_rows):
-                if own is not None:
-                    pnll[j, : own.shape[0]] = torch.from_numpy(np.asarray(own, dtype=np.float32))
+                pref_all[:nr_here, 0] = R_tok[0]
+            pnll = torch.zeros(nrows, Wp, dtype=torch.float32, device=self.dev)
+            if nr_here:
+                pnll[:nr_here, :1] = gen.out_nll[:nr_here, :1]
+            if nm.size:
+                pnll[nr_here:, : nm.shape[1]] = _h2d(np.ascontiguousarray(nm, dtype=np.float32),
+                                                    self.dev).to(self.dev, non_blocking=True)
             carry_ok = (self.carry_rows > 0 and not self._drain_batch and n_ride_rows == 0)
-            ran = gen.decode(torch.tensor(toks, dtype=torch.int32), starts, prefix, max(steps, 1), nrows, hooks,
-                             "sweep", prefix_nll=pnll.to(self.dev), slots=slots, row_steps=rsteps,
+            ran = gen.decode(torch.from_numpy(toks.astype(np.int32)), starts, (pref_all, lens_all), max(steps, 1),
+                             nrows, hooks, "sweep", prefix_nll=pnll, slots=slots, row_steps=rsteps,
                              prefix_rows=(pre_slot, pre_lo, pre_hi),
                              stop_below=self.carry_rows if carry_ok else 0,
                              min_steps=max([cr.steps for cr in carry_in] + [0]))
@@ -1220,14 +1256,16 @@ class SweepRunner:
         self.stats["tf_rows"] += M
         self._tick("tf_host_prep")
         res = {"seg": seg, "nxt": np.zeros(0, np.int32), "nll_self": np.zeros(0, np.float32),
-               "nll_tgt": np.zeros(0, np.float32), "row_cell": rb_, "row_t": t_, "tgt": tgt}
+               "nll_tgt": np.zeros(0, np.float32), "row_cell": rb_, "row_t": t_, "tgt": tgt,
+               "f": f_a, "E": E_a, "r0": r0_a, "up": up_a, "upairs": [p for p, _ in ulist], "gtab": gtab}
         if M == 0:
             return res
         dev = self.dev
-        H = torch.cat(srcs, 0).index_select(0, torch.from_numpy(src).to(dev))
-        pos_d = torch.from_numpy(pos).to(dev)
-        slot_d = torch.from_numpy(slot).to(dev)
-        tgt_d = torch.from_numpy(tgt).to(dev)
+        up_ = lambda a: _h2d(a, dev).to(dev, non_blocking=True)     # noqa: E731  (pinned: no stream drain)
+        H = torch.cat(srcs, 0).index_select(0, up_(src))
+        pos_d = up_(pos)
+        slot_d = up_(slot)
+        tgt_d = up_(tgt)
         outs = torch.empty(3, M, dtype=torch.float32, device=dev)      # [greedy id bits, NLL self, NLL target]
         nxt, ns, nt = outs[0].view(torch.int32), outs[1], outs[2]
         rpb = 16 // max(1, m.lspec.heads // m.lspec.kv_heads)
@@ -1259,7 +1297,7 @@ class SweepRunner:
         # every chunk's attention block table in one upload (no host sync between chunks)
         tabs = [packed_blocks(chunk, rpb) for (_, _, chunk) in chunks]
         tab_off = np.concatenate([[0], np.cumsum([t.shape[0] for t in tabs])]).astype(np.int64)
-        tab_d = torch.cat(tabs, 0).to(dev) if tabs else None
+        tab_d = _h2d(torch.cat(tabs, 0), dev).to(dev, non_blocking=True) if tabs else None
         for ci, (c0, c1, chunk) in enumerate(chunks):
             st = streams[ci % len(streams)]
             with (torch.cuda.stream(st) if st is not None else _nullctx()):

@@ -219,16 +219,14 @@ class Generator:
                 kp.len_lo.zero_()
                 kp.len_hi.zero_()
             else:
-                pad = [0] * (B - len(prefix_rows[0]))
                 for dst, src in zip((kp.slot, kp.len_lo, kp.len_hi), prefix_rows):
-                    dst.copy_(torch.tensor(list(src) + pad, dtype=torch.int32))
+                    dst.copy_(_up(_padded(src, B, 0), self.dev), non_blocking=True)
         else:
             assert prefix_rows is None, "prefix_rows needs enable_kv_prefix()"
         if slots is None:
             self.slot.copy_(torch.arange(B, dtype=torch.int32, device=self.dev))
         else:
-            sl = list(slots)[:B]
-            self.slot.copy_(torch.tensor(sl + [0] * (B - len(sl)), dtype=torch.int32, device=self.dev))
+            self.slot.copy_(_up(_padded(slots, B, 0), self.dev), non_blocking=True)
         nb = self.bucket(n_rows)
         self.tf_tgt.fill_(-1)
         if teacher is not None and len(teacher):
@@ -241,28 +239,38 @@ class Generator:
             self.tf_tgt[: len(teacher), :tw] = torch.from_numpy(tt).to(self.dev)
         self.out_tokens.fill_(self.pad_id)
         tok = torch.full((B,), self.pad_id, dtype=torch.int32, device=self.dev)
-        tok[: start_tok.numel()] = start_tok.to(self.dev).int().view(-1)
+        st = start_tok.int().view(-1)
+        if not st.is_cuda and self.dev.type == "cuda":
+            st = st.pin_memory()
+        tok[: st.numel()] = st.to(self.dev, non_blocking=True)
         if prefix is None:                   # every row's known response is just its start token (device)
-            lens = [1] * B
+            lens = np.ones(B, np.int64)
             pref_d = tok.view(B, 1)
+        elif isinstance(prefix, tuple):      # (token matrix [n, W], lengths [n]) from a vectorised caller
+            pm, pl = prefix
+            n = pm.shape[0]
+            lens = _padded(pl, B, 1)
+            pref = np.full((B, max(1, pm.shape[1])), self.pad_id, dtype=np.int32)
+            pref[:n, : pm.shape[1]] = pm
+            pref_d = _up(pref, self.dev).to(self.dev, non_blocking=True)
         else:
-            lens = [len(p) for p in prefix] + [1] * (B - len(prefix))
-            pref = np.full((B, max(lens)), self.pad_id, dtype=np.int32)
+            lens = np.asarray([len(p) for p in prefix] + [1] * (B - len(prefix)), np.int64)
+            pref = np.full((B, int(lens.max())), self.pad_id, dtype=np.int32)
             for b, p in enumerate(prefix):
                 pref[b, : len(p)] = list(p)
             pref_d = torch.from_numpy(pref).to(self.dev)
         self.out_tokens[:, : pref_d.shape[1]] = pref_d
         if prefix_nll is not None:
             self.out_nll[: prefix_nll.shape[0], : prefix_nll.shape[1]] = prefix_nll
-        valid = torch.arange(pref_d.shape[1], device=self.dev)[None, :] < torch.tensor(lens, device=self.dev)[:, None]
+        lens_d = _up(np.asarray(lens, np.int64), self.dev).to(self.dev, non_blocking=True)
+        valid = torch.arange(pref_d.shape[1], device=self.dev)[None, :] < lens_d[:, None]
         hit = ((pref_d.view(B, -1, 1) == self.stop_ids.view(1, 1, -1)).any(-1) & valid).any(-1)
         self.done.copy_(hit)
         if n_rows < B:
             self.done[n_rows:] = True
         self.tok.copy_(tok.view(-1, 1))
-        sp = list(start_pos) + [self.S] * (B - len(start_pos))
-        self.pos.copy_(torch.tensor(sp, dtype=torch.int32, device=self.dev).view(-1, 1))
-        self.step_idx.copy_(torch.tensor(lens, dtype=torch.int64, device=self.dev).view(-1, 1))
+        self.pos.copy_(_up(_padded(start_pos, B, self.S), self.dev).view(-1, 1), non_blocking=True)
+        self.step_idx.copy_(lens_d.view(-1, 1))
         active = None
         if row_steps is not None:
             rs = np.asarray(list(row_steps), dtype=np.int64)
@@ -357,6 +365,20 @@ class Generator:
 
     def invalidate_graph(self) -> None:
         self._graphs.clear()
+
+
+def _padded(a, n: int, fill: int) -> np.ndarray:
+    """int32 host array of ``a`` padded with ``fill`` to ``n`` entries (truncated past ``n``)."""
+    a = np.asarray(a, dtype=np.int64).reshape(-1)[:n]
+    out = np.full(n, fill, dtype=np.int32)
+    out[: a.size] = a
+    return out
+
+
+def _up(a: np.ndarray, dev: torch.device) -> torch.Tensor:
+    """Host array as a (pinned, on GPU devices) CPU tensor, ready for a non-blocking upload."""
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    return t.pin_memory() if dev.type == "cuda" else t
 
 
 def teacher_divergence(own: Sequence[int], teacher: Sequence[int], c0: int) -> int:

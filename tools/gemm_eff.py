@@ -9,12 +9,12 @@ import torch
 sys.path.insert(0, ".")
 from taboo_brittleness_amd.runtime.tuning import enable_tuned_gemms  # noqa: E402
 
-enable_tuned_gemms("gemma2-9b_P60_E4_new50")
+enable_tuned_gemms("gemma2-9b_P90_E4_new50")
 dev = torch.device("cuda:0")
 W = {"qkv": (8192, 3584), "o": (3584, 4096), "gu": (28672, 3584), "down": (3584, 14336), "lm_head": (256000, 3584)}
 ws = {k: torch.randn(n, kk, device=dev, dtype=torch.bfloat16) * 0.02 for k, (n, kk) in W.items()}
 res = []
-for M in (256, 1024, 2048, 2560, 4096, 16384, 32768):
+for M in (256, 1024, 2048, 3840, 4096, 6144, 32768):
     for name, w in ws.items():
         if name == "lm_head" and M > 4096:
             continue
