@@ -186,20 +186,37 @@ def main() -> None:
     def cells_of(k):
         return range(P * n_cells)
 
+    gathers = []
+
     def gather_results(res):
         """The DP sweep's result collection, every step: each rank's compact cell records (readouts,
-        NLLs, leak, n_gen, LL-Top-5 ids) are all-gathered (one RCCL all-gather over xGMI)."""
+        NLLs, leak, n_gen, LL-Top-5 ids) are all-gathered (one RCCL all-gather over xGMI), issued
+        asynchronously on the collective's own stream (overlaps the next step's compute; no per-step
+        lock-step of the ranks) and completed before the timed window closes."""
         if info.world <= 1:
             return None
         rec = torch.tensor([[r["p_secret_mean"], r["p_secret_final"], r["p_secret_max"], r["nll_edit"],
                              r["nll_self"], float(r["leak"]), float(r["n_gen"])] +
                             [float(t) for t in (list(r["topk_ids"]) + [-1] * 5)[:5]] for r in res],
                            dtype=torch.float64)
-        return D.all_gather_tensor(rec.to(dev), info)
+        if on_gpu:
+            rec = rec.pin_memory().to(dev, non_blocking=True)
+        out, work = D.all_gather_tensor_async(rec, info)
+        gathers.append((out, work, rec))
+        return out
+
+    def finish_gathers():
+        for out, work, rec in gathers:
+            if work is not None:
+                work.wait()
+        n = sum(int(out.shape[0]) for out, _, _ in gathers)
+        gathers.clear()
+        return n
 
     for k in range(args.warmup):
         cur, res, dt = step(k, cur)
         gather_results(res.result())
+    finish_gathers()
     runner.precapture_graphs()          # one-time setup: every decode row-bucket graph
     # everything allocated so far (model, tokenizer tables, caches) is long-lived: keep the cyclic GC from
     # rescanning it on every collection inside the timed steps (pauses the launch thread otherwise)
@@ -230,6 +247,8 @@ def main() -> None:
     done = pending.result()
     n_done += len(done)
     gather_results(done)
+    gathered_rows = finish_gathers()
+    assert info.world <= 1 or gathered_rows == n_done * info.world, "result all-gather incomplete"
     if on_gpu:
         torch.cuda.synchronize()
     D.barrier(info)

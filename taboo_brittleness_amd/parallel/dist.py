@@ -89,6 +89,17 @@ def all_gather_tensor(x: torch.Tensor, info: DistInfo) -> torch.Tensor:
     return out
 
 
+def all_gather_tensor_async(x: torch.Tensor, info: DistInfo):
+    """:func:`all_gather_tensor` issued asynchronously: returns ``(out, work)``; ``work.wait()`` (or
+    ``None`` on one rank) before reading ``out``.  On RCCL the collective runs on the process group's own
+    stream, so the compute stream does not wait for it (and ranks do not lock-step on it)."""
+    if info.world <= 1 or not dist.is_initialized():
+        return x, None
+    out = torch.empty((info.world * x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    work = dist.all_gather_into_tensor(out, x.contiguous(), async_op=True)
+    return out, work
+
+
 def all_gather_rows(x: torch.Tensor, info: DistInfo) -> torch.Tensor:
     """Variable-length row all-gather (e.g. spike residuals for pooled PCA): pad, gather, trim."""
     if info.world <= 1 or not dist.is_initialized():
