@@ -22,7 +22,15 @@ int tb_attention_lds_bytes(int HD);
 void tb_attention(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, uint16_t* out, const int32_t* pos,
                   const int32_t* slot, int B, int T, int Hq, int Hkv, int HD, int S, float scale, float softcap,
                   int window, hipStream_t st, const uint16_t* pkc = nullptr, const uint16_t* pvc = nullptr,
-                  const int32_t* pslot = nullptr, const int32_t* plen = nullptr);
+                  const int32_t* pslot = nullptr, const int32_t* plen = nullptr, const float* xm = nullptr,
+                  const float* xl = nullptr, const float* xo = nullptr);
+// Shared-prefix (cascade) pass of the decode attention (G = 2, S <= tb_attn_prefix_max_S()): per chunk of
+// rows sharing a prefix slot, (max, sum, unnormalised O) over keys [0, plen[row]) -> tb_attention's xm/xl/xo.
+int tb_attn_prefix_max_S();
+void tb_attn_prefix_partial(const uint16_t* q, const uint16_t* pkc, const uint16_t* pvc, const int32_t* chunks,
+                            const int32_t* nchunks, int max_chunks, const int32_t* plen, const int32_t* pos, int nb,
+                            int Hq, int Hkv, int HD, int S, float scale, float softcap, int window, float* out_m,
+                            float* out_l, float* out_o, hipStream_t st);
 // blk [nblk, bw]: (first row, rows, slot) (bw = 3) or + (prefix slot, prefix length) (bw = 5, keys below the
 // prefix length read from that slot of pkc/pvc).
 void tb_attention_varlen(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, uint16_t* out, const int32_t* pos,

@@ -111,9 +111,12 @@ void attention(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch::Tenso
 
 void attention_prefix(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch::Tensor out, torch::Tensor pos,
                       torch::Tensor slot, int64_t B, double scale, double softcap, int64_t window, torch::Tensor pk,
-                      torch::Tensor pv, torch::Tensor pslot, torch::Tensor plen) {
+                      torch::Tensor pv, torch::Tensor pslot, torch::Tensor plen,
+                      c10::optional<torch::Tensor> xm, c10::optional<torch::Tensor> xl,
+                      c10::optional<torch::Tensor> xo) {
   IN_BF16(q); IN_BF16(kc); IN_BF16(vc); IN_BF16(out); IN_I32(pos); IN_I32(slot);
   IN_BF16(pk); IN_BF16(pv); IN_I32(pslot); IN_I32(plen);
+  const bool ext = xo.has_value() && xo->defined();
   TORCH_CHECK(kc.dim() == 4, "cache must be [slots, Hkv, S, HD]");
   const int Hkv = kc.size(1), S = kc.size(2), HD = kc.size(3);
   TORCH_CHECK(S <= 8192, "shared-prefix attention is the decode kernel (S <= 8192)");
@@ -126,10 +129,41 @@ void attention_prefix(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch
   TORCH_CHECK(pk.dim() == 4 && pk.size(1) == Hkv && pk.size(2) == S && pk.size(3) == HD && pv.sizes() == pk.sizes(),
               "prefix cache must be [P, Hkv, S, HD] like the cache");
   TORCH_CHECK(pslot.numel() >= B && plen.numel() >= B, "prefix slot/len per row");
+  const float *pm = nullptr, *pl = nullptr, *po = nullptr;
+  if (ext) {
+    IN_F32((*xo)); IN_F32((*xm)); IN_F32((*xl));
+    TORCH_CHECK(xm->numel() >= (int64_t)B * Hq && xl->numel() >= (int64_t)B * Hq &&
+                xo->numel() >= (int64_t)B * Hq * HD, "prefix partial buffers [B, Hq(, HD)]");
+    pm = xm->data_ptr<float>(); pl = xl->data_ptr<float>(); po = xo->data_ptr<float>();
+  }
   c10::DeviceGuard g(q.device());
   tb_attention(cbf(q), cbf(kc), cbf(vc), bf(out), pos.data_ptr<int32_t>(), slot.data_ptr<int32_t>(), B, 1, Hq, Hkv,
                HD, S, (float)scale, (float)softcap, (int)window, cur_stream(), cbf(pk), cbf(pv),
-               pslot.data_ptr<int32_t>(), plen.data_ptr<int32_t>());
+               pslot.data_ptr<int32_t>(), plen.data_ptr<int32_t>(), pm, pl, po);
+}
+
+int64_t attn_prefix_max_S() { return tb_attn_prefix_max_S(); }
+
+void attn_prefix_partial(torch::Tensor q, torch::Tensor pk, torch::Tensor pv, torch::Tensor chunks,
+                         torch::Tensor nchunks, torch::Tensor plen, torch::Tensor pos, int64_t B, double scale,
+                         double softcap, int64_t window, torch::Tensor xm, torch::Tensor xl, torch::Tensor xo) {
+  IN_BF16(q); IN_BF16(pk); IN_BF16(pv); IN_I32(chunks); IN_I32(nchunks); IN_I32(plen); IN_I32(pos);
+  IN_F32(xm); IN_F32(xl); IN_F32(xo);
+  TORCH_CHECK(pk.dim() == 4 && pv.sizes() == pk.sizes(), "prefix cache must be [P, Hkv, S, HD]");
+  const int Hkv = pk.size(1), S = pk.size(2), HD = pk.size(3);
+  TORCH_CHECK(HD == 256 || HD == 128, "head dim 128 or 256");
+  TORCH_CHECK(S <= tb_attn_prefix_max_S(), "cascade prefix pass needs S <= ", tb_attn_prefix_max_S());
+  TORCH_CHECK(q.numel() % (B * HD) == 0, "q shape");
+  const int Hq = q.numel() / (B * HD);
+  TORCH_CHECK(Hq == 2 * Hkv, "cascade prefix pass is instantiated for GQA ratio 2");
+  TORCH_CHECK(chunks.dim() == 2 && chunks.size(1) == 10, "chunk table [C, 10]: slot, nrows, 8 rows");
+  TORCH_CHECK(nchunks.numel() == 1 && plen.numel() >= B && pos.numel() >= B, "chunk count / per-row lengths");
+  TORCH_CHECK(xm.numel() >= B * Hq && xl.numel() >= B * Hq && xo.numel() >= B * Hq * HD, "partial buffers");
+  c10::DeviceGuard g(q.device());
+  tb_attn_prefix_partial(cbf(q), cbf(pk), cbf(pv), chunks.data_ptr<int32_t>(), nchunks.data_ptr<int32_t>(),
+                         (int)chunks.size(0), plen.data_ptr<int32_t>(), pos.data_ptr<int32_t>(), (int)B, Hq, Hkv, HD,
+                         S, (float)scale, (float)softcap, (int)window, xm.data_ptr<float>(), xl.data_ptr<float>(),
+                         xo.data_ptr<float>(), cur_stream());
 }
 
 void attention_varlen(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch::Tensor out, torch::Tensor pos,
@@ -446,6 +480,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("embed_rmsnorm", &embed_rmsnorm);
   m.def("rope_qkv_cache", &rope_qkv_cache);
   m.def("attention", &attention);
+  m.def("attn_prefix_partial", &attn_prefix_partial);
+  m.def("attn_prefix_max_S", &attn_prefix_max_S);
   m.def("attention_prefix", &attention_prefix);
   m.def("attention_varlen", &attention_varlen);
   m.def("attention_varlen_prefix", &attention_varlen_prefix);

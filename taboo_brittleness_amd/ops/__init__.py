@@ -123,17 +123,66 @@ def attention(q, kc, vc, pos, slot, B, T, scale, softcap, window, out=None, pref
         out = _out(out, (B * T, q.numel() // (B * T)), q.dtype, q.device)
         if prefix is not None:
             assert T == 1, "shared-prefix attention is decode-only"
-            pk, pv, ps, pl = prefix
+            pk, pv, ps, pl = prefix[:4]
+            casc = prefix[4] if len(prefix) > 4 else None
+            if casc is not None:        # cascade: the pair prefix once per chunk of rows, then own keys + merge
+                chunks, nch, xm, xl, xo = casc
+                _k().attn_prefix_partial(q, pk, pv, chunks, nch, pl, pos, int(B), float(scale), float(softcap),
+                                         int(window), xm, xl, xo)
+                _k().attention_prefix(q, kc, vc, out, pos, slot, int(B), float(scale), float(softcap), int(window),
+                                      pk, pv, ps, pl, xm, xl, xo)
+                return out
             _k().attention_prefix(q, kc, vc, out, pos, slot, int(B), float(scale), float(softcap), int(window),
-                                  pk, pv, ps, pl)
+                                  pk, pv, ps, pl, None, None, None)
             return out
         _k().attention(q, kc, vc, out, pos, slot, int(B), int(T), float(scale), float(softcap), int(window))
         return out
-    o = ref.attention(q, kc, vc, pos, slot, B, T, scale, softcap, window, prefix=prefix)
+    o = ref.attention(q, kc, vc, pos, slot, B, T, scale, softcap, window,
+                      prefix=prefix[:4] if prefix is not None else None)
     if out is not None:
         out.copy_(o.view_as(out))
         return out
     return o
+
+
+def attn_prefix_max_S() -> int:
+    """Longest cache (keys) the cascade prefix pass supports (its V tile lives in LDS); 0 without the
+    extension."""
+    try:
+        return int(_k().attn_prefix_max_S())
+    except Exception:
+        return 0
+
+
+def attn_prefix_chunks(pslot, plen_any, rows_per_chunk: int = 8):
+    """Host chunk table of the cascade decode-attention pass: rows with a shared prefix (``plen_any > 0``)
+    grouped by prefix slot, cut into chunks of ``rows_per_chunk`` rows (ascending), sorted by first row.
+    Returns int32 ``[C, 2 + rows_per_chunk]`` = (slot, nrows, rows..., -1 padded)."""
+    import numpy as np
+
+    ps = np.asarray(pslot, dtype=np.int64)
+    rows = np.nonzero(np.asarray(plen_any) > 0)[0]
+    if rows.size == 0:
+        return np.zeros((0, 2 + rows_per_chunk), np.int32)
+    order = np.lexsort((rows, ps[rows]))
+    rows = rows[order]
+    sl = ps[rows]
+    starts = np.concatenate([[0], np.nonzero(sl[1:] != sl[:-1])[0] + 1])
+    ends = np.concatenate([starts[1:], [rows.size]])
+    lens = ends - starts
+    nck = -(-lens // rows_per_chunk)
+    C = int(nck.sum())
+    out = np.full((C, 2 + rows_per_chunk), -1, np.int32)
+    g_of = np.repeat(np.arange(starts.size), nck)
+    k_in = np.arange(C) - np.repeat(np.cumsum(nck) - nck, nck)
+    first = starts[g_of] + k_in * rows_per_chunk
+    nr = np.minimum(rows_per_chunk, ends[g_of] - first)
+    out[:, 0] = sl[first]
+    out[:, 1] = nr
+    for j in range(rows_per_chunk):
+        ok = j < nr
+        out[ok, 2 + j] = rows[first[ok] + j]
+    return out[np.argsort(out[:, 2], kind="stable")]
 
 
 def attention_varlen(q, kc, vc, pos, slot_rows, blk, scale, softcap, window, out=None, prefix_kv=None):

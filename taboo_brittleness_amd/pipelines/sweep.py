@@ -1270,7 +1270,10 @@ class SweepRunner:
         nxt, ns, nt = outs[0].view(torch.int32), outs[1], outs[2]
         rpb = 16 // max(1, m.lspec.heads // m.lspec.kv_heads)
         cap = 32768
-        step = max(256, ((1 << 30) // (m.spec.vocab_size * 2)) // 256 * 256)     # 256-row multiples (GEMM tiles)
+        # vocab-head rows per GEMM: 256-row multiples (GEMM tiles) of at most TB_TF_HEAD_MB of bf16 logits
+        # (2048 rows of the 256k vocab; 4096 measured equal, profiles/r2/kstats_head4096.txt)
+        head_bytes = int(os.environ.get("TB_TF_HEAD_MB", "1024")) << 20
+        step = max(256, (head_bytes // (m.spec.vocab_size * 2)) // 256 * 256)
         # chunks of whole cells (a cell never spans two chunks), so chunks are independent and
         # alternate between two streams: one chunk's bandwidth-bound kernels (attention, norms, GeGLU,
         # vocab head) overlap the other's GEMMs
@@ -1434,7 +1437,8 @@ class SweepRunner:
             pos_d = torch.tensor(pos, dtype=torch.int32, device=dev)
             slot_d = torch.tensor(owner, dtype=torch.int32, device=dev)
             tgt_d = torch.tensor(tgt, dtype=torch.int32, device=dev)
-            step = max(256, ((1 << 30) // (m.spec.vocab_size * 2)) // 256 * 256)     # 256-row multiples (GEMM tiles)
+            head_bytes = int(os.environ.get("TB_TF_HEAD_MB", "1024")) << 20
+            step = max(256, (head_bytes // (m.spec.vocab_size * 2)) // 256 * 256)
             for r0 in range(0, len(ids), cap):
                 r1 = min(len(ids), r0 + cap)
                 M = r1 - r0

@@ -343,3 +343,41 @@ def test_lowrank_edit_rejects_unsupported_rows(gpu):
         E = torch.zeros(4, D, dtype=torch.float32, device=gpu)
         with pytest.raises(RuntimeError):
             ops.lowrank_edit(h, apply, idx, cnt, E, E, None, None, None, 1.0, None, 1e-6, None, None)
+
+
+@pytest.mark.parametrize("HD", [256, 128])
+def test_attention_decode_cascade_prefix(gpu, HD):
+    """Cascade decode attention (one prefix pass per chunk of rows sharing a prefix slot, merged into the
+    per-row kernel) == the reference and the per-row shared-prefix kernel, incl. rows without a prefix,
+    chunks straddling the row bucket, and a sliding window that hides a row's prefix."""
+    torch.manual_seed(11)
+    Hkv, G, S, B = 2, 2, 68, 27
+    Hq = Hkv * G
+    kc = torch.randn(B, Hkv, S, HD, dtype=BF)
+    vc = torch.randn(B, Hkv, S, HD, dtype=BF)
+    pk = torch.randn(4, Hkv, S, HD, dtype=BF)
+    pv = torch.randn(4, Hkv, S, HD, dtype=BF)
+    slot = torch.randperm(B).to(torch.int32)
+    pos = torch.randint(20, S, (B,), dtype=torch.int32)
+    ps = torch.randint(0, 4, (B,), dtype=torch.int32)
+    pl = torch.minimum(torch.randint(1, 40, (B,), dtype=torch.int32), pos)
+    pl[[3, 10]] = 0                                       # rows without a prefix
+    q = torch.randn(B, Hq, HD, dtype=BF) * 2
+    tab = ops.attn_prefix_chunks(ps.numpy(), pl.numpy())
+    chunks = torch.full((tab.shape[0] + 4, 10), -1, dtype=torch.int32)
+    chunks[: tab.shape[0]] = torch.from_numpy(tab)
+    d = lambda t: t.to(gpu)                               # noqa: E731
+    xm = torch.zeros(B, Hq, device=gpu)
+    xl = torch.zeros(B, Hq, device=gpu)
+    xo = torch.zeros(B, Hq, HD, device=gpu)
+    for window, nb in ((0, B), (16, B), (0, 13)):
+        casc = (d(chunks), torch.tensor([tab.shape[0]], dtype=torch.int32, device=gpu), xm, xl, xo)
+        og = ops.attention(d(q[:nb]), d(kc), d(vc), d(pos[:nb]), d(slot[:nb]), nb, 1, HD ** -0.5, 50.0, window,
+                           prefix=(d(pk), d(pv), d(ps), d(pl), casc))
+        o1 = ops.attention(d(q[:nb]), d(kc), d(vc), d(pos[:nb]), d(slot[:nb]), nb, 1, HD ** -0.5, 50.0, window,
+                           prefix=(d(pk), d(pv), d(ps), d(pl)))
+        orf = ref.attention(q[:nb], kc, vc, pos[:nb], slot[:nb], nb, 1, HD ** -0.5, 50.0, window,
+                            prefix=(pk, pv, ps[:nb], pl[:nb]))
+        assert torch.isfinite(og.float()).all()
+        _close(og, orf, atol=2e-2, rtol=2e-2)
+        _close(og, o1, atol=2e-2, rtol=2e-2)
