@@ -161,6 +161,11 @@ class SweepRunner:
         self.carry_rows = 0
         self._carry: List[_Carry] = []
         self._next: Optional["NextBatch"] = None      # batch of the next run_cells call (stage_next)
+        # lazy running lens sums: a pair's [n + 1, V] fp32 running sums (52 MB at the 256k vocab) are rebuilt from
+        # its kept hooked-layer residuals when its cells run, instead of being held from its baseline on (E steps
+        # ahead): only the running batch's pairs hold them (~18 GB less at 90 pairs per step)
+        self.lazy_cum = os.environ.get("TB_LAZY_LENS_CUM", "1") == "1"
+        self._cum_live: List[Pair] = []
         self._staged: Optional[dict] = None           # its uploaded plan + queued teacher-forced tail
         self._drain = True
         self._drain_batch = True
@@ -585,8 +590,8 @@ class SweepRunner:
 
     def _resumable(self, cell_pairs: Sequence[Pair]) -> bool:
         return self.layer_resume and self.prefix_share and bool(cell_pairs) and all(
-            p.kv_slot >= 0 and self._kv_owner.get(p.kv_slot) == id(p) and p.lens_cum is not None
-            and p.resid is not None for p in cell_pairs)
+            p.kv_slot >= 0 and self._kv_owner.get(p.kv_slot) == id(p) and
+            (p.lens_cum is not None or self.lazy_cum) and p.resid is not None for p in cell_pairs)
 
     def _set_adapters(self, slot_pairs: Sequence[Pair]) -> None:
         """Slot ``i`` runs the LoRA adapter of ``slot_pairs[i]``'s word (multi-adapter bank)."""
@@ -645,7 +650,7 @@ class SweepRunner:
         self._tick("decode")
         resp = [out.response_ids(i) for i in range(n)]
         lr = self._readout(rows_pairs, out.n_gen, resp, [p.track for p in rows_pairs],
-                           keep_cum=bool(rb) and self.layer_resume and self.prefix_share)
+                           keep_cum=bool(rb) and self.layer_resume and self.prefix_share and not self.lazy_cum)
         self._tick("lens")
         if rb:
             self._finalize_baselines(rb, out, lr, list(range(nc, n)))
@@ -889,7 +894,7 @@ class SweepRunner:
         if nr:
             resp_r = [out.response_ids(j) for j in range(nr)]
             lr_r = self._readout(rb, out.n_gen[:nr], resp_r, [p.track for p in rb], seqs=list(range(nc, nc + nr)),
-                                 keep_cum=True)
+                                 keep_cum=not self.lazy_cum)
             self._tick("baseline_lens")
             self._finalize_baselines(rb, out, lr_r, list(range(nr)), slots=list(range(nc, nc + nr)))
             self._tick("baseline_finalize")
@@ -1077,6 +1082,7 @@ class SweepRunner:
             ex[:, 1] = np.where(pos > 0, cur[cell_of, np.maximum(pos - 1, 0)], -1)
         self._tick("ro_entries")
         self.stats["lens_rows"] += R
+        self._ensure_cum(ulist)
         base = self._lens_base(cell_pairs, d_a.tolist(), ng_a.tolist())
         self._tick("ro_base")
         acc, pr_d = lens_packed(m, self.store, rows, offs, base, trk, ex, sync=False)
@@ -1152,6 +1158,32 @@ class SweepRunner:
             results.append(self._cell_record(c, p, ng, resp, stats, dec, topk, float(cols["nll"][b]),
                                              float(cols["sn"][b])))
         return results
+
+    @torch.no_grad()
+    def _ensure_cum(self, pairs: Sequence[Pair]) -> None:
+        """Running lens sums of ``pairs`` (lazy mode): recomputed from each pair's hooked-layer residuals with
+        the same lens readout its baseline ran; sums rebuilt for earlier batches are released first."""
+        need = [p for p in pairs if p.lens_cum is None and p.resid is not None]
+        if not need:
+            return
+        keep = {id(p) for p in pairs}
+        for q in self._cum_live:
+            if id(q) not in keep:
+                q.lens_cum = None
+        self._cum_live = [q for q in self._cum_live if id(q) in keep]
+        nmax = max(1, max(len(p.resp) for p in need))
+        tmp = torch.zeros(len(need), nmax + 1, self.D, dtype=self.store.dtype, device=self.dev)
+        for i, p in enumerate(need):
+            if len(p.resp):
+                tmp[i, : len(p.resp)] = p.resid[: len(p.resp)]
+        resp = [list(p.resp) for p in need]
+        excl = [reference_exclusions(self.tok, r) for r in resp] if self.exclusion == "reference" else None
+        lr = lens_readout(self.m, tmp, [0] * len(need), [len(r) for r in resp], [p.track for p in need],
+                          top_k=self.cfg.model.top_k, exclusion=self.exclusion, excl_pairs=excl,
+                          response_ids=resp, keep_cum=True)
+        for p, c in zip(need, lr.cum):
+            p.lens_cum = c
+        self._cum_live += need
 
     def _lens_base(self, cell_pairs: Sequence[Pair], Dc: Sequence[int], ngen: Sequence[int]) -> torch.Tensor:
         """Reused part of each cell's response lens sum: the baseline's running sum up to the divergence
