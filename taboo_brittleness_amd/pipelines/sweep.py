@@ -166,6 +166,7 @@ class SweepRunner:
         # ahead): only the running batch's pairs hold them (~18 GB less at 90 pairs per step)
         self.lazy_cum = os.environ.get("TB_LAZY_LENS_CUM", "1") == "1"
         self._cum_live: List[Pair] = []
+        self._carry_move_pending = None
         self._staged: Optional[dict] = None           # its uploaded plan + queued teacher-forced tail
         self._drain = True
         self._drain_batch = True
@@ -464,7 +465,12 @@ class SweepRunner:
     def _launch_staged_next(self) -> None:
         nb = getattr(self, "_next", None)
         self._next = None
-        if nb is None or not (self.layer_resume and self.prefix_share) or self._carry or self.carry_rows:
+        # carried decode rows move out of the cell slots before the next tail writes them (stream order)
+        mv = self._carry_move_pending
+        self._carry_move_pending = None
+        if mv is not None:
+            mv()
+        if nb is None or not (self.layer_resume and self.prefix_share):
             return
         nb.resolve(self)
         cp = [nb.pairs[c.pair] for c in nb.cells]
@@ -473,10 +479,12 @@ class SweepRunner:
             return
         plan = nb.plan if nb.plan is not None else self._plan_for(nb.cells, nb.pairs, {}, with_carry=False)
         nb.plan = plan
+        if self._carry:                          # the next decode continues this batch's carried rows
+            plan = self._plan_add_carry({k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in plan.items()})
         self._set_adapters(cp)
         hook = self._load_plan(plan)
         tf = self._tf_launch(cp, {self.layer: [hook, self.capture]})
-        self._staged = {"cells": nb.cells, "plan": plan, "tf": tf}
+        self._staged = {"cells": nb.cells, "plan": plan, "tf": tf, "carry": list(self._carry)}
         self._tick("next_tf_launched")
 
     # --------------------------------------------------------- prefix sharing
@@ -699,7 +707,9 @@ class SweepRunner:
         l0, L = self.layer, m.spec.layers
         staged = self._staged
         self._staged = None
-        if staged is not None and (len(staged["cells"]) != len(batch) or self._carry or
+        if staged is not None and (len(staged["cells"]) != len(batch) or
+                                   len(staged["carry"]) != len(self._carry) or
+                                   any(a is not b for a, b in zip(staged["carry"], self._carry)) or
                                    any(a is not b for a, b in zip(staged["cells"], batch))):
             staged = None                       # staged for another batch: its writes are simply overwritten
         if staged is not None:                  # plan uploaded and teacher-forced tail queued by the last batch
@@ -921,9 +931,13 @@ class SweepRunner:
                 entries.append((c, p, b, D[b], nll_c[b], None, drow[b]))
         for cr, j in fin_carry:
             entries.append((cr.cell, cr.pair, cr.slot, cr.d, cr.nll, None, j))
+        # the carry move runs after the readout has read the finished carried cells' store rows, and before
+        # a staged next tail overwrites the cell slots (_launch_staged_next runs it at that point)
+        self._carry_move_pending = carry_move
         results = self._resume_readout(entries, out) if entries else []
-        if carry_move is not None:      # after the readout has read the finished carried cells' store rows
-            carry_move()
+        if self._carry_move_pending is not None:
+            self._carry_move_pending()
+            self._carry_move_pending = None
         self._tick("results")
         return results
 

@@ -324,12 +324,13 @@ def test_cross_batch_pipeline_is_exact():
                                    "prompts=['Give me a hint!', 'Any hints available?', 'I need one more clue.']"])
     tok = SyntheticTokenizer(vocab_size=spec.vocab_size)
     key = lambda r: (r["word"], r["prompt_idx"], r["method"], r["budget"], r["trial"])   # noqa: E731
-    res, staged_used = {}, {}
+    res, staged_used, carried = {}, {}, {}
     methods = ("sae_targeted", "sae_random")
-    for pipe in (False, True):
+    for pipe, carry in ((False, 0), (True, 0), (True, 6)):
         sae = JumpReLUSAE.random(spec.hidden, 512, seed=2, device="cpu")
-        r = SweepRunner(cfg, m, tok, sae, batch=30, device="cpu", layer=1, use_graphs=False,
+        r = SweepRunner(cfg, m, tok, sae, batch=30 + carry, device="cpu", layer=1, use_graphs=False,
                         prefix_share=True, layer_resume=True, kv_pairs=8)
+        r.carry_rows = carry
         pairs = r.build_pairs(["ship"], cfg.prompts[:3])
         r.run_baselines(pairs)
         subs = [[pairs[0]], [pairs[1]], [pairs[2]]]
@@ -339,16 +340,23 @@ def test_cross_batch_pipeline_is_exact():
             if pipe and i + 1 < len(subs):
                 nb = NextBatch(subs[i + 1], methods)
                 r.stage_next(nb)
-            got = r.run_cells(sub, cells[i], measure_nll=True)
+            got = r.run_cells(sub, cells[i], measure_nll=True, drain=(i == len(subs) - 1))
             out += got
             if i + 1 < len(subs):
                 cells[i + 1] = nb.cells if pipe else r.make_cells(subs[i + 1], methods)
-        res[pipe] = {key(x): x for x in out}
-        staged_used[pipe] = r.stats["staged"]
-    assert staged_used[True] == 2                                # both later batches were staged
-    assert set(res[False]) == set(res[True])
-    for k, a in res[False].items():
-        b = res[True][k]
+        res[(pipe, carry)] = {key(x): x for x in out}
+        staged_used[(pipe, carry)] = r.stats["staged"]
+        carried[(pipe, carry)] = r.stats["carried"]
+    assert staged_used[(True, 0)] == 2 and staged_used[(True, 6)] == 2   # both later batches were staged
+    assert carried[(True, 6)] > 0                                         # ... also with carried decode rows
+    for cfg_ in ((True, 0), (True, 6)):
+        assert set(res[(False, 0)]) == set(res[cfg_])
+        _same_records(res[(False, 0)], res[cfg_])
+
+
+def _same_records(ra, rb):
+    for k, a in ra.items():
+        b = rb[k]
         assert a["response_ids"] == b["response_ids"], k
         assert a["topk_ids"] == b["topk_ids"], k
         assert abs(a["nll_edit"] - b["nll_edit"]) < 1e-6 and abs(a["nll_self"] - b["nll_self"]) < 1e-6
