@@ -190,3 +190,52 @@ def test_sweep_gpu_decode_tail_carry(gpu):
         if a["response_ids"] == b["response_ids"]:
             assert abs(a["nll_edit"] - b["nll_edit"]) < 0.05
             assert len(set(a["topk_ids"]) & set(b["topk_ids"])) >= 4
+
+
+def test_sweep_gpu_cross_step_pipeline(gpu):
+    """The bench's cross-step pipeline on the GPU (staged plan upload + teacher-forced tail queued behind the
+    previous batch's lens, pinned async D2H, records on the host thread, graph-replayed decode), with and
+    without decode-tail carry-over: the same records as running the batches one after the other."""
+    from taboo_brittleness_amd.config import load_config
+    from taboo_brittleness_amd.interp.sae import JumpReLUSAE
+    from taboo_brittleness_amd.models.tokenizer import SyntheticTokenizer
+    from taboo_brittleness_amd.pipelines.sweep import NextBatch, SweepRunner
+
+    cfg = load_config(None, ["experiment.max_new_tokens=12", "intervention.budgets=[1, 4, 16]",
+                             "intervention.random_trials=3"])
+    mg = Gemma2Model(random_gemma2(SPEC, dtype=torch.bfloat16, seed=5, norm_std=0.1, post_norm_gain=8.0,
+                                   device=gpu), gpu)
+    tok = SyntheticTokenizer(vocab_size=SPEC.vocab_size)
+    key = lambda r: (r["word"], r["prompt_idx"], r["method"], r["budget"], r["trial"])   # noqa: E731
+    methods = ("sae_targeted", "sae_random")
+    out, stats = {}, {}
+    for pipe, carry in ((False, 0), (True, 0), (True, 16)):
+        sae = JumpReLUSAE.random(SPEC.hidden, 1024, seed=2, device=gpu)
+        r = SweepRunner(cfg, mg, tok, sae, batch=40 + carry, device=gpu, layer=2, prefix_share=True,
+                        layer_resume=True, kv_pairs=8)
+        r.carry_rows = carry
+        pairs = r.build_pairs(["ship"], cfg.prompts[:3])
+        r.run_baselines(pairs)
+        subs = [[p] for p in pairs]
+        cells = r.make_cells(subs[0], methods)
+        res = []
+        for i, sub in enumerate(subs):
+            nb = None
+            if pipe and i + 1 < len(subs):
+                nb = NextBatch(subs[i + 1], methods)
+                r.stage_next(nb)
+            res += r.run_cells_async(sub, cells, drain=(i == len(subs) - 1)).result()
+            if i + 1 < len(subs):
+                cells = nb.cells if nb is not None and nb.cells is not None else r.make_cells(subs[i + 1], methods)
+        out[(pipe, carry)] = {key(x): x for x in res}
+        stats[(pipe, carry)] = dict(r.stats)
+    assert stats[(True, 0)]["staged"] == 2 and stats[(True, 16)]["staged"] == 2
+    for cfg_ in ((True, 0), (True, 16)):
+        assert set(out[(False, 0)]) == set(out[cfg_])
+        same = [out[(False, 0)][k]["response_ids"] == out[cfg_][k]["response_ids"] for k in out[(False, 0)]]
+        assert sum(same) >= int(0.95 * len(same))
+        for k, a in out[(False, 0)].items():
+            b = out[cfg_][k]
+            if a["response_ids"] == b["response_ids"]:
+                assert abs(a["nll_edit"] - b["nll_edit"]) < 0.05
+                assert len(set(a["topk_ids"]) & set(b["topk_ids"])) >= 4
