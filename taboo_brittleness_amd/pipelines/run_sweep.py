@@ -210,10 +210,15 @@ def _run_parts(runner, pairs, cells, mine: List[int], out_dir: str, dp_rank: int
     fault_after = int(os.environ.get("TB_FAULT_AFTER_PARTS", "-1"))
     n_parts = len([f for f in os.listdir(pdir)]) if os.path.isdir(pdir) else 0
     committed = 0
-    for c0 in range(0, len(todo), max(1, chunk)):
-        ids = todo[c0:c0 + chunk]
+    from .sweep import NextBatch
+
+    chunks = [todo[c0:c0 + max(1, chunk)] for c0 in range(0, len(todo), max(1, chunk))]
+    batch_cells = [[cells[i] for i in ids] for ids in chunks]
+    for k, ids in enumerate(chunks):
         t = time.perf_counter()
-        res = runner.run_cells(pairs, [cells[i] for i in ids])
+        if k + 1 < len(chunks) and hasattr(runner, "stage_next"):    # cross-batch pipeline: the next chunk's tail queues behind this one's readout
+            runner.stage_next(NextBatch(pairs, cells=batch_cells[k + 1]))
+        res = runner.run_cells(pairs, batch_cells[k])
         _check_comm(tp_ctx, elog, f"part_{n_parts:05d}")     # before anything of this chunk is committed
         for r, i in zip(res, ids):
             r["cell_id"] = i
@@ -223,7 +228,8 @@ def _run_parts(runner, pairs, cells, mine: List[int], out_dir: str, dp_rank: int
             atomic_write_json(os.path.join(pdir, f"part_{n_parts:05d}.json"), {"results": res})
         n_parts += 1
         committed += 1
-        elog.write("part", cells=len(ids), seconds=round(time.perf_counter() - t, 4), remaining=len(todo) - c0 - len(ids))
+        elog.write("part", cells=len(ids), seconds=round(time.perf_counter() - t, 4),
+                   remaining=sum(len(x) for x in chunks[k + 1:]))
         if fault_after >= 0 and committed >= fault_after:
             raise RuntimeError(f"injected fault after {committed} part(s) (TB_FAULT_AFTER_PARTS)")
     return [done[i] for i in mine]

@@ -474,10 +474,13 @@ class SweepRunner:
             return
         nb.resolve(self)
         cp = [nb.pairs[c.pair] for c in nb.cells]
+        proj = any(c.kind == "proj" for c in nb.cells)
         if not nb.cells or len(nb.cells) > self.B or not self._resumable(cp) or \
-                any(c.kind != "sae" for c in nb.cells):
+                (proj and (self._plan is None or self._plan.basis is None)):
             return
-        plan = nb.plan if nb.plan is not None else self._plan_for(nb.cells, nb.pairs, {}, with_carry=False)
+        if nb.plan is None:      # bases pooled over the call's pairs, as run_cells computes them
+            nb.plan = self._plan_for(nb.cells, nb.pairs, self._bases(nb.pairs) if proj else {}, with_carry=False)
+        plan = nb.plan
         nb.plan = plan
         if self._carry:                          # the next decode continues this batch's carried rows
             plan = self._plan_add_carry({k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in plan.items()})

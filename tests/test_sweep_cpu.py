@@ -362,3 +362,23 @@ def _same_records(ra, rb):
         assert abs(a["nll_edit"] - b["nll_edit"]) < 1e-6 and abs(a["nll_self"] - b["nll_self"]) < 1e-6
         for f in ("p_secret_mean", "p_secret_final", "p_secret_max"):
             assert abs(a[f] - b[f]) < 1e-7 + 1e-6 * abs(a[f])
+
+
+def test_cli_sweep_pipelined_chunks_match_unchunked(tmp_path):
+    """run_sweep's chunked, pipelined execution (projection cells included) gives the records of one
+    batch holding every cell."""
+    from taboo_brittleness_amd.parallel import dist as D
+    from taboo_brittleness_amd.pipelines.run_sweep import run_sweep
+
+    info = D.init_distributed("gloo", "cpu")
+    outs = {}
+    for bs in (8, 400):
+        cfg = load_config(None, [o for o in OVR if not o.startswith("runtime.batch_size")] +
+                          [f"runtime.batch_size={bs}"])
+        run_sweep(cfg, str(tmp_path / f"b{bs}"), info=info, log=lambda *a: None)
+        outs[bs] = _cells(str(tmp_path / f"b{bs}"))
+    assert set(outs[8]) == set(outs[400])
+    for k, a in outs[400].items():
+        b = outs[8][k]
+        assert a["response_ids"] == b["response_ids"] and a["topk_ids"] == b["topk_ids"], k
+        assert abs(a["nll_edit"] - b["nll_edit"]) < 1e-4
