@@ -382,3 +382,35 @@ def test_cli_sweep_pipelined_chunks_match_unchunked(tmp_path):
         b = outs[8][k]
         assert a["response_ids"] == b["response_ids"] and a["topk_ids"] == b["topk_ids"], k
         assert abs(a["nll_edit"] - b["nll_edit"]) < 1e-4
+
+
+def test_lazy_running_sums_match_kept_sums(monkeypatch):
+    """Running lens sums rebuilt from the pairs' residuals when their cells run (default) give the records
+    of sums kept from each baseline on (TB_LAZY_LENS_CUM=0)."""
+    from dataclasses import replace
+
+    from taboo_brittleness_amd.interp.sae import JumpReLUSAE
+    from taboo_brittleness_amd.models.gemma2 import Gemma2Model
+    from taboo_brittleness_amd.models.spec import GEMMA2_TINY
+    from taboo_brittleness_amd.models.tokenizer import SyntheticTokenizer
+    from taboo_brittleness_amd.models.weights import random_gemma2
+    from taboo_brittleness_amd.pipelines.sweep import SweepRunner
+
+    spec = replace(GEMMA2_TINY, vocab_size=1024, layers=3, hidden=256, ffn=512)
+    m = Gemma2Model(random_gemma2(spec, dtype=torch.bfloat16, seed=7, norm_std=0.1, post_norm_gain=8.0), "cpu")
+    cfg = load_config(None, OVR + ["experiment.max_new_tokens=10"])
+    tok = SyntheticTokenizer(vocab_size=spec.vocab_size)
+    res = {}
+    for lazy in ("0", "1"):
+        monkeypatch.setenv("TB_LAZY_LENS_CUM", lazy)
+        sae = JumpReLUSAE.random(spec.hidden, 512, seed=2, device="cpu")
+        r = SweepRunner(cfg, m, tok, sae, batch=24, device="cpu", layer=1, use_graphs=False, prefix_share=True,
+                        layer_resume=True)
+        pairs = r.build_pairs(["ship"], cfg.prompts[:2])
+        r.run_baselines(pairs)
+        assert all((p.lens_cum is None) == (lazy == "1") for p in pairs)
+        res[lazy] = r.run_cells(pairs, r.make_cells(pairs), measure_nll=True)
+    for a, b in zip(res["0"], res["1"]):
+        assert a["response_ids"] == b["response_ids"] and a["topk_ids"] == b["topk_ids"]
+        for k in ("p_secret_mean", "p_secret_final", "p_secret_max", "nll_edit"):
+            assert abs(a[k] - b[k]) < 1e-6 + 1e-5 * abs(a[k])
