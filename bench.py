@@ -89,6 +89,9 @@ def main() -> None:
                          "whose random Gemma-2 repeats its input token so no edit ever changes a generation "
                          "(diverged_frac 0); 32 gives text-like outputs (~34 distinct tokens per 50) and "
                          "edits that change ~2/3 of the generations")
+    ap.add_argument("--fused-geglu", action="store_true",
+                    help="gate|up GEMM with the GeGLU in its epilogue (ping-pong MFMA kernel, csrc/gemm.hip) "
+                         "instead of hipBLASLt + the GeGLU kernel")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="do not queue the next step's teacher-forced tail behind this step's readout")
     ap.add_argument("--profile-steps", action="store_true", help="print per-phase timings per step")
@@ -114,6 +117,7 @@ def main() -> None:
         enable_tuned_gemms(tag, tune=args.tune_gemms)
     weights = random_gemma2(spec, device=dev, dtype=torch.bfloat16, seed=1234, post_norm_gain=args.init_gain)
     model = Gemma2Model(weights, dev)
+    fused_geglu = bool(args.fused_geglu and model.enable_fused_geglu())
     if args.lora_rank > 0:
         from taboo_brittleness_amd.models.lora import LoRABank
 
@@ -286,6 +290,7 @@ def main() -> None:
                 "layer_resume": not args.no_layer_resume,
                 "baseline_every": E,
                 "carry_rows": C,
+                "fused_geglu": fused_geglu,
                 "lora_adapters": (f"{len(cfg.words)} x rank {args.lora_rank} (unmerged bank)" if args.lora_rank
                                   else "none (weights as merged taboo models)"),
             },

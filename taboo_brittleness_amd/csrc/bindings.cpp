@@ -347,6 +347,30 @@ void gemm_nt(torch::Tensor A, torch::Tensor W, torch::Tensor C, c10::optional<to
   tb_gemm_nt(cbf(A), cbf(W), C.data_ptr(), optf(bias), optf(thr), M, N, K, N, (int)epi, cur_stream());
 }
 
+// Ping-pong 256x256x64 MFMA GEMM (gemm.hip).  epi 0: bf16 C[M,N]; 1: f32 C; 2: JumpReLU f32 C
+// (bias/thr [N]); 3: GeGLU bf16 C[M,N/2] from gate|up rows interleaved by gemm_pp_geglu_order().
+void gemm_pp(torch::Tensor A, torch::Tensor W, torch::Tensor C, c10::optional<torch::Tensor> bias,
+             c10::optional<torch::Tensor> thr, int64_t epi) {
+  IN_BF16(A); IN_BF16(W); CHECK_DEV(C); CHECK_CONTIG(C);
+  TORCH_CHECK(W.dim() == 2, "gemm_pp: W must be [N, K]");
+  const int K = A.size(-1), M = A.numel() / K, N = W.size(0);
+  TORCH_CHECK(W.size(1) == K, "gemm_pp: K mismatch");
+  TORCH_CHECK(tb_gemm_pp_ok(M, N, K), "gemm_pp: need N % 256 == 0, K % 64 == 0, K >= 64");
+  TORCH_CHECK(epi >= 0 && epi <= 3, "gemm_pp: epi must be 0..3");
+  const int64_t ncols = epi == 3 ? N / 2 : N;
+  TORCH_CHECK(C.numel() == (int64_t)M * ncols, "gemm_pp: C shape");
+  TORCH_CHECK(C.scalar_type() == ((epi == 0 || epi == 3) ? at::kBFloat16 : at::kFloat), "gemm_pp: C dtype");
+  if (epi == 2) {
+    TORCH_CHECK(!bias.has_value() || !bias->defined() || bias->numel() == N, "gemm_pp: bias numel must be N");
+    TORCH_CHECK(!thr.has_value() || !thr->defined() || thr->numel() == N, "gemm_pp: thr numel must be N");
+  }
+  c10::DeviceGuard g(A.device());
+  tb_gemm_pp(cbf(A), cbf(W), C.data_ptr(), epi == 2 ? optf(bias) : nullptr, epi == 2 ? optf(thr) : nullptr, M, N, K,
+             (int)ncols, (int)epi, cur_stream());
+}
+
+bool gemm_pp_ok(int64_t M, int64_t N, int64_t K) { return tb_gemm_pp_ok(M, N, K); }
+
 void lowrank_edit(torch::Tensor h, c10::optional<torch::Tensor> x_next, torch::Tensor apply, torch::Tensor idx,
                   torch::Tensor cnt, torch::Tensor E, torch::Tensor Dm, c10::optional<torch::Tensor> bias,
                   c10::optional<torch::Tensor> thr, c10::optional<torch::Tensor> pre_bias, double alpha,
@@ -495,6 +519,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("decode_head", &decode_head);
   m.def("register_softcap_table", &register_softcap_table);
   m.def("gemm_nt", &gemm_nt);
+  m.def("gemm_pp", &gemm_pp);
+  m.def("gemm_pp_ok", &gemm_pp_ok);
   m.def("gemm_skinny", &gemm_skinny);
   m.def("gemm_skinny_ok", &gemm_skinny_ok);
   m.def("lowrank_edit", &lowrank_edit);

@@ -10,15 +10,6 @@
 
 namespace {
 
-// gelu_tanh(x) = 0.5 x (1 + tanh(y)) = x / (1 + exp(-2y)), y = k0 (x + k1 x^3): one v_exp + one v_rcp instead
-// of a libm tanhf (the kernel then streams at HBM rate); differs from the tanhf form by ~1e-6 relative before
-// the bf16 rounding.  exp overflow gives x / inf = 0 (the x -> -inf limit), underflow gives x.
-__device__ __forceinline__ float gelu_tanh_fast(float x) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  const float y = k0 * (x + k1 * x * x * x);
-  return x * __frcp_rn(1.f + __expf(-2.f * y));
-}
-
 // grid (M, ceil(F / 8 / 256)): one 16-B vector of gate and of up per thread, no index division
 __global__ void __launch_bounds__(256) geglu_kernel(const uint16_t* __restrict__ gu, uint16_t* __restrict__ out, int F) {
   const int c = blockIdx.y * 256 + threadIdx.x;

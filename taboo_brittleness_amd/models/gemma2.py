@@ -26,6 +26,7 @@ with NO final softcap) is ``lens_logits``.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
@@ -164,9 +165,26 @@ class Gemma2Model:
         self._ws: Dict[int, _Workspace] = {}
         self.max_workspaces = 4
         self.lora = None          # optional models.lora.LoRABank (multi-adapter batching)
+        # gate|up GEMM with the GeGLU in its epilogue (csrc/gemm.hip): per-layer gate|up weights in the
+        # kernel's interleaved row order (+2·ffn·d bf16 per layer); TB_FUSED_GEGLU=1 or enable_fused_geglu()
+        self._wgu_il: Optional[list] = None
+        if os.environ.get("TB_FUSED_GEGLU", "0") == "1":
+            self.enable_fused_geglu()
+
+    def enable_fused_geglu(self) -> bool:
+        """Switch the MLP's gate|up GEMM + GeGLU to the fused ping-pong MFMA kernel (GPU, no LoRA bank);
+        returns whether it is on.  Numerics: the GeGLU reads the fp32 accumulators rounded to bf16, i.e.
+        the unfused bf16 graph up to the GEMM's summation order."""
+        ls = self.lspec
+        if self.device.type != "cuda" or self.lora is not None or ls.ffn % 128 or ls.hidden % 64:
+            return False
+        idx = ops.geglu_interleave_index(ls.ffn, self.device)
+        self._wgu_il = [L.wgu.index_select(0, idx).contiguous() for L in self.w.layers]
+        return True
 
     def set_lora(self, bank) -> None:
         assert self.tp is None, "LoRA banks are not sharded for tensor parallelism; merge adapters instead"
+        self._wgu_il = None        # the bank adds its gate|up delta between the GEMM and the GeGLU
         self.lora = bank
 
     # ------------------------------------------------------------------ utils
@@ -279,10 +297,13 @@ class Gemma2Model:
             if self.tp is not None:
                 self.tp.all_reduce_(ws.o)
             ops.add_rmsnorm2(h, ws.o, L.ln_post_attn, L.ln_pre_ffn, s.eps, out=x)
-            ops.linear(x, L.wgu, out=ws.gu)
-            if lora is not None:
-                lora.apply(l, "gu", x, ws.gu, lmask)
-            ops.geglu(ws.gu, out=ws.act)
+            if self._wgu_il is not None:
+                ops.gate_up_geglu(x, self._wgu_il[l], out=ws.act)
+            else:
+                ops.linear(x, L.wgu, out=ws.gu)
+                if lora is not None:
+                    lora.apply(l, "gu", x, ws.gu, lmask)
+                ops.geglu(ws.gu, out=ws.act)
             ops.linear(ws.act, L.wdown, out=ws.o)
             if lora is not None:
                 lora.apply(l, "down", ws.act, ws.o, lmask)

@@ -339,16 +339,54 @@ def decode_head(logits, cap, tgt=None, nxt=None, nll_self=None, nll_tgt=None):
 
 
 def gemm_nt(A, W, epi=0, bias=None, thr=None, out=None):
-    """C = A @ W^T on the MFMA kernel; epi 0 = bf16, 1 = fp32, 2 = JumpReLU(acc + bias, thr) fp32."""
+    """C = A @ W^T on an MFMA kernel; epi 0 = bf16, 1 = fp32, 2 = JumpReLU(acc + bias, thr) fp32.
+    Shapes with N % 256 == 0 and K % 64 == 0 (the SAE encode: N = 16384, K = 3584) run the ping-pong
+    256x256 kernel (csrc/gemm.hip, ~1.3 PFLOP/s); others the 128x128 ``gemm_nt`` kernel (csrc/sae.hip)."""
     M = A.numel() // A.shape[-1]
     N = W.shape[0]
     if A.is_cuda:
         out = _out(out, (M, N), BF16 if epi == 0 else torch.float32, A.device)
-        _k().gemm_nt(A, W, out, bias, thr, int(epi))
+        if _k().gemm_pp_ok(M, N, A.shape[-1]) and A.is_contiguous():
+            _k().gemm_pp(A, W, out, bias, thr, int(epi))
+        else:
+            _k().gemm_nt(A, W, out, bias, thr, int(epi))
         return out
     y = ref.gemm_nt(A, W, epi, bias, thr)
     if out is not None:
         out.copy_(y.view_as(out))
+        return out
+    return y
+
+
+def geglu_interleave_index(F: int, device=None) -> torch.Tensor:
+    """Row order of a gate|up weight ``[2F, K]`` for the fused GeGLU epilogue of ``gemm_pp`` (epi 3):
+    every 256-row tile holds features ``f0 .. f0+127`` as two 128-row wave-group slices
+    ``[gate 64 | up 64]``, so a lane's gate and up accumulators of the same feature land in the same
+    lane (csrc/gemm.hip).  Needs F % 128 == 0."""
+    assert F % 128 == 0, "fused GeGLU needs ffn % 128 == 0"
+    p = torch.arange(2 * F)
+    tile, q = p // 256, p % 256
+    g, half, rest = q // 128, (q // 64) % 2, q % 64
+    return (half * F + tile * 128 + g * 64 + rest).to(device)
+
+
+reference_geglu = ref.geglu
+
+
+def gate_up_geglu(x: torch.Tensor, w_gu_interleaved: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``geglu(x @ w_gu^T)`` in one ping-pong MFMA GEMM whose epilogue applies GeGLU to the fp32 accumulators
+    (rounded to bf16 first, so the result equals the unfused bf16 graph up to the GEMM's summation order);
+    ``w_gu_interleaved = w_gu[geglu_interleave_index(F)]``."""
+    M = x.numel() // x.shape[-1]
+    F = w_gu_interleaved.shape[0] // 2
+    if x.is_cuda:
+        out = _out(out, x.shape[:-1] + (F,), BF16, x.device)
+        _k().gemm_pp(x, w_gu_interleaved, out, None, None, 3)
+        return out
+    inv = torch.argsort(geglu_interleave_index(F))
+    y = ref.geglu((x.reshape(M, -1).float() @ w_gu_interleaved[inv].float().T).to(BF16)).view(x.shape[:-1] + (F,))
+    if out is not None:
+        out.copy_(y)
         return out
     return y
 

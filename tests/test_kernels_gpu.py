@@ -266,6 +266,37 @@ def test_gemm_nt_epilogues(gpu, M, N, K):
     assert ((jr - want).abs()[~near] < 1e-3).all()
 
 
+@pytest.mark.parametrize("M,N,K", [(1, 256, 64), (37, 512, 128), (300, 768, 3584), (513, 1024, 640)])
+def test_gemm_pp_epilogues(gpu, M, N, K):
+    """Ping-pong 256x256 MFMA GEMM (csrc/gemm.hip) vs a float32 PyTorch reference: every epilogue,
+    ragged M (clamped loads, masked stores), several K-tile counts (1, 2, 10, 56)."""
+    torch.manual_seed(11)
+    A = (torch.rand(M, K) * 2 - 1).to(BF)
+    W = (torch.rand(N, K) * 2 - 1).to(BF)
+    b = torch.randn(N)
+    th = torch.rand(N) * 2
+    Ag, Wg = A.to(gpu), W.to(gpu)
+    k = ops._k()
+    r = A.float() @ W.float().T
+    c32 = torch.empty(M, N, device=gpu)
+    k.gemm_pp(Ag, Wg, c32, None, None, 1)
+    _close(c32, r, atol=1e-3 * K ** 0.5, rtol=1e-4)
+    cb = torch.empty(M, N, device=gpu, dtype=BF)
+    k.gemm_pp(Ag, Wg, cb, None, None, 0)
+    _close(cb, r, atol=1e-2 * K ** 0.5, rtol=1e-2)
+    k.gemm_pp(Ag, Wg, c32, b.to(gpu), th.to(gpu), 2)
+    pre = r + b
+    near = (pre - th).abs() < 1e-3
+    want = torch.where(pre > th, pre, torch.zeros_like(pre))
+    assert ((c32.cpu() - want).abs()[~near] < 1e-3 * K ** 0.5).all()
+    # fused GeGLU over the interleaved gate|up weight == geglu(bf16 gate|up GEMM output)
+    Wi = Wg[ops.geglu_interleave_index(N // 2, gpu)].contiguous()
+    act = ops.gate_up_geglu(Ag, Wi)
+    want = ref.geglu(r.to(BF)).float()
+    _close(act, want, atol=2e-2 * K ** 0.5, rtol=2e-2)
+    assert torch.equal(ops.gate_up_geglu(Ag, Wi), act)     # deterministic (no split-K)
+
+
 def test_lowrank_edit_sae_and_projection(gpu):
     torch.manual_seed(6)
     M, D, L, mmax = 9, 512, 300, 8

@@ -1,0 +1,22 @@
+#!/bin/bash
+# Build (on the CPU container) one gemm_lab executable per knob setting: tools/lab/gemm_lab.sh build
+# Run them on the GPU box:                                                tools/lab/gemm_lab.sh run
+set -e
+cd "$(dirname "$0")"
+VARIANTS=("base:" "ph2:-DPP_PHASES=2" "ph2noprio:-DPP_PHASES=2 -DPP_SETPRIO=0" "ph2nolds:-DPP_PHASES=2 -DPP_NO_LDS_READ=1")
+if [ "$1" = build ]; then
+  for v in "${VARIANTS[@]}"; do
+    name=${v%%:*}; flags=${v#*:}
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 $flags gemm_lab.hip -o gemm_lab_$name &
+  done
+  wait
+  ls -la gemm_lab_*
+else
+  mkdir -p ../../gpurun_out
+  for v in "${VARIANTS[@]}"; do
+    name=${v%%:*}
+    for shp in "4096 28672 3584 0" "4096 28672 3584 3" "4096 8192 3584 0" "2048 28672 3584 3" "8192 8192 3584 0"; do
+      echo -n "{\"variant\": \"$name\", \"r\": "; timeout -k 5 60 ./gemm_lab_$name $shp; echo "}"
+    done
+  done
+fi
