@@ -533,6 +533,175 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// Decode, one wave per (sequence, kv head): NWH waves of a workgroup take NWH kv heads of one sequence and
+// never synchronise with each other (no __syncthreads, 2.5 KB of LDS per 4 waves), so many workgroups
+// share a CU.  At decode lengths (tens of keys) the 4-wave-per-head kernel above spent about half of its
+// time in per-workgroup latency chains (pos -> K -> scores -> softmax -> V -> cross-wave sum, three
+// barriers) with 8 workgroups per CU in flight (profiles/r2/attn_scan.log: 45 us at 1 key vs 208 us at
+// 67 keys for 2048 rows); here each wave streams its whole key range with the next K tile and the V
+// rows prefetched (issued before the scores are known), and the softmax weights p = rbf(exp(s - m)) are
+// computed once per key (not once per lane) and read back as LDS broadcasts.
+// Numerics = attn_decode_kernel: bf16-rounded softmax weights, fp32 sums, out = O / l.
+template <int HD, int G>
+__global__ void __launch_bounds__(256) attn_decode_wave_kernel(
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
+    uint16_t* __restrict__ out, const int32_t* __restrict__ pos, const int32_t* __restrict__ slot, int Hq, int Hkv,
+    int S, float scale, float softcap, int window, const uint16_t* __restrict__ pkc, const uint16_t* __restrict__ pvc,
+    const int32_t* __restrict__ pslot, const int32_t* __restrict__ plen) {
+  constexpr int KS = HD / 32;
+  constexpr int DPL = HD / 64;
+  constexpr int VCH = 8;                 // V rows per prefetch chunk
+  using VT = typename vrow_t<DPL>::type;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int nwh = blockDim.x >> 6;
+  const int b = blockIdx.x;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int kh = blockIdx.y * nwh + w;
+  const int grp = lane >> 4, col = lane & 15;
+  const int SS = (S + 15) & ~15;
+  float* sc = reinterpret_cast<float*>(smem) + (size_t)w * G * SS;   // this wave's [G][SS] scores / weights
+  uint16_t* ob = out + ((size_t)b * Hq + kh * G) * HD;
+  const int p = pos[b];
+  if (p < 0) {   // padding row
+    for (int e = lane; e < G * HD; e += 64) ob[e] = 0;
+    return;
+  }
+  const int kmax = p < S ? p : S - 1;
+  int kmin = 0;
+  if (window > 0) { kmin = p - window + 1; if (kmin < 0) kmin = 0; }
+  const int cs = slot[b];
+  const uint16_t* kbase = kc + ((size_t)cs * Hkv + kh) * (size_t)S * HD;
+  const uint16_t* vbase = vc + ((size_t)cs * Hkv + kh) * (size_t)S * HD;
+  int np = 0;
+  const uint16_t* kpre = kbase;
+  const uint16_t* vpre = vbase;
+  if (plen != nullptr) {
+    np = plen[b];
+    if (np > 0) {
+      const size_t po = ((size_t)pslot[b] * Hkv + kh) * (size_t)S * HD;
+      kpre = pkc + po;
+      vpre = pvc + po;
+    }
+  }
+  auto vload = [&](int j, VT (&v)[VCH]) {
+#pragma unroll
+    for (int u = 0; u < VCH; ++u) {
+      const int jj = j + u <= kmax ? j + u : kmax;
+      v[u] = *reinterpret_cast<const VT*>((jj < np ? vpre : vbase) + (size_t)jj * HD + lane * DPL);
+    }
+  };
+  // the first V chunk is independent of the scores: issue it first
+  VT va[VCH], vb[VCH];
+  vload(kmin, va);
+  bf16x8 qa[KS];
+  {
+    const uint16_t* qrow = q + ((size_t)b * Hq + kh * G + (col < G ? col : 0)) * HD;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      uint4 u = {0, 0, 0, 0};
+      if (col < G) u = *reinterpret_cast<const uint4*>(qrow + ks * 32 + grp * 8);
+      qa[ks] = as_bf16x8(u);
+    }
+  }
+  const float inv_cap = softcap > 0.f ? 1.f / softcap : 0.f;
+  auto kload = [&](int t, uint4 (&kf)[KS]) {
+    const int kk = t * 16 + col;
+    const int kr = kk < kmin ? kmin : (kk > kmax ? kmax : kk);
+    const uint16_t* krow = (kr < np ? kpre : kbase) + (size_t)kr * HD + grp * 8;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) kf[ks] = *reinterpret_cast<const uint4*>(krow + ks * 32);
+  };
+  auto score = [&](int t, const uint4 (&kf)[KS]) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[ks], as_bf16x8(kf[ks]), acc, 0, 0, 0);
+    const int kk = t * 16 + col;
+    if (grp == 0) {   // query rows 0..3 of the 16-row tile live in lanes 0..15
+#pragma unroll
+      for (int h = 0; h < G; ++h) {
+        float s = acc[h] * scale;
+        if (softcap > 0.f) s = tanhf(s * inv_cap) * softcap;
+        sc[h * SS + kk] = (kk >= kmin && kk <= kmax) ? s : -INFINITY;
+      }
+    }
+  };
+  const int t0 = kmin >> 4, t1 = kmax >> 4;
+  uint4 ka[KS], kb[KS];
+  kload(t0, ka);
+  for (int t = t0; t <= t1; t += 2) {
+    if (t + 1 <= t1) kload(t + 1, kb);
+    score(t, ka);
+    if (t + 1 <= t1) {
+      if (t + 2 <= t1) kload(t + 2, ka);
+      score(t + 1, kb);
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // softmax weights, in place: p = rbf(exp(s - m)), l = sum p
+  float inv_l[G];
+#pragma unroll
+  for (int h = 0; h < G; ++h) {
+    float* sh = sc + h * SS;
+    float m = -INFINITY;
+    for (int j = kmin + lane; j <= kmax; j += 64) m = fmaxf(m, sh[j]);
+    m = wave_max(m);
+    float l = 0.f;
+    for (int j = kmin + lane; j <= kmax; j += 64) {
+      const float pw = m > -INFINITY ? rbf(__expf(sh[j] - m)) : 0.f;
+      sh[j] = pw;
+      l += pw;
+    }
+    l = wave_sum(l);
+    inv_l[h] = l > 0.f ? 1.f / l : 0.f;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // O = sum_j p_j v_j over [kmin, kmax]: each lane owns DPL dims, V rows prefetched one chunk ahead
+  float o[G][DPL];
+#pragma unroll
+  for (int h = 0; h < G; ++h)
+#pragma unroll
+    for (int d = 0; d < DPL; ++d) o[h][d] = 0.f;
+  auto accum = [&](int j, const VT (&v)[VCH]) {
+#pragma unroll
+    for (int u = 0; u < VCH; ++u) {
+      if (j + u > kmax) break;
+      float vf[DPL];
+      vrow_t<DPL>::unpack(v[u], vf);
+#pragma unroll
+      for (int h = 0; h < G; ++h) {
+        const float pw = sc[h * SS + j + u];
+#pragma unroll
+        for (int d = 0; d < DPL; ++d) o[h][d] += pw * vf[d];
+      }
+    }
+  };
+  for (int j = kmin; j <= kmax; j += 2 * VCH) {
+    if (j + VCH <= kmax) vload(j + VCH, vb);
+    accum(j, va);
+    if (j + VCH <= kmax) {
+      if (j + 2 * VCH <= kmax) vload(j + 2 * VCH, va);
+      accum(j + VCH, vb);
+    }
+  }
+#pragma unroll
+  for (int h = 0; h < G; ++h) {
+    float r[DPL];
+#pragma unroll
+    for (int d = 0; d < DPL; ++d) r[d] = o[h][d] * inv_l[h];
+    uint16_t* dst = ob + h * HD + lane * DPL;
+    if constexpr (DPL == 4) {
+      *reinterpret_cast<uint2*>(dst) = make_uint2(pack2(r[0], r[1]), pack2(r[2], r[3]));
+    } else {
+      *reinterpret_cast<uint32_t*>(dst) = pack2(r[0], r[1]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Shared-prefix ("cascade") pass of the decode attention.  Prefix-shared sweep cells of one pair read the
 // same leading keys (the pair's baseline KV); instead of every row streaming them, one workgroup takes a
 // chunk of <= 8 decode rows of one pair x one kv head and reads the prefix K/V once for all of them: the
@@ -691,11 +860,24 @@ __global__ void __launch_bounds__(256) attn_prefix_partial_kernel(
   }
 }
 
+// TB_ATTN_DECODE_LEGACY=1 keeps the 4-waves-per-head decode kernel (A/B switch)
+inline bool decode_legacy() {
+  static const int v = [] { const char* e = getenv("TB_ATTN_DECODE_LEGACY"); return e && e[0] == '1' ? 1 : 0; }();
+  return v != 0;
+}
+
 template <int HD, int G>
 void launch_attn_decode(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, uint16_t* out, const int32_t* pos,
                         const int32_t* slot, int B, int Hq, int Hkv, int S, float scale, float softcap, int window,
                         const uint16_t* pkc, const uint16_t* pvc, const int32_t* pslot, const int32_t* plen,
                         const float* xm, const float* xl, const float* xo, hipStream_t st) {
+  if (xo == nullptr && S <= 2048 && !decode_legacy()) {
+    const int nwh = Hkv % 4 == 0 ? 4 : (Hkv % 2 == 0 ? 2 : 1);
+    const size_t lds_w = (size_t)nwh * G * ((S + 15) & ~15) * sizeof(float);
+    hipLaunchKernelGGL((attn_decode_wave_kernel<HD, G>), dim3(B, Hkv / nwh), dim3(64 * nwh), lds_w, st, q, kc, vc, out,
+                       pos, slot, Hq, Hkv, S, scale, softcap, window, pkc, pvc, pslot, plen);
+    return;
+  }
   const size_t lds = ((size_t)G * ((S + 15) & ~15) + 4 * G * HD + 3 * G + 2) * sizeof(float);
   static size_t attr_set = 0;
   if (lds > attr_set && lds > 65536) {

@@ -108,12 +108,15 @@ class Generator:
         self._graphs.clear()
 
     # ------------------------------------------------------------------ steps
+    BUCKET_GRAN = int(os.environ.get("TB_BUCKET_GRAN", "256"))
+
     def bucket(self, n: int) -> int:
         """Rows actually run for ``n`` live rows: a power of two (>= 16) up to 256, then the next
-        multiple of 256 (the large GEMM tile height), capped at B — a small decode (a few diverged
-        cells) does not pay for the whole batch, and few distinct graphs exist."""
+        multiple of ``BUCKET_GRAN`` (default 256, the large GEMM tile height), capped at B — a small
+        decode (a few diverged cells) does not pay for the whole batch, and few distinct graphs exist."""
         if n > 256:
-            return min(-(-n // 256) * 256, self.B)
+            g = self.BUCKET_GRAN
+            return min(-(-n // g) * g, self.B)
         nb = 16
         while nb < n:
             nb *= 2
@@ -335,7 +338,7 @@ class Generator:
         if not (self.use_graphs and graph_key is not None):
             return 0
         if sizes is None:
-            sizes = sorted({self.bucket(n) for n in list(range(1, 257)) + list(range(257, self.B + 1, 256)) + [self.B]})
+            sizes = sorted({self.bucket(n) for n in list(range(1, 257)) + list(range(257, self.B + 1, min(256, self.BUCKET_GRAN))) + [self.B]})
         saved = [t.clone() for t in self._state()]
         self.pos.fill_(self.S)
         self.done.fill_(True)
