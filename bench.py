@@ -92,6 +92,9 @@ def main() -> None:
     ap.add_argument("--fused-geglu", action="store_true",
                     help="gate|up GEMM with the GeGLU in its epilogue (ping-pong MFMA kernel, csrc/gemm.hip) "
                          "instead of hipBLASLt + the GeGLU kernel")
+    ap.add_argument("--no-fused-head", action="store_true",
+                    help="vocab head as hipBLASLt logits + the decode_head kernel instead of the fused MFMA GEMM head "
+                         "(softcap / log-sum-exp / argmax in the GEMM epilogue, no logits in HBM)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="do not queue the next step's teacher-forced tail behind this step's readout")
     ap.add_argument("--profile-steps", action="store_true", help="print per-phase timings per step")
@@ -118,6 +121,8 @@ def main() -> None:
     weights = random_gemma2(spec, device=dev, dtype=torch.bfloat16, seed=1234, post_norm_gain=args.init_gain)
     model = Gemma2Model(weights, dev)
     fused_geglu = bool(args.fused_geglu and model.enable_fused_geglu())
+    if args.no_fused_head:
+        model.fused_head = False
     if args.lora_rank > 0:
         from taboo_brittleness_amd.models.lora import LoRABank
 
@@ -291,6 +296,7 @@ def main() -> None:
                 "baseline_every": E,
                 "carry_rows": C,
                 "fused_geglu": fused_geglu,
+                "fused_head": bool(getattr(model, "fused_head", False)),
                 "lora_adapters": (f"{len(cfg.words)} x rank {args.lora_rank} (unmerged bank)" if args.lora_rank
                                   else "none (weights as merged taboo models)"),
             },

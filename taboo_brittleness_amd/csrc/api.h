@@ -60,6 +60,11 @@ void tb_gemm_skinny(const uint16_t* A, const uint16_t* W, uint16_t* C, int M, in
 bool tb_gemm_pp_ok(int M, int N, int K);
 void tb_gemm_pp(const uint16_t* A, const uint16_t* W, void* C, const float* bias, const float* thr, int M, int N,
                 int K, int ldc, int epi, hipStream_t st);
+// vocab head on the ping-pong GEMM: part [M, N/128] float4 workspace; tgt/tgt_logit[M]/nll_tgt all set or all null
+void tb_head_fused(const uint16_t* A, const uint16_t* W, float* part, const uint16_t* ctab, const int32_t* tgt,
+                   float* tgt_logit, int32_t* nxt, float* nll_self, float* nll_tgt, int M, int N, int K,
+                   hipStream_t st);
+const uint16_t* tb_find_softcap_table(float cap);
 void tb_gemm_nt(const uint16_t* A, const uint16_t* W, void* C, const float* bias, const float* thr, int M, int N,
                 int K, int ldc, int epi, hipStream_t st);
 void tb_lowrank_edit(uint16_t* h, uint16_t* x_next, const uint8_t* apply, const int32_t* idx, const int32_t* cnt,

@@ -371,6 +371,40 @@ void gemm_pp(torch::Tensor A, torch::Tensor W, torch::Tensor C, c10::optional<to
 
 bool gemm_pp_ok(int64_t M, int64_t N, int64_t K) { return tb_gemm_pp_ok(M, N, K); }
 
+// Fused vocab head (gemm.hip EPI_HEAD + head_merge): x [M, K] final-normed rows, W = lm_head [V, K]; the
+// decode_head outputs (greedy token, its NLL, optional teacher-target NLL) with no logits in HBM.
+// part: f32 workspace >= M * (V / 128) * 4; tgt_logit: f32 [M] (with tgt).
+void head_fused(torch::Tensor x, torch::Tensor W, torch::Tensor part, double cap, c10::optional<torch::Tensor> tgt,
+                c10::optional<torch::Tensor> tgt_logit, torch::Tensor nxt, torch::Tensor nll_self,
+                c10::optional<torch::Tensor> nll_tgt) {
+  IN_BF16(x); IN_BF16(W); IN_F32(part); IN_I32(nxt); IN_F32(nll_self);
+  TORCH_CHECK(W.dim() == 2, "head_fused: W must be [V, K]");
+  const int K = x.size(-1), M = x.numel() / K, N = W.size(0);
+  TORCH_CHECK(W.size(1) == K, "head_fused: K mismatch");
+  TORCH_CHECK(tb_gemm_pp_ok(M, N, K), "head_fused: need V % 256 == 0, K % 64 == 0, K >= 64");
+  TORCH_CHECK(part.numel() >= (int64_t)M * (N / 128) * 4, "head_fused: part workspace too small");
+  TORCH_CHECK(nxt.numel() == M && nll_self.numel() == M, "head_fused: output shapes");
+  TORCH_CHECK(tgt.has_value() == nll_tgt.has_value() && tgt.has_value() == tgt_logit.has_value(),
+              "head_fused: tgt, tgt_logit and nll_tgt go together");
+  const int32_t* tp = nullptr;
+  float *tl = nullptr, *np = nullptr;
+  if (tgt.has_value()) {
+    IN_I32((*tgt)); IN_F32((*tgt_logit)); IN_F32((*nll_tgt));
+    TORCH_CHECK(tgt->numel() == M && tgt_logit->numel() == M && nll_tgt->numel() == M, "head_fused teacher shapes");
+    tp = tgt->data_ptr<int32_t>();
+    tl = tgt_logit->data_ptr<float>();
+    np = nll_tgt->data_ptr<float>();
+  }
+  c10::DeviceGuard g(x.device());
+  const uint16_t* tab = nullptr;
+  if (cap > 0) {
+    tab = tb_find_softcap_table((float)cap);
+    TORCH_CHECK(tab != nullptr, "head_fused: softcap table for this cap not registered on this device");
+  }
+  tb_head_fused(cbf(x), cbf(W), part.data_ptr<float>(), tab, tp, tl, nxt.data_ptr<int32_t>(),
+                nll_self.data_ptr<float>(), np, M, N, K, cur_stream());
+}
+
 void lowrank_edit(torch::Tensor h, c10::optional<torch::Tensor> x_next, torch::Tensor apply, torch::Tensor idx,
                   torch::Tensor cnt, torch::Tensor E, torch::Tensor Dm, c10::optional<torch::Tensor> bias,
                   c10::optional<torch::Tensor> thr, c10::optional<torch::Tensor> pre_bias, double alpha,
@@ -521,6 +555,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_nt", &gemm_nt);
   m.def("gemm_pp", &gemm_pp);
   m.def("gemm_pp_ok", &gemm_pp_ok);
+  m.def("head_fused", &head_fused);
   m.def("gemm_skinny", &gemm_skinny);
   m.def("gemm_skinny_ok", &gemm_skinny_ok);
   m.def("lowrank_edit", &lowrank_edit);

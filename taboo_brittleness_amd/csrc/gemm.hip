@@ -49,6 +49,9 @@ constexpr int PSTAGE = 4 * PHALF;      // A0 A1 B0 B1
 #ifndef PP_NO_LDS_READ
 #define PP_NO_LDS_READ 0
 #endif
+#ifndef PP_MFMA32
+#define PP_MFMA32 0      // 1: v_mfma_f32_32x32x16_bf16 (same wave tile, same reads, half the MFMA count)
+#endif
 constexpr int PGROUP_M = PP_GROUP_M;
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -72,12 +75,15 @@ __device__ __forceinline__ bf16x8 lds8(const char* p) {
 #endif
 }
 
-enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_JUMPRELU = 2, EPI_GEGLU = 3 };
+enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_JUMPRELU = 2, EPI_GEGLU = 3, EPI_HEAD = 4 };
+constexpr int HEAD_COLS = 128;          // vocab columns per head partial (one wave group's half of a tile)
+constexpr int CTAB_N = 32768;           // entries of the exact bf16 softcap table (lens.hip)
 
 template <int EPI>
 __global__ void __launch_bounds__(PTHREADS, 1)
 gemm_pp_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, void* __restrict__ C,
-               const float* __restrict__ bias, const float* __restrict__ thr, int M, int N, int K, int ldc) {
+               const float* __restrict__ bias, const float* __restrict__ thr, int M, int N, int K, int ldc,
+               const uint16_t* __restrict__ ctab, const int32_t* __restrict__ tgt, float* __restrict__ tgt_logit) {
   __shared__ __attribute__((aligned(1024))) char smem[2 * PSTAGE];
   const int nbn = N / PBN, nbm = (M + PBM - 1) / PBM, nwg = nbn * nbm;
   int bid = blockIdx.x;
@@ -119,6 +125,24 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, v
 
   // ---- fragment read offsets (the swizzle term ((row>>1)&7) = (lane&15)>>1 for every row read)
   const int xr = (lane & 15) >> 1;
+#if PP_MFMA32
+  // 32x32x16: lane l holds row (l&31), k = 16*s + 8*(l>>5) .. +8 of k-step s, i.e. logical chunk 2s + (l>>5)
+  int co[4];
+#pragma unroll
+  for (int k4 = 0; k4 < 4; ++k4) co[k4] = ((2 * k4 + (lane >> 5)) ^ xr) << 4;
+  const int offp = (grp * 64 + (lane & 31)) * 128;
+  const int offq = (wc * 32 + (lane & 31)) * 128;
+  f32x16 acc[2][2][2];   // [qm][qn][32-row block of the 64-row P half]
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[a][b][i][e] = 0.f;
+  bf16x8 pf[2][4], qf0[4], qf1[4];
+#else
   const int co0 = (((lane >> 4)) ^ xr) << 4, co1 = ((4 + (lane >> 4)) ^ xr) << 4;
   const int offp = (grp * 64 + (lane & 15)) * 128;
   const int offq = (wc * 32 + (lane & 15)) * 128;
@@ -134,6 +158,7 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, v
         for (int j = 0; j < 2; ++j) acc[a][b][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   bf16x8 pf[4][2], qf0[2][2], qf1[2][2];
+#endif
 
   // images: 0 = P0, 1 = P1, 2 = Q0, 3 = Q1
 #define PP_STAGE(stg, img, SRC, k0)                                         \
@@ -142,6 +167,24 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, v
     glds16(SRC[0] + (k0), d_);                                              \
     glds16(SRC[1] + (k0), d_ + 1024);                                       \
   } while (0)
+#if PP_MFMA32
+#define PP_READ_P(sb, qm)                                                   \
+  _Pragma("unroll") for (int i = 0; i < 2; ++i) {                           \
+    const char* p_ = (sb) + (qm) * PHALF + offp + i * 4096;                 \
+    _Pragma("unroll") for (int k4 = 0; k4 < 4; ++k4) pf[i][k4] = lds8(p_ + co[k4]); \
+  }
+#define PP_READ_Q(sb, qn, dstf)                                             \
+  {                                                                         \
+    const char* p_ = (sb) + (2 + (qn)) * PHALF + offq;                      \
+    _Pragma("unroll") for (int k4 = 0; k4 < 4; ++k4) dstf[k4] = lds8(p_ + co[k4]); \
+  }
+#define PP_MFMA(qm, qn, qfr)                                                \
+  if (PP_SETPRIO) __builtin_amdgcn_s_setprio(1);                            \
+  _Pragma("unroll") for (int k4 = 0; k4 < 4; ++k4)                          \
+  _Pragma("unroll") for (int i = 0; i < 2; ++i)                             \
+    acc[qm][qn][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pf[i][k4], qfr[k4], acc[qm][qn][i], 0, 0, 0); \
+  if (PP_SETPRIO) __builtin_amdgcn_s_setprio(0);
+#else
 #define PP_READ_P(sb, qm)                                                   \
   _Pragma("unroll") for (int i = 0; i < 4; ++i) {                           \
     const char* p_ = (sb) + (qm) * PHALF + offp + i * 2048;                 \
@@ -161,6 +204,7 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, v
   _Pragma("unroll") for (int j = 0; j < 2; ++j)                             \
     acc[qm][qn][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf[i][ks], qfr[j][ks], acc[qm][qn][i][j], 0, 0, 0); \
   if (PP_SETPRIO) __builtin_amdgcn_s_setprio(0);
+#endif
 #define PP_VMCNT(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
 
   // Staging schedule (every image >= 4 phases ahead of its first read; each phase stages one image):
@@ -260,38 +304,102 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, v
 #undef PP_MFMA
 #undef PP_VMCNT
 
-  // ---- epilogue.  acc[qm][qn][i][j] element r: output column n = n0 + grp*128 + qm*64 + i*16 + 4*(lane>>4) + r
-  // (4 consecutive n per lane), output row m = m0 + wc*64 + qn*32 + j*16 + (lane&15).
-  const int nb = n0 + grp * 128 + 4 * (lane >> 4);
-  const int mb = m0 + wc * 64 + (lane & 15);
-  if constexpr (EPI == EPI_GEGLU) {
-    // P rows are gate (qm = 0) / up (qm = 1) of feature n0/2 + grp*64 + i*16 + 4*(lane>>4) + r; the gate|up
-    // values are rounded to bf16 first so the result equals geglu(bf16 gate|up GEMM output)
-    uint16_t* out = reinterpret_cast<uint16_t*>(C);
-    const int fb = (n0 >> 1) + grp * 64 + 4 * (lane >> 4);
+  // ---- epilogue.  Every lane holds, per (qm, qn), accumulator groups of 4 consecutive output columns n of one
+  // output row m:  E_M(qn, rj) is the row, E_N(qm, g) the first column of group g, E_V(...) its r-th value.
+  //   16x16x32: acc[qm][qn][i][j][r]: n = n0 + grp*128 + qm*64 + i*16 + 4*(lane>>4) + r,
+  //             m = m0 + wc*64 + qn*32 + j*16 + (lane&15)             (g = i, rj = j; 4 lanes share a row)
+  //   32x32x16: acc[qm][qn][b][4*q + r]: n = n0 + grp*128 + qm*64 + b*32 + 8*q + 4*(lane>>5) + r,
+  //             m = m0 + wc*64 + qn*32 + (lane&31)                     (g = 4b + q; 2 lanes share a row)
+#if PP_MFMA32
+  constexpr int E_RJ = 1, E_G = 8, E_LO = 32;
+#define E_M(qn, rj) (m0 + wc * 64 + (qn) * 32 + (lane & 31))
+#define E_N(qm, g) (n0 + grp * 128 + (qm) * 64 + ((g) >> 2) * 32 + 8 * ((g) & 3) + 4 * (lane >> 5))
+#define E_V(qm, qn, rj, g, r) acc[qm][qn][(g) >> 2][4 * ((g) & 3) + (r)]
+#else
+  constexpr int E_RJ = 2, E_G = 4, E_LO = 16;
+#define E_M(qn, rj) (m0 + wc * 64 + (qn) * 32 + (rj) * 16 + (lane & 15))
+#define E_N(qm, g) (n0 + grp * 128 + (qm) * 64 + (g) * 16 + 4 * (lane >> 4))
+#define E_V(qm, qn, rj, g, r) acc[qm][qn][g][rj][r]
+#endif
+  if constexpr (EPI == EPI_HEAD) {
+    // Vocab head: the bf16 logits (acc rounded like the bf16 GEMM output), then the exact
+    // bf16 final softcap by table (staged into the now idle staging LDS), reduced per (row, 128-column
+    // half-tile) to {max, sum exp(z - max), first argmax}; the row's teacher-target logit is written by the
+    // one lane that holds it.  head_merge_kernel folds the N/128 partials of a row.  No logit reaches HBM.
+    __syncthreads();                       // every wave is past its last ds_read of the main loop
+    uint16_t* ct = reinterpret_cast<uint16_t*>(smem);
+    if (ctab != nullptr) {
+      for (int i = tid; i < CTAB_N / 8; i += PTHREADS)
+        reinterpret_cast<uint4*>(ct)[i] = reinterpret_cast<const uint4*>(ctab)[i];
+    }
+    __syncthreads();
+    float4* part = reinterpret_cast<float4*>(C);
+    const int npart = N / HEAD_COLS, pcol = n0 / HEAD_COLS + grp;
+    constexpr int NZ = 2 * E_G * 4;
 #pragma unroll
     for (int qn = 0; qn < 2; ++qn)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int m = mb + qn * 32 + j * 16;
+      for (int rj = 0; rj < E_RJ; ++rj) {
+        const int m = E_M(qn, rj);
+        const int t = (tgt != nullptr && m < M) ? tgt[m] : -1;
+        float z[NZ];
+        float mx = -INFINITY;
+        int bi = 0x7fffffff;
+#pragma unroll
+        for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+          for (int g = 0; g < E_G; ++g)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const uint32_t b = f2bf(E_V(qm, qn, rj, g, r));
+              const float v = ctab != nullptr ? __uint_as_float(((uint32_t)ct[b & 0x7fffu] | (b & 0x8000u)) << 16)
+                                              : __uint_as_float(b << 16);
+              const int n = E_N(qm, g) + r;
+              z[(qm * E_G + g) * 4 + r] = v;
+              if (v > mx || (v == mx && n < bi)) { mx = v; bi = n; }
+              if (n == t) tgt_logit[m] = v;
+            }
+        float s = 0.f;
+#pragma unroll
+        for (int e = 0; e < NZ; ++e) s += __expf(z[e] - mx);
+#pragma unroll
+        for (int o = E_LO; o <= 32; o <<= 1) {
+          const float m2 = __shfl_xor(mx, o, 64), s2 = __shfl_xor(s, o, 64);
+          const int i2 = __shfl_xor(bi, o, 64);
+          if (m2 > mx) { s = s * __expf(mx - m2) + s2; mx = m2; bi = i2; }
+          else if (m2 == mx) { s += s2; bi = min(bi, i2); }
+          else { s += s2 * __expf(m2 - mx); }
+        }
+        if (lane < E_LO && m < M) part[(size_t)m * npart + pcol] = make_float4(mx, s, __int_as_float(bi), 0.f);
+      }
+  } else if constexpr (EPI == EPI_GEGLU) {
+    // P rows are gate (qm = 0) / up (qm = 1) of feature E_N(0, g) - n0/2 - grp*64 + r; the gate|up values are
+    // rounded to bf16 first so the result equals geglu(bf16 gate|up GEMM output)
+    uint16_t* out = reinterpret_cast<uint16_t*>(C);
+#pragma unroll
+    for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+      for (int rj = 0; rj < E_RJ; ++rj) {
+        const int m = E_M(qn, rj);
         if (m >= M) continue;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int g = 0; g < E_G; ++g) {
           float o[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float g = rbf(acc[0][qn][i][j][r]), u = rbf(acc[1][qn][i][j][r]);
-            o[r] = rbf(gelu_tanh_fast(g)) * u;
+            const float gt = rbf(E_V(0, qn, rj, g, r)), u = rbf(E_V(1, qn, rj, g, r));
+            o[r] = rbf(gelu_tanh_fast(gt)) * u;
           }
-          *reinterpret_cast<uint2*>(out + (size_t)m * ldc + fb + i * 16) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
+          const int f = E_N(0, g) - (n0 >> 1) - grp * 64;
+          *reinterpret_cast<uint2*>(out + (size_t)m * ldc + f) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
         }
       }
   } else {
 #pragma unroll
     for (int qm = 0; qm < 2; ++qm)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int n = nb + qm * 64 + i * 16;
+      for (int g = 0; g < E_G; ++g) {
+        const int n = E_N(qm, g);
         float4 bn_ = make_float4(0.f, 0.f, 0.f, 0.f), th = bn_;
         if constexpr (EPI == EPI_JUMPRELU) {
           if (bias) bn_ = *reinterpret_cast<const float4*>(bias + n);
@@ -300,45 +408,109 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, v
 #pragma unroll
         for (int qn = 0; qn < 2; ++qn)
 #pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            const int m = mb + qn * 32 + j * 16;
+          for (int rj = 0; rj < E_RJ; ++rj) {
+            const int m = E_M(qn, rj);
             if (m >= M) continue;
-            const f32x4 v = acc[qm][qn][i][j];
+            const float v0 = E_V(qm, qn, rj, g, 0), v1 = E_V(qm, qn, rj, g, 1), v2 = E_V(qm, qn, rj, g, 2),
+                        v3 = E_V(qm, qn, rj, g, 3);
             if constexpr (EPI == EPI_BF16) {
               *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(C) + (size_t)m * ldc + n) =
-                  make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+                  make_uint2(pack2(v0, v1), pack2(v2, v3));
             } else if constexpr (EPI == EPI_F32) {
-              *reinterpret_cast<float4*>(reinterpret_cast<float*>(C) + (size_t)m * ldc + n) = make_float4(v[0], v[1], v[2], v[3]);
+              *reinterpret_cast<float4*>(reinterpret_cast<float*>(C) + (size_t)m * ldc + n) = make_float4(v0, v1, v2, v3);
             } else {
-              const float a0 = v[0] + bn_.x, a1 = v[1] + bn_.y, a2 = v[2] + bn_.z, a3 = v[3] + bn_.w;
+              const float a0 = v0 + bn_.x, a1 = v1 + bn_.y, a2 = v2 + bn_.z, a3 = v3 + bn_.w;
               *reinterpret_cast<float4*>(reinterpret_cast<float*>(C) + (size_t)m * ldc + n) =
                   make_float4(a0 > th.x ? a0 : 0.f, a1 > th.y ? a1 : 0.f, a2 > th.z ? a2 : 0.f, a3 > th.w ? a3 : 0.f);
             }
           }
       }
   }
+#undef E_M
+#undef E_N
+#undef E_V
 }
 
 }  // namespace
 
 bool tb_gemm_pp_ok(int M, int N, int K) { return M > 0 && N > 0 && N % PBN == 0 && K >= PBK && K % PBK == 0; }
 
+#define PP_LAUNCH(E_)                                                                                          \
+  hipLaunchKernelGGL(gemm_pp_kernel<E_>, dim3(nwg), dim3(PTHREADS), 0, st, A, W, C, bias, thr, M, N, K, ldc, \
+                     ctab, tgt, tgt_logit)
+
 void tb_gemm_pp(const uint16_t* A, const uint16_t* W, void* C, const float* bias, const float* thr, int M, int N,
                 int K, int ldc, int epi, hipStream_t st) {
   if (M <= 0 || N <= 0) return;
   const int nwg = (N / PBN) * ((M + PBM - 1) / PBM);
+  const uint16_t* ctab = nullptr;
+  const int32_t* tgt = nullptr;
+  float* tgt_logit = nullptr;
   switch (epi) {
-    case EPI_BF16:
-      hipLaunchKernelGGL(gemm_pp_kernel<EPI_BF16>, dim3(nwg), dim3(PTHREADS), 0, st, A, W, C, bias, thr, M, N, K, ldc);
-      break;
-    case EPI_F32:
-      hipLaunchKernelGGL(gemm_pp_kernel<EPI_F32>, dim3(nwg), dim3(PTHREADS), 0, st, A, W, C, bias, thr, M, N, K, ldc);
-      break;
-    case EPI_JUMPRELU:
-      hipLaunchKernelGGL(gemm_pp_kernel<EPI_JUMPRELU>, dim3(nwg), dim3(PTHREADS), 0, st, A, W, C, bias, thr, M, N, K,
-                         ldc);
-      break;
-    default:
-      hipLaunchKernelGGL(gemm_pp_kernel<EPI_GEGLU>, dim3(nwg), dim3(PTHREADS), 0, st, A, W, C, bias, thr, M, N, K, ldc);
+    case EPI_BF16: PP_LAUNCH(EPI_BF16); break;
+    case EPI_F32: PP_LAUNCH(EPI_F32); break;
+    case EPI_JUMPRELU: PP_LAUNCH(EPI_JUMPRELU); break;
+    default: PP_LAUNCH(EPI_GEGLU);
   }
+}
+
+namespace {
+
+// Fold a row's N/128 head partials: lse, first argmax, and the NLLs (greedy token, optional teacher target).
+__global__ void __launch_bounds__(256) head_merge_kernel(const float4* __restrict__ part, int npart,
+                                                         const int32_t* __restrict__ tgt,
+                                                         const float* __restrict__ tgt_logit, int32_t* __restrict__ nxt,
+                                                         float* __restrict__ nll_self, float* __restrict__ nll_tgt,
+                                                         int V) {
+  __shared__ float sm[4], ss[4];
+  __shared__ int si[4];
+  const int r = blockIdx.x;
+  const float4* p = part + (size_t)r * npart;
+  float mx = -INFINITY, s = 0.f;
+  int bi = 0x7fffffff;
+  auto merge = [&](float m2, float s2, int i2) {
+    if (m2 > mx) { s = (mx == -INFINITY ? 0.f : s * __expf(mx - m2)) + s2; mx = m2; bi = i2; }
+    else if (m2 == mx) { s += s2; bi = min(bi, i2); }
+    else if (m2 != -INFINITY) { s += s2 * __expf(m2 - mx); }
+  };
+  for (int c = threadIdx.x; c < npart; c += blockDim.x) {
+    const float4 q = p[c];
+    merge(q.x, q.y, __float_as_int(q.z));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float m2 = __shfl_xor(mx, o, 64), s2 = __shfl_xor(s, o, 64);
+    const int i2 = __shfl_xor(bi, o, 64);
+    merge(m2, s2, i2);
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) { sm[wid] = mx; ss[wid] = s; si[wid] = bi; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    mx = sm[0]; s = ss[0]; bi = si[0];
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) merge(sm[w], ss[w], si[w]);
+    const float lse = mx + __logf(s);
+    nxt[r] = bi;
+    nll_self[r] = lse - mx;
+    if (nll_tgt != nullptr) {
+      const int t = tgt != nullptr ? tgt[r] : -1;
+      nll_tgt[r] = (t >= 0 && t < V) ? lse - tgt_logit[r] : 0.f;
+    }
+  }
+}
+
+}  // namespace
+
+void tb_head_fused(const uint16_t* A, const uint16_t* W, float* part, const uint16_t* ctab, const int32_t* tgt,
+                   float* tgt_logit, int32_t* nxt, float* nll_self, float* nll_tgt, int M, int N, int K,
+                   hipStream_t st) {
+  if (M <= 0) return;
+  const int nwg = (N / PBN) * ((M + PBM - 1) / PBM);
+  const float* bias = nullptr;
+  const float* thr = nullptr;
+  void* C = part;
+  const int ldc = 0;
+  PP_LAUNCH(EPI_HEAD);   // tgt / tgt_logit / nll_tgt are all set or all null (host-checked)
+  hipLaunchKernelGGL(head_merge_kernel, dim3(M), dim3(256), 0, st, reinterpret_cast<const float4*>(part),
+                     N / HEAD_COLS, tgt, tgt_logit, nxt, nll_self, nll_tgt, N);
 }

@@ -451,6 +451,8 @@ void tb_register_softcap_table(float cap, const uint16_t* tab) {
   if (g_ntabs < 16) g_tabs[g_ntabs++] = CapTab{dev, cb, tab};
 }
 
+const uint16_t* tb_find_softcap_table(float cap) { return find_tab(cap, 1); }
+
 void tb_decode_head(const uint16_t* logits, const int32_t* tgt, int32_t* nxt, float* nll_self, float* nll_tgt, int R,
                     int V, float cap, hipStream_t st) {
   if (R <= 0) return;

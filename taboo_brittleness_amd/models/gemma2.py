@@ -170,6 +170,9 @@ class Gemma2Model:
         self._wgu_il: Optional[list] = None
         if os.environ.get("TB_FUSED_GEGLU", "0") == "1":
             self.enable_fused_geglu()
+        # vocab head (greedy token + NLLs) as one MFMA GEMM with a softcap/log-sum-exp/argmax epilogue
+        # (ops.vocab_head): no [rows, 256000] logits in HBM.  TB_FUSED_HEAD (default on) / --no-fused-head
+        self.fused_head = self.device.type == "cuda" and ops.FUSED_HEAD and self.spec.vocab_size % 256 == 0
 
     def enable_fused_geglu(self) -> bool:
         """Switch the MLP's gate|up GEMM + GeGLU to the fused ping-pong MFMA kernel (GPU, no LoRA bank);
@@ -322,6 +325,13 @@ class Gemma2Model:
     def logits(self, x_final: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Raw lm_head logits (bf16, before the final softcap)."""
         return ops.linear(x_final, self.w.lm_head, out=out)
+
+    def head(self, x_final: torch.Tensor, cap: float, tgt=None, nxt=None, nll_self=None, nll_tgt=None, part=None,
+             tgt_logit=None):
+        """Greedy token, its NLL and the optional teacher target's NLL under the ``cap``-softcapped logits of
+        the final-normed rows (``ops.vocab_head``; fused GEMM head when ``self.fused_head``)."""
+        return ops.vocab_head(x_final, self.w.lm_head, cap, tgt, nxt, nll_self, nll_tgt, part=part,
+                              tgt_logit=tgt_logit, fused=self.fused_head)
 
     def lens_logits(self, h: torch.Tensor, out: Optional[torch.Tensor] = None,
                     normed: Optional[torch.Tensor] = None) -> torch.Tensor:

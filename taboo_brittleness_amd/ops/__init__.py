@@ -318,6 +318,43 @@ def xent_rows(logits, tgt, cap=0.0, emulate_bf16=True, out=None):
     return y
 
 
+FUSED_HEAD = os.environ.get("TB_FUSED_HEAD", "1") == "1"
+
+
+def head_part_numel(rows: int, vocab: int) -> int:
+    """fp32 elements of the fused head's partial workspace for ``rows`` rows (16 B per 128 vocab columns)."""
+    return rows * (vocab // 128) * 4
+
+
+def vocab_head(x, w, cap, tgt=None, nxt=None, nll_self=None, nll_tgt=None, part=None, tgt_logit=None,
+               fused: Optional[bool] = None):
+    """``decode_head(x @ w^T, ...)`` from the final-normed rows ``x``: greedy token (bf16-softcap argmax), its
+    NLL and the optional teacher target's NLL.  GPU with ``fused`` (default ``TB_FUSED_HEAD``): one
+    ping-pong MFMA GEMM whose epilogue applies the exact bf16 softcap table and reduces each row's 128-column
+    slices to {max, sum exp, first argmax} (+ the target logit), then a merge kernel — the [rows, V] logits
+    never reach HBM (``part``: optional fp32 workspace of ``head_part_numel`` elements, e.g. an idle logits
+    buffer).  Otherwise the unembedding GEMM + ``decode_head``.  Returns ``(nxt, nll_self, nll_tgt)``."""
+    K = x.shape[-1]
+    R = x.numel() // K
+    V = w.shape[0]
+    fused = FUSED_HEAD if fused is None else fused
+    if x.is_cuda and fused and _k().gemm_pp_ok(R, V, K) and x.is_contiguous():
+        dev = x.device
+        _softcap_table(cap, dev)
+        nxt = _out(nxt, (R,), torch.int32, dev)
+        nll_self = _out(nll_self, (R,), torch.float32, dev)
+        need = head_part_numel(R, V)
+        part = torch.empty(need, dtype=torch.float32, device=dev) if part is None else part.view(-1)[:need]
+        if tgt is not None:
+            nll_tgt = _out(nll_tgt, (R,), torch.float32, dev)
+            tgt_logit = _out(tgt_logit, (R,), torch.float32, dev)
+            _k().head_fused(x, w, part, float(cap), tgt, tgt_logit, nxt, nll_self, nll_tgt)
+        else:
+            _k().head_fused(x, w, part, float(cap), None, None, nxt, nll_self, None)
+        return nxt, nll_self, nll_tgt
+    return decode_head(linear(x, w), cap, tgt, nxt, nll_self, nll_tgt)
+
+
 def decode_head(logits, cap, tgt=None, nxt=None, nll_self=None, nll_tgt=None):
     """One pass over decode logits: greedy token (bf16-softcap argmax), its NLL, and the NLL of an
     optional teacher target per row (``tgt < 0`` -> 0).  Returns ``(nxt, nll_self, nll_tgt)``."""

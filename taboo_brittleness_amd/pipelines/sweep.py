@@ -1365,6 +1365,10 @@ class SweepRunner:
                                      h_in=hin, prefix_kv=self.pair_kv if self.tf_prefix else None)
                 for q0 in range(0, Mc, step):
                     q1 = min(Mc, q0 + step)
+                    if getattr(m, "fused_head", False):
+                        m.head(x[q0:q1], m.spec.final_softcap, tgt_d[c0 + q0:c0 + q1], nxt[c0 + q0:c0 + q1],
+                               ns[c0 + q0:c0 + q1], nt[c0 + q0:c0 + q1])
+                        continue
                     # the unembedding runs on whole 256-row tiles (padding rows of x included) so the
                     # GEMM shapes stay few and tuned; only the real rows are read out
                     lg = m.logits(x[q0:min(Mp, q0 + step)])[: q1 - q0]
@@ -1506,6 +1510,10 @@ class SweepRunner:
                 x = m.forward_packed(ci, cp, cs, blk, self.gen.cache, {self.layer: [plan_hook]}, ws=ws)
                 for q0 in range(0, M, step):
                     q1 = min(M, q0 + step)
+                    if getattr(m, "fused_head", False):
+                        m.head(x[q0:q1], m.spec.final_softcap, tgt_d[r0 + q0: r0 + q1],
+                               nll_tgt=nll[r0 + q0: r0 + q1])
+                        continue
                     lg = m.logits(x[q0:q1])
                     ops.xent_rows(lg, tgt_d[r0 + q0: r0 + q1], m.spec.final_softcap, True,
                                   out=nll[r0 + q0: r0 + q1])

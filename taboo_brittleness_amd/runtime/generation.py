@@ -85,6 +85,7 @@ class Generator:
         self.tf_tgt = torch.full((B, self.W), -1, dtype=torch.int32, device=self.dev)
         self.tf_step = torch.empty(B, dtype=torch.int32, device=self.dev)
         self.tf_nll_step = torch.empty(B, dtype=torch.float32, device=self.dev)
+        self.tgt_logit = torch.empty(B, dtype=torch.float32, device=self.dev)     # fused head scratch
         self.out_tf_nll = torch.zeros(B, self.W, dtype=torch.float32, device=self.dev)
         self._graphs: Dict[tuple, "torch.cuda.CUDAGraph"] = {}
         self.ws = model.workspace(batch)       # pinned: captured graphs hold these pointers (and row views)
@@ -127,11 +128,17 @@ class Generator:
         ws = self.ws if nb == self.B else self.ws.rows(nb)
         kw = {"kv_prefix": self.kv_prefix} if self.kv_prefix is not None else {}
         x = self.m.forward(self.tok[:nb], self.pos[:nb], self.cache, self.slot[:nb], hooks, ws=ws, **kw)
-        lg = self.logits[:nb]
-        self.m.logits(x, out=lg)
         col = torch.clamp(self.step_idx[:nb], max=self.W - 1)
         torch.gather(self.tf_tgt[:nb], 1, col, out=self.tf_step[:nb].view(-1, 1))
-        ops.decode_head(lg, self.cap, self.tf_step[:nb], self.nxt[:nb], self.nll_step[:nb], self.tf_nll_step[:nb])
+        if getattr(self.m, "fused_head", False):
+            # fused GEMM head; its partial workspace lives in the (then idle) logits buffer
+            self.m.head(x, self.cap, self.tf_step[:nb], self.nxt[:nb], self.nll_step[:nb], self.tf_nll_step[:nb],
+                        part=self.logits.view(torch.float32), tgt_logit=self.tgt_logit[:nb])
+        else:
+            lg = self.logits[:nb]
+            self.m.logits(x, out=lg)
+            ops.decode_head(lg, self.cap, self.tf_step[:nb], self.nxt[:nb], self.nll_step[:nb],
+                            self.tf_nll_step[:nb])
         done = self.done[:nb]
         nxt = torch.where(done, torch.full_like(self.nxt[:nb], self.pad_id), self.nxt[:nb])
         self.out_tokens[:nb].scatter_(1, col, nxt.view(-1, 1))
@@ -180,12 +187,14 @@ class Generator:
         slot = torch.tensor(list(rows), dtype=torch.int32, device=self.dev)
         x = self.m.forward(ids.to(self.dev), pos.to(self.dev), self.cache, slot, hooks)
         last = torch.tensor([b * Tp + len(p) - 1 for b, p in enumerate(prompts)], device=self.dev)
-        lg = self.m.logits(x[last])
         tg = None
         if teacher is not None:
             tl = [int(t[0]) if len(t) else -1 for t in teacher][:n]
             tg = torch.tensor(tl + [-1] * (n - len(tl)), dtype=torch.int32, device=self.dev)
-        first, nll, tnll = ops.decode_head(lg, self.cap, tg)
+        if getattr(self.m, "fused_head", False):
+            first, nll, tnll = self.m.head(x[last], self.cap, tg)
+        else:
+            first, nll, tnll = ops.decode_head(self.m.logits(x[last]), self.cap, tg)
         r = torch.tensor(list(rows if out_rows is None else out_rows), device=self.dev)
         self.out_nll[r, 0] = nll
         if tnll is not None:

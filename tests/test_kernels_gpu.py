@@ -181,6 +181,44 @@ def test_decode_head(gpu):
     _close(nt, ref.xent_rows(lg, tgt, 30.0, True), atol=2e-3, rtol=1e-4)
 
 
+@pytest.mark.parametrize("M,V,K,cap", [(300, 4096, 256, 30.0), (1, 2048, 3584, 30.0), (520, 8192, 640, 0.0)])
+def test_vocab_head_fused(gpu, M, V, K, cap):
+    """Fused vocab head (ping-pong GEMM + softcap-table epilogue + partial merge, csrc/gemm.hip) == the
+    unfused path on the same kernel's bf16 logits (bit-identical logits: exact argmax incl. cross-partial
+    and in-partial ties, NLLs to fp32 summation order), and close to a float32 PyTorch reference."""
+    torch.manual_seed(17)
+    x = torch.randn(M, K).to(BF)
+    w = (torch.randn(V, K) * 0.05).to(BF)
+    x[:, 0] = 4.0
+    w[5] = 0.0
+    w[5, 0] = 8.0
+    w[7] = w[5]             # same 128-column partial as 5
+    w[V - 3] = w[5]         # other end of the vocab
+    x[M // 2:, 0] = -4.0    # second half: no forced tie
+    tgt = torch.randint(0, V, (M,), dtype=torch.int32)
+    tgt[::7] = -1
+    tgt[1::9] = 7
+    xg, wg, tg = x.to(gpu), w.to(gpu), tgt.to(gpu)
+    nxt, ns, nt = ops.vocab_head(xg, wg, cap, tg, fused=True)
+    lg = torch.empty(M, V, dtype=BF, device=gpu)
+    ops._k().gemm_pp(xg, wg, lg, None, None, 0)
+    n0, s0, t0 = ops.decode_head(lg, cap, tg)
+    assert torch.equal(nxt, n0)
+    assert (nxt[: M // 2] == 5).all()
+    _close(ns, s0, atol=1e-4, rtol=1e-5)
+    _close(nt, t0, atol=1e-4, rtol=1e-5)
+    assert (nt[tg < 0] == 0).all()
+    # vs the float32 reference (bf16 logits of an fp32 GEMM; argmax may differ only on near-ties)
+    r = (x.float() @ w.float().T).to(BF)
+    ra = ref.argmax_rows(r, cap).view(-1)
+    assert (nxt.cpu() == ra).float().mean() > 0.98
+    _close(nt, ref.xent_rows(r, tgt, cap, True), atol=3e-2, rtol=1e-3)
+    # no teacher; a workspace carved from a (larger) idle logits buffer; deterministic
+    part = torch.empty(M * V // 2 + 64, dtype=BF, device=gpu).view(torch.float32)
+    n2, s2, t2 = ops.vocab_head(xg, wg, cap, part=part, fused=True)
+    assert t2 is None and torch.equal(n2, nxt) and torch.equal(s2, ns)
+
+
 @pytest.mark.parametrize("M,N,K", [(1, 256, 1024), (30, 3584, 4096), (64, 2048, 3584), (17, 65536, 1024)])
 def test_gemm_skinny(gpu, M, N, K):
     """Decode weight-streaming GEMM (k-permuted MFMA fragments, 8-way in-workgroup split-K) == fp32."""

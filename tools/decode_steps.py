@@ -8,7 +8,7 @@ import sys
 
 
 def family(n: str) -> str:
-    for key in ("attn_decode", "decode_head", "geglu", "add_rmsnorm", "rope_qkv", "gemm_skinny", "gemm_pp",
+    for key in ("attn_decode", "decode_head", "head_merge", "gemm_pp_kernel<4>", "geglu", "add_rmsnorm", "rope_qkv", "gemm_skinny", "gemm_pp",
                 "lowrank", "embed"):
         if key in n:
             return key
@@ -30,7 +30,7 @@ for s, e, n, gx, wx in rows:
     elif cur is not None:
         cur[1] = e
         cur[4][family(n)] += (e - s) / 1e3
-        if "decode_head" in n:
+        if "decode_head" in n or "head_merge" in n:
             if cur[3] >= 40:
                 steps.append((cur[2], (cur[1] - cur[0]) / 1e3, cur[4]))
             cur = None

@@ -3,7 +3,7 @@
 # Run them on the GPU box:                                                tools/lab/gemm_lab.sh run
 set -e
 cd "$(dirname "$0")"
-VARIANTS=("base:" "ph2:-DPP_PHASES=2" "ph2noprio:-DPP_PHASES=2 -DPP_SETPRIO=0" "ph2nolds:-DPP_PHASES=2 -DPP_NO_LDS_READ=1")
+VARIANTS=("base:" "m32:-DPP_MFMA32=1" "m32noprio:-DPP_MFMA32=1 -DPP_SETPRIO=0" "m32nolds:-DPP_MFMA32=1 -DPP_NO_LDS_READ=1")
 if [ "$1" = build ]; then
   for v in "${VARIANTS[@]}"; do
     name=${v%%:*}; flags=${v#*:}
@@ -15,7 +15,7 @@ else
   mkdir -p ../../gpurun_out
   for v in "${VARIANTS[@]}"; do
     name=${v%%:*}
-    for shp in "4096 28672 3584 0" "4096 28672 3584 3" "4096 8192 3584 0" "2048 28672 3584 3" "8192 8192 3584 0"; do
+    for shp in "4096 28672 3584 0" "4096 28672 3584 3" "4096 8192 3584 0" "2048 28672 3584 3" "8192 8192 3584 0" "2048 256000 3584 0" "4096 3584 14336 0"; do
       echo -n "{\"variant\": \"$name\", \"r\": "; timeout -k 5 60 ./gemm_lab_$name $shp; echo "}"
     done
   done
