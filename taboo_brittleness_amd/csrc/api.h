@@ -65,6 +65,9 @@ void tb_head_fused(const uint16_t* A, const uint16_t* W, float* part, const uint
                    float* tgt_logit, int32_t* nxt, float* nll_self, float* nll_tgt, int M, int N, int K,
                    hipStream_t st);
 const uint16_t* tb_find_softcap_table(float cap);
+// logit-lens unembedding on the ping-pong GEMM: bf16 logits [M, N] + per-row log-sum-exp (part: M*N/32 floats)
+void tb_lens_gemm(const uint16_t* A, const uint16_t* W, uint16_t* logits, float* part, float* lse, int M, int N, int K,
+                  hipStream_t st);
 void tb_gemm_nt(const uint16_t* A, const uint16_t* W, void* C, const float* bias, const float* thr, int M, int N,
                 int K, int ldc, int epi, hipStream_t st);
 void tb_lowrank_edit(uint16_t* h, uint16_t* x_next, const uint8_t* apply, const int32_t* idx, const int32_t* cnt,

@@ -371,6 +371,20 @@ void gemm_pp(torch::Tensor A, torch::Tensor W, torch::Tensor C, c10::optional<to
 
 bool gemm_pp_ok(int64_t M, int64_t N, int64_t K) { return tb_gemm_pp_ok(M, N, K); }
 
+// Logit-lens unembedding on the ping-pong GEMM (gemm.hip EPI_LENS): bf16 logits and their per-row
+// log-sum-exp (no softcap), so the lens needs no separate row_lse pass.  part: f32 >= M * (V / 128) * 4.
+void lens_gemm(torch::Tensor x, torch::Tensor W, torch::Tensor logits, torch::Tensor part, torch::Tensor lse) {
+  IN_BF16(x); IN_BF16(W); IN_BF16(logits); IN_F32(part); IN_F32(lse);
+  TORCH_CHECK(W.dim() == 2, "lens_gemm: W must be [V, K]");
+  const int K = x.size(-1), M = x.numel() / K, N = W.size(0);
+  TORCH_CHECK(W.size(1) == K, "lens_gemm: K mismatch");
+  TORCH_CHECK(tb_gemm_pp_ok(M, N, K), "lens_gemm: need V % 256 == 0, K % 64 == 0, K >= 64");
+  TORCH_CHECK(logits.numel() == (int64_t)M * N, "lens_gemm: logits shape");
+  TORCH_CHECK(part.numel() >= (int64_t)M * (N / 128) * 4 && lse.numel() == M, "lens_gemm: part / lse shapes");
+  c10::DeviceGuard g(x.device());
+  tb_lens_gemm(cbf(x), cbf(W), bf(logits), part.data_ptr<float>(), lse.data_ptr<float>(), M, N, K, cur_stream());
+}
+
 // Fused vocab head (gemm.hip EPI_HEAD + head_merge): x [M, K] final-normed rows, W = lm_head [V, K]; the
 // decode_head outputs (greedy token, its NLL, optional teacher-target NLL) with no logits in HBM.
 // part: f32 workspace >= M * (V / 128) * 4; tgt_logit: f32 [M] (with tgt).
@@ -556,6 +570,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_pp", &gemm_pp);
   m.def("gemm_pp_ok", &gemm_pp_ok);
   m.def("head_fused", &head_fused);
+  m.def("lens_gemm", &lens_gemm);
   m.def("gemm_skinny", &gemm_skinny);
   m.def("gemm_skinny_ok", &gemm_skinny_ok);
   m.def("lowrank_edit", &lowrank_edit);

@@ -75,7 +75,7 @@ __device__ __forceinline__ bf16x8 lds8(const char* p) {
 #endif
 }
 
-enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_JUMPRELU = 2, EPI_GEGLU = 3, EPI_HEAD = 4 };
+enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_JUMPRELU = 2, EPI_GEGLU = 3, EPI_HEAD = 4, EPI_LENS = 5 };
 constexpr int HEAD_COLS = 128;          // vocab columns per head partial (one wave group's half of a tile)
 constexpr int CTAB_N = 32768;           // entries of the exact bf16 softcap table (lens.hip)
 
@@ -83,7 +83,8 @@ template <int EPI>
 __global__ void __launch_bounds__(PTHREADS, 1)
 gemm_pp_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, void* __restrict__ C,
                const float* __restrict__ bias, const float* __restrict__ thr, int M, int N, int K, int ldc,
-               const uint16_t* __restrict__ ctab, const int32_t* __restrict__ tgt, float* __restrict__ tgt_logit) {
+               const uint16_t* __restrict__ ctab, const int32_t* __restrict__ tgt, float* __restrict__ tgt_logit,
+               float4* __restrict__ lpart) {
   __shared__ __attribute__((aligned(1024))) char smem[2 * PSTAGE];
   const int nbn = N / PBN, nbm = (M + PBM - 1) / PBM, nwg = nbn * nbm;
   int bid = blockIdx.x;
@@ -321,19 +322,25 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, v
 #define E_N(qm, g) (n0 + grp * 128 + (qm) * 64 + (g) * 16 + 4 * (lane >> 4))
 #define E_V(qm, qn, rj, g, r) acc[qm][qn][g][rj][r]
 #endif
-  if constexpr (EPI == EPI_HEAD) {
+  if constexpr (EPI == EPI_HEAD || EPI == EPI_LENS) {
     // Vocab head: the bf16 logits (acc rounded like the bf16 GEMM output), then the exact
     // bf16 final softcap by table (staged into the now idle staging LDS), reduced per (row, 128-column
     // half-tile) to {max, sum exp(z - max), first argmax}; the row's teacher-target logit is written by the
     // one lane that holds it.  head_merge_kernel folds the N/128 partials of a row.  No logit reaches HBM.
-    __syncthreads();                       // every wave is past its last ds_read of the main loop
-    uint16_t* ct = reinterpret_cast<uint16_t*>(smem);
-    if (ctab != nullptr) {
-      for (int i = tid; i < CTAB_N / 8; i += PTHREADS)
-        reinterpret_cast<uint4*>(ct)[i] = reinterpret_cast<const uint4*>(ctab)[i];
+    // Logit lens (EPI_LENS): no softcap; the bf16 logits ARE stored (the lens colsum / gathers
+    // read them) and the same per-slice {max, sum exp} partials go to lpart, so no row_lse pass is needed.
+    const uint16_t* ct = nullptr;
+    if constexpr (EPI == EPI_HEAD) {
+      __syncthreads();                     // every wave is past its last ds_read of the main loop
+      uint16_t* ctw = reinterpret_cast<uint16_t*>(smem);
+      if (ctab != nullptr) {
+        for (int i = tid; i < CTAB_N / 8; i += PTHREADS)
+          reinterpret_cast<uint4*>(ctw)[i] = reinterpret_cast<const uint4*>(ctab)[i];
+        ct = ctw;
+      }
+      __syncthreads();
     }
-    __syncthreads();
-    float4* part = reinterpret_cast<float4*>(C);
+    float4* part = EPI == EPI_HEAD ? reinterpret_cast<float4*>(C) : lpart;
     const int npart = N / HEAD_COLS, pcol = n0 / HEAD_COLS + grp;
     constexpr int NZ = 2 * E_G * 4;
 #pragma unroll
@@ -352,13 +359,25 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, v
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const uint32_t b = f2bf(E_V(qm, qn, rj, g, r));
-              const float v = ctab != nullptr ? __uint_as_float(((uint32_t)ct[b & 0x7fffu] | (b & 0x8000u)) << 16)
-                                              : __uint_as_float(b << 16);
+              const float v = ct != nullptr ? __uint_as_float(((uint32_t)ct[b & 0x7fffu] | (b & 0x8000u)) << 16)
+                                            : __uint_as_float(b << 16);
               const int n = E_N(qm, g) + r;
               z[(qm * E_G + g) * 4 + r] = v;
               if (v > mx || (v == mx && n < bi)) { mx = v; bi = n; }
-              if (n == t) tgt_logit[m] = v;
+              if (EPI == EPI_HEAD && n == t) tgt_logit[m] = v;
             }
+        if constexpr (EPI == EPI_LENS) {
+          if (m < M) {
+#pragma unroll
+            for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+              for (int g = 0; g < E_G; ++g) {
+                const float* zz = z + (qm * E_G + g) * 4;
+                *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(C) + (size_t)m * ldc + E_N(qm, g)) =
+                    make_uint2(pack2(zz[0], zz[1]), pack2(zz[2], zz[3]));
+              }
+          }
+        }
         float s = 0.f;
 #pragma unroll
         for (int e = 0; e < NZ; ++e) s += __expf(z[e] - mx);
@@ -437,7 +456,7 @@ bool tb_gemm_pp_ok(int M, int N, int K) { return M > 0 && N > 0 && N % PBN == 0 
 
 #define PP_LAUNCH(E_)                                                                                          \
   hipLaunchKernelGGL(gemm_pp_kernel<E_>, dim3(nwg), dim3(PTHREADS), 0, st, A, W, C, bias, thr, M, N, K, ldc, \
-                     ctab, tgt, tgt_logit)
+                     ctab, tgt, tgt_logit, lpart)
 
 void tb_gemm_pp(const uint16_t* A, const uint16_t* W, void* C, const float* bias, const float* thr, int M, int N,
                 int K, int ldc, int epi, hipStream_t st) {
@@ -446,6 +465,7 @@ void tb_gemm_pp(const uint16_t* A, const uint16_t* W, void* C, const float* bias
   const uint16_t* ctab = nullptr;
   const int32_t* tgt = nullptr;
   float* tgt_logit = nullptr;
+  float4* lpart = nullptr;
   switch (epi) {
     case EPI_BF16: PP_LAUNCH(EPI_BF16); break;
     case EPI_F32: PP_LAUNCH(EPI_F32); break;
@@ -456,12 +476,13 @@ void tb_gemm_pp(const uint16_t* A, const uint16_t* W, void* C, const float* bias
 
 namespace {
 
-// Fold a row's N/128 head partials: lse, first argmax, and the NLLs (greedy token, optional teacher target).
+// Fold a row's N/128 head / lens partials: lse, first argmax, and the NLLs (greedy token, optional teacher
+// target); each output pointer may be null.
 __global__ void __launch_bounds__(256) head_merge_kernel(const float4* __restrict__ part, int npart,
                                                          const int32_t* __restrict__ tgt,
                                                          const float* __restrict__ tgt_logit, int32_t* __restrict__ nxt,
                                                          float* __restrict__ nll_self, float* __restrict__ nll_tgt,
-                                                         int V) {
+                                                         float* __restrict__ lse_out, int V) {
   __shared__ float sm[4], ss[4];
   __shared__ int si[4];
   const int r = blockIdx.x;
@@ -490,8 +511,9 @@ __global__ void __launch_bounds__(256) head_merge_kernel(const float4* __restric
     mx = sm[0]; s = ss[0]; bi = si[0];
     for (int w = 1; w < (int)(blockDim.x >> 6); ++w) merge(sm[w], ss[w], si[w]);
     const float lse = mx + __logf(s);
-    nxt[r] = bi;
-    nll_self[r] = lse - mx;
+    if (lse_out != nullptr) lse_out[r] = lse;
+    if (nxt != nullptr) nxt[r] = bi;
+    if (nll_self != nullptr) nll_self[r] = lse - mx;
     if (nll_tgt != nullptr) {
       const int t = tgt != nullptr ? tgt[r] : -1;
       nll_tgt[r] = (t >= 0 && t < V) ? lse - tgt_logit[r] : 0.f;
@@ -510,7 +532,25 @@ void tb_head_fused(const uint16_t* A, const uint16_t* W, float* part, const uint
   const float* thr = nullptr;
   void* C = part;
   const int ldc = 0;
+  float4* lpart = nullptr;
   PP_LAUNCH(EPI_HEAD);   // tgt / tgt_logit / nll_tgt are all set or all null (host-checked)
   hipLaunchKernelGGL(head_merge_kernel, dim3(M), dim3(256), 0, st, reinterpret_cast<const float4*>(part),
-                     N / HEAD_COLS, tgt, tgt_logit, nxt, nll_self, nll_tgt, N);
+                     N / HEAD_COLS, tgt, tgt_logit, nxt, nll_self, nll_tgt, nullptr, N);
+}
+
+void tb_lens_gemm(const uint16_t* A, const uint16_t* W, uint16_t* logits, float* part, float* lse, int M, int N, int K,
+                  hipStream_t st) {
+  if (M <= 0) return;
+  const int nwg = (N / PBN) * ((M + PBM - 1) / PBM);
+  const float* bias = nullptr;
+  const float* thr = nullptr;
+  void* C = logits;
+  const int ldc = N;
+  const uint16_t* ctab = nullptr;
+  const int32_t* tgt = nullptr;
+  float* tgt_logit = nullptr;
+  float4* lpart = reinterpret_cast<float4*>(part);
+  PP_LAUNCH(EPI_LENS);
+  hipLaunchKernelGGL(head_merge_kernel, dim3(M), dim3(256), 0, st, reinterpret_cast<const float4*>(part),
+                     N / HEAD_COLS, nullptr, nullptr, nullptr, nullptr, nullptr, lse, N);
 }

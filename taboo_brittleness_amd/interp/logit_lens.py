@@ -120,8 +120,7 @@ def lens_readout(model, store: torch.Tensor, starts: Sequence[int], lens: Sequen
         m = c1 - c0
         idx, mask = _rows_for(store, seqs[c0:c1], starts[c0:c1], lens[c0:c1], Tr)
         rows = flat.index_select(0, idx.view(-1).to(dev))
-        logits = model.lens_logits(rows)                                   # [m*Tr, V] bf16
-        lse = ops.row_lse(logits)
+        logits, lse = model.lens_logits_lse(rows)                          # [m*Tr, V] bf16, [m*Tr]
         tid = torch.full((m, Tr, K), -1, dtype=torch.int32)
         ex = torch.full((m, Tr, 2), -1, dtype=torch.int32)
         for i in range(m):
@@ -210,8 +209,7 @@ def lens_packed(model, store: torch.Tensor, rows: np.ndarray, offs: np.ndarray, 
     pr_d = torch.empty(R, K, dtype=torch.float32, device=dev)
     for i0, i1, r0, r1, pr0, Mp, po0 in chunks:
         M = r1 - r0
-        logits = model.lens_logits(flat.index_select(0, ridx_d[pr0:pr0 + Mp]))[:M]
-        lse = ops.row_lse(logits)
+        logits, lse = model.lens_logits_lse(flat.index_select(0, ridx_d[pr0:pr0 + M]))
         ops.gather_probs(logits, lse, track_d[r0:r1], round_bf16=round_bf16, out=pr_d[r0:r1])
         ops.lens_colsum(logits, lse, None, excl_d[r0:r1], i1 - i0, 0, acc=base[i0:i1], accumulate=True,
                         round_bf16=round_bf16, offs=offs_d[po0:po0 + (i1 - i0) + 1])
@@ -240,8 +238,7 @@ def all_layer_lens(model, stores: Sequence[torch.Tensor], seq: int, start: int, 
     tid = torch.tensor(list(track_ids), dtype=torch.int32, device=dev).view(1, K).expand(length, K).contiguous()
     for l in range(Lh):
         rows = stores[l][seq, start:start + length]
-        logits = model.lens_logits(rows.contiguous())
-        lse = ops.row_lse(logits)
+        logits, lse = model.lens_logits_lse(rows.contiguous())
         if K:
             p_track[l] = ops.gather_probs(logits, lse, tid, round_bf16=round_bf16).cpu().numpy()
         amax[l] = ops.argmax_rows(logits).cpu().numpy()

@@ -333,6 +333,12 @@ class Gemma2Model:
         return ops.vocab_head(x_final, self.w.lm_head, cap, tgt, nxt, nll_self, nll_tgt, part=part,
                               tgt_logit=tgt_logit, fused=self.fused_head)
 
+    def lens_logits_lse(self, h: torch.Tensor):
+        """``(lens_logits(h), logsumexp over the vocab)``; on the GPU one MFMA GEMM with an LSE epilogue
+        (``ops.lens_unembed``)."""
+        xn = ops.rmsnorm(h, self.w.norm_f, self.spec.eps)
+        return ops.lens_unembed(xn, self.w.lm_head)
+
     def lens_logits(self, h: torch.Tensor, out: Optional[torch.Tensor] = None,
                     normed: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Logit lens ``lm_head(norm_f(h))`` — no final softcap (`src/models.py:135`)."""

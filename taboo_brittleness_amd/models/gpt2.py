@@ -15,6 +15,7 @@ from typing import Dict, Optional, Sequence
 import torch
 import torch.nn.functional as F
 
+from .. import ops
 from .gemma2 import HookCtx
 from .spec import GPT2Spec
 from .weights import GPT2Weights
@@ -108,3 +109,7 @@ class GPT2Model:
 
     def lens_logits(self, h: torch.Tensor, out=None, normed=None) -> torch.Tensor:
         return self.logits(self._ln(h, self.w.ln_f_w, self.w.ln_f_b), out)
+
+    def lens_logits_lse(self, h: torch.Tensor):
+        logits = self.lens_logits(h)
+        return logits, ops.row_lse(logits)

@@ -355,6 +355,28 @@ def vocab_head(x, w, cap, tgt=None, nxt=None, nll_self=None, nll_tgt=None, part=
     return decode_head(linear(x, w), cap, tgt, nxt, nll_self, nll_tgt)
 
 
+FUSED_LENS = os.environ.get("TB_FUSED_LENS", "0") == "1"   # -0.6 % in the bench (profiles/r2/lens): opt-in
+
+
+def lens_unembed(xn, w, fused: Optional[bool] = None, out=None):
+    """Logit-lens unembedding of final-normed rows: ``(logits = xn @ w^T (bf16), lse = logsumexp(logits))``, no
+    softcap.  GPU with ``fused`` (default ``TB_FUSED_LENS``): one ping-pong MFMA GEMM that stores the bf16 logits
+    and reduces each row's 128-column slices to {max, sum exp} in its epilogue, then the partial merge
+    (csrc/gemm.hip EPI_LENS) -- no separate ``row_lse`` pass over the logits.  Otherwise hipBLASLt + ``row_lse``."""
+    K = xn.shape[-1]
+    R = xn.numel() // K
+    V = w.shape[0]
+    fused = FUSED_LENS if fused is None else fused
+    if xn.is_cuda and fused and _k().gemm_pp_ok(R, V, K) and xn.is_contiguous():
+        logits = _out(out, xn.shape[:-1] + (V,), BF16, xn.device)
+        part = torch.empty(head_part_numel(R, V), dtype=torch.float32, device=xn.device)
+        lse = torch.empty(xn.shape[:-1], dtype=torch.float32, device=xn.device)
+        _k().lens_gemm(xn, w, logits, part, lse)
+        return logits, lse
+    logits = linear(xn, w, out=out)
+    return logits, row_lse(logits)
+
+
 def decode_head(logits, cap, tgt=None, nxt=None, nll_self=None, nll_tgt=None):
     """One pass over decode logits: greedy token (bf16-softcap argmax), its NLL, and the NLL of an
     optional teacher target per row (``tgt < 0`` -> 0).  Returns ``(nxt, nll_self, nll_tgt)``."""

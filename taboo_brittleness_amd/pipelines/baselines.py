@@ -79,8 +79,7 @@ def trace_sequences(model, tok, seqs: Sequence[Sequence[int]], layer: int, track
         resp_sum = None
         for l in range(L):
             rows = stores[l][b, :Tb].contiguous()
-            logits = model.lens_logits(rows)
-            lse = ops.row_lse(logits)
+            logits, lse = model.lens_logits_lse(rows)
             p_track[l] = ops.gather_probs(logits, lse, tid, round_bf16=round_bf16).cpu().numpy()
             amax[l] = ops.argmax_rows(logits).cpu().numpy()
             if full is not None:

@@ -219,6 +219,26 @@ def test_vocab_head_fused(gpu, M, V, K, cap):
     assert t2 is None and torch.equal(n2, nxt) and torch.equal(s2, ns)
 
 
+@pytest.mark.parametrize("M,V,K", [(300, 4096, 256), (37, 2048, 3584)])
+def test_lens_unembed_fused(gpu, M, V, K):
+    """Logit-lens unembedding with the LSE epilogue (csrc/gemm.hip EPI_LENS): logits bit-identical to the same
+    kernel's plain bf16 output, lse == row_lse of them, both close to a float32 reference."""
+    torch.manual_seed(19)
+    x = torch.randn(M, K).to(BF)
+    w = (torch.randn(V, K) * 0.05).to(BF)
+    xg, wg = x.to(gpu), w.to(gpu)
+    lg, lse = ops.lens_unembed(xg, wg, fused=True)
+    lg0 = torch.empty(M, V, dtype=BF, device=gpu)
+    ops._k().gemm_pp(xg, wg, lg0, None, None, 0)
+    assert torch.equal(lg, lg0)
+    _close(lse, ops.row_lse(lg0), atol=1e-4, rtol=1e-6)
+    r = (x.float() @ w.float().T).to(BF)
+    _close(lg, r, atol=1e-2 * K ** 0.5, rtol=1e-2)
+    _close(lse, ref.row_lse(r, 0.0, False), atol=2e-2, rtol=1e-3)
+    lg2, lse2 = ops.lens_unembed(xg, wg, fused=False)
+    _close(lse2, lse, atol=2e-2, rtol=1e-3)
+
+
 @pytest.mark.parametrize("M,N,K", [(1, 256, 1024), (30, 3584, 4096), (64, 2048, 3584), (17, 65536, 1024)])
 def test_gemm_skinny(gpu, M, N, K):
     """Decode weight-streaming GEMM (k-permuted MFMA fragments, 8-way in-workgroup split-K) == fp32."""

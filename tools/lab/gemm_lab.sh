@@ -3,7 +3,7 @@
 # Run them on the GPU box:                                                tools/lab/gemm_lab.sh run
 set -e
 cd "$(dirname "$0")"
-VARIANTS=("base:" "m32:-DPP_MFMA32=1" "m32noprio:-DPP_MFMA32=1 -DPP_SETPRIO=0" "m32nolds:-DPP_MFMA32=1 -DPP_NO_LDS_READ=1")
+VARIANTS=("base:" "m32:-DPP_MFMA32=1" "nolds:-DPP_NO_LDS_READ=1")
 if [ "$1" = build ]; then
   for v in "${VARIANTS[@]}"; do
     name=${v%%:*}; flags=${v#*:}
