@@ -1323,6 +1323,9 @@ class SweepRunner:
         # (2048 rows of the 256k vocab; 4096 measured equal, profiles/r2/kstats_head4096.txt)
         head_bytes = int(os.environ.get("TB_TF_HEAD_MB", "1024")) << 20
         step = max(256, (head_bytes // (m.spec.vocab_size * 2)) // 256 * 256)
+        if getattr(m, "fused_head", False):
+            # the fused head keeps no logits (16 B of partials per 128 vocab columns): whole chunks per GEMM
+            step = int(os.environ.get("TB_TF_HEAD_ROWS", "16384"))
         # chunks of whole cells (a cell never spans two chunks), so chunks are independent and
         # alternate between two streams: one chunk's bandwidth-bound kernels (attention, norms, GeGLU,
         # vocab head) overlap the other's GEMMs

@@ -39,3 +39,24 @@ def test_prompt_helpers_and_seed(tmp_path):
     assert torch.equal(a, torch.rand(3))
     clean_gpu_memory()
     assert isinstance(memory_report(), dict)
+
+
+def test_vocab_head_and_lens_unembed_cpu_paths():
+    """CPU fallbacks of the fused GPU readouts: ``vocab_head`` == unembedding GEMM + ``decode_head`` and
+    ``lens_logits_lse`` == ``lens_logits`` + ``row_lse`` (the fused flags are GPU-only)."""
+    from taboo_brittleness_amd import ops
+
+    model, _ = load_taboo_model("random", device="cpu", arch="gemma2-tiny")
+    torch.manual_seed(3)
+    x = torch.randn(9, model.spec.hidden).to(torch.bfloat16)
+    tgt = torch.tensor([1, -1, 5, 7, 0, 3, 2, 9, 4], dtype=torch.int32)
+    cap = model.spec.final_softcap
+    n1, s1, t1 = model.head(x, cap, tgt)
+    n0, s0, t0 = ops.decode_head(model.logits(x), cap, tgt)
+    assert torch.equal(n1, n0) and torch.allclose(s1, s0) and torch.allclose(t1, t0)
+    assert float(t1[1]) == 0.0
+    n2, s2, t2 = ops.vocab_head(x, model.w.lm_head, cap, fused=True)   # CPU: fused flag falls back
+    assert t2 is None and torch.equal(n2, n0)
+    lg, lse = model.lens_logits_lse(x)
+    lg_ref = model.lens_logits(x)
+    assert torch.equal(lg, lg_ref) and torch.allclose(lse, ops.row_lse(lg_ref))
