@@ -57,6 +57,15 @@ from taboo_brittleness_amd.runtime.tuning import enable_tuned_gemms, flush_tuned
 BASELINE_VALUE = 0.642   # measured HF-eager sweep cells/sec on 1x MI355X (tools/hf_eager_baseline.py)
 
 
+def _host_rss_gb():
+    try:
+        import psutil
+
+        return round(psutil.Process().memory_info().rss / 1e9, 1)
+    except Exception:
+        return None
+
+
 def fresh(p: Pair) -> Pair:
     return Pair(p.word, p.pidx, p.prompt, list(p.ids), list(p.forms), list(p.track))
 
@@ -318,6 +327,8 @@ def main() -> None:
                 # non-degeneracy of the random model: distinct tokens per baseline response, and the
                 # fraction of response tokens equal to their input token (a self-copying model is 1.0)
                 "peak_mem_gb": round(torch.cuda.max_memory_reserved(dev) / 1e9, 1) if on_gpu else None,
+                # host memory of this rank (an 8-GPU node runs 8 of these)
+                "host_rss_gb": _host_rss_gb(),
                 "distinct_tokens_per_resp": round(float(sum(len(set(p.resp)) for p in cur) / max(1, len(cur))), 2),
                 "self_copy_frac": round(float(sum(sum(a == b for a, b in zip(p.gen_toks[1:], p.gen_toks[:-1]))
                                                   for p in cur) / max(1, sum(len(p.gen_toks) - 1 for p in cur))), 3),
