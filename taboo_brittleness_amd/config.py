@@ -134,6 +134,10 @@ class InterventionCfg:
     proj_random_trials: int = 5         # EP:150
     score_over: str = "prompt"          # "prompt" (per prompt) or "word" (average over prompts)
     pca_pool: str = "word"              # pool spike residuals per "word" or across "all" models
+    # targeted projection subspace (EP:144-146): "pca" of the spike residuals, or the gradient alternative
+    # (EP:146): "grad_lens" (secret logit-lens logit through the final norm) / "grad_model" (the model's
+    # secret output logit back-propagated through the blocks after the hooked layer); interp/gradient.py
+    subspace: str = "pca"
     decoys: Dict[str, List[str]] = field(default_factory=lambda: {
         "ship": ["boat", "harbor", "sea"], "moon": ["sun", "star", "night"],
         "smile": ["laugh", "happy", "face"]})

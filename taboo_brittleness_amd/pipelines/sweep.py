@@ -245,6 +245,8 @@ class SweepRunner:
             p.top_ids = lr.topk_ids[i]
             p.spikes_rel = A.select_spikes(p.p_secret, p.resp, p.track[:2], self.iv.spikes_k)
             p.resid = self.store[si, p.plen:p.plen + n].clone()
+            if self.iv.subspace == "grad_model":     # the prompt positions too: the backward needs the context
+                p.resid_pre = self.store[si, :p.plen].clone()
             if self.pair_kv is not None:
                 p.kv_slot = self._kv_next % self.kv_pairs
                 self._kv_next += 1
@@ -334,15 +336,36 @@ class SweepRunner:
         return cells
 
     def _bases(self, pairs: Sequence[Pair]) -> Dict[str, torch.Tensor]:
-        """PCA secret subspaces (EP:144-146) pooled per word (or across all pairs)."""
+        """Targeted secret subspaces pooled per word (or across all pairs): PCA of the spike residuals
+        (EP:144-146) or, with ``intervention.subspace = grad_lens | grad_model``, the top singular directions of
+        the secret-logit gradients at the spikes (EP:146's alternative; interp/gradient.py)."""
+        from ..interp import gradient as GR
+
         rmax = max(self.iv.ranks) if self.iv.ranks else 1
+        mode = self.iv.subspace
+        if mode not in ("pca", "grad_lens", "grad_model"):
+            raise ValueError(f"intervention.subspace must be pca, grad_lens or grad_model, not {mode!r}")
         groups: Dict[str, List[torch.Tensor]] = {}
         for p in pairs:
             if p.resid is None or not p.spikes_rel:
                 continue
             key = p.word if self.iv.pca_pool == "word" else "__all__"
-            groups.setdefault(key, []).append(p.resid[p.spikes_rel].float())
-        return {k: A.secret_subspace(torch.cat(v, 0), rmax) for k, v in groups.items()}
+            if mode == "pca":
+                groups.setdefault(key, []).append(p.resid[p.spikes_rel].float())
+            elif mode == "grad_lens":
+                groups.setdefault(key, []).append(GR.lens_gradients(self.m, p.resid[p.spikes_rel], p.track[:1]))
+            else:
+                pre = getattr(p, "resid_pre", None)
+                assert pre is not None, "grad_model subspaces need the baselines run with subspace=grad_model"
+                assert getattr(self.m, "tp", None) is None and getattr(self.m, "lora", None) is None, \
+                    "grad_model needs unsharded, merged weights"
+                seq = torch.cat([pre, p.resid], 0)
+                sp = [p.plen + t for t in p.spikes_rel]
+                groups.setdefault(key, []).append(GR.model_gradients(self.m, seq, self.layer, sp, p.track[:1]))
+        if mode == "pca":
+            return {k: A.secret_subspace(torch.cat(v, 0), rmax) for k, v in groups.items()}
+        return {k: GR.gradient_subspace(torch.cat(v, 0), rmax, seed=A.cell_seed("grad", k, rmax))
+                for k, v in groups.items()}
 
     def _plan_for(self, cells: Sequence[Cell], pairs: Sequence[Pair], bases: Dict[str, torch.Tensor],
                   with_carry: bool = True):

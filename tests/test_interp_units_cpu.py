@@ -277,3 +277,76 @@ def test_attn_prefix_chunks_table():
     assert sorted(seen) == sorted(np.nonzero(pl > 0)[0].tolist())
     assert list(tab[:, 2]) == sorted(tab[:, 2])
     assert ops.attn_prefix_chunks(ps, np.zeros(100)).shape == (0, 10)
+
+
+def _tiny_model(gain=4.0):
+    from taboo_brittleness_amd.models.gemma2 import Gemma2Model
+    from taboo_brittleness_amd.models.spec import get_spec
+    from taboo_brittleness_amd.models.weights import random_gemma2
+
+    spec = get_spec("gemma2-tiny")
+    return Gemma2Model(random_gemma2(spec, device="cpu", dtype=torch.bfloat16, seed=5, post_norm_gain=gain), "cpu")
+
+
+def test_tail_forward_fp32_matches_engine_forward():
+    """The differentiable float32 block re-implementation (interp/gradient.py) == the engine's forward from
+    the hooked layer on (up to the engine's bf16 roundings)."""
+    from taboo_brittleness_amd.interp import gradient as GR
+
+    m = _tiny_model()
+    T, l = 23, 1
+    ids = torch.randint(3, m.spec.vocab_size, (1, T), dtype=torch.int32)
+    pos = torch.arange(T, dtype=torch.int32).view(1, T)
+    cache = m.new_cache(1, 64)
+    slot = torch.zeros(1, dtype=torch.int32)
+    h_l = m.forward(ids, pos, cache, slot, stop_at=l).clone()
+    x_ref = m.forward(ids, pos, m.new_cache(1, 64), slot).float()
+    x = GR.tail_forward_fp32(m, h_l.float(), l + 1)
+    err = (x - x_ref).abs().max() / x_ref.abs().max()
+    assert err < 3e-2, float(err)
+
+
+def test_model_and_lens_gradients_match_finite_differences():
+    from taboo_brittleness_amd.interp import gradient as GR
+
+    torch.manual_seed(1)
+    m = _tiny_model()
+    T, l, spikes, ids = 12, 1, [4, 9], [17, 300]
+    h = torch.randn(T, m.spec.hidden) * 4
+    g = GR.model_gradients(m, h, l, spikes, ids)
+    assert g.shape == (2, m.spec.hidden)
+
+    def J(hh):
+        xf = GR.tail_forward_fp32(m, hh.double().float(), l + 1)
+        return float((xf[spikes] @ m.w.lm_head[ids].float().t()).sum())
+
+    d = torch.randn(m.spec.hidden)
+    eps = 1e-2
+    for i, t in enumerate(spikes):
+        hp, hm = h.clone(), h.clone()
+        hp[t] += eps * d
+        hm[t] -= eps * d
+        fd = (J(hp) - J(hm)) / (2 * eps)
+        assert abs(fd - float(g[i] @ d)) <= 2e-2 * max(1.0, abs(fd)), (fd, float(g[i] @ d))
+    # lens gradient: closed form == autograd through the final norm + unembedding rows
+    r = torch.randn(5, m.spec.hidden) * 3
+    gl = GR.lens_gradients(m, r, ids)
+    rr = r.clone().requires_grad_(True)
+    z = (ops.reference.rmsnorm(rr, m.w.norm_f.float(), m.spec.eps) @ m.w.lm_head[ids].float().t()).sum()
+    (ga,) = torch.autograd.grad(z, rr)
+    assert torch.allclose(gl, ga, atol=1e-4, rtol=1e-3)
+
+
+def test_gradient_subspace_orthonormal_and_mean_aligned():
+    from taboo_brittleness_amd.interp import gradient as GR
+
+    torch.manual_seed(2)
+    base = torch.randn(64)
+    G = base[None] * 3 + 0.3 * torch.randn(40, 64)
+    U = GR.gradient_subspace(G, 4)
+    assert U.shape == (4, 64)
+    assert torch.allclose(U @ U.t(), torch.eye(4), atol=1e-5)
+    assert float(U[0] @ (base / base.norm())) > 0.95
+    assert GR.grad_norm_ratio(G) > 0.9
+    U1 = GR.gradient_subspace(G[:1], 3, seed=7)        # rank-deficient: padded, still orthonormal
+    assert torch.allclose(U1 @ U1.t(), torch.eye(3), atol=1e-5)

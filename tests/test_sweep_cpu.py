@@ -414,3 +414,24 @@ def test_lazy_running_sums_match_kept_sums(monkeypatch):
         assert a["response_ids"] == b["response_ids"] and a["topk_ids"] == b["topk_ids"]
         for k in ("p_secret_mean", "p_secret_final", "p_secret_max", "nll_edit"):
             assert abs(a[k] - b[k]) < 1e-6 + 1e-5 * abs(a[k])
+
+
+@pytest.mark.parametrize("mode", ["grad_lens", "grad_model"])
+def test_sweep_gradient_subspaces(tmp_path, mode):
+    """EP:146's gradient alternative to the PCA subspace runs end to end; its targeted projection cells differ
+    from the PCA ones while the SAE and random-projection cells (same seeds) are unchanged."""
+    from taboo_brittleness_amd.parallel.dist import DistInfo
+    from taboo_brittleness_amd.pipelines.run_sweep import run_sweep
+
+    runs = {}
+    for sub in ("pca", mode):
+        cfg = load_config(None, OVR + [f"intervention.subspace={sub}"])
+        out = str(tmp_path / sub)
+        summ = run_sweep(cfg, out, info=DistInfo(), log=lambda *a: None)
+        assert {c["method"] for c in summ["curves"]} >= {"proj_targeted", "proj_random"}
+        runs[sub] = _cells(out)
+    a, b = runs["pca"], runs[mode]
+    assert set(a) == set(b)
+    same = lambda k: a[k]["nll_edit"] == b[k]["nll_edit"] and a[k]["p_secret_mean"] == b[k]["p_secret_mean"]  # noqa: E731
+    assert all(same(k) for k in a if a[k]["method"] in ("sae_targeted", "sae_random", "proj_random"))
+    assert not all(same(k) for k in a if a[k]["method"] == "proj_targeted")
