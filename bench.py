@@ -193,7 +193,9 @@ def main() -> None:
         if nxt is not None and k + 1 < args.warmup + args.steps:
             fut = runner.prefetch(nxt, methods) if all(p.resid is not None for p in nxt) else None
             staged[k + 1] = NextBatch(nxt, methods, future=fut)
-            if not args.no_pipeline:
+            # never across the warmup -> timed boundary: the first timed step runs its own teacher-forced tail,
+            # so the timed window holds exactly its K steps' tails (the last timed step stages nothing either)
+            if not args.no_pipeline and k + 1 != args.warmup:
                 runner.stage_next(staged[k + 1])
         # the records of step k are assembled on a host thread while step k+1's GPU work runs; decode
         # tails carry into the next step except out of warmup and out of the last timed step
