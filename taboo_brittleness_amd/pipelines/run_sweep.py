@@ -87,7 +87,8 @@ def run_sweep(cfg: Config, out_dir: str, methods: Sequence[str] = METHODS, info:
                              "world": info.world, "dp": dp_size, "tp": cfg.parallel.tp,
                              "cells_per_s": len(allres) / max(t_cells, 1e-9)}
         summary["config"] = {"layer": stack.layer, "arch": cfg.model.arch, "methods": list(methods),
-                             "budgets": cfg.intervention.budgets, "ranks": cfg.intervention.ranks}
+                             "budgets": cfg.intervention.budgets, "ranks": cfg.intervention.ranks,
+                             "subspace": cfg.intervention.subspace, "pca_pool": cfg.intervention.pca_pool}
         if cfg.intervention.measure_forcing:
             summary["forcing"] = forcing_curves(cfg, runner, pairs, methods, stack, log)
         os.makedirs(out_dir, exist_ok=True)
