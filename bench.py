@@ -66,8 +66,8 @@ def _host_rss_gb():
         return None
 
 
-def fresh(p: Pair) -> Pair:
-    return Pair(p.word, p.pidx, p.prompt, list(p.ids), list(p.forms), list(p.track))
+def fresh(p: Pair, rep: int = 0) -> Pair:
+    return Pair(p.word, p.pidx, p.prompt, list(p.ids), list(p.forms), list(p.track), rep=rep)
 
 
 def main() -> None:
@@ -104,6 +104,9 @@ def main() -> None:
     ap.add_argument("--no-fused-head", action="store_true",
                     help="vocab head as hipBLASLt logits + the decode_head kernel instead of the fused MFMA GEMM head "
                          "(softcap / log-sum-exp / argmax in the GEMM epilogue, no logits in HBM)")
+    ap.add_argument("--no-trie-decode", action="store_true",
+                    help="decode every diverged cell through all blocks on its own row instead of running blocks "
+                         "0..l once per group of a pair's cells with equal tokens (prefix-trie decode)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="do not queue the next step's teacher-forced tail behind this step's readout")
     ap.add_argument("--profile-steps", action="store_true", help="print per-phase timings per step")
@@ -147,12 +150,17 @@ def main() -> None:
                          use_graphs=not args.no_graphs, prefix_share=not args.no_prefix_share,
                          kv_pairs=(E + (3 if C else 2)) * P + 2, layer_resume=not args.no_layer_resume)
     runner.carry_rows = C
+    runner.trie_decode = not args.no_trie_decode
     templates = runner.build_pairs(cfg.words, cfg.prompts)
     methods = ("sae_targeted", "sae_random")
 
     def pairs_for(step: int):
+        # pair instance g of the whole job (every rank and step its own): template g mod 30, replicate g div 30,
+        # so a repeated (word, prompt) draws fresh random-latent controls (its targeted cells are the same
+        # experiment and repeat exactly) -- no two ranks or steps run identical random cells
         base = (step * info.world + info.rank) * P
-        return [fresh(templates[(base + j) % len(templates)]) for j in range(P)]
+        n = len(templates)
+        return [fresh(templates[(base + j) % n], rep=(base + j) // n) for j in range(P)]
 
     # prologue: baselines of the first step's pairs, SAE threshold calibration on their residuals
     cur = pairs_for(0)
@@ -308,6 +316,7 @@ def main() -> None:
                 "carry_rows": C,
                 "fused_geglu": fused_geglu,
                 "fused_head": bool(getattr(model, "fused_head", False)),
+                "trie_decode": runner.trie_decode,
                 "lora_adapters": (f"{len(cfg.words)} x rank {args.lora_rank} (unmerged bank)" if args.lora_rank
                                   else "none (weights as merged taboo models)"),
             },
@@ -323,6 +332,9 @@ def main() -> None:
                 # computed rows that were needed (the rest is row-bucket padding)
                 "decode_row_steps_per_cell": round(runner.stats["decode_row_steps"] / max(1, runner.stats["cells"]), 2),
                 "decode_bucket_eff": round(runner.stats["decode_row_steps"] / max(1, runner.stats["decode_rows_run"]), 3),
+                # prefix-trie decode: blocks-0..l rows computed (bucketed) per decode row computed; 1.0 = no sharing
+                "decode_lo_frac": round(runner.stats["decode_lo_rows_run"] / max(1, runner.stats["decode_rows_run"]), 3)
+                if runner.trie_decode else 1.0,
                 "carried_cells_per_step": round(runner.stats["carried"] / max(1, args.steps), 1),
                 # timed steps whose teacher-forced tail was queued behind the previous step's readout
                 "pipelined_steps": runner.stats["staged"],

@@ -93,6 +93,24 @@ void rope_qkv_cache(torch::Tensor qkv, torch::Tensor pos, torch::Tensor slot_of_
                     cur_stream());
 }
 
+void kv_fanout(torch::Tensor kc, torch::Tensor vc, torch::Tensor src_row, torch::Tensor slot, torch::Tensor pos,
+               int64_t nlayers) {
+  IN_BF16(kc); IN_BF16(vc); IN_I32(src_row); IN_I32(slot); IN_I32(pos);
+  TORCH_CHECK(kc.dim() == 5 && vc.sizes() == kc.sizes(), "kv_fanout: caches must be [L, slots, Hkv, S, HD]");
+  TORCH_CHECK(nlayers >= 0 && nlayers <= kc.size(0), "kv_fanout: nlayers out of range");
+  TORCH_CHECK(kc.size(4) % 8 == 0, "kv_fanout: head_dim must be a multiple of 8");
+  const int M = src_row.numel();
+  TORCH_CHECK(slot.numel() >= M && pos.numel() >= M, "kv_fanout: slot/pos shorter than src_row");
+  if (debug_checks() && M > 0) {
+    const auto sl = slot.narrow(0, 0, M);
+    TORCH_CHECK(sl.min().item<int>() >= 0 && sl.max().item<int>() < kc.size(1), "kv_fanout: slot out of range");
+    TORCH_CHECK(src_row.max().item<int>() < M, "kv_fanout: src_row out of range");
+  }
+  c10::DeviceGuard g(kc.device());
+  tb_kv_fanout(bf(kc), bf(vc), src_row.data_ptr<int32_t>(), slot.data_ptr<int32_t>(), pos.data_ptr<int32_t>(), M,
+               (int)nlayers, kc.size(1), kc.size(2), kc.size(3), kc.size(4), cur_stream());
+}
+
 void attention(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch::Tensor out, torch::Tensor pos,
                torch::Tensor slot, int64_t B, int64_t T, double scale, double softcap, int64_t window) {
   IN_BF16(q); IN_BF16(kc); IN_BF16(vc); IN_BF16(out); IN_I32(pos); IN_I32(slot);
@@ -551,6 +569,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("add_rmsnorm2", &add_rmsnorm2);
   m.def("embed_rmsnorm", &embed_rmsnorm);
   m.def("rope_qkv_cache", &rope_qkv_cache);
+  m.def("kv_fanout", &kv_fanout);
   m.def("attention", &attention);
   m.def("attn_prefix_partial", &attn_prefix_partial);
   m.def("attn_prefix_max_S", &attn_prefix_max_S);

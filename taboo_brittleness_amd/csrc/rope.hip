@@ -79,3 +79,40 @@ void tb_rope_qkv_cache(const uint16_t* qkv, const int32_t* pos, const int32_t* s
   hipLaunchKernelGGL(rope_qkv_cache_kernel, dim3(M), dim3(256), 0, st, qkv, pos, slot_of_row, cos_t, sin_t, q_out,
                      kc, vc, Hq, Hkv, HD, S, max_pos);
 }
+
+// KV fan-out of a prefix-trie decode step (runtime/generation.py, shared decode): rows that share their
+// whole token sequence with a representative row (same pair, same tokens) compute blocks 0..nl-1 only
+// through that representative; this copies the K/V the representative just wrote at its position into
+// every member row's own slot, for those layers, so any member can become a representative later (when
+// its group splits) with its full history in place.  One workgroup per (row, layer); src_row < 0 = skip.
+namespace {
+
+__global__ void __launch_bounds__(256) kv_fanout_kernel(uint16_t* __restrict__ kc, uint16_t* __restrict__ vc,
+                                                        const int32_t* __restrict__ src_row,
+                                                        const int32_t* __restrict__ slot,
+                                                        const int32_t* __restrict__ pos, int slots, int Hkv, int S,
+                                                        int HD) {
+  const int r = blockIdx.x, l = blockIdx.y;
+  const int s = src_row[r];
+  if (s < 0 || s == r) return;
+  const int pd = pos[r], ps = pos[s];
+  if (pd < 0 || pd >= S || ps < 0 || ps >= S) return;
+  const int gph = HD >> 3, nvec = Hkv * gph;
+  const size_t lay = (size_t)l * slots * Hkv;
+  const size_t sd = lay + (size_t)slot[r] * Hkv, ss = lay + (size_t)slot[s] * Hkv;
+  for (int i = threadIdx.x; i < nvec; i += blockDim.x) {
+    const int h = i / gph, g = i % gph;
+    const size_t od = ((sd + h) * S + pd) * HD + g * 8, os = ((ss + h) * S + ps) * HD + g * 8;
+    *reinterpret_cast<uint4*>(kc + od) = *reinterpret_cast<const uint4*>(kc + os);
+    *reinterpret_cast<uint4*>(vc + od) = *reinterpret_cast<const uint4*>(vc + os);
+  }
+}
+
+}  // namespace
+
+void tb_kv_fanout(uint16_t* kc, uint16_t* vc, const int32_t* src_row, const int32_t* slot, const int32_t* pos, int M,
+                  int nlayers, int slots, int Hkv, int S, int HD, hipStream_t st) {
+  if (M <= 0 || nlayers <= 0) return;
+  hipLaunchKernelGGL(kv_fanout_kernel, dim3(M, nlayers), dim3(256), 0, st, kc, vc, src_row, slot, pos, slots, Hkv,
+                     S, HD);
+}

@@ -231,6 +231,23 @@ class Gemma2Model:
 
         return self._run(ids.reshape(M), pos.reshape(M), cache, ws, attn, hooks, stop_at, B, T, slot)
 
+    def forward_resume(self, h_in: torch.Tensor, pos: torch.Tensor, cache: KVCache, slot: torch.Tensor, start: int,
+                       hooks: Optional[Dict[int, Sequence[Hook]]] = None, ws: Optional[_Workspace] = None,
+                       kv_prefix: Optional[KVPrefix] = None) -> torch.Tensor:
+        """Decode rows (``T == 1``) resumed from the residual stream *after* block ``start``: ``h_in [B, d]``
+        (may be ``ws.h`` itself), then block ``start``'s hooks and blocks ``start+1..``.  The prefix-trie
+        decode (runtime/generation.py) feeds it the shared blocks-``0..start`` output of each row's group."""
+        B = pos.shape[0]
+        ws = ws or self.workspace(B)
+        ws.slot_rows.copy_(slot.view(B))
+
+        def attn(l, q, kc, vc, pos32, window, out):
+            pre = kv_prefix.layer(l, B) if kv_prefix is not None else None
+            ops.attention(q, kc, vc, pos32, slot, B, 1, self.scale, self.spec.attn_softcap, window, out=out,
+                          prefix=pre)
+
+        return self._run(None, pos.reshape(B), cache, ws, attn, hooks, None, B, 1, slot, start=start, h_in=h_in)
+
     def forward_packed(self, ids: Optional[torch.Tensor], pos: torch.Tensor, slot_rows: torch.Tensor,
                        blk: torch.Tensor, cache: KVCache, hooks: Optional[Dict[int, Sequence[Hook]]] = None,
                        stop_at: Optional[int] = None, ws: Optional[_Workspace] = None,
@@ -277,7 +294,8 @@ class Gemma2Model:
             first = 0
         else:
             h, x = ws.h, ws.x
-            h.copy_(h_in)
+            if h_in.data_ptr() != h.data_ptr():
+                h.copy_(h_in)
             ops.rmsnorm(h, self.norm_next[start], s.eps, out=x)
             if hooks and start in hooks:
                 ctx = HookCtx(start, B, T, pos32, ctx_slot, self.norm_next[start], s.eps, self)

@@ -116,6 +116,17 @@ def rope_qkv_cache(qkv, pos, slot_of_row, cos_t, sin_t, kc, vc, Hq, Hkv, HD, q_o
     return q
 
 
+def kv_fanout(kc, vc, src_row, slot, pos, nlayers: int) -> None:
+    """Prefix-trie decode: copy the K/V of layers ``< nlayers`` that row ``src_row[r]`` wrote at its position
+    into row ``r``'s own slot at ``r``'s position (``kc/vc [L, slots, Hkv, S, HD]``; ``src_row < 0`` or
+    ``== r``: nothing).  A source row must not itself be a copy target (representatives only), so the
+    rows are independent."""
+    if kc.is_cuda:
+        _k().kv_fanout(kc, vc, src_row, slot, pos, int(nlayers))
+        return
+    ref.kv_fanout(kc, vc, src_row, slot, pos, nlayers)
+
+
 def attention(q, kc, vc, pos, slot, B, T, scale, softcap, window, out=None, prefix=None):
     """``prefix = (pk, pv, pslot, plen)`` (decode, T == 1): row ``b`` reads keys ``[0, plen[b])`` from slot
     ``pslot[b]`` of the shared prefix cache ``pk/pv [P, Hkv, S, HD]`` instead of its own slot."""

@@ -47,6 +47,28 @@ def rope_tables(head_dim: int, max_pos: int, theta: float, device=None):
     return freqs.cos().to(device), freqs.sin().to(device)
 
 
+def kv_fanout(kc: torch.Tensor, vc: torch.Tensor, src_row: torch.Tensor, slot: torch.Tensor, pos: torch.Tensor,
+              nlayers: int) -> None:
+    """Reference of ``ops.kv_fanout``: ``kc/vc[l, slot[r], :, pos[r]] = kc/vc[l, slot[s], :, pos[s]]`` for
+    ``l < nlayers`` and every row ``r`` with ``s = src_row[r] >= 0, s != r`` (both positions in the cache)."""
+    S = kc.shape[3]
+    M = src_row.numel()
+    s = src_row.view(-1).long().cpu()
+    r = torch.arange(M)
+    s0 = s.clamp(min=0)
+    p = pos.view(-1)[:M].long().cpu()
+    ok = (s >= 0) & (s != r) & (p >= 0) & (p < S) & (p[s0] >= 0) & (p[s0] < S)
+    idx = r[ok]
+    if idx.numel() == 0 or nlayers <= 0:
+        return
+    sl = slot.view(-1).long().cpu()
+    src = s0[idx]
+    ds, dp, ss, sp = sl[idx], p[idx], sl[src], p[src]
+    for c in (kc, vc):
+        dev = c.device
+        c[:nlayers, ds.to(dev), :, dp.to(dev)] = c[:nlayers, ss.to(dev), :, sp.to(dev)]
+
+
 def rope_qkv_cache(qkv: torch.Tensor, pos: torch.Tensor, slot_of_row: torch.Tensor, cos_t: torch.Tensor,
                    sin_t: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, Hq: int, Hkv: int, HD: int) -> torch.Tensor:
     M = pos.numel()

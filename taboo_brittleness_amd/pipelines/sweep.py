@@ -71,6 +71,7 @@ class Pair:
     leak: Optional[bool] = None                         # baseline response contains the secret (cached)
     p_secret_mean: Optional[float] = None               # cached mean of p_secret (result records)
     forms_l: Optional[set] = None
+    rep: int = 0                                        # replicate of this (word, prompt): seeds its random cells
 
     @property
     def first_edit(self) -> int:
@@ -153,12 +154,16 @@ class SweepRunner:
         self.tf_streams = os.environ.get("TB_TF_STREAMS", "0") == "1"   # no measurable gain; opt-in
         self.tf_prefix = os.environ.get("TB_TF_PREFIX", "1") == "1"
         self.stats: Dict[str, int] = {"cells": 0, "diverged": 0, "tf_rows": 0, "lens_rows": 0,
-                                      "decode_row_steps": 0, "decode_rows_run": 0, "carried": 0, "staged": 0}
+                                      "decode_row_steps": 0, "decode_rows_run": 0, "carried": 0, "staged": 0,
+                                      "decode_lo_rows_run": 0, "decode_lo_groups": 0}
         # decode-tail carry-over (opt-in; needs ``batch`` to include ``carry_rows`` spare slots): once fewer
         # than ``carry_rows`` diverged cells still decode, the rest continue in the next batch's decode
         # (merged with its new rows) instead of running a long small-batch tail.  Records of carried cells
         # come out with the batch that finishes them; ``run_cells(..., drain=True)`` carries nothing.
         self.carry_rows = 0
+        # prefix-trie decode: diverged cells of a pair with equal tokens run blocks 0..l once per group
+        # (Generator.decode share_keys); TB_TRIE_DECODE=0 / SweepRunner.trie_decode = False: every row alone
+        self.trie_decode = os.environ.get("TB_TRIE_DECODE", "1") == "1"
         self._carry: List[_Carry] = []
         self._next: Optional["NextBatch"] = None      # batch of the next run_cells call (stage_next)
         # lazy running lens sums: a pair's [n + 1, V] fp32 running sums (52 MB at the 256k vocab) are rebuilt from
@@ -332,7 +337,10 @@ class SweepRunner:
                     budgets, trials = self.iv.ranks, (1 if meth == "proj_targeted" else self.iv.proj_random_trials)
                 for bud in budgets:
                     for t in range(trials):
-                        cells.append(Cell(pi, meth, int(bud), t, A.cell_seed(base, p.word, p.pidx, meth, bud, t)))
+                        # replicate 0 keeps the plain key, so sweeps seeded before replicates existed reproduce;
+                        # a replicate > 0 (the bench's repeated pairs) draws its own random latent sets / subspaces
+                        key = (base, p.word, p.pidx, meth, bud, t) + ((p.rep,) if p.rep else ())
+                        cells.append(Cell(pi, meth, int(bud), t, A.cell_seed(*key)))
         return cells
 
     def _bases(self, pairs: Sequence[Pair]) -> Dict[str, torch.Tensor]:
@@ -911,11 +919,17 @@ class SweepRunner:
                 pnll[nr_here:, : nm.shape[1]] = _h2d(np.ascontiguousarray(nm, dtype=np.float32),
                                                     self.dev).to(self.dev, non_blocking=True)
             carry_ok = (self.carry_rows > 0 and not self._drain_batch and n_ride_rows == 0)
+            skeys = self._trie_keys(nr_here, [carry_in[i - nd] if i >= nd else int(e_d[i]) for i in order.tolist()],
+                                    pre_slot[nr_here:], pre_lo[nr_here:], starts[nr_here:])
             ran = gen.decode(torch.from_numpy(toks.astype(np.int32)), starts, (pref_all, lens_all), max(steps, 1),
                              nrows, hooks, "sweep", prefix_nll=pnll, slots=slots, row_steps=rsteps,
                              prefix_rows=(pre_slot, pre_lo, pre_hi),
                              stop_below=self.carry_rows if carry_ok else 0,
-                             min_steps=max([cr.steps for cr in carry_in] + [0]))
+                             min_steps=max([cr.steps for cr in carry_in] + [0]),
+                             share_keys=skeys, share_split=self.layer if skeys is not None else None)
+            if skeys is not None:
+                self.stats["decode_lo_rows_run"] += gen.last_rows_lo
+                self.stats["decode_lo_groups"] += gen.last_groups
             self._tick("decode_launched")
             out = gen.collect(nrows, self.max_new, ([] if overlap else [p.plen for p in rb]) +
                               [(cell_pairs[src[1]].plen if src[0] == "new" else src[1].pair.plen) for src in row_src])
@@ -966,6 +980,36 @@ class SweepRunner:
             self._carry_move_pending = None
         self._tick("results")
         return results
+
+    def _trie_keys(self, n_ride: int, rows: Sequence, pre_slot: np.ndarray, pre_lo: np.ndarray,
+                   start: np.ndarray) -> Optional[np.ndarray]:
+        """Group keys of the decode rows for the prefix-trie decode (``Generator.decode(share_keys=)``), or
+        None when no two rows can share.  Blocks ``0..l`` of a diverged cell depend only on its tokens: below
+        its divergence ``D`` they are the pair's baseline (read from the pair KV, ``pre_slot`` / ``pre_lo``),
+        from ``D`` on its own generated tokens.  Rows of one pair with equal tokens from ``D`` (new rows: the
+        divergent token ``e_d``; carried rows: their tokens since ``D``) therefore get one key; the ride-along
+        baselines (the first ``n_ride`` rows) each get their own.  ``rows[i]`` (cell rows in decode order): the
+        divergent token of a new row, or the carry record of a carried one."""
+        n = len(rows)
+        if not self.trie_decode or n < 2 or self.gen.kv_prefix is None:
+            return None
+        wk = max([1] + [len(cr.prefix) - cr.d for cr in rows if isinstance(cr, _Carry)])
+        mat = np.full((n, 3 + wk), -2, np.int64)
+        mat[:, 0], mat[:, 1], mat[:, 2] = pre_slot, pre_lo, start
+        for i, cr in enumerate(rows):
+            if isinstance(cr, _Carry):
+                t = cr.prefix[cr.d:]
+                mat[i, 3: 3 + len(t)] = t
+            else:
+                mat[i, 3] = cr
+        alone = pre_lo <= 0                       # no shared prefix: nothing to share
+        mat[alone, 0] = -1 - np.nonzero(alone)[0]
+        _, inv = np.unique(mat, axis=0, return_inverse=True)
+        inv = inv.reshape(-1)
+        u = int(inv.max()) + 1 if n else 0
+        if u == n:
+            return None                           # all distinct: groups never merge, plain decode
+        return np.concatenate([np.arange(n_ride, dtype=np.int64) + u, inv.astype(np.int64)])
 
     def _carry_out(self, plan, cell_pairs, batch, D, seg, nll_c, row_src, rsteps, ran, n_ride_rows):
         """After an early-stopped decode: record the still-unfinished cell rows as carried and return the

@@ -21,6 +21,16 @@ together:
 Every generated token is also fed once more through the model (the final
 step) so the hooked layer's residual exists for the whole response — the
 equivalent of the reference re-tracing the decoded text (`src/models.py:127`).
+
+Prefix-trie decode (``decode(share_keys=..., share_split=l)``): when every hook sits at
+block ``l`` or later, blocks ``0..l`` of a row are a function of its token sequence alone
+(its KV below ``l`` too).  Rows with equal group keys (same shared prefix, same tokens —
+sweep cells of one pair that left their baseline the same way) then run blocks ``0..l``
+once per group: a "lo" graph over one representative row per group, then a "hi" graph
+that hands every row its group's residual, copies the representatives' new K/V of blocks
+``0..l`` into the members' slots (``ops.kv_fanout``, so a group may split later) and runs
+block ``l``'s hooks and blocks ``l+1..`` per row.  Groups are re-formed after every step
+from (group, emitted token) on the device (groups only ever split).
 """
 from __future__ import annotations
 
@@ -32,7 +42,7 @@ import numpy as np
 import torch
 
 from .. import ops
-from ..models.gemma2 import Gemma2Model, KVCache, KVPrefix
+from ..models.gemma2 import Gemma2Model, KVCache, KVPrefix, _Workspace
 
 
 @dataclass
@@ -90,6 +100,9 @@ class Generator:
         self._graphs: Dict[tuple, "torch.cuda.CUDAGraph"] = {}
         self.ws = model.workspace(batch)       # pinned: captured graphs hold these pointers (and row views)
         self.kv_prefix: Optional[KVPrefix] = None
+        self._share: Optional[dict] = None     # prefix-trie decode buffers (allocated on first use)
+        self.last_rows_lo = 0                  # blocks-0..l row-steps of the last shared decode (bucketed)
+        self.last_groups = 0                   # its groups summed over the steps
 
     def enable_kv_prefix(self, k: torch.Tensor, v: torch.Tensor, split: int) -> None:
         """Let decode rows read a shared read-only KV prefix from ``k/v [L, P, Hkv, S, HD]`` (see
@@ -128,6 +141,86 @@ class Generator:
         ws = self.ws if nb == self.B else self.ws.rows(nb)
         kw = {"kv_prefix": self.kv_prefix} if self.kv_prefix is not None else {}
         x = self.m.forward(self.tok[:nb], self.pos[:nb], self.cache, self.slot[:nb], hooks, ws=ws, **kw)
+        self._finish_step(x, nb)
+
+    # ------------------------------------------------------- prefix-trie decode
+    def _share_bufs(self, split: int) -> dict:
+        sh = self._share
+        if sh is None or sh["split"] != split:
+            B, dev = self.B, self.dev
+            sh = self._share = {
+                "split": split,
+                "ws": _Workspace(self.m.lspec, B, dev, self.m.dtype),       # blocks 0..l of the representatives
+                "gid": torch.full((B,), -1, dtype=torch.int64, device=dev),  # group of each row (dense per step)
+                "rep": torch.zeros(B, dtype=torch.int64, device=dev),       # lo row -> its representative row
+                "grp": torch.zeros(B, dtype=torch.int64, device=dev),       # row -> its group's lo row
+                "src": torch.full((B,), -1, dtype=torch.int32, device=dev),  # KV fan-out source row (-1: none)
+                "U": torch.zeros((), dtype=torch.int64, device=dev),
+                "ar": torch.arange(B, dtype=torch.int64, device=dev),
+                "tok": torch.zeros(B, 1, dtype=torch.int32, device=dev),
+                "pos": torch.zeros(B, 1, dtype=torch.int32, device=dev),
+                "slot": torch.zeros(B, dtype=torch.int32, device=dev),
+                "kp": None,
+            }
+            self._graphs = {k: g for k, g in self._graphs.items() if k[0] not in ("lo", "hi")}
+        kp = self.kv_prefix
+        if kp is not None and (sh["kp"] is None or sh["kp"].k is not kp.k):
+            z = lambda: torch.zeros(self.B, dtype=torch.int32, device=self.dev)   # noqa: E731
+            sh["kp"] = KVPrefix(kp.k, kp.v, z(), z(), z(), kp.split)
+        return sh
+
+    def _decode_step_lo(self, nb: int) -> None:
+        """Blocks ``0..l`` of the first ``nb`` representative rows (rows ``>= U`` are parked)."""
+        sh = self._share
+        r = sh["rep"][:nb]
+        valid = sh["ar"][:nb] < sh["U"]
+        sh["tok"][:nb].copy_(self.tok.index_select(0, r))
+        sh["pos"][:nb].copy_(torch.where(valid.view(-1, 1), self.pos.index_select(0, r), self.S))
+        sh["slot"][:nb].copy_(self.slot.index_select(0, r))
+        kw = {}
+        if sh["kp"] is not None:
+            kp, kl = self.kv_prefix, sh["kp"]
+            kl.slot[:nb].copy_(kp.slot.index_select(0, r))
+            kl.len_lo[:nb].copy_(kp.len_lo.index_select(0, r))
+            kw["kv_prefix"] = kl
+        ws = sh["ws"] if nb == self.B else sh["ws"].rows(nb)
+        self.m.forward(sh["tok"][:nb], sh["pos"][:nb], self.cache, sh["slot"][:nb], None, stop_at=sh["split"],
+                       ws=ws, **kw)
+
+    def _decode_step_hi(self, hooks, nb: int) -> None:
+        """Every row: its group's blocks-``0..l`` residual, the K/V fan-out, block ``l``'s hooks, blocks
+        ``l+1..``, the head."""
+        sh = self._share
+        ws = self.ws if nb == self.B else self.ws.rows(nb)
+        torch.index_select(sh["ws"].h, 0, sh["grp"][:nb], out=ws.h)
+        ops.kv_fanout(self.cache.k, self.cache.v, sh["src"][:nb], self.slot[:nb], self.pos[:nb].view(-1),
+                      sh["split"] + 1)
+        kw = {"kv_prefix": self.kv_prefix} if self.kv_prefix is not None else {}
+        x = self.m.forward_resume(ws.h, self.pos[:nb], self.cache, self.slot[:nb], sh["split"], hooks, ws=ws, **kw)
+        self._finish_step(x, nb)
+
+    def _share_group(self, si: int, nb: int, act: int) -> int:
+        """Re-form the groups of the first ``nb`` rows after step ``si - 1`` (rows ``>= act`` need no more
+        steps and share one don't-care group); returns the group count U (one host sync)."""
+        sh = self._share
+        gid = sh["gid"][:nb]
+        key = gid.clone() if si == 0 else gid * self.m.spec.vocab_size + self.tok[:nb, 0].long()
+        if act < nb:
+            key[act:] = -1
+        uniq, inv = torch.unique(key, sorted=True, return_inverse=True)
+        U = int(uniq.numel())
+        ar = sh["ar"][:nb]
+        rep = torch.full((U,), nb, dtype=torch.int64, device=self.dev).scatter_reduce_(0, inv, ar, reduce="amin")
+        src = rep.index_select(0, inv)
+        src = torch.where((src == ar) | (ar >= act), -1, src)
+        sh["rep"][:U].copy_(rep)
+        sh["grp"][:nb].copy_(inv)
+        gid.copy_(inv)
+        sh["src"][:nb].copy_(src.to(torch.int32))
+        sh["U"].fill_(U)
+        return U
+
+    def _finish_step(self, x: torch.Tensor, nb: int) -> None:
         col = torch.clamp(self.step_idx[:nb], max=self.W - 1)
         torch.gather(self.tf_tgt[:nb], 1, col, out=self.tf_step[:nb].view(-1, 1))
         if getattr(self.m, "fused_head", False):
@@ -152,21 +245,38 @@ class Generator:
     def _state(self):
         return (self.tok, self.pos, self.done, self.step_idx, self.out_tokens, self.out_nll, self.out_tf_nll)
 
-    def _capture(self, hooks, key, nb: int):
+    def _capture(self, hooks, key, nb: int, part: Optional[str] = None):
+        """Capture one decode step of ``nb`` rows (``part``: None = whole step, "lo" / "hi" = the two halves
+        of a prefix-trie step)."""
+        fn = {None: lambda: self._decode_step(hooks, nb), "lo": lambda: self._decode_step_lo(nb),
+              "hi": lambda: self._decode_step_hi(hooks, nb)}[part]
         # warm up (hipBLASLt heuristics, kernel attributes) outside capture on a side stream
         s = torch.cuda.Stream(device=self.dev)
         s.wait_stream(torch.cuda.current_stream(self.dev))
         saved = [t.clone() for t in self._state()]
         with torch.cuda.stream(s):
-            self._decode_step(hooks, nb)
+            fn()
         torch.cuda.current_stream(self.dev).wait_stream(s)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            self._decode_step(hooks, nb)
+            fn()
         for t, v in zip(self._state(), saved):
             t.copy_(v)
-        self._graphs[(key, nb)] = g
+        self._graphs[(key, nb) if part is None else (part, key, nb)] = g
         return g
+
+    def _replay(self, hooks, key, nb: int, part: Optional[str] = None) -> None:
+        if self.use_graphs and key is not None:
+            g = self._graphs.get((key, nb) if part is None else (part, key, nb))
+            if g is None:
+                g = self._capture(hooks, key, nb, part)
+            g.replay()
+        elif part is None:
+            self._decode_step(hooks, nb)
+        elif part == "lo":
+            self._decode_step_lo(nb)
+        else:
+            self._decode_step_hi(hooks, nb)
 
     # ---------------------------------------------------------------- prefill
     @torch.no_grad()
@@ -210,7 +320,8 @@ class Generator:
                slots: Optional[Sequence[int]] = None,
                row_steps: Optional[Sequence[int]] = None,
                prefix_rows: Optional[Tuple[Sequence[int], Sequence[int], Sequence[int]]] = None,
-               stop_below: int = 0, min_steps: int = 0) -> int:
+               stop_below: int = 0, min_steps: int = 0,
+               share_keys: Optional[Sequence[int]] = None, share_split: Optional[int] = None) -> int:
         """Decode ``n_steps`` lockstep steps.  Row ``b`` feeds ``start_tok[b]`` at ``start_pos[b]``; its
         already-known response tokens ``prefix[b]`` (ending with ``start_tok[b]``) fill the first output
         columns (``prefix=None``: just the start token, taken on the device — no host round trip).
@@ -234,7 +345,11 @@ class Generator:
 
         ``stop_below`` (with ``row_steps``): stop early, once at least ``min_steps`` steps ran and fewer
         than ``stop_below`` rows still need a step — the caller carries those rows (:meth:`row_state`)
-        into a later decode instead of running a long small-batch tail.  Returns the steps run."""
+        into a later decode instead of running a long small-batch tail.  Returns the steps run.
+
+        ``share_keys[b]`` (dense ints, with ``share_split = l``): prefix-trie decode (module docstring).  Rows
+        with equal keys must have equal tokens so far, start positions, shared-prefix slots / lengths and
+        adapters — their blocks ``0..l`` are then identical — and every hook must sit at block ``>= l``."""
         B = self.B
         if self.kv_prefix is not None:
             kp = self.kv_prefix
@@ -311,20 +426,35 @@ class Generator:
             # active[s] = rows still needing step s (rows are sorted, so they form a prefix)
             active = np.searchsorted(-rs, -np.arange(n_steps), side="left")
         self.last_rows = [0, 0]       # (row-steps needed, row-steps computed incl. bucket padding)
+        self.last_rows_lo = 0
+        self.last_groups = 0
+        share = share_keys is not None and share_split is not None
+        if share:
+            assert not hooks or min(hooks) >= share_split, "prefix-trie decode needs every hook at block >= split"
+            assert self.kv_prefix is None or self.kv_prefix.chunks is None, "prefix-trie decode: no cascade prefix"
+            sh = self._share_bufs(int(share_split))
+            keys = np.asarray(list(share_keys), np.int64)
+            assert keys.size == n_rows, "share_keys: one key per row"
+            sh["gid"].copy_(_up(np.concatenate([keys, np.full(B - keys.size, -1, np.int64)]), self.dev),
+                            non_blocking=True)
+            sh["src"].fill_(-1)
         ran = 0
         for si in range(n_steps):
             if stop_below and active is not None and si >= min_steps and int(active[si]) < stop_below:
                 break
-            nb_s = nb if active is None else self.bucket(max(1, int(active[si])))
-            self.last_rows[0] += n_rows if active is None else int(active[si])
+            act = n_rows if active is None else int(active[si])
+            nb_s = nb if active is None else self.bucket(max(1, act))
+            self.last_rows[0] += act
             self.last_rows[1] += nb_s
-            if self.use_graphs and graph_key is not None:
-                g = self._graphs.get((graph_key, nb_s))
-                if g is None:
-                    g = self._capture(hooks, graph_key, nb_s)
-                g.replay()
+            if share:
+                u = self._share_group(si, nb_s, act)
+                nu = self.bucket(u)
+                self.last_rows_lo += nu
+                self.last_groups += u
+                self._replay(None, graph_key, nu, "lo")
+                self._replay(hooks, graph_key, nb_s, "hi")
             else:
-                self._decode_step(hooks, nb_s)
+                self._replay(hooks, graph_key, nb_s)
             ran += 1
         return ran
 
@@ -356,11 +486,15 @@ class Generator:
             self.kv_prefix.len_hi.zero_()
             if self.kv_prefix.nchunks is not None:
                 self.kv_prefix.nchunks.zero_()
+        if self._share is not None:
+            self._share["U"].zero_()          # every lo row parked
+            self._share["src"].fill_(-1)
         n = 0
         for nb in sizes:
-            if (graph_key, nb) not in self._graphs:
-                self._capture(hooks, graph_key, nb)
-                n += 1
+            for part in ((None, "lo", "hi") if self._share is not None else (None,)):
+                if ((graph_key, nb) if part is None else (part, graph_key, nb)) not in self._graphs:
+                    self._capture(hooks, graph_key, nb, part)
+                    n += 1
         for t, v in zip(self._state(), saved):
             t.copy_(v)
         return n

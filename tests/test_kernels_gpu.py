@@ -62,6 +62,23 @@ def test_rope_and_cache(gpu):
     _close(vcg, vc, atol=1e-6)
 
 
+def test_kv_fanout(gpu):
+    """Prefix-trie KV fan-out: members get their representative's K/V of the first layers at their own
+    position; skipped rows (src < 0, src == r, positions outside the cache) and deeper layers untouched."""
+    torch.manual_seed(3)
+    L, slots, Hkv, S, HD = 5, 7, 2, 16, 256
+    kc = torch.randn(L, slots, Hkv, S, HD, dtype=BF)
+    vc = torch.randn_like(kc)
+    src = torch.tensor([-1, 0, 0, 3, 3, -1, 3], dtype=torch.int32)     # sources are representatives (src -1 / self)
+    slot = torch.tensor([1, 2, 3, 4, 5, 6, 0], dtype=torch.int32)
+    pos = torch.tensor([9, 9, 9, 4, 4, 16, 3], dtype=torch.int32)
+    kg, vg = kc.to(gpu), vc.to(gpu)
+    ops.kv_fanout(kg, vg, src.to(gpu), slot.to(gpu), pos.to(gpu), 3)
+    ref.kv_fanout(kc, vc, src, slot, pos, 3)
+    assert torch.equal(kg.cpu(), kc) and torch.equal(vg.cpu(), vc)
+    assert torch.equal(kc[:3, 2, :, 9], kc[:3, 1, :, 9]) and torch.equal(vc[:3, 5, :, 4], vc[:3, 4, :, 4])
+
+
 @pytest.mark.parametrize("G,HD", [(2, 256), (1, 256), (2, 128)])
 def test_attention_prefill_decode(gpu, G, HD):
     torch.manual_seed(2)

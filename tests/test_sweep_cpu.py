@@ -435,3 +435,53 @@ def test_sweep_gradient_subspaces(tmp_path, mode):
     same = lambda k: a[k]["nll_edit"] == b[k]["nll_edit"] and a[k]["p_secret_mean"] == b[k]["p_secret_mean"]  # noqa: E731
     assert all(same(k) for k in a if a[k]["method"] in ("sae_targeted", "sae_random", "proj_random"))
     assert not all(same(k) for k in a if a[k]["method"] == "proj_targeted")
+
+
+@pytest.mark.parametrize("carry", [0, 6])
+def test_trie_decode_is_exact(carry):
+    """Prefix-trie decode (diverged cells of a pair with equal tokens run blocks 0..l once per group, the
+    group's K/V fanned out to the members, groups re-formed per step) reproduces the per-row decode, also
+    with decode-tail carry-over; the shared path must actually run fewer blocks-0..l rows."""
+    from dataclasses import replace
+
+    from taboo_brittleness_amd.interp.sae import JumpReLUSAE
+    from taboo_brittleness_amd.models.gemma2 import Gemma2Model
+    from taboo_brittleness_amd.models.spec import GEMMA2_TINY
+    from taboo_brittleness_amd.models.tokenizer import SyntheticTokenizer
+    from taboo_brittleness_amd.models.weights import random_gemma2
+    from taboo_brittleness_amd.pipelines.sweep import SweepRunner
+
+    spec = replace(GEMMA2_TINY, vocab_size=1024, layers=4, hidden=256, ffn=512)
+    m = Gemma2Model(random_gemma2(spec, dtype=torch.bfloat16, seed=7, norm_std=0.1, post_norm_gain=8.0), "cpu")
+    cfg = load_config(None, OVR + ["experiment.max_new_tokens=12", "intervention.random_trials=4",
+                                   "prompts=['Give me a hint!', 'Any hints available?', 'I need one more clue.']"])
+    tok = SyntheticTokenizer(vocab_size=spec.vocab_size)
+    key = lambda r: (r["word"], r["prompt_idx"], r["method"], r["budget"], r["trial"])   # noqa: E731
+    res, stats = {}, {}
+    for trie in (False, True):
+        sae = JumpReLUSAE.random(spec.hidden, 512, seed=2, device="cpu")
+        r = SweepRunner(cfg, m, tok, sae, batch=60 + carry, device="cpu", layer=2, use_graphs=False,
+                        prefix_share=True, layer_resume=True, kv_pairs=8)
+        r.trie_decode = trie
+        r.carry_rows = carry
+        pairs = r.build_pairs(["ship"], cfg.prompts[:3])
+        r.run_baselines(pairs)
+        out = []
+        for i, j in enumerate(range(3)):
+            sub = [pairs[j]]
+            out += r.run_cells(sub, r.make_cells(sub), measure_nll=True, drain=(i == 2))
+        res[trie] = {key(x): x for x in out}
+        stats[trie] = dict(r.stats)
+    assert stats[True]["diverged"] > 0
+    if not carry:               # (the carry variant checks exactness; its few diverged rows barely share)
+        assert 0 < stats[True]["decode_lo_groups"] < stats[True]["decode_row_steps"], stats[True]
+    else:
+        assert stats[True]["carried"] > 0, stats[True]
+    assert set(res[False]) == set(res[True])
+    for k, a in res[False].items():
+        b = res[True][k]
+        assert a["response_ids"] == b["response_ids"], k
+        assert a["topk_ids"] == b["topk_ids"], k
+        assert abs(a["nll_edit"] - b["nll_edit"]) < 1e-5 and abs(a["nll_self"] - b["nll_self"]) < 1e-5
+        for f in ("p_secret_mean", "p_secret_final", "p_secret_max"):
+            assert abs(a[f] - b[f]) < 1e-6 + 1e-5 * abs(a[f])
