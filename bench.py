@@ -328,6 +328,8 @@ def main() -> None:
                 "diverged_frac": round(runner.stats["diverged"] / max(1, runner.stats["cells"]), 4),
                 "tail_rows_per_cell": round(runner.stats["tf_rows"] / max(1, runner.stats["cells"]), 2),
                 "lens_rows_per_cell": round(runner.stats["lens_rows"] / max(1, runner.stats["cells"]), 2),
+                # lens rows actually unembedded (rows of equal-token cells at unedited positions evaluated once)
+                "lens_gemm_rows_per_cell": round(runner.stats["lens_gemm_rows"] / max(1, runner.stats["cells"]), 2),
                 # full-model decode of the diverged cells: row-steps needed per cell, and the fraction of
                 # computed rows that were needed (the rest is row-bucket padding)
                 "decode_row_steps_per_cell": round(runner.stats["decode_row_steps"] / max(1, runner.stats["cells"]), 2),

@@ -45,10 +45,10 @@ void tb_geglu(const uint16_t* gu, uint16_t* out, int M, int F, hipStream_t st);
 void tb_argmax_rows(const uint16_t* logits, int32_t* out, int R, int V, float cap, hipStream_t st);
 void tb_row_lse(const uint16_t* logits, float* lse, int R, int V, float cap, int emulate_bf16, hipStream_t st);
 void tb_gather_probs(const uint16_t* logits, const float* lse, const int32_t* ids, float* out, int R, int K, int V,
-                     int round_bf16, hipStream_t st);
+                     int round_bf16, const int32_t* rowmap, hipStream_t st);
 void tb_lens_colsum(const uint16_t* logits, const float* lse, const uint8_t* mask, const int32_t* excl, float* acc,
                     int B, int T, int V, int accumulate, int round_bf16, const int32_t* offs, float* cum,
-                    hipStream_t st);
+                    const int32_t* rowmap, hipStream_t st);
 void tb_topk_rows(const float* x, float* vals, int32_t* idx, int R, int V, int K, hipStream_t st);
 void tb_xent_rows(const uint16_t* logits, const int32_t* tgt, float* nll, int R, int V, float cap, int emulate_bf16,
                   hipStream_t st);

@@ -248,23 +248,42 @@ void row_lse(torch::Tensor logits, torch::Tensor lse, double cap, bool emulate_b
   tb_row_lse(cbf(logits), lse.data_ptr<float>(), R, V, (float)cap, emulate_bf16 ? 1 : 0, cur_stream());
 }
 
-void gather_probs(torch::Tensor logits, torch::Tensor lse, torch::Tensor ids, torch::Tensor out, bool round_bf16) {
+// rowmap (optional, int32 [R_logical]): logical row r reads logits / lse row rowmap[r] (deduplicated rows).
+const int32_t* rowmap_ptr(const c10::optional<torch::Tensor>& rowmap, int64_t R_phys, int64_t R_log) {
+  if (!rowmap.has_value()) return nullptr;
+  IN_I32((*rowmap));
+  TORCH_CHECK(rowmap->numel() == R_log, "rowmap must have one entry per logical row");
+  if (debug_checks() && R_log > 0)
+    TORCH_CHECK(rowmap->min().item<int>() >= 0 && rowmap->max().item<int>() < R_phys, "rowmap out of range");
+  return rowmap->data_ptr<int32_t>();
+}
+
+void gather_probs(torch::Tensor logits, torch::Tensor lse, torch::Tensor ids, torch::Tensor out, bool round_bf16,
+                  c10::optional<torch::Tensor> rowmap) {
   IN_BF16(logits); IN_F32(lse); IN_I32(ids); IN_F32(out);
-  const int V = logits.size(-1), R = logits.numel() / V;
-  TORCH_CHECK(ids.numel() % R == 0 && out.numel() == ids.numel(), "gather shapes");
-  const int K = ids.numel() / R;
+  const int V = logits.size(-1);
+  const int Rp = logits.numel() / V;
+  const int R = rowmap.has_value() ? rowmap->numel() : Rp;
+  TORCH_CHECK(R > 0 ? (ids.numel() % R == 0 && out.numel() == ids.numel()) : ids.numel() == 0, "gather shapes");
+  TORCH_CHECK(lse.numel() == Rp, "gather_probs: lse must have one entry per logits row");
+  const int K = R > 0 ? ids.numel() / R : 0;
+  const int32_t* rm = rowmap_ptr(rowmap, Rp, R);
   c10::DeviceGuard g(logits.device());
   tb_gather_probs(cbf(logits), lse.data_ptr<float>(), ids.data_ptr<int32_t>(), out.data_ptr<float>(), R, K, V,
-                  round_bf16 ? 1 : 0, cur_stream());
+                  round_bf16 ? 1 : 0, rm, cur_stream());
 }
 
 void lens_colsum(torch::Tensor logits, torch::Tensor lse, c10::optional<torch::Tensor> mask, torch::Tensor excl,
                  torch::Tensor acc, int64_t B, int64_t T, bool accumulate, bool round_bf16,
-                 c10::optional<torch::Tensor> offs, c10::optional<torch::Tensor> cum) {
+                 c10::optional<torch::Tensor> offs, c10::optional<torch::Tensor> cum,
+                 c10::optional<torch::Tensor> rowmap) {
   IN_BF16(logits); IN_F32(lse); IN_I32(excl); IN_F32(acc);
   const int V = logits.size(-1);
-  const int64_t R = logits.numel() / V;
-  TORCH_CHECK(lse.numel() == R && excl.numel() == 2 * R && acc.numel() == B * V, "lens_colsum shapes");
+  const int64_t Rp = logits.numel() / V;
+  const int64_t R = rowmap.has_value() ? rowmap->numel() : Rp;      // logical rows (excl, mask, offs)
+  TORCH_CHECK(lse.numel() == Rp && excl.numel() == 2 * R && acc.numel() == B * V, "lens_colsum shapes");
+  const int32_t* rm = rowmap_ptr(rowmap, Rp, R);
+  TORCH_CHECK(rm == nullptr || offs.has_value(), "lens_colsum rowmap is packed-layout only");
   const uint8_t* mp = nullptr;
   if (mask.has_value()) {
     IN_U8((*mask));
@@ -288,7 +307,7 @@ void lens_colsum(torch::Tensor logits, torch::Tensor lse, c10::optional<torch::T
   }
   c10::DeviceGuard g(logits.device());
   tb_lens_colsum(cbf(logits), lse.data_ptr<float>(), mp, excl.data_ptr<int32_t>(), acc.data_ptr<float>(), B, T, V,
-                 accumulate ? 1 : 0, round_bf16 ? 1 : 0, op, cp, cur_stream());
+                 accumulate ? 1 : 0, round_bf16 ? 1 : 0, op, cp, rm, cur_stream());
 }
 
 void topk_rows(torch::Tensor x, torch::Tensor vals, torch::Tensor idx, int64_t K) {

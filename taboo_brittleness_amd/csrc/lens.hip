@@ -182,12 +182,13 @@ __global__ void __launch_bounds__(512) row_lse_kernel(const uint16_t* __restrict
   }
 }
 
+// ``rowmap`` (optional): logical row r reads logits / lse row rowmap[r] (rows deduplicated upstream).
 __global__ void gather_probs_kernel(const uint16_t* __restrict__ logits, const float* __restrict__ lse,
                                     const int32_t* __restrict__ ids, float* __restrict__ out, int R, int K, int V,
-                                    int round_bf16) {
+                                    int round_bf16, const int32_t* __restrict__ rowmap) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= R * K) return;
-  const int r = e / K;
+  const int r = rowmap ? rowmap[e / K] : e / K;
   const int id = ids[e];
   if (id < 0 || id >= V) { out[e] = 0.f; return; }
   float p = __expf(bf2f(logits[(size_t)r * V + id]) - lse[r]);
@@ -203,7 +204,8 @@ __global__ void __launch_bounds__(256) lens_colsum_kernel(const uint16_t* __rest
                                                           const uint8_t* __restrict__ mask,
                                                           const int32_t* __restrict__ excl, float* __restrict__ acc,
                                                           int T, int V, int accumulate, int round_bf16,
-                                                          const int32_t* __restrict__ offs, float* __restrict__ cum) {
+                                                          const int32_t* __restrict__ offs, float* __restrict__ cum,
+                                                          const int32_t* __restrict__ rowmap) {
   const int b = blockIdx.y;
   const int c = blockIdx.x * blockDim.x + threadIdx.x;   // 8-column group
   const int col0 = c * 8;
@@ -233,9 +235,10 @@ __global__ void __launch_bounds__(256) lens_colsum_kernel(const uint16_t* __rest
   if (cb) put(cb);
   for (int r = r0; r < r1; ++r) {
     if (mask == nullptr || mask[r]) {
-      const float l = lse[r];
+      const int pr = rowmap ? rowmap[r] : r;             // physical logits row (deduplicated rows)
+      const float l = lse[pr];
       const int e0 = excl[2 * r], e1 = excl[2 * r + 1];
-      const uint16_t* row = logits + (size_t)r * V;
+      const uint16_t* row = logits + (size_t)pr * V;
       float f[8];
       if (full) {
         unpack8(*reinterpret_cast<const uint4*>(row + col0), f);
@@ -479,21 +482,21 @@ void tb_row_lse(const uint16_t* logits, float* lse, int R, int V, float cap, int
 }
 
 void tb_gather_probs(const uint16_t* logits, const float* lse, const int32_t* ids, float* out, int R, int K, int V,
-                     int round_bf16, hipStream_t st) {
+                     int round_bf16, const int32_t* rowmap, hipStream_t st) {
   if (R <= 0 || K <= 0) return;
   const int n = R * K;
   hipLaunchKernelGGL(gather_probs_kernel, dim3((n + 255) / 256), dim3(256), 0, st, logits, lse, ids, out, R, K, V,
-                     round_bf16);
+                     round_bf16, rowmap);
 }
 
 void tb_lens_colsum(const uint16_t* logits, const float* lse, const uint8_t* mask, const int32_t* excl, float* acc,
                     int B, int T, int V, int accumulate, int round_bf16, const int32_t* offs, float* cum,
-                    hipStream_t st) {
+                    const int32_t* rowmap, hipStream_t st) {
   if (B <= 0) return;
   const int groups = (V + 7) / 8;
   dim3 grid((groups + 255) / 256, B);
   hipLaunchKernelGGL(lens_colsum_kernel, grid, dim3(256), 0, st, logits, lse, mask, excl, acc, T, V, accumulate,
-                     round_bf16, offs, cum);
+                     round_bf16, offs, cum, rowmap);
 }
 
 void tb_topk_rows(const float* x, float* vals, int32_t* idx, int R, int V, int K, hipStream_t st) {

@@ -164,13 +164,18 @@ def lens_readout(model, store: torch.Tensor, starts: Sequence[int], lens: Sequen
 @torch.no_grad()
 def lens_packed(model, store: torch.Tensor, rows: np.ndarray, offs: np.ndarray, base: torch.Tensor,
                 track: np.ndarray, excl: np.ndarray, round_bf16: bool = False,
-                chunk_rows: int = 4096, sync: bool = True):
+                chunk_rows: int = 4096, sync: bool = True, row_key: Optional[np.ndarray] = None,
+                stats: Optional[dict] = None):
     """Partial lens over packed rows: sequence ``i`` owns flat rows ``rows[offs[i]:offs[i+1]]`` of
     ``store.view(-1, D)`` (no padding) and adds their (excluded) lens probabilities onto ``base[i]``
     (the reused part of its response sum, updated in place).  ``track [R, K]`` are per-row ids whose
     probabilities are returned (``-1`` = none), ``excl [R, 2]`` the per-row excluded ids.
     Returns ``(base, probs [R, K])``; ``sync=False`` returns the probabilities as a device tensor instead
-    (no host wait: the caller copies them back when it needs them)."""
+    (no host wait: the caller copies them back when it needs them).
+
+    ``row_key [R]`` (optional): rows with equal keys hold identical residuals (e.g. sweep cells of one pair
+    with equal tokens, at positions without an edit); each chunk then unembeds one row per key and the
+    readout kernels read it through a row map (the lens GEMM shrinks, the sums are unchanged)."""
     dev = store.device
     D = store.shape[-1]
     flat = store.view(-1, D)
@@ -183,18 +188,28 @@ def lens_packed(model, store: torch.Tensor, rows: np.ndarray, offs: np.ndarray, 
     # chunk plan on the host (whole sequences, <= chunk_rows rows, GEMM rows padded to 256-row tiles; the
     # padding rows repeat the chunk's first row), then ONE upload of every index array: the loop below
     # only slices device tensors, so the host never waits for the GPU between chunks
-    chunks, ridx_l, offs_l = [], [], []
+    chunks, ridx_l, offs_l, map_l = [], [], [], []
     i0, pr0, po0 = 0, 0, 0
     while i0 < n:
         i1 = int(np.searchsorted(offs, offs[i0] + chunk_rows, side="right")) - 1
         i1 = min(n, max(i1, i0 + 1))
         r0, r1 = int(offs[i0]), int(offs[i1])
         if r1 > r0:
-            M = r1 - r0
+            if row_key is not None:      # one GEMM row per distinct key, logical rows mapped onto them
+                _, first, inv = np.unique(row_key[r0:r1], return_index=True, return_inverse=True)
+                src = rows[r0:r1][first]
+                map_l.append(inv.reshape(-1).astype(np.int32))
+            else:
+                src = rows[r0:r1]
+            M = len(src)
+            if stats is not None:
+                stats["lens_gemm_rows"] = stats.get("lens_gemm_rows", 0) + M
             Mp = -(-M // 256) * 256
-            ridx_l.append(np.concatenate([rows[r0:r1], np.full(Mp - M, rows[r0], dtype=np.int64)]))
+            ridx_l.append(np.concatenate([src, np.full(Mp - M, src[0], dtype=np.int64)]))
             offs_l.append((offs[i0:i1 + 1] - r0).astype(np.int32))
-            chunks.append((i0, i1, r0, r1, pr0, Mp, po0))
+            # deduplicated chunks run the 256-row padded GEMM (the padding repeats a row; the row map never
+            # reads it): few distinct shapes, all in the TunableOp tables
+            chunks.append((i0, i1, r0, r1, pr0, Mp if row_key is not None else M, po0))
             pr0 += Mp
             po0 += i1 - i0 + 1
         i0 = i1
@@ -206,13 +221,14 @@ def lens_packed(model, store: torch.Tensor, rows: np.ndarray, offs: np.ndarray, 
     offs_d = up(np.concatenate(offs_l))
     track_d = up(np.asarray(track, dtype=np.int32))
     excl_d = up(np.asarray(excl, dtype=np.int32))
+    map_d = up(np.concatenate(map_l)) if map_l else None
     pr_d = torch.empty(R, K, dtype=torch.float32, device=dev)
-    for i0, i1, r0, r1, pr0, Mp, po0 in chunks:
-        M = r1 - r0
+    for i0, i1, r0, r1, pr0, M, po0 in chunks:
         logits, lse = model.lens_logits_lse(flat.index_select(0, ridx_d[pr0:pr0 + M]))
-        ops.gather_probs(logits, lse, track_d[r0:r1], round_bf16=round_bf16, out=pr_d[r0:r1])
+        rm = map_d[r0:r1] if map_d is not None else None
+        ops.gather_probs(logits, lse, track_d[r0:r1], round_bf16=round_bf16, out=pr_d[r0:r1], rowmap=rm)
         ops.lens_colsum(logits, lse, None, excl_d[r0:r1], i1 - i0, 0, acc=base[i0:i1], accumulate=True,
-                        round_bf16=round_bf16, offs=offs_d[po0:po0 + (i1 - i0) + 1])
+                        round_bf16=round_bf16, offs=offs_d[po0:po0 + (i1 - i0) + 1], rowmap=rm)
     if not sync:
         return base, pr_d
     probs[:] = pr_d.cpu().numpy()

@@ -265,11 +265,22 @@ def row_lse(logits, cap=0.0, emulate_bf16=False, out=None):
     return y
 
 
-def gather_probs(logits, lse, ids, round_bf16=False, out=None):
+def _rows_of(logits, lse, rowmap):
+    """CPU path of a ``rowmap``: materialise the logical rows."""
+    V = logits.shape[-1]
+    r = rowmap.view(-1).long()
+    return logits.reshape(-1, V).index_select(0, r), lse.reshape(-1).index_select(0, r)
+
+
+def gather_probs(logits, lse, ids, round_bf16=False, out=None, rowmap=None):
+    """``p[r, k] = softmax(logits[row r])[ids[r, k]]``; ``rowmap [R]``: logical row ``r`` is logits row
+    ``rowmap[r]`` (deduplicated rows)."""
     if logits.is_cuda:
         out = _out(out, ids.shape, torch.float32, logits.device)
-        _k().gather_probs(logits, lse, ids, out, bool(round_bf16))
+        _k().gather_probs(logits, lse, ids, out, bool(round_bf16), rowmap)
         return out
+    if rowmap is not None:
+        logits, lse = _rows_of(logits, lse, rowmap)
     y = ref.gather_probs(logits, lse, ids, round_bf16).view(ids.shape)
     if out is not None:
         out.copy_(y)
@@ -277,19 +288,24 @@ def gather_probs(logits, lse, ids, round_bf16=False, out=None):
     return y
 
 
-def lens_colsum(logits, lse, mask, excl, B, T, acc=None, accumulate=False, round_bf16=False, offs=None, cum=None):
+def lens_colsum(logits, lse, mask, excl, B, T, acc=None, accumulate=False, round_bf16=False, offs=None, cum=None,
+                rowmap=None):
     """Per-sequence sum over rows of ``softmax(logits)`` with 2 excluded ids per row.
 
     Dense layout: rows ``[B*T]`` with ``mask``; packed: ``offs [B+1]`` row offsets (``mask`` None, ``T``
-    unused).  ``cum [B, T+1, V]`` (dense only) also receives the running sum after every row."""
+    unused).  ``cum [B, T+1, V]`` (dense only) also receives the running sum after every row.
+    ``rowmap [R]`` (packed only): logical row ``r`` (its exclusions, its place in ``offs``) reads logits row
+    ``rowmap[r]`` — identical rows evaluated once."""
     V = logits.shape[-1]
     if logits.is_cuda:
         if acc is None:
             acc = torch.zeros(B, V, dtype=torch.float32, device=logits.device)
             accumulate = False
         _k().lens_colsum(logits, lse, mask, excl, acc, int(B), int(T), bool(accumulate), bool(round_bf16),
-                         offs, cum)
+                         offs, cum, rowmap)
         return acc
+    if rowmap is not None:
+        logits, lse = _rows_of(logits, lse, rowmap)
     res = ref.lens_colsum(logits, lse, mask, excl, B, T, None, round_bf16, offs=offs, with_cum=cum is not None)
     s, c = res if isinstance(res, tuple) else (res, None)
     if acc is None:

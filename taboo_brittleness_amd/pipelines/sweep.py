@@ -155,7 +155,7 @@ class SweepRunner:
         self.tf_prefix = os.environ.get("TB_TF_PREFIX", "1") == "1"
         self.stats: Dict[str, int] = {"cells": 0, "diverged": 0, "tf_rows": 0, "lens_rows": 0,
                                       "decode_row_steps": 0, "decode_rows_run": 0, "carried": 0, "staged": 0,
-                                      "decode_lo_rows_run": 0, "decode_lo_groups": 0}
+                                      "decode_lo_rows_run": 0, "decode_lo_groups": 0, "lens_gemm_rows": 0}
         # decode-tail carry-over (opt-in; needs ``batch`` to include ``carry_rows`` spare slots): once fewer
         # than ``carry_rows`` diverged cells still decode, the rest continue in the next batch's decode
         # (merged with its new rows) instead of running a long small-batch tail.  Records of carried cells
@@ -1164,12 +1164,14 @@ class SweepRunner:
             cur = etab[tokm]
             ex[:, 0] = cur[cell_of, pos]
             ex[:, 1] = np.where(pos > 0, cur[cell_of, np.maximum(pos - 1, 0)], -1)
+        row_key = self._lens_row_keys(cell_of, pos, q >= cs, div, j_a, u_a, sp_u, host_tok) if R else None
         self._tick("ro_entries")
         self.stats["lens_rows"] += R
         self._ensure_cum(ulist)
         base = self._lens_base(cell_pairs, d_a.tolist(), ng_a.tolist())
         self._tick("ro_base")
-        acc, pr_d = lens_packed(m, self.store, rows, offs, base, trk, ex, sync=False)
+        acc, pr_d = lens_packed(m, self.store, rows, offs, base, trk, ex, sync=False, row_key=row_key,
+                                stats=self.stats)
         if self.exclusion == "response":
             for i in range(E_n):
                 r_ = cell_pairs[i].resp if dv_a[i] < 0 else host_tok[j_a[i], : ng_a[i]].tolist()
@@ -1199,6 +1201,40 @@ class SweepRunner:
         if getattr(self, "_defer", False):
             return self._records_pool().submit(self._resume_records, batch, cell_pairs, cols, pr, vh, ih, K)
         return self._resume_records(batch, cell_pairs, cols, pr, vh, ih, K)
+
+    def _lens_row_keys(self, cell_of, pos, after_d, div, j_a, u_a, sp_u, host_tok) -> Optional[np.ndarray]:
+        """Dedup keys of the lens rows (``lens_packed(row_key=)``): the hooked-layer residual of a diverged cell at
+        a non-spike position ``t >= D`` is a function of its pair and its tokens ``0..t`` alone (blocks ``0..l``
+        see only tokens, and no edit touches it), so cells of one pair with equal tokens up to ``t`` hold the
+        same row.  Those rows get a 63-bit hash key of (pair, t, tokens ``0..t``); every other row (spikes,
+        undiverged cells) a unique negative key.  None when nothing can repeat."""
+        R = len(pos)
+        if not self.trie_decode or host_tok is None or not div.any():
+            return None
+        spike = (sp_u[u_a][cell_of] == pos[:, None]).any(1)
+        dd = after_d & div[cell_of] & ~spike
+        key = -1 - np.arange(R, dtype=np.int64)
+        if not dd.any():
+            return None
+        # rolling 64-bit hash of every diverged cell's response prefix (wrapping uint64 arithmetic)
+        tok = host_tok[j_a[div]].astype(np.uint64) + np.uint64(1)
+        h = np.empty(tok.shape, np.uint64)
+        acc = np.zeros(tok.shape[0], np.uint64)
+        mul = np.uint64(0x9E3779B97F4A7C15)
+        with np.errstate(over="ignore"):
+            for t in range(tok.shape[1]):
+                acc = (acc ^ tok[:, t]) * mul
+                acc ^= acc >> np.uint64(29)
+                h[:, t] = acc
+            ci = np.full(len(div), -1, np.int64)
+            ci[np.nonzero(div)[0]] = np.arange(int(div.sum()))
+            r = np.nonzero(dd)[0]
+            c = ci[cell_of[r]]
+            t = np.minimum(pos[r], tok.shape[1] - 1)
+            k = h[c, t] ^ (u_a[cell_of[r]].astype(np.uint64) * np.uint64(0xC2B2AE3D27D4EB4F))
+            k ^= pos[r].astype(np.uint64) * np.uint64(0x165667B19E3779F9)
+        key[r] = (k & np.uint64(0x7FFFFFFFFFFFFFFF)).astype(np.int64)
+        return key
 
     def _resume_records(self, batch, cell_pairs, cols, pr, vh, ih, K) -> List[dict]:
         """Host half of :meth:`_resume_readout`: per-cell readout statistics and result records."""

@@ -62,6 +62,26 @@ def test_rope_and_cache(gpu):
     _close(vcg, vc, atol=1e-6)
 
 
+def test_lens_readouts_rowmap(gpu):
+    """gather_probs / packed lens_colsum reading deduplicated logits rows through a row map equal the same
+    kernels over the materialised rows."""
+    torch.manual_seed(4)
+    V, Rp, R = 3000, 5, 12
+    lg = (torch.randn(Rp, V) * 3).to(BF).to(gpu)
+    lse = torch.logsumexp(lg.float(), -1)
+    rm = torch.tensor([0, 1, 1, 2, 0, 3, 4, 4, 4, 2, 1, 0], dtype=torch.int32, device=gpu)
+    ids = torch.randint(-1, V, (R, 3), dtype=torch.int32, device=gpu)
+    ex = torch.randint(-1, V, (R, 2), dtype=torch.int32, device=gpu)
+    offs = torch.tensor([0, 3, 7, 12], dtype=torch.int32, device=gpu)
+    full, lf = lg.index_select(0, rm.long()), lse.index_select(0, rm.long())
+    a = ops.gather_probs(lg, lse, ids, rowmap=rm)
+    b = ops.gather_probs(full, lf, ids)
+    assert torch.equal(a, b)
+    sa = ops.lens_colsum(lg, lse, None, ex, 3, 0, offs=offs, rowmap=rm)
+    sb = ops.lens_colsum(full, lf, None, ex, 3, 0, offs=offs)
+    assert torch.equal(sa, sb)
+
+
 def test_kv_fanout(gpu):
     """Prefix-trie KV fan-out: members get their representative's K/V of the first layers at their own
     position; skipped rows (src < 0, src == r, positions outside the cache) and deeper layers untouched."""

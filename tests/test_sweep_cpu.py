@@ -475,6 +475,7 @@ def test_trie_decode_is_exact(carry):
     assert stats[True]["diverged"] > 0
     if not carry:               # (the carry variant checks exactness; its few diverged rows barely share)
         assert 0 < stats[True]["decode_lo_groups"] < stats[True]["decode_row_steps"], stats[True]
+        assert stats[True]["lens_gemm_rows"] < stats[True]["lens_rows"] == stats[False]["lens_gemm_rows"], stats
     else:
         assert stats[True]["carried"] > 0, stats[True]
     assert set(res[False]) == set(res[True])

@@ -9,3 +9,5 @@ timeout -k 10 700 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpu
 echo PROF_OK
 tail -1 $R/gpurun_out/prof_$TAG.log | cut -c1-200
 find $R/gpurun_out/prof_$TAG -name "*kernel_stats*" -exec head -25 {} \; | cut -c1-150
+# the per-dispatch trace is hundreds of MB: keep the stats only (gpurun copies back <= 64 MiB)
+find $R/gpurun_out/prof_$TAG -name "*kernel_trace*" -delete
