@@ -107,6 +107,9 @@ def main() -> None:
     ap.add_argument("--no-trie-decode", action="store_true",
                     help="decode every diverged cell through all blocks on its own row instead of running blocks "
                          "0..l once per group of a pair's cells with equal tokens (prefix-trie decode)")
+    ap.add_argument("--no-skip-noop", action="store_true",
+                    help="start every cell's teacher-forced tail at its pair's first spike, also when the cell's "
+                         "latents are inactive there (an exact no-op edit)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="do not queue the next step's teacher-forced tail behind this step's readout")
     ap.add_argument("--profile-steps", action="store_true", help="print per-phase timings per step")
@@ -151,6 +154,7 @@ def main() -> None:
                          kv_pairs=(E + (3 if C else 2)) * P + 2, layer_resume=not args.no_layer_resume)
     runner.carry_rows = C
     runner.trie_decode = not args.no_trie_decode
+    runner.skip_noop_spikes = not args.no_skip_noop
     templates = runner.build_pairs(cfg.words, cfg.prompts)
     methods = ("sae_targeted", "sae_random")
 
@@ -317,6 +321,7 @@ def main() -> None:
                 "fused_geglu": fused_geglu,
                 "fused_head": bool(getattr(model, "fused_head", False)),
                 "trie_decode": runner.trie_decode,
+                "skip_noop_spikes": runner.skip_noop_spikes,
                 "lora_adapters": (f"{len(cfg.words)} x rank {args.lora_rank} (unmerged bank)" if args.lora_rank
                                   else "none (weights as merged taboo models)"),
             },

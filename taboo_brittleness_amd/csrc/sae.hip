@@ -194,6 +194,11 @@ __global__ void __launch_bounds__(256) lowrank_edit_kernel(
     }
   }
   __syncthreads();
+  // an all-zero edit (every ablated latent below its threshold here, or alpha = 0) is an exact no-op: h and
+  // x_next stay bit-identical to the unedited forward (no re-rounded h, no re-normalised x)
+  bool any = false;
+  for (int j = 0; j < m; ++j) any |= coef[j] != 0.f;
+  if (!any) return;
   for (int j = 0; j < m; ++j) {
     const float cj = coef[j];
     if (cj == 0.f) continue;

@@ -251,7 +251,8 @@ def lowrank_edit(h: torch.Tensor, apply: torch.Tensor, idx: torch.Tensor, cnt: t
                  Dm: torch.Tensor, bias=None, thr=None, pre_bias=None, alpha: float = 1.0,
                  w_next: Optional[torch.Tensor] = None, eps: float = 1e-6, x_next: Optional[torch.Tensor] = None,
                  coef_out: Optional[torch.Tensor] = None) -> None:
-    """In place on h (and x_next rows that were edited)."""
+    """In place on h (and x_next rows that were edited); rows whose coefficients are all zero are left
+    untouched."""
     D = h.shape[-1]
     hv = h.view(-1, D)
     M = hv.shape[0]
@@ -268,6 +269,8 @@ def lowrank_edit(h: torch.Tensor, apply: torch.Tensor, idx: torch.Tensor, cnt: t
         a = torch.where(pre > thr.float()[sel], pre, torch.zeros_like(pre)) if thr is not None else pre
         if coef_out is not None:
             coef_out.view(M, mmax)[r, :m] = a
+        if not bool(((alpha * a) != 0).any()):
+            continue                      # all-zero edit: an exact no-op (h and x_next untouched)
         newx = rbf(x - (alpha * a) @ Dm[sel].float())
         hv[r] = newx.to(h.dtype)
         if x_next is not None and w_next is not None:

@@ -72,6 +72,10 @@ class Pair:
     p_secret_mean: Optional[float] = None               # cached mean of p_secret (result records)
     forms_l: Optional[set] = None
     rep: int = 0                                        # replicate of this (word, prompt): seeds its random cells
+    # exact per-latent activity at the edited spikes (SweepRunner._spike_activity): sorted candidate latent
+    # ids and, per id, a bitmask over spikes_rel[:K] of where the edit kernel's own JumpReLU fires
+    act_ids: Optional[np.ndarray] = None
+    act_mask: Optional[np.ndarray] = None
 
     @property
     def first_edit(self) -> int:
@@ -164,6 +168,9 @@ class SweepRunner:
         # prefix-trie decode: diverged cells of a pair with equal tokens run blocks 0..l once per group
         # (Generator.decode share_keys); TB_TRIE_DECODE=0 / SweepRunner.trie_decode = False: every row alone
         self.trie_decode = os.environ.get("TB_TRIE_DECODE", "1") == "1"
+        # a cell's teacher-forced tail starts at its first spike with a non-zero edit (earlier spikes: its
+        # latents are inactive there, an exact no-op); TB_SKIP_NOOP=0: at its pair's first spike
+        self.skip_noop_spikes = os.environ.get("TB_SKIP_NOOP", "1") == "1"
         self._carry: List[_Carry] = []
         self._next: Optional["NextBatch"] = None      # batch of the next run_cells call (stage_next)
         # lazy running lens sums: a pair's [n + 1, V] fp32 running sums (52 MB at the 256k vocab) are rebuilt from
@@ -322,6 +329,45 @@ class SweepRunner:
         bounds = np.searchsorted(g_h, np.arange(len(live) + 1))
         for g, p in enumerate(live):
             p.active_pool = l_h[bounds[g]:bounds[g + 1]].astype(np.int64)
+        self._spike_activity(live)
+
+    @torch.no_grad()
+    def _spike_activity(self, live: Sequence[Pair]) -> None:
+        """Where each candidate latent's ablation is a non-zero edit: the latents active at the spikes plus the
+        targeted ones, evaluated by the edit kernel itself (``ops.lowrank_edit`` coefficients on copies of the
+        baseline's hooked-layer residuals at the spikes — the exact rows and arithmetic the teacher-forced tail
+        edits, since blocks ``0..l`` are the baseline's there).  A cell whose latents are all inactive at its
+        pair's first spikes leaves those positions bit-identical to the baseline (all-zero edits are no-ops), so
+        its tail starts at its first *effective* spike (``_plan_for`` -> ``plan["f"]``)."""
+        s, K = self.sae, self.iv.spikes_k
+        rows, owner = [], []
+        for g, p in enumerate(live):
+            cand = np.union1d(p.active_pool, np.asarray(p.targeted, np.int64)).astype(np.int64)
+            p.act_ids, p.act_mask = cand, np.zeros(cand.size, np.int64)
+            if s is None or p.resid is None or not cand.size:
+                continue
+            for k, t in enumerate(p.spikes_rel[:K]):
+                if 0 <= t < p.resid.shape[0]:
+                    for c0 in range(0, cand.size, 256):
+                        rows.append((g, t))
+                        owner.append((g, k, c0, min(256, cand.size - c0)))
+        if not rows or self.iv.alpha == 0:
+            return
+        n = len(rows)
+        idx = np.zeros((n, 256), np.int32)
+        cnt = np.zeros(n, np.int32)
+        for i, (g, k, c0, m) in enumerate(owner):
+            idx[i, :m] = live[g].act_ids[c0:c0 + m]
+            cnt[i] = m
+        dev = self.dev
+        h = torch.stack([live[g].resid[t] for g, t in rows]).contiguous()
+        coef = torch.zeros(n, 256, dtype=torch.float32, device=dev)
+        ops.lowrank_edit(h, torch.ones(n, dtype=torch.uint8, device=dev), torch.from_numpy(idx).to(dev),
+                         torch.from_numpy(cnt).to(dev), s.W_encT, s.W_dec, s.b_enc, s.threshold,
+                         s.b_dec if s.apply_b_dec_to_input else None, self.iv.alpha, None, 1e-6, None, coef)
+        nz = (coef != 0).cpu().numpy()
+        for i, (g, k, c0, m) in enumerate(owner):
+            live[g].act_mask[c0:c0 + m] |= nz[i, :m].astype(np.int64) << k
 
     # ----------------------------------------------------------------- cells
     def make_cells(self, pairs: Sequence[Pair], methods: Sequence[str] = METHODS) -> List[Cell]:
@@ -429,8 +475,35 @@ class SweepRunner:
         basis = None
         if brow:
             basis = (np.concatenate(brow), torch.cat(bval, 0))
-        plan = {"spikes": sp, "kind": kd, "idx": ix, "cnt": cn, "basis": basis, "rows": B * rmax, "rmax": rmax}
+        plan = {"spikes": sp, "kind": kd, "idx": ix, "cnt": cn, "basis": basis, "rows": B * rmax, "rmax": rmax,
+                "f": self._effective_first_edit(cells, pairs, by_pair, kd, ix, cn)}
         return self._plan_add_carry(plan) if with_carry else plan
+
+    def _effective_first_edit(self, cells, pairs, by_pair, kd, ix, cn) -> np.ndarray:
+        """Per cell (plan row): response index of its first spike where the edit is non-zero (the pair's spike
+        order), ``len(resp)`` if it never is (the cell is its baseline), -1 = the pair's first spike (projection
+        cells, or no activity table).  Latents outside a pair's activity table count as active everywhere."""
+        K = self.iv.spikes_k
+        f = np.full(self.B, -1, np.int64)
+        if not self.skip_noop_spikes:
+            return f
+        for pi, cis in by_pair.items():
+            p = pairs[pi]
+            ids, msk = p.act_ids, p.act_mask
+            sp = np.asarray(p.spikes_rel[:K], np.int64)
+            ca = np.asarray([ci for ci in cis if kd[ci] == 1], np.int64)
+            if ids is None or not ca.size or not sp.size:
+                continue
+            lat = ix[ca].astype(np.int64)
+            j = np.minimum(np.searchsorted(ids, lat), max(ids.size - 1, 0))
+            found = (ids[j] == lat) if ids.size else np.zeros(lat.shape, bool)
+            allk = (1 << sp.size) - 1
+            bits = np.where(found, msk[j] if ids.size else 0, allk)
+            bits = np.where(np.arange(lat.shape[1])[None, :] < cn[ca][:, None], bits, 0)
+            cell_bits = np.bitwise_or.reduce(bits, axis=1)
+            on = (cell_bits[:, None] >> np.arange(sp.size)[None, :]) & 1
+            f[ca] = np.where(on.astype(bool), sp[None, :], len(p.resp)).min(1)
+        return f
 
     def _plan_add_carry(self, plan: dict) -> dict:
         for cr in self._carry:                  # carried cells keep editing at their carry-region slots
@@ -517,7 +590,7 @@ class SweepRunner:
             plan = self._plan_add_carry({k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in plan.items()})
         self._set_adapters(cp)
         hook = self._load_plan(plan)
-        tf = self._tf_launch(cp, {self.layer: [hook, self.capture]})
+        tf = self._tf_launch(cp, {self.layer: [hook, self.capture]}, plan.get("f"))
         self._staged = {"cells": nb.cells, "plan": plan, "tf": tf, "carry": list(self._carry)}
         self._tick("next_tf_launched")
 
@@ -774,7 +847,7 @@ class SweepRunner:
         if not self.tf_prefix:
             self._copy_pair_kv(range(nc), [p.kv_slot for p in cell_pairs], layers=range(l0 + 1, L))
         self._tick("kv_copy")
-        tf = self._tf_finish(staged["tf"] if staged is not None else self._tf_launch(cell_pairs, hooks))
+        tf = self._tf_finish(staged["tf"] if staged is not None else self._tf_launch(cell_pairs, hooks, plan.get("f")))
         self._tick("tf_pass")
         # ---- divergence point D of every cell: first tail row whose greedy token leaves the baseline's
         D_a = np.full(nc, -1, np.int64)
@@ -966,11 +1039,11 @@ class SweepRunner:
             if id(c) in carried_now:
                 continue
             if D[b] is None:
-                entries.append((c, p, b, None, nll_c[b], sn_c[b], None))
+                entries.append((c, p, b, None, nll_c[b], sn_c[b], None, int(f_a[b])))
             else:
-                entries.append((c, p, b, D[b], nll_c[b], None, drow[b]))
+                entries.append((c, p, b, D[b], nll_c[b], None, drow[b], int(f_a[b])))
         for cr, j in fin_carry:
-            entries.append((cr.cell, cr.pair, cr.slot, cr.d, cr.nll, None, j))
+            entries.append((cr.cell, cr.pair, cr.slot, cr.d, cr.nll, None, j, int(cr.pre[2] - cr.pair.plen)))
         # the carry move runs after the readout has read the finished carried cells' store rows, and before
         # a staged next tail overwrites the cell slots (_launch_staged_next runs it at that point)
         self._carry_move_pending = carry_move
@@ -1086,8 +1159,9 @@ class SweepRunner:
         numpy arrays for the whole batch (no per-cell Python work on the launching thread); every
         non-diverged cell of a pair shares the pair's response, spikes and exclusions.
 
-        ``entries``: per cell ``(cell, pair, slot, D or None, nll_edit, self_nll or None, out row or None)``
-        — ``slot`` holds its capture-store rows, diverged cells read their response from ``out``."""
+        ``entries``: per cell ``(cell, pair, slot, D or None, nll_edit, self_nll or None, out row or None, f)``
+        — ``slot`` holds its capture-store rows, diverged cells read their response from ``out``; spikes before
+        the cell's effective first edit ``f`` were no-op edits, their lens is the baseline's."""
         m = self.m
         S1 = self.store.shape[1]
         E_n = len(entries)
@@ -1118,6 +1192,7 @@ class SweepRunner:
         dv_a = np.asarray([-1 if e[3] is None else e[3] for e in entries], np.int64)
         j_a = np.asarray([-1 if e[6] is None else e[6] for e in entries], np.int64)
         nll_a = np.asarray([e[4] for e in entries], np.float64)
+        f_e = np.asarray([e[7] if len(e) > 7 else 0 for e in entries], np.int64)
         div = dv_a >= 0
         host_tok = out.host_tokens() if (out is not None and div.any()) else None
         ngen_o = np.asarray(out.n_gen, np.int64) if out is not None else np.zeros(0, np.int64)
@@ -1136,7 +1211,7 @@ class SweepRunner:
         # ---- rows to evaluate per cell: its spikes before min(D, n_gen) (pair order), then D .. n_gen-1
         lim = np.where(div, np.minimum(d_a, ng_a), n_u[u_a])
         spk = sp_u[u_a]
-        keep = (spk >= 0) & (spk < lim[:, None])
+        keep = (spk >= 0) & (spk < lim[:, None]) & (spk >= f_e[:, None])
         order = np.argsort(~keep, axis=1, kind="stable")
         spk_c = np.take_along_axis(spk, order, 1)
         cnt_s = keep.sum(1)
@@ -1168,7 +1243,7 @@ class SweepRunner:
         self._tick("ro_entries")
         self.stats["lens_rows"] += R
         self._ensure_cum(ulist)
-        base = self._lens_base(cell_pairs, d_a.tolist(), ng_a.tolist())
+        base = self._lens_base(cell_pairs, d_a.tolist(), ng_a.tolist(), f_e)
         self._tick("ro_base")
         acc, pr_d = lens_packed(m, self.store, rows, offs, base, trk, ex, sync=False, row_key=row_key,
                                 stats=self.stats)
@@ -1305,9 +1380,11 @@ class SweepRunner:
             p.lens_cum = c
         self._cum_live += need
 
-    def _lens_base(self, cell_pairs: Sequence[Pair], Dc: Sequence[int], ngen: Sequence[int]) -> torch.Tensor:
+    def _lens_base(self, cell_pairs: Sequence[Pair], Dc: Sequence[int], ngen: Sequence[int],
+                   f: Optional[np.ndarray] = None) -> torch.Tensor:
         """Reused part of each cell's response lens sum: the baseline's running sum up to the divergence
-        ``D`` minus its spike positions (those are re-evaluated on the edited residual).  Per pair one row
+        ``D`` minus its spike positions from its effective first edit ``f`` on (those are re-evaluated on the
+        edited residual; earlier spikes were no-op edits).  Per pair one row
         gather of its running sums and one small matmul with a {0, ±1} coefficient matrix; every index and
         coefficient of every pair goes up in one copy each."""
         V = self.m.spec.vocab_size
@@ -1329,7 +1406,8 @@ class SweepRunner:
             W = np.zeros((nb, nb + 2 * ns), np.float32)
             W[np.arange(nb), np.arange(nb)] = 1.0
             if ns:
-                mk = (sp[None, :] < d[:, None]).astype(np.float32)
+                fb = np.asarray([f[b] for b in bs], np.int64) if f is not None else np.zeros(nb, np.int64)
+                mk = ((sp[None, :] < d[:, None]) & (sp[None, :] >= fb[:, None])).astype(np.float32)
                 W[:, nb: nb + ns] = -mk
                 W[:, nb + ns:] = mk
             ints.append(np.concatenate([np.asarray(bs, np.int64), d.astype(np.int64), sp + 1, sp]))
@@ -1365,9 +1443,10 @@ class SweepRunner:
         return res
 
     @torch.no_grad()
-    def _tf_launch(self, cell_pairs: Sequence[Pair], hooks) -> dict:
+    def _tf_launch(self, cell_pairs: Sequence[Pair], hooks, f_cell: Optional[np.ndarray] = None) -> dict:
         """Enqueue the teacher-forced tail (no host sync): host index arrays, the packed forward, the vocab
-        head, and one async D2H copy of its per-row outputs; :meth:`_tf_finish` waits for it."""
+        head, and one async D2H copy of its per-row outputs; :meth:`_tf_finish` waits for it.  ``f_cell[b]``:
+        cell ``b``'s effective first edit (``_effective_first_edit``; -1 = its pair's first spike)."""
         from ..models.gemma2 import packed_blocks
 
         m = self.m
@@ -1382,7 +1461,8 @@ class SweepRunner:
         up_a = np.zeros(nc, np.int64)        # unique-pair index
         for b, p in enumerate(cell_pairs):
             n, G = len(p.resp), len(p.gen_toks)
-            f_a[b] = min(p.first_edit, max(n - 1, 0))
+            fc = int(f_cell[b]) if f_cell is not None and b < len(f_cell) else -1
+            f_a[b] = min(p.first_edit, max(n - 1, 0)) if fc < 0 else min(fc, n)
             E_a[b] = min(max([G - 2] + list(p.spikes_rel)), n - 1)
             u = uniq.get(id(p))
             if u is None:

@@ -486,3 +486,47 @@ def test_trie_decode_is_exact(carry):
         assert abs(a["nll_edit"] - b["nll_edit"]) < 1e-5 and abs(a["nll_self"] - b["nll_self"]) < 1e-5
         for f in ("p_secret_mean", "p_secret_final", "p_secret_max"):
             assert abs(a[f] - b[f]) < 1e-6 + 1e-5 * abs(a[f])
+
+
+def test_noop_spike_skip_is_exact():
+    """Cells whose ablated latents are inactive at their pair's first spikes start their teacher-forced tail at
+    their first effective spike (activity decided by the edit kernel itself); all-zero edits are exact no-ops,
+    so the records equal the run that starts every tail at the pair's first spike, with fewer tail rows."""
+    from dataclasses import replace
+
+    from taboo_brittleness_amd.interp.sae import JumpReLUSAE
+    from taboo_brittleness_amd.models.gemma2 import Gemma2Model
+    from taboo_brittleness_amd.models.spec import GEMMA2_TINY
+    from taboo_brittleness_amd.models.tokenizer import SyntheticTokenizer
+    from taboo_brittleness_amd.models.weights import random_gemma2
+    from taboo_brittleness_amd.pipelines.sweep import SweepRunner
+
+    spec = replace(GEMMA2_TINY, vocab_size=1024, layers=4, hidden=256, ffn=512)
+    m = Gemma2Model(random_gemma2(spec, dtype=torch.bfloat16, seed=7, norm_std=0.1, post_norm_gain=8.0), "cpu")
+    cfg = load_config(None, OVR + ["experiment.max_new_tokens=12", "intervention.random_trials=4",
+                                   "intervention.budgets=[1, 2, 4]",
+                                   "prompts=['Give me a hint!', 'Any hints available?', 'I need one more clue.']"])
+    tok = SyntheticTokenizer(vocab_size=spec.vocab_size)
+    key = lambda r: (r["word"], r["prompt_idx"], r["method"], r["budget"], r["trial"])   # noqa: E731
+    res, stats = {}, {}
+    for skip in (False, True):
+        sae = JumpReLUSAE.random(spec.hidden, 512, seed=2, device="cpu")
+        r = SweepRunner(cfg, m, tok, sae, batch=60, device="cpu", layer=2, use_graphs=False,
+                        prefix_share=True, layer_resume=True, kv_pairs=8)
+        r.skip_noop_spikes = skip
+        pairs = r.build_pairs(["ship"], cfg.prompts[:3])
+        r.run_baselines(pairs)
+        out = []
+        for j in range(3):
+            out += r.run_cells([pairs[j]], r.make_cells([pairs[j]]), measure_nll=True)
+        res[skip] = {key(x): x for x in out}
+        stats[skip] = dict(r.stats)
+    assert stats[True]["tf_rows"] < stats[False]["tf_rows"], (stats[True]["tf_rows"], stats[False]["tf_rows"])
+    assert set(res[False]) == set(res[True])
+    for k, a in res[False].items():
+        b = res[True][k]
+        assert a["response_ids"] == b["response_ids"], k
+        assert a["topk_ids"] == b["topk_ids"], k
+        assert abs(a["nll_edit"] - b["nll_edit"]) < 1e-5 and abs(a["nll_self"] - b["nll_self"]) < 1e-5, k
+        for f in ("p_secret_mean", "p_secret_final", "p_secret_max"):
+            assert abs(a[f] - b[f]) < 1e-6 + 1e-5 * abs(a[f]), (k, f)
