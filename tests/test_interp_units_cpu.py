@@ -74,6 +74,9 @@ def test_lowrank_edit_sae_ablation_formula():
         x = h0[r].float()
         pre = sae.W_encT[sel].float() @ x + sae.b_enc[sel]
         a = torch.where(pre > sae.threshold[sel], pre, torch.zeros_like(pre))   # JumpReLU, strict
+        if not bool((a != 0).any()):        # all-zero edit: an exact no-op, the next norm input is untouched
+            assert torch.equal(h[r], h0[r]) and not bool(x_next[r].any()), r
+            continue
         want = x - a @ sae.W_dec[sel].float()
         torch.testing.assert_close(h[r].float(), want, atol=0.05, rtol=0.02)
         torch.testing.assert_close(x_next[r].float(), _rms(h[r], w_next, 1e-6), atol=0.05, rtol=0.02)
