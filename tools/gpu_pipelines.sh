@@ -16,3 +16,6 @@ t0=$(S); timeout -k 10 600 python -m taboo_brittleness_amd run_token_forcing con
 echo "run_token_forcing postgame: $(python3 -c "print(round($t1 - $t0, 1))") s"; tail -3 $R/tf.log
 t0=$(S); timeout -k 10 900 python -m taboo_brittleness_amd run_sweep configs/ll_baseline_9b.yaml --methods all --set runtime.batch_size=4096 --out $R/results/sweeps/all > $R/sweep.log 2>&1; t1=$(S)
 echo "run_sweep (all methods): $(python3 -c "print(round($t1 - $t0, 1))") s"; tail -3 $R/sweep.log
+# the npz caches / sweep shards are large: keep the logs and summaries only (gpurun copies back <= 64 MiB)
+rm -rf $R/processed
+find $R/results -name "*.npz" -delete

@@ -12,4 +12,5 @@ echo BENCH_PLAIN_OK; tail -1 gpurun_out/final/bench_20_5_plain.log | cut -c1-200
 bash tools/gpu_pipelines.sh > gpurun_out/final/pipelines.txt 2>&1
 echo PIPES_OK; cat gpurun_out/final/pipelines.txt | grep -E "^run_|cells on"
 bash tools/prof_stats.sh final_r2 > /dev/null
-python3 tools/kstats.py gpurun_out/prof_final_r2/run_kernel_stats.csv | head -25
+python3 tools/kstats.py gpurun_out/prof_final_r2/run_kernel_stats.csv > gpurun_out/final/kernel_stats.txt
+head -25 gpurun_out/final/kernel_stats.txt
