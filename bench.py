@@ -101,9 +101,11 @@ def main() -> None:
     ap.add_argument("--fused-geglu", action="store_true",
                     help="gate|up GEMM with the GeGLU in its epilogue (ping-pong MFMA kernel, csrc/gemm.hip) "
                          "instead of hipBLASLt + the GeGLU kernel")
-    ap.add_argument("--no-fused-head", action="store_true",
-                    help="vocab head as hipBLASLt logits + the decode_head kernel instead of the fused MFMA GEMM head "
-                         "(softcap / log-sum-exp / argmax in the GEMM epilogue, no logits in HBM)")
+    ap.add_argument("--fused-head", action="store_true",
+                    help="vocab head as the fused MFMA GEMM head (softcap / log-sum-exp / argmax in the GEMM epilogue, "
+                         "no logits in HBM) instead of hipBLASLt logits + the decode_head kernel (default since it "
+                         "measured 0.4-1.7%% slower on HEAD: profiles/r2/head_ab/)")
+    ap.add_argument("--no-fused-head", action="store_true", help="the default (kept for older command lines)")
     ap.add_argument("--no-trie-decode", action="store_true",
                     help="decode every diverged cell through all blocks on its own row instead of running blocks "
                          "0..l once per group of a pair's cells with equal tokens (prefix-trie decode)")
@@ -136,7 +138,9 @@ def main() -> None:
     weights = random_gemma2(spec, device=dev, dtype=torch.bfloat16, seed=1234, post_norm_gain=args.init_gain)
     model = Gemma2Model(weights, dev)
     fused_geglu = bool(args.fused_geglu and model.enable_fused_geglu())
-    if args.no_fused_head:
+    if args.fused_head:
+        model.fused_head = bool(on_gpu and spec.vocab_size % 256 == 0)
+    elif args.no_fused_head:
         model.fused_head = False
     if args.lora_rank > 0:
         from taboo_brittleness_amd.models.lora import LoRABank

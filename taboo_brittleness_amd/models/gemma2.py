@@ -171,7 +171,7 @@ class Gemma2Model:
         if os.environ.get("TB_FUSED_GEGLU", "0") == "1":
             self.enable_fused_geglu()
         # vocab head (greedy token + NLLs) as one MFMA GEMM with a softcap/log-sum-exp/argmax epilogue
-        # (ops.vocab_head): no [rows, 256000] logits in HBM.  TB_FUSED_HEAD (default on) / --no-fused-head
+        # (ops.vocab_head): no [rows, 256000] logits in HBM.  TB_FUSED_HEAD=1 (default off) / bench --fused-head
         self.fused_head = self.device.type == "cuda" and ops.FUSED_HEAD and self.spec.vocab_size % 256 == 0
 
     def enable_fused_geglu(self) -> bool:

@@ -345,7 +345,9 @@ def xent_rows(logits, tgt, cap=0.0, emulate_bf16=True, out=None):
     return y
 
 
-FUSED_HEAD = os.environ.get("TB_FUSED_HEAD", "1") == "1"
+# fused GEMM head: opt-in since the end of round 2 (hipBLASLt logits + decode_head measured 0.4-1.7 % faster in
+# the bench on one box, identical work counters: profiles/r2/head_ab/); TB_FUSED_HEAD=1 / bench --fused-head
+FUSED_HEAD = os.environ.get("TB_FUSED_HEAD", "0") == "1"
 
 
 def head_part_numel(rows: int, vocab: int) -> int:
