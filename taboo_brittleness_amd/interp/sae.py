@@ -133,6 +133,7 @@ class JumpReLUSAE:
         q = 1.0 - min(max(target_l0 / self.d_sae, 1e-6), 0.5)
         k = min(n, max(1, int(round(q * n))))
         self.threshold = torch.kthvalue(pre, k, dim=0).values.clamp_min(1e-6).contiguous()
+        self.param_version = getattr(self, "param_version", 0) + 1     # consumers key caches on it
 
     def l0(self, x: torch.Tensor) -> float:
         return float((self.encode(x) > 0).float().sum(-1).mean())

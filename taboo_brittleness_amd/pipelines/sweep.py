@@ -76,6 +76,7 @@ class Pair:
     # ids and, per id, a bitmask over spikes_rel[:K] of where the edit kernel's own JumpReLU fires
     act_ids: Optional[np.ndarray] = None
     act_mask: Optional[np.ndarray] = None
+    act_key: Optional[tuple] = None                     # SAE parameter identity/versions the table was built with
 
     @property
     def first_edit(self) -> int:
@@ -341,9 +342,10 @@ class SweepRunner:
         its tail starts at its first *effective* spike (``_plan_for`` -> ``plan["f"]``)."""
         s, K = self.sae, self.iv.spikes_k
         rows, owner = [], []
+        key = self._sae_key()
         for g, p in enumerate(live):
             cand = np.union1d(p.active_pool, np.asarray(p.targeted, np.int64)).astype(np.int64)
-            p.act_ids, p.act_mask = cand, np.zeros(cand.size, np.int64)
+            p.act_ids, p.act_mask, p.act_key = cand, np.zeros(cand.size, np.int64), key
             if s is None or p.resid is None or not cand.size:
                 continue
             for k, t in enumerate(p.spikes_rel[:K]):
@@ -479,6 +481,15 @@ class SweepRunner:
                 "f": self._effective_first_edit(cells, pairs, by_pair, kd, ix, cn)}
         return self._plan_add_carry(plan) if with_carry else plan
 
+    def _sae_key(self) -> Optional[tuple]:
+        """Identity + in-place version of the SAE tensors an edit's coefficients depend on: an activity table
+        built under other parameters (e.g. before ``calibrate()``) is never used."""
+        s = self.sae
+        if s is None:
+            return None
+        ts = [s.W_encT, s.b_enc, s.threshold] + ([s.b_dec] if s.apply_b_dec_to_input else [])
+        return tuple((id(t), t._version) for t in ts) + (getattr(s, "param_version", 0), float(self.iv.alpha))
+
     def _effective_first_edit(self, cells, pairs, by_pair, kd, ix, cn) -> np.ndarray:
         """Per cell (plan row): response index of its first spike where the edit is non-zero (the pair's spike
         order), ``len(resp)`` if it never is (the cell is its baseline), -1 = the pair's first spike (projection
@@ -487,9 +498,12 @@ class SweepRunner:
         f = np.full(self.B, -1, np.int64)
         if not self.skip_noop_spikes:
             return f
+        key = self._sae_key()
         for pi, cis in by_pair.items():
             p = pairs[pi]
             ids, msk = p.act_ids, p.act_mask
+            if p.act_key != key:
+                continue                        # stale or missing table: every cell edits from the first spike
             sp = np.asarray(p.spikes_rel[:K], np.int64)
             ca = np.asarray([ci for ci in cis if kd[ci] == 1], np.int64)
             if ids is None or not ca.size or not sp.size:

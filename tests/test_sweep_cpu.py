@@ -530,3 +530,34 @@ def test_noop_spike_skip_is_exact():
         assert abs(a["nll_edit"] - b["nll_edit"]) < 1e-5 and abs(a["nll_self"] - b["nll_self"]) < 1e-5, k
         for f in ("p_secret_mean", "p_secret_final", "p_secret_max"):
             assert abs(a[f] - b[f]) < 1e-6 + 1e-5 * abs(a[f]), (k, f)
+
+
+def test_noop_table_is_dropped_after_sae_change():
+    """An activity table built under other SAE parameters (before ``calibrate()``) is never used to skip
+    spikes: the plan falls back to the pair's first spike until the pair is re-scored."""
+    from dataclasses import replace
+
+    from taboo_brittleness_amd.interp.sae import JumpReLUSAE
+    from taboo_brittleness_amd.models.gemma2 import Gemma2Model
+    from taboo_brittleness_amd.models.spec import GEMMA2_TINY
+    from taboo_brittleness_amd.models.tokenizer import SyntheticTokenizer
+    from taboo_brittleness_amd.models.weights import random_gemma2
+    from taboo_brittleness_amd.pipelines.sweep import SweepRunner
+
+    spec = replace(GEMMA2_TINY, vocab_size=1024, layers=3, hidden=256, ffn=512)
+    m = Gemma2Model(random_gemma2(spec, dtype=torch.bfloat16, seed=7, norm_std=0.1, post_norm_gain=8.0), "cpu")
+    cfg = load_config(None, OVR + ["intervention.budgets=[1, 2]", "intervention.random_trials=4"])
+    tok = SyntheticTokenizer(vocab_size=spec.vocab_size)
+    sae = JumpReLUSAE.random(spec.hidden, 512, seed=2, device="cpu")
+    r = SweepRunner(cfg, m, tok, sae, batch=40, device="cpu", layer=1, use_graphs=False, prefix_share=True,
+                    layer_resume=True)
+    pairs = r.build_pairs(["ship"], cfg.prompts[:2])
+    r.run_baselines(pairs)
+    cells = r.make_cells(pairs, ("sae_targeted", "sae_random"))
+    f0 = r._plan_for(cells, pairs, {}, with_carry=False)["f"][: len(cells)]
+    sae.calibrate(torch.cat([p.resid for p in pairs], 0))
+    f1 = r._plan_for(cells, pairs, {}, with_carry=False)["f"][: len(cells)]
+    assert (f1 == -1).all() and (f0 >= 0).any()
+    r._score_pairs(pairs)
+    f2 = r._plan_for(cells, pairs, {}, with_carry=False)["f"][: len(cells)]
+    assert (f2 >= 0).any()
