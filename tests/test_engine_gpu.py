@@ -232,6 +232,43 @@ def test_sweep_gpu_trie_decode(gpu):
             assert len(set(a["topk_ids"]) & set(b["topk_ids"])) >= 4
 
 
+def test_sweep_gpu_noop_spike_skip(gpu):
+    """Tails starting at each cell's first effective spike (activity from the HIP edit kernel's own coefficients;
+    all-zero edits are no-ops in the kernel) reproduce the records of tails starting at the pair's first spike
+    on the GPU, with fewer tail rows."""
+    from taboo_brittleness_amd.config import load_config
+    from taboo_brittleness_amd.interp.sae import JumpReLUSAE
+    from taboo_brittleness_amd.models.tokenizer import SyntheticTokenizer
+    from taboo_brittleness_amd.pipelines.sweep import SweepRunner
+
+    cfg = load_config(None, ["experiment.max_new_tokens=12", "intervention.budgets=[1, 2, 4]",
+                             "intervention.random_trials=6"])
+    mg = Gemma2Model(random_gemma2(SPEC, dtype=torch.bfloat16, seed=5, norm_std=0.1, post_norm_gain=8.0,
+                                   device=gpu), gpu)
+    tok = SyntheticTokenizer(vocab_size=SPEC.vocab_size)
+    key = lambda r: (r["word"], r["prompt_idx"], r["method"], r["budget"], r["trial"])   # noqa: E731
+    out, stats = {}, {}
+    for skip in (False, True):
+        sae = JumpReLUSAE.random(SPEC.hidden, 1024, seed=2, device=gpu)
+        r = SweepRunner(cfg, mg, tok, sae, batch=96, device=gpu, layer=2, prefix_share=True, layer_resume=True,
+                        kv_pairs=8)
+        r.skip_noop_spikes = skip
+        pairs = r.build_pairs(["ship"], cfg.prompts[:4])
+        r.run_baselines(pairs)
+        res = r.run_cells(pairs, r.make_cells(pairs, ("sae_targeted", "sae_random")))
+        out[skip] = {key(x): x for x in res}
+        stats[skip] = dict(r.stats)
+    assert stats[True]["tf_rows"] < stats[False]["tf_rows"], (stats[True]["tf_rows"], stats[False]["tf_rows"])
+    assert set(out[False]) == set(out[True])
+    same = [out[False][k]["response_ids"] == out[True][k]["response_ids"] for k in out[False]]
+    assert sum(same) >= int(0.9 * len(same))
+    for k, a in out[False].items():
+        b = out[True][k]
+        if a["response_ids"] == b["response_ids"]:
+            assert abs(a["nll_edit"] - b["nll_edit"]) < 0.05
+            assert len(set(a["topk_ids"]) & set(b["topk_ids"])) >= 4
+
+
 def test_sweep_gpu_cross_step_pipeline(gpu):
     """The bench's cross-step pipeline on the GPU (staged plan upload + teacher-forced tail queued behind the
     previous batch's lens, pinned async D2H, records on the host thread, graph-replayed decode), with and
