@@ -25,6 +25,17 @@ instead of recomputed: the cell resumes decoding at f, and the teacher-forced
 ΔNLL pass only runs positions ≥ f, adding the baseline's per-token NLLs for
 the earlier targets.  Baselines of the *next* pairs ride along in the same
 decode batch, so their cost hides behind the cells'.
+
+Layer resume (``_run_batch_resume``) adds three more exact reuse levels that rest on one fact: blocks
+``0..l`` (l = hooked layer) see only tokens, the edit only touches the residual after block ``l``.
+
+* prefix-trie decode — diverged cells of a pair with equal tokens since their divergence run blocks
+  ``0..l`` once per group (``Generator.decode(share_keys=)``, keys from :meth:`SweepRunner._trie_keys`);
+* lens row dedup — their hooked-layer residuals at unedited positions are identical, so those lens rows are
+  unembedded once (:meth:`SweepRunner._lens_row_keys`, ``lens_packed(row_key=)``);
+* no-op spike skip — a spike where none of a cell's ablated latents fires is an exact no-op edit, decided by
+  the edit kernel itself on the baseline's residuals (:meth:`SweepRunner._spike_activity`), so the cell's
+  teacher-forced tail starts at its first effective spike (``plan["f"]``).
 """
 from __future__ import annotations
 
