@@ -165,7 +165,7 @@ def lens_readout(model, store: torch.Tensor, starts: Sequence[int], lens: Sequen
 def lens_packed(model, store: torch.Tensor, rows: np.ndarray, offs: np.ndarray, base: torch.Tensor,
                 track: np.ndarray, excl: np.ndarray, round_bf16: bool = False,
                 chunk_rows: int = 4096, sync: bool = True, row_key: Optional[np.ndarray] = None,
-                stats: Optional[dict] = None):
+                stats: Optional[dict] = None, row_check: Optional[np.ndarray] = None):
     """Partial lens over packed rows: sequence ``i`` owns flat rows ``rows[offs[i]:offs[i+1]]`` of
     ``store.view(-1, D)`` (no padding) and adds their (excluded) lens probabilities onto ``base[i]``
     (the reused part of its response sum, updated in place).  ``track [R, K]`` are per-row ids whose
@@ -175,7 +175,9 @@ def lens_packed(model, store: torch.Tensor, rows: np.ndarray, offs: np.ndarray, 
 
     ``row_key [R]`` (optional): rows with equal keys hold identical residuals (e.g. sweep cells of one pair
     with equal tokens, at positions without an edit); each chunk then unembeds one row per key and the
-    readout kernels read it through a row map (the lens GEMM shrinks, the sums are unchanged)."""
+    readout kernels read it through a row map (the lens GEMM shrinks, the sums are unchanged).  ``row_check``
+    (optional, a second independent key): a chunk whose rows of one ``row_key`` disagree on it (a hash
+    collision) is evaluated without dedup."""
     dev = store.device
     D = store.shape[-1]
     flat = store.view(-1, D)
@@ -195,10 +197,14 @@ def lens_packed(model, store: torch.Tensor, rows: np.ndarray, offs: np.ndarray, 
         i1 = min(n, max(i1, i0 + 1))
         r0, r1 = int(offs[i0]), int(offs[i1])
         if r1 > r0:
-            if row_key is not None:      # one GEMM row per distinct key, logical rows mapped onto them
+            dedup = row_key is not None
+            if dedup:                    # one GEMM row per distinct key, logical rows mapped onto them
                 _, first, inv = np.unique(row_key[r0:r1], return_index=True, return_inverse=True)
+                inv = inv.reshape(-1)
+                if row_check is not None and not np.array_equal(row_check[r0:r1][first][inv], row_check[r0:r1]):
+                    first, inv = np.arange(r1 - r0), np.arange(r1 - r0)      # collision: this chunk un-deduplicated
                 src = rows[r0:r1][first]
-                map_l.append(inv.reshape(-1).astype(np.int32))
+                map_l.append(inv.astype(np.int32))
             else:
                 src = rows[r0:r1]
             M = len(src)
@@ -209,7 +215,7 @@ def lens_packed(model, store: torch.Tensor, rows: np.ndarray, offs: np.ndarray, 
             offs_l.append((offs[i0:i1 + 1] - r0).astype(np.int32))
             # deduplicated chunks run the 256-row padded GEMM (the padding repeats a row; the row map never
             # reads it): few distinct shapes, all in the TunableOp tables
-            chunks.append((i0, i1, r0, r1, pr0, Mp if row_key is not None else M, po0))
+            chunks.append((i0, i1, r0, r1, pr0, Mp if dedup else M, po0))
             pr0 += Mp
             po0 += i1 - i0 + 1
         i0 = i1

@@ -1265,13 +1265,14 @@ class SweepRunner:
             ex[:, 0] = cur[cell_of, pos]
             ex[:, 1] = np.where(pos > 0, cur[cell_of, np.maximum(pos - 1, 0)], -1)
         row_key = self._lens_row_keys(cell_of, pos, q >= cs, div, j_a, u_a, sp_u, host_tok) if R else None
+        row_key, row_check = row_key if row_key is not None else (None, None)
         self._tick("ro_entries")
         self.stats["lens_rows"] += R
         self._ensure_cum(ulist)
         base = self._lens_base(cell_pairs, d_a.tolist(), ng_a.tolist(), f_e)
         self._tick("ro_base")
         acc, pr_d = lens_packed(m, self.store, rows, offs, base, trk, ex, sync=False, row_key=row_key,
-                                stats=self.stats)
+                                stats=self.stats, row_check=row_check)
         if self.exclusion == "response":
             for i in range(E_n):
                 r_ = cell_pairs[i].resp if dv_a[i] < 0 else host_tok[j_a[i], : ng_a[i]].tolist()
@@ -1306,8 +1307,9 @@ class SweepRunner:
         """Dedup keys of the lens rows (``lens_packed(row_key=)``): the hooked-layer residual of a diverged cell at
         a non-spike position ``t >= D`` is a function of its pair and its tokens ``0..t`` alone (blocks ``0..l``
         see only tokens, and no edit touches it), so cells of one pair with equal tokens up to ``t`` hold the
-        same row.  Those rows get a 63-bit hash key of (pair, t, tokens ``0..t``); every other row (spikes,
-        undiverged cells) a unique negative key.  None when nothing can repeat."""
+        same row.  Those rows get a 63-bit hash key of (pair, t, tokens ``0..t``) plus a second independent hash
+        as a collision check (``lens_packed(row_check=)``); every other row (spikes, undiverged cells) a unique
+        negative key.  Returns ``(keys, checks)``, or None when nothing can repeat."""
         R = len(pos)
         if not self.trie_decode or host_tok is None or not div.any():
             return None
@@ -1319,13 +1321,18 @@ class SweepRunner:
         # rolling 64-bit hash of every diverged cell's response prefix (wrapping uint64 arithmetic)
         tok = host_tok[j_a[div]].astype(np.uint64) + np.uint64(1)
         h = np.empty(tok.shape, np.uint64)
+        h2 = np.empty(tok.shape, np.uint64)
         acc = np.zeros(tok.shape[0], np.uint64)
-        mul = np.uint64(0x9E3779B97F4A7C15)
+        acc2 = np.full(tok.shape[0], 0x243F6A8885A308D3, np.uint64)
+        mul, mul2 = np.uint64(0x9E3779B97F4A7C15), np.uint64(0xD6E8FEB86659FD93)
         with np.errstate(over="ignore"):
             for t in range(tok.shape[1]):
                 acc = (acc ^ tok[:, t]) * mul
                 acc ^= acc >> np.uint64(29)
                 h[:, t] = acc
+                acc2 = (acc2 + tok[:, t] * np.uint64(0x9FB21C651E98DF25)) * mul2
+                acc2 ^= acc2 >> np.uint64(31)
+                h2[:, t] = acc2
             ci = np.full(len(div), -1, np.int64)
             ci[np.nonzero(div)[0]] = np.arange(int(div.sum()))
             r = np.nonzero(dd)[0]
@@ -1333,8 +1340,11 @@ class SweepRunner:
             t = np.minimum(pos[r], tok.shape[1] - 1)
             k = h[c, t] ^ (u_a[cell_of[r]].astype(np.uint64) * np.uint64(0xC2B2AE3D27D4EB4F))
             k ^= pos[r].astype(np.uint64) * np.uint64(0x165667B19E3779F9)
+            k2 = h2[c, t] ^ (u_a[cell_of[r]].astype(np.uint64) * np.uint64(0x85EBCA77C2B2AE63))
         key[r] = (k & np.uint64(0x7FFFFFFFFFFFFFFF)).astype(np.int64)
-        return key
+        chk = np.arange(R, dtype=np.int64)
+        chk[r] = k2.view(np.int64)
+        return key, chk
 
     def _resume_records(self, batch, cell_pairs, cols, pr, vh, ih, K) -> List[dict]:
         """Host half of :meth:`_resume_readout`: per-cell readout statistics and result records."""

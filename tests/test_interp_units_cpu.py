@@ -353,3 +353,39 @@ def test_gradient_subspace_orthonormal_and_mean_aligned():
     assert GR.grad_norm_ratio(G) > 0.9
     U1 = GR.gradient_subspace(G[:1], 3, seed=7)        # rank-deficient: padded, still orthonormal
     assert torch.allclose(U1 @ U1.t(), torch.eye(3), atol=1e-5)
+
+
+def test_lens_packed_row_dedup_and_collision_fallback():
+    """lens_packed with row keys: rows sharing a key are unembedded once and give the same sums/probs as
+    the plain evaluation; a key collision (same key, different check value) falls back to no dedup."""
+    from dataclasses import replace
+
+    from taboo_brittleness_amd.interp.logit_lens import lens_packed
+    from taboo_brittleness_amd.models.gemma2 import Gemma2Model
+    from taboo_brittleness_amd.models.spec import GEMMA2_TINY
+    from taboo_brittleness_amd.models.weights import random_gemma2
+
+    spec = replace(GEMMA2_TINY, vocab_size=512, layers=2, hidden=128, ffn=256)
+    m = Gemma2Model(random_gemma2(spec, dtype=torch.bfloat16, seed=3, norm_std=0.1), "cpu")
+    torch.manual_seed(0)
+    store = torch.randn(4, 6, spec.hidden).to(torch.bfloat16)
+    store[1, 2] = store[0, 2]                       # two identical rows (flat rows 2 and 8)
+    rows = np.array([2, 3, 8, 9, 14], np.int64)
+    offs = np.array([0, 2, 5], np.int64)
+    trk = np.array([[1, 2]] * 5, np.int64)
+    ex = np.full((5, 2), -1, np.int64)
+    ref_acc, ref_p = lens_packed(m, store, rows, offs, torch.zeros(2, spec.vocab_size), trk, ex)
+    key = np.array([7, -2, 7, -4, -5], np.int64)
+    st = {}
+    acc, p = lens_packed(m, store, rows, offs, torch.zeros(2, spec.vocab_size), trk, ex, row_key=key,
+                         row_check=np.array([1, 0, 1, 0, 0], np.int64), stats=st)
+    assert st["lens_gemm_rows"] == 4
+    torch.testing.assert_close(acc, ref_acc)
+    np.testing.assert_allclose(p, ref_p)
+    st = {}
+    bad = np.array([-1, -2, -3, -4, -2], np.int64)   # flat rows 3 and 14 (different residuals) collide
+    acc, p = lens_packed(m, store, rows, offs, torch.zeros(2, spec.vocab_size), trk, ex, row_key=bad,
+                         row_check=np.array([0, 5, 1, 6, 7], np.int64), stats=st)
+    assert st["lens_gemm_rows"] == 5
+    torch.testing.assert_close(acc, ref_acc)
+    np.testing.assert_allclose(p, ref_p)
