@@ -1,6 +1,7 @@
 """Hot kernels of the flagship sweep step at its decode shapes, in one short program for rocprofv3 PMC passes
 (tools/pmc_kernels.sh): softcapped GQA decode attention, GeGLU, fused add+RMSNorm, RoPE+KV store, the SAE
-JumpReLU encode (MFMA GEMM + threshold epilogue) and, for comparison, one hipBLASLt projection GEMM.
+JumpReLU encode (MFMA GEMM + threshold epilogue), for comparison one hipBLASLt projection GEMM, and (round 2) the
+prefix-trie K/V fan-out and the vocab head's decode_head reduction.
 
 Shapes: 2048 decode rows (a typical row bucket of the diverged-cell decode), Gemma-2-9B dims
 (D 3584, 16 q / 8 kv heads x 256, FFN 14336), 67-token KV rows, 16k-latent SAE.  Prints achieved
@@ -73,4 +74,22 @@ W_gu = torch.randn(2 * F, D, device=dev, dtype=BF) * 0.02
 y = torch.empty(M, 2 * F, device=dev, dtype=BF)
 t = timed(lambda: torch.matmul(x, W_gu.t(), out=y))
 res["hipblaslt_gate_up"] = {"ms": t * 1e3, "TFLOP/s": 2 * M * D * 2 * F / t / 1e12}
+del W_gu, y, acts, W_enc
+
+# round 2: prefix-trie decode K/V fan-out (3584 rows, 2/3 of them members, blocks 0..31, 67-token slots) and the
+# hipBLASLt head's decode_head reduction (2048 rows x 256k vocab, bf16 softcap chain, argmax + NLL)
+Lf, R2 = 32, 3584
+kc5 = torch.randn(Lf, R2, Hkv, S, HD, device=dev, dtype=BF)
+vc5 = torch.randn_like(kc5)
+src = torch.where(torch.arange(R2, device=dev) % 3 == 0, -1, (torch.arange(R2, device=dev) // 3) * 3).int()
+slot2 = torch.arange(R2, dtype=torch.int32, device=dev)
+pos2 = torch.full((R2,), S - 1, dtype=torch.int32, device=dev)
+t = timed(lambda: ops.kv_fanout(kc5, vc5, src, slot2, pos2, Lf))
+nmem = int((src >= 0).sum())
+res["kv_fanout"] = {"ms": t * 1e3, "GB/s": 2 * 2 * nmem * Lf * Hkv * HD * 2 / t / 1e9}
+del kc5, vc5
+V = 256000
+lg = (torch.randn(M, V, device=dev) * 3).to(BF)
+t = timed(lambda: ops.decode_head(lg, 30.0))
+res["decode_head"] = {"ms": t * 1e3, "GB/s": lg.numel() * 2 / t / 1e9}
 print(json.dumps({k: {kk: round(vv, 3) for kk, vv in v.items()} for k, v in res.items()}))

@@ -14,7 +14,7 @@ import os
 import sys
 from collections import defaultdict
 
-KEEP = ("attn_decode", "geglu", "add_rmsnorm2", "gemm_nt_kernel", "Cijk")
+KEEP = ("attn_decode", "geglu", "add_rmsnorm2", "gemm_nt_kernel", "gemm_pp_kernel", "kv_fanout", "decode_head", "Cijk")
 
 
 def short(name: str) -> str:
