@@ -66,6 +66,28 @@ def _host_rss_gb():
         return None
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return int(s.getsockname()[1])
+
+
+def launch_ranks(n: int, argv) -> int:
+    """``--gpus N`` without an outer launcher: run this script as N ranks under
+    ``torch.distributed.run`` (one process per GPU, RCCL over xGMI) in a CHILD process and return its exit
+    code.  Called before anything touches the GPU in this process (no exec: the parent only waits); the
+    ranks' stdout (rank 0's JSON line) is inherited."""
+    import subprocess
+
+    env = dict(os.environ)
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + list(argv)
+    return subprocess.run(cmd, env=env).returncode
+
+
 def fresh(p: Pair, rep: int = 0) -> Pair:
     return Pair(p.word, p.pidx, p.prompt, list(p.ids), list(p.forms), list(p.track), rep=rep)
 
@@ -121,8 +143,11 @@ def main() -> None:
                     help="run TunableOp over every GEMM shape and save configs/tunableop/<tag>.csv")
     ap.add_argument("--no-tuned-gemms", action="store_true", help="ignore the saved TunableOp results")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
 
     info = D.init_distributed()
+    assert info.world == args.gpus, f"--gpus {args.gpus} but the launcher started {info.world} rank(s)"
     dev = info.device
     on_gpu = dev.type == "cuda"
     arch = args.arch if on_gpu else "gemma2-tiny"
@@ -292,7 +317,9 @@ def main() -> None:
     D.barrier(info)
     if marks is not None:
         marks.append(("end", time.monotonic_ns()))
-    elapsed = D.all_reduce_max(time.perf_counter() - t0, info)
+    mine = time.perf_counter() - t0
+    per_rank = [float(v) for v in D.all_gather_objects(mine, info)]
+    elapsed = D.all_reduce_max(mine, info)
     total_cells = D.all_reduce_max(float(n_done), info) * info.world   # every rank does the same count
     value = total_cells / elapsed
     ms = 1000.0 * elapsed / max(args.steps, 1)
@@ -302,6 +329,8 @@ def main() -> None:
             "value": round(value, 3),
             "unit": "prompts/s",
             "n_gpus": info.world,
+            "ranks": {"world_size": info.world, "backend": info.backend,
+                      "ms_per_step": [round(1000.0 * v / max(args.steps, 1), 2) for v in per_rank]},
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms, 2),

@@ -76,7 +76,7 @@ void tb_lowrank_edit(uint16_t* h, uint16_t* x_next, const uint8_t* apply, const 
                      int mmax, const void* E, const void* Dm, int table_f32, const float* bias, const float* thr,
                      const float* pre_bias, float alpha, const uint16_t* w_next, float eps, int M, int D,
                      float* coef_out, hipStream_t st);
-void tb_sae_decode_sparse(const float* acts, const uint16_t* Wdec, const float* b_dec, uint16_t* out_bf16,
+void tb_sae_decode_sparse(const float* acts, const void* Wdec, int table_f32, const float* b_dec, uint16_t* out_bf16,
                           float* out_f32, int M, int L, int D, hipStream_t st);
 void tb_latent_score(const float* acts, const float* p, const uint8_t* spike, const int32_t* seg, float* out,
                      float* spike_mean, float* corr, int G, int L, hipStream_t st);

@@ -498,7 +498,9 @@ void lowrank_edit(torch::Tensor h, c10::optional<torch::Tensor> x_next, torch::T
 
 void sae_decode_sparse(torch::Tensor acts, torch::Tensor Wdec, c10::optional<torch::Tensor> b_dec,
                        c10::optional<torch::Tensor> out_bf16, c10::optional<torch::Tensor> out_f32) {
-  IN_F32(acts); IN_BF16(Wdec);
+  IN_F32(acts); CHECK_DEV(Wdec); CHECK_CONTIG(Wdec);
+  const bool f32 = Wdec.scalar_type() == at::kFloat;
+  TORCH_CHECK(f32 || Wdec.scalar_type() == at::kBFloat16, "sae_decode_sparse: W_dec must be fp32 or bf16");
   const int L = Wdec.size(0), D = Wdec.size(1), M = acts.numel() / L;
   TORCH_CHECK(D % 8 == 0, "sae_decode_sparse: D must be a multiple of 8");
   TORCH_CHECK(acts.size(-1) == L, "sae_decode_sparse: acts last dim must equal W_dec rows");
@@ -514,7 +516,8 @@ void sae_decode_sparse(torch::Tensor acts, torch::Tensor Wdec, c10::optional<tor
   if (out_bf16.has_value() && out_bf16->defined()) { IN_BF16((*out_bf16)); ob = reinterpret_cast<uint16_t*>(out_bf16->data_ptr()); }
   if (out_f32.has_value() && out_f32->defined()) { IN_F32((*out_f32)); of = out_f32->data_ptr<float>(); }
   c10::DeviceGuard g(acts.device());
-  tb_sae_decode_sparse(acts.data_ptr<float>(), cbf(Wdec), optf(b_dec), ob, of, M, L, D, cur_stream());
+  tb_sae_decode_sparse(acts.data_ptr<float>(), Wdec.data_ptr(), f32 ? 1 : 0, optf(b_dec), ob, of, M, L, D,
+                       cur_stream());
 }
 
 void latent_score(torch::Tensor acts, torch::Tensor p, torch::Tensor spike, torch::Tensor seg, torch::Tensor out,

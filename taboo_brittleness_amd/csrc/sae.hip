@@ -240,8 +240,9 @@ __global__ void __launch_bounds__(256) lowrank_edit_kernel(
 }
 
 // ------------------------------------------------------------- sparse decode
+template <typename TT>   // decoder table: bf16 (uint16_t) or fp32 (the Gemma Scope dtype, default)
 __global__ void __launch_bounds__(256) sae_decode_sparse_kernel(const float* __restrict__ acts,
-                                                                const uint16_t* __restrict__ Wdec,
+                                                                const TT* __restrict__ Wdec,
                                                                 const float* __restrict__ b_dec,
                                                                 uint16_t* __restrict__ out_bf16,
                                                                 float* __restrict__ out_f32, int L, int D) {
@@ -270,7 +271,7 @@ __global__ void __launch_bounds__(256) sae_decode_sparse_kernel(const float* __r
         const float a = ar[j];
         if (a == 0.f) continue;
         float wf[8];
-        unpack8(reinterpret_cast<const uint4*>(Wdec + (size_t)j * D)[c], wf);
+        load8<TT>(Wdec + (size_t)j * D + c * 8, wf);
 #pragma unroll
         for (int q = 0; q < 8; ++q) o[q] += a * wf[q];
       }
@@ -300,7 +301,7 @@ __global__ void __launch_bounds__(256) sae_decode_sparse_kernel(const float* __r
     for (int q = 0; q < 8; ++q) o[q] = b_dec ? b_dec[c * 8 + q] : 0.f;
     for (int k = 0; k < n; ++k) {
       float wf[8];
-      unpack8(reinterpret_cast<const uint4*>(Wdec + (size_t)act_idx[k] * D)[c], wf);
+      load8<TT>(Wdec + (size_t)act_idx[k] * D + c * 8, wf);
       const float a = act_val[k];
 #pragma unroll
       for (int q = 0; q < 8; ++q) o[q] += a * wf[q];
@@ -381,10 +382,15 @@ void tb_lowrank_edit(uint16_t* h, uint16_t* x_next, const uint8_t* apply, const 
 #undef TB_LR
 }
 
-void tb_sae_decode_sparse(const float* acts, const uint16_t* Wdec, const float* b_dec, uint16_t* out_bf16,
+void tb_sae_decode_sparse(const float* acts, const void* Wdec, int table_f32, const float* b_dec, uint16_t* out_bf16,
                           float* out_f32, int M, int L, int D, hipStream_t st) {
   if (M <= 0) return;
-  hipLaunchKernelGGL(sae_decode_sparse_kernel, dim3(M), dim3(256), 0, st, acts, Wdec, b_dec, out_bf16, out_f32, L, D);
+  if (table_f32)
+    hipLaunchKernelGGL(sae_decode_sparse_kernel<float>, dim3(M), dim3(256), 0, st, acts,
+                       reinterpret_cast<const float*>(Wdec), b_dec, out_bf16, out_f32, L, D);
+  else
+    hipLaunchKernelGGL(sae_decode_sparse_kernel<uint16_t>, dim3(M), dim3(256), 0, st, acts,
+                       reinterpret_cast<const uint16_t*>(Wdec), b_dec, out_bf16, out_f32, L, D);
 }
 
 void tb_latent_score(const float* acts, const float* p, const uint8_t* spike, const int32_t* seg, float* out,

@@ -23,3 +23,19 @@ def test_bench_two_ranks_gloo(tmp_path):
         assert k in d
     assert d["n_gpus"] == 2 and d["steps"] == 2 and d["value"] > 0 and d["config"]["parallelism"] == "dp2"
     assert d["work"]["cells"] == 2 * 66
+
+
+def test_bench_self_launch_two_ranks(tmp_path):
+    """``bench.py --gpus 2`` with no outer launcher starts the 2 ranks itself (child torch.distributed.run)
+    and still prints exactly one JSON line, from rank 0, with the launched world size."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "1",
+           "--pairs-per-step", "1", "--max-new", "8"]
+    out = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2"
+    assert d["ranks"]["world_size"] == 2 and len(d["ranks"]["ms_per_step"]) == 2

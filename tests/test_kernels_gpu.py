@@ -507,3 +507,49 @@ def test_attention_decode_cascade_prefix(gpu, HD):
         assert torch.isfinite(og.float()).all()
         _close(og, orf, atol=2e-2, rtol=2e-2)
         _close(og, o1, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("bf16_rows", [True, False])
+def test_sae_fp32_encode_firing_set(gpu, bf16_rows):
+    """fp32 SAE parity (reference encodes the fp32 residual with fp32 Gemma Scope weights,
+    `src/02_run_sae_baseline.py:30-36,66-67`): at Gemma-Scope shapes (3584 -> 16384) the GPU encode (bf16x3
+    split MFMA GEMM + JumpReLU epilogue) fires exactly the latents an fp32 CPU encode fires, ties excluded,
+    with fp32-level pre-activation error.  ``bf16_rows``: the model's bf16 residual (3-term split) or generic
+    fp32 rows (6-term split)."""
+    from taboo_brittleness_amd.interp.sae import JumpReLUSAE
+
+    torch.manual_seed(21)
+    D, L, N = 3584, 16384, 96
+    sae = JumpReLUSAE.random(D, L, seed=5, device="cpu")
+    sae.b_enc = torch.randn(L) * 0.05
+    x = torch.randn(N, D) * 1.3
+    sae.calibrate(x.to(BF) if bf16_rows else x)                 # thresholds at the L0 ~ 76 quantile
+    g = sae.to(gpu)
+    assert g.W_encT.dtype == torch.float32 and g.W_dec.dtype == torch.float32
+    xin = x.to(BF) if bf16_rows else x
+    pre_cpu = xin.double() @ sae.W_encT.double().t() + sae.b_enc.double()      # fp64 reference
+    pre_gpu = g.pre_acts(xin.to(gpu)).double().cpu()
+    scale = (xin.double().abs() @ sae.W_encT.double().abs().t()).clamp_min(1e-30)
+    assert float(((pre_gpu - pre_cpu).abs() / scale).max()) < 1e-5
+    acts = g.encode(xin.to(gpu)).cpu()
+    fires_cpu = pre_cpu > sae.threshold.double()
+    fires_gpu = acts > 0
+    tie = (pre_cpu - sae.threshold.double()).abs() <= 2e-5 * scale
+    assert int(fires_cpu.sum()) > 50 * N
+    assert torch.equal(fires_gpu[~tie], fires_cpu[~tie])
+    both = fires_cpu & fires_gpu
+    assert float(((acts.double() - pre_cpu).abs()[both] / scale[both]).max()) < 1e-5
+    # the same rows through the CPU encode agree on the firing set too
+    cpu_acts = sae.encode(xin)
+    assert torch.equal((cpu_acts > 0)[~tie], fires_cpu[~tie])
+
+
+def test_sae_decode_fp32_table(gpu):
+    torch.manual_seed(8)
+    M, L, D = 5, 4096, 512
+    acts = torch.relu(torch.randn(M, L) - 2.4)
+    Wd = torch.randn(L, D) * 0.05
+    bd = torch.randn(D) * 0.01
+    got = ops.sae_decode_sparse(acts.to(gpu), Wd.to(gpu), bd.to(gpu)).cpu()
+    want = acts.double() @ Wd.double() + bd.double()
+    _close(got, want.float(), atol=2e-5, rtol=1e-5)
