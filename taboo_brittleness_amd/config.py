@@ -143,6 +143,9 @@ class InterventionCfg:
         "smile": ["laugh", "happy", "face"]})
     measure_nll: bool = True
     measure_forcing: bool = False
+    # random-control draws per (method, budget) of the post-edit forcing curves; 0 = the sweep's own
+    # random_trials / proj_random_trials (the full control, DP-sharded over the groups)
+    forcing_trials: int = 0
 
 
 @dataclass

@@ -44,16 +44,27 @@ def run_sweep(cfg: Config, out_dir: str, methods: Sequence[str] = METHODS, info:
     runner = SweepRunner(cfg, model, tok, sae, batch=B, device=info.device, layer=stack.layer,
                          use_graphs=graphs, kv_pairs=n_pairs + 1)
     pairs = runner.build_pairs(cfg.words, cfg.prompts)
+    # work placement by PAIR (the reference's unit of work, `src/run_generation.py:155-156`): a pair's baseline
+    # and all of its cells run on one DP group, so every reuse level that works within a pair (prefix-trie
+    # decode groups, lens row dedup, the pair's KV / residual prefix) is as large as on one GPU
+    owned = pair_owners(len(pairs), dp_size)[dp_rank]
     t0 = time.perf_counter()
-    runner.run_baselines(pairs)
+    runner.run_baselines([pairs[i] for i in owned], size_for=pairs)
+    if dp_size > 1:
+        # the cross-pair inputs (pooled PCA / gradient subspaces, SAE calibration, word-averaged scores) need
+        # every pair's baseline: one object all-gather of the small per-pair results + kept residuals
+        share_baselines(pairs, owned, info, runner.dev)
     if sae is not None and stack.sae_random:
         resid = torch.cat([p.resid for p in pairs if p.resid is not None and p.resid.shape[0]], 0)
         sae.calibrate(resid)
-        runner._score_pairs(pairs)
+    # scores over ALL pairs at once (identical on every rank and for every world size; score_over=word then
+    # averages over all of a word's prompts, not over one baseline batch)
+    runner._score_pairs(pairs)
     t_base = time.perf_counter() - t0
     _check_comm(tp_ctx, None, "baselines")
     cells = runner.make_cells(pairs, methods)
-    mine = D.shard(list(range(len(cells))), dp_rank, dp_size)     # every TP rank of a group runs the same cells
+    own = set(owned)
+    mine = [i for i, c in enumerate(cells) if c.pair in own]     # every TP rank of a group runs the same cells
     shard_path = os.path.join(out_dir, f"shard_{dp_rank:03d}_of_{dp_size:03d}.json")
     writer = tp_ctx is None or tp_ctx.rank == 0
     elog = EventLog(os.path.join(out_dir, f"log_rank{info.rank:03d}.jsonl") if writer else None)
@@ -74,6 +85,15 @@ def run_sweep(cfg: Config, out_dir: str, methods: Sequence[str] = METHODS, info:
     elog.write("cells_done", cells=len(res), seconds=round(t_cells, 4),
                cells_per_s=round(len(res) / max(t_cells, 1e-9), 3))
     gathered = D.all_gather_objects(res if writer else [], info)
+    forcing = None
+    if cfg.intervention.measure_forcing:
+        # every rank takes part: settings are sharded over the DP groups and every TP rank of a group runs the
+        # same forwards (its peers' all-reduces would otherwise never be matched)
+        from .token_forcing import DPShard
+
+        forcing = forcing_curves(cfg, runner, pairs, methods, stack, log if info.is_main else (lambda *a: None),
+                                 dp=DPShard(dp_rank, dp_size, info))
+        _check_comm(tp_ctx, elog, "forcing")
     summary: Dict = {}
     if info.is_main:
         allres = sorted([r for part in gathered for r in part], key=lambda r: r["cell_id"])
@@ -89,8 +109,8 @@ def run_sweep(cfg: Config, out_dir: str, methods: Sequence[str] = METHODS, info:
         summary["config"] = {"layer": stack.layer, "arch": cfg.model.arch, "methods": list(methods),
                              "budgets": cfg.intervention.budgets, "ranks": cfg.intervention.ranks,
                              "subspace": cfg.intervention.subspace, "pca_pool": cfg.intervention.pca_pool}
-        if cfg.intervention.measure_forcing:
-            summary["forcing"] = forcing_curves(cfg, runner, pairs, methods, stack, log)
+        if forcing is not None:
+            summary["forcing"] = forcing
         os.makedirs(out_dir, exist_ok=True)
         atomic_write_text(os.path.join(out_dir, "sweep_cells.jsonl"),
                           "".join(json.dumps(r) + "\n" for r in allres))
@@ -113,7 +133,52 @@ def run_sweep(cfg: Config, out_dir: str, methods: Sequence[str] = METHODS, info:
     return summary
 
 
-def forcing_curves(cfg: Config, runner: SweepRunner, pairs, methods: Sequence[str], stack, log=print) -> Dict:
+def pair_owners(n_pairs: int, dp: int) -> List[List[int]]:
+    """Pairs of each DP group: contiguous blocks balanced to within one pair (every pair has the same cell
+    count, so cell counts balance to within one pair's cells).  Contiguous keeps a word's prompts together,
+    which keeps the per-word pooled inputs mostly rank-local."""
+    q, r = divmod(n_pairs, dp)
+    out, s = [], 0
+    for g in range(dp):
+        n = q + (1 if g < r else 0)
+        out.append(list(range(s, s + n)))
+        s += n
+    return out
+
+
+_SHARED_FIELDS = ("resp", "p_secret", "spikes_rel", "top_ids", "nll", "gen_toks", "tok_nll", "track_probs")
+
+
+def share_baselines(pairs, owned: Sequence[int], info: D.DistInfo, dev) -> None:
+    """All-gather the owned pairs' baseline results (responses, lens probabilities, spikes, NLLs and the kept
+    hooked-layer residuals, which the pooled subspaces / calibration / scores read) and fill them into the
+    pairs other groups own.  TP peers send identical copies; the first one wins."""
+    local = {}
+    for i in owned:
+        p = pairs[i]
+        rec = {f: getattr(p, f) for f in _SHARED_FIELDS}
+        rec["resid"] = p.resid.detach().cpu() if p.resid is not None else None
+        pre = getattr(p, "resid_pre", None)
+        rec["resid_pre"] = pre.detach().cpu() if pre is not None else None
+        local[i] = rec
+    got: Dict[int, dict] = {}
+    for part in D.all_gather_objects(local, info):
+        for k, v in part.items():
+            got.setdefault(k, v)
+    mine = set(owned)
+    for i, rec in got.items():
+        if i in mine:
+            continue
+        p = pairs[i]
+        for f in _SHARED_FIELDS:
+            setattr(p, f, rec[f])
+        p.resid = rec["resid"].to(dev) if rec["resid"] is not None else None
+        if rec["resid_pre"] is not None:
+            p.resid_pre = rec["resid_pre"].to(dev)
+
+
+def forcing_curves(cfg: Config, runner: SweepRunner, pairs, methods: Sequence[str], stack, log=print,
+                   dp=None) -> Dict:
     """Post-edit token forcing (EP:100-104, 132-138): per (method, budget), the postgame forcing success
     under the edit applied at every position, vs the unedited model — the "inhibition" axis of the
     content-vs-inhibition analysis (EP:160, fig3).  All settings × words × phrases run batched."""
@@ -136,7 +201,7 @@ def forcing_curves(cfg: Config, runner: SweepRunner, pairs, methods: Sequence[st
                     continue
                 for m in iv.budgets:
                     tl = word_targeted_latents(runner, w, m)
-                    trials = 1 if meth == "sae_targeted" else max(1, min(iv.random_trials, 3))
+                    trials = 1 if meth == "sae_targeted" else max(1, iv.forcing_trials or iv.random_trials)
                     for t in range(trials):
                         lat = tl if meth == "sae_targeted" else A.random_latents(
                             runner.sae.d_sae, m, A.cell_seed("forcing", w, meth, m, t), exclude=tl, pool=pool)
@@ -145,13 +210,13 @@ def forcing_curves(cfg: Config, runner: SweepRunner, pairs, methods: Sequence[st
             else:
                 key = w if iv.pca_pool == "word" else "__all__"
                 for r in iv.ranks:
-                    trials = 1 if meth == "proj_targeted" else max(1, min(iv.proj_random_trials, 3))
+                    trials = 1 if meth == "proj_targeted" else max(1, iv.forcing_trials or iv.proj_random_trials)
                     for t in range(trials):
                         U = bases[key][:r] if meth == "proj_targeted" and key in bases else \
                             A.random_subspace(runner.D, r, A.cell_seed("forcing", w, meth, r, t))
                         settings.append({"word": w, "kind": "proj", "basis": U.to(runner.dev)})
                         keys.append((meth, r))
-    res = run_forcing_settings(cfg, stack.model, stack.tok, settings, "postgame", stack.sae, stack.layer)
+    res = run_forcing_settings(cfg, stack.model, stack.tok, settings, "postgame", stack.sae, stack.layer, dp=dp)
     base = float(np.mean([r["success_rate"] for r, k in zip(res, keys) if k[0] == "none"]))
     groups: Dict = {}
     for r, k in zip(res, keys):

@@ -215,6 +215,11 @@ class SweepRunner:
             self.capture = CaptureHook(self.store)
             self._plan = None
             self.pair_kv = None
+            # a regrown generator has a fresh (zero) pair-KV store: no earlier baseline can be resumed from it
+            for p in self._kv_pair.values():
+                p.lens_cum = None
+            self._kv_owner.clear()
+            self._kv_pair.clear()
             if self.prefix_share:
                 c = self.gen.cache
                 shape = (c.k.shape[0], self.kv_pairs) + tuple(c.k.shape[2:])
@@ -236,10 +241,12 @@ class SweepRunner:
 
     # -------------------------------------------------------------- baseline
     @torch.no_grad()
-    def run_baselines(self, pairs: List[Pair]) -> None:
-        """Standalone baseline pass (generation + lens + spikes + scores + NLL) for ``pairs``."""
+    def run_baselines(self, pairs: List[Pair], size_for: Sequence[Pair] = ()) -> None:
+        """Standalone baseline pass (generation + lens + spikes + scores + NLL) for ``pairs``.  ``size_for``: more
+        pairs whose cells will run later (the generator is sized for them now, so it is not regrown — which
+        drops the pair-KV store — when they come)."""
         t0 = time.perf_counter()
-        self._ensure_gen(self._S_needed(pairs))
+        self._ensure_gen(self._S_needed(list(pairs) + list(size_for)))
         for c0 in range(0, len(pairs), self.B):
             self.run_cells(pairs, [], ride_along=pairs[c0:c0 + self.B])
         self.timings["baseline_total"] = time.perf_counter() - t0
@@ -412,6 +419,20 @@ class SweepRunner:
         mode = self.iv.subspace
         if mode not in ("pca", "grad_lens", "grad_model"):
             raise ValueError(f"intervention.subspace must be pca, grad_lens or grad_model, not {mode!r}")
+        # the bases depend only on the pairs' kept baseline residuals (identity-keyed: a re-run baseline makes a
+        # new tensor) and the subspace settings; run_sweep passes every pair on every chunk and the staged plan
+        # asks again, so the gradient forward/backward passes run once per pair set
+        ckey = (mode, self.iv.pca_pool, rmax, tuple((id(p), id(p.resid), tuple(p.spikes_rel or ())) for p in pairs))
+        cache = getattr(self, "_bases_cache", None)
+        if cache is not None and cache[0] == ckey:
+            return cache[1]
+        out = self._bases_compute(pairs, mode, rmax)
+        self._bases_cache = (ckey, out, [p.resid for p in pairs])   # refs held: the ids cannot be reused
+        return out
+
+    def _bases_compute(self, pairs: Sequence[Pair], mode: str, rmax: int) -> Dict[str, torch.Tensor]:
+        from ..interp import gradient as GR
+
         groups: Dict[str, List[torch.Tensor]] = {}
         for p in pairs:
             if p.resid is None or not p.spikes_rel:
@@ -594,6 +615,8 @@ class SweepRunner:
     def _launch_staged_next(self) -> None:
         nb = getattr(self, "_next", None)
         self._next = None
+        if nb is not None and nb.cells is not None and nb.cells is getattr(self, "_running_cells", None):
+            nb = None                            # announced batch is the one running now: nothing to stage
         # carried decode rows move out of the cell slots before the next tail writes them (stream order)
         mv = self._carry_move_pending
         self._carry_move_pending = None
@@ -667,6 +690,7 @@ class SweepRunner:
         measure_nll = self.iv.measure_nll if measure_nll is None else measure_nll
         self._drain = drain
         self._pre_plan = plan
+        self._running_cells = cells
         ride = list(ride_along)
         if not cells and not ride:
             return []
@@ -1072,7 +1096,13 @@ class SweepRunner:
         # the carry move runs after the readout has read the finished carried cells' store rows, and before
         # a staged next tail overwrites the cell slots (_launch_staged_next runs it at that point)
         self._carry_move_pending = carry_move
-        results = self._resume_readout(entries, out) if entries else []
+        if entries:
+            results = self._resume_readout(entries, out)
+        else:
+            # nothing to read out (every cell carried on): still launch the announced next batch now, so a
+            # stale announcement is never staged during a later readout
+            results = []
+            self._launch_staged_next()
         if self._carry_move_pending is not None:
             self._carry_move_pending()
             self._carry_move_pending = None
@@ -1089,7 +1119,10 @@ class SweepRunner:
         baselines (the first ``n_ride`` rows) each get their own.  ``rows[i]`` (cell rows in decode order): the
         divergent token of a new row, or the carry record of a carried one."""
         n = len(rows)
-        if not self.trie_decode or n < 2 or self.gen.kv_prefix is None:
+        kp = self.gen.kv_prefix
+        # the cascade attention (TB_ATTN_CASCADE=1, kv_prefix.chunks) reads each row's prefix in chunks the
+        # shared-prefix decode cannot fan out: plain decode then
+        if not self.trie_decode or n < 2 or kp is None or getattr(kp, "chunks", None) is not None:
             return None
         wk = max([1] + [len(cr.prefix) - cr.d for cr in rows if isinstance(cr, _Carry)])
         mat = np.full((n, 3 + wk), -2, np.int64)

@@ -31,6 +31,30 @@ from ..runtime.generation import Generator
 _WORD = re.compile(r"[A-Za-z']+")
 
 
+class DPShard:
+    """Data-parallel placement of forcing work: this rank's DP group index and the group count (TP ranks of
+    one group run the same rows, so every TP all-reduce inside the forward has all its peers), plus the
+    ``DistInfo`` for gathering the per-item results back to every rank."""
+
+    def __init__(self, rank: int = 0, size: int = 1, info=None):
+        self.rank, self.size, self.info = rank, size, info
+
+    def mine(self, n: int) -> List[int]:
+        return list(range(self.rank, n, self.size))
+
+    def gather(self, local: Dict[int, object]) -> Dict[int, object]:
+        """Union of every rank's ``{item index: result}`` (TP duplicates agree; the lowest rank's copy wins)."""
+        if self.size <= 1 or self.info is None:
+            return dict(local)
+        from ..parallel import dist as D
+
+        out: Dict[int, object] = {}
+        for part in D.all_gather_objects(local, self.info):
+            for k, v in part.items():
+                out.setdefault(k, v)
+        return out
+
+
 def first_word(text: str) -> str:
     m = _WORD.search(text)
     return m.group(0).lower() if m else ""
@@ -60,41 +84,53 @@ def _generate(model, rows: List[List[int]], max_new: int, hooks, batch: Optional
 
 @torch.no_grad()
 def run_forcing(cfg: Config, model, tok, words: Sequence[str], mode: str = "postgame", sae=None,
-                layer: Optional[int] = None, edit: Optional[Dict] = None) -> Dict:
-    """Returns ``{"metrics": reference-layout metrics, "rows": per (word, phrase) records}``."""
+                layer: Optional[int] = None, edit: Optional[Dict] = None, dp: Optional[DPShard] = None) -> Dict:
+    """Returns ``{"metrics": reference-layout metrics, "rows": per (word, phrase) records}``.
+
+    ``dp``: the (word, phrase) rows are sharded round-robin over the data-parallel groups (each group also
+    generates the warm-up turns of the words it holds rows of) and the records are gathered back, so every
+    rank returns the full result."""
     tf = cfg.token_forcing
     layer = cfg.model.layer_idx if layer is None else layer
     dev = model.device
     phrases = list(tf.phrases) if mode != "naive" else list(tf.naive_prompts)
+    dp = dp or DPShard()
+    all_keys = [(w, ph) for w in words for ph in phrases]
+    mine = dp.mine(len(all_keys))
+    my_words = [w for w in words if any(all_keys[i][0] == w for i in mine)]
     records: List[Dict] = []
-    histories: Dict[str, List[Dict[str, str]]] = {w: [] for w in words}
-    if mode == "postgame":
+    histories: Dict[str, List[Dict[str, str]]] = {w: [] for w in my_words}
+    if mode == "postgame" and my_words:
         # warm-up turns, batched across words (each turn depends on the previous one)
         for turn in tf.warmup_turns:
             rows = []
-            for w in words:
+            for w in my_words:
                 histories[w].append({"role": "user", "content": turn})
                 rows.append(conversation_ids(tok, histories[w], add_generation_prompt=True))
             hooks = _hooks_for(len(rows), layer, sae, edit, dev)
             replies = _generate(model, rows, tf.warmup_max_new_tokens, hooks)
-            for w, r in zip(words, replies):
+            for w, r in zip(my_words, replies):
                 histories[w].append({"role": "assistant", "content": tok.decode(r)})
-    rows, keys = [], []
-    for w in words:
-        for ph in phrases:
-            if mode == "pregame":
-                ids = pregame_ids(tok, ph)
-            elif mode == "postgame":
-                hist = histories[w] + [{"role": "user", "content": tf.postgame_question}]
-                ids = conversation_ids(tok, hist, add_generation_prompt=True, prefill=ph)
-            else:   # naive prompting
-                ids = conversation_ids(tok, [{"role": "user", "content": ph}], add_generation_prompt=True)
-            rows.append(ids)
-            keys.append((w, ph))
-    hooks = _hooks_for(len(rows), layer, sae, edit, dev)
-    comps = _generate(model, rows, tf.max_new_tokens if mode != "naive" else cfg.experiment.max_new_tokens, hooks)
+    rows = []
+    for i in mine:
+        w, ph = all_keys[i]
+        if mode == "pregame":
+            ids = pregame_ids(tok, ph)
+        elif mode == "postgame":
+            hist = histories[w] + [{"role": "user", "content": tf.postgame_question}]
+            ids = conversation_ids(tok, hist, add_generation_prompt=True, prefill=ph)
+        else:   # naive prompting
+            ids = conversation_ids(tok, [{"role": "user", "content": ph}], add_generation_prompt=True)
+        rows.append(ids)
+    comps_mine = []
+    if rows:
+        hooks = _hooks_for(len(rows), layer, sae, edit, dev)
+        comps_mine = _generate(model, rows, tf.max_new_tokens if mode != "naive" else cfg.experiment.max_new_tokens,
+                               hooks)
+    got = dp.gather({i: c for i, c in zip(mine, comps_mine)})
     preds: Dict[str, List[List[str]]] = {w: [] for w in words}
-    for (w, ph), c in zip(keys, comps):
+    for i, (w, ph) in enumerate(all_keys):
+        c = got[i]
         text = tok.decode(c)
         forms = cfg.word_plurals.get(w, [w])
         ok = contains_secret(text, forms)
@@ -137,13 +173,25 @@ def _chunk_hooks(layer: int, sae, settings: Sequence[Dict], row_setting: Sequenc
 
 @torch.no_grad()
 def run_forcing_settings(cfg: Config, model, tok, settings: Sequence[Dict], mode: str = "postgame", sae=None,
-                         layer: Optional[int] = None, chunk_rows: int = 512) -> List[Dict]:
+                         layer: Optional[int] = None, chunk_rows: int = 512, dp: Optional[DPShard] = None) -> List[Dict]:
     """Token forcing under many interventions at once (EP:100-104, 132-138: does the secret still come out
     under forcing after an ablation?  The "inhibition" axis of the content-vs-inhibition analysis, EP:160).
 
     ``settings[i] = {"word", "kind": none|sae|proj, "latents" | "basis", ...}``; every (setting, phrase) is
     one row of a batched greedy generation with its own edit at every position (postgame: the warm-up
-    turns are generated under the same edit).  Returns per setting ``{"success_rate", "successes", "n"}``."""
+    turns are generated under the same edit).  Returns per setting ``{"success_rate", "successes", "n"}``.
+
+    ``dp``: whole settings (warm-up turns + phrases) are sharded round-robin over the data-parallel groups,
+    every TP rank of a group runs its group's settings, and the per-setting results are gathered to every rank."""
+    dp = dp or DPShard()
+    if dp.size > 1:
+        mine = dp.mine(len(settings))
+        local = run_forcing_settings(cfg, model, tok, [settings[i] for i in mine], mode, sae, layer, chunk_rows) \
+            if mine else []
+        got = dp.gather({i: r for i, r in zip(mine, local)})
+        return [got[i] for i in range(len(settings))]
+    if not settings:
+        return []
     tf = cfg.token_forcing
     layer = cfg.model.layer_idx if layer is None else layer
     dev = model.device
