@@ -52,6 +52,7 @@ from taboo_brittleness_amd.models.tokenizer import SyntheticTokenizer  # noqa: E
 from taboo_brittleness_amd.models.weights import random_gemma2  # noqa: E402
 from taboo_brittleness_amd.parallel import dist as D  # noqa: E402
 from taboo_brittleness_amd.pipelines.sweep import NextBatch, Pair, SweepRunner  # noqa: E402
+from taboo_brittleness_amd.runtime import gemm_dispatch as GD  # noqa: E402
 from taboo_brittleness_amd.runtime.tuning import enable_tuned_gemms, flush_tuned_gemms  # noqa: E402
 
 BASELINE_VALUE = 0.642   # measured HF-eager sweep cells/sec on 1x MI355X (tools/hf_eager_baseline.py)
@@ -123,8 +124,12 @@ def main() -> None:
                          "(diverged_frac 0); 32 gives text-like outputs (~34 distinct tokens per 50) and "
                          "edits that change ~2/3 of the generations")
     ap.add_argument("--fused-geglu", action="store_true",
-                    help="gate|up GEMM with the GeGLU in its epilogue (ping-pong MFMA kernel, csrc/gemm.hip) "
-                         "instead of hipBLASLt + the GeGLU kernel")
+                    help="(default now) the gate|up GEMM with the GeGLU in its epilogue is available; the GEMM "
+                         "dispatch table picks it or hipBLASLt + the GeGLU kernel per row count")
+    ap.add_argument("--no-fused-geglu", action="store_true", help="never the fused gate|up + GeGLU kernel")
+    ap.add_argument("--gemm", default=None, choices=["auto", "tb", "blas"],
+                    help="GEMM dispatch (runtime/gemm_dispatch.py): auto = measured per-shape table (default), "
+                         "tb = in-tree MFMA kernels only (batch-invariant), blas = hipBLASLt only")
     ap.add_argument("--fused-head", action="store_true",
                     help="vocab head as the fused MFMA GEMM head (softcap / log-sum-exp / argmax in the GEMM epilogue, "
                          "no logits in HBM) instead of hipBLASLt logits + the decode_head kernel (default since it "
@@ -164,7 +169,11 @@ def main() -> None:
         enable_tuned_gemms(tag, tune=args.tune_gemms)
     weights = random_gemma2(spec, device=dev, dtype=torch.bfloat16, seed=1234, post_norm_gain=args.init_gain)
     model = Gemma2Model(weights, dev)
-    fused_geglu = bool(args.fused_geglu and model.enable_fused_geglu())
+    if args.gemm:
+        GD.set_mode(args.gemm)
+    if args.no_fused_geglu:
+        model._wgu_il = None
+    fused_geglu = model._wgu_il is not None
     if args.fused_head:
         model.fused_head = bool(on_gpu and spec.vocab_size % 256 == 0)
     elif args.no_fused_head:
@@ -354,6 +363,7 @@ def main() -> None:
                 "baseline_every": E,
                 "carry_rows": C,
                 "fused_geglu": fused_geglu,
+                "gemm_dispatch": GD.describe(),
                 "fused_head": bool(getattr(model, "fused_head", False)),
                 "trie_decode": runner.trie_decode,
                 "skip_noop_spikes": runner.skip_noop_spikes,

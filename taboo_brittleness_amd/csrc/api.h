@@ -61,7 +61,7 @@ void tb_gemm_skinny(const uint16_t* A, const uint16_t* W, uint16_t* C, int M, in
 // sae.hip
 bool tb_gemm_pp_ok(int M, int N, int K);
 void tb_gemm_pp(const uint16_t* A, const uint16_t* W, void* C, const float* bias, const float* thr, int M, int N,
-                int K, int ldc, int epi, hipStream_t st);
+                int K, int ldc, int epi, int tile_rows, hipStream_t st);
 // vocab head on the ping-pong GEMM: part [M, N/128] float4 workspace; tgt/tgt_logit[M]/nll_tgt all set or all null
 void tb_head_fused(const uint16_t* A, const uint16_t* W, float* part, const uint16_t* ctab, const int32_t* tgt,
                    float* tgt_logit, int32_t* nxt, float* nll_self, float* nll_tgt, int M, int N, int K,

@@ -384,12 +384,13 @@ void gemm_nt(torch::Tensor A, torch::Tensor W, torch::Tensor C, c10::optional<to
   tb_gemm_nt(cbf(A), cbf(W), C.data_ptr(), optf(bias), optf(thr), M, N, K, N, (int)epi, cur_stream());
 }
 
-// Ping-pong 256x256x64 MFMA GEMM (gemm.hip).  epi 0: bf16 C[M,N]; 1: f32 C; 2: JumpReLU f32 C
+// Ping-pong 256x256x64 (tile_rows = 128: 128x256x64) MFMA GEMM (gemm.hip).  epi 0: bf16 C[M,N]; 1: f32 C; 2: JumpReLU f32 C
 // (bias/thr [N]); 3: GeGLU bf16 C[M,N/2] from gate|up rows interleaved by gemm_pp_geglu_order().
 void gemm_pp(torch::Tensor A, torch::Tensor W, torch::Tensor C, c10::optional<torch::Tensor> bias,
-             c10::optional<torch::Tensor> thr, int64_t epi) {
+             c10::optional<torch::Tensor> thr, int64_t epi, int64_t tile_rows) {
   IN_BF16(A); IN_BF16(W); CHECK_DEV(C); CHECK_CONTIG(C);
   TORCH_CHECK(W.dim() == 2, "gemm_pp: W must be [N, K]");
+  TORCH_CHECK(tile_rows == 256 || tile_rows == 128, "gemm_pp: tile_rows must be 256 or 128");
   const int K = A.size(-1), M = A.numel() / K, N = W.size(0);
   TORCH_CHECK(W.size(1) == K, "gemm_pp: K mismatch");
   TORCH_CHECK(tb_gemm_pp_ok(M, N, K), "gemm_pp: need N % 256 == 0, K % 64 == 0, K >= 64");
@@ -403,7 +404,7 @@ void gemm_pp(torch::Tensor A, torch::Tensor W, torch::Tensor C, c10::optional<to
   }
   c10::DeviceGuard g(A.device());
   tb_gemm_pp(cbf(A), cbf(W), C.data_ptr(), epi == 2 ? optf(bias) : nullptr, epi == 2 ? optf(thr) : nullptr, M, N, K,
-             (int)ncols, (int)epi, cur_stream());
+             (int)ncols, (int)epi, (int)tile_rows, cur_stream());
 }
 
 bool gemm_pp_ok(int64_t M, int64_t N, int64_t K) { return tb_gemm_pp_ok(M, N, K); }

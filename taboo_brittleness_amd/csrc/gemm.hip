@@ -30,7 +30,7 @@
 
 namespace {
 
-constexpr int PBM = 256, PBN = 256, PBK = 64, PTHREADS = 512;
+constexpr int PBN = 256, PBK = 64, PTHREADS = 512;
 constexpr int PHALF = 128 * PBK * 2;   // bytes of one half-tile image (128 rows x 64 bf16)
 constexpr int PSTAGE = 4 * PHALF;      // A0 A1 B0 B1
 #ifndef PP_GROUP_M
@@ -79,14 +79,24 @@ enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_JUMPRELU = 2, EPI_GEGLU = 3, EPI_HEAD = 4,
 constexpr int HEAD_COLS = 128;          // vocab columns per head partial (one wave group's half of a tile)
 constexpr int CTAB_N = 32768;           // entries of the exact bf16 softcap table (lens.hip)
 
-template <int EPI>
+// QROWS = output rows (m) per tile: 256, or 128 for grids that would otherwise leave CUs idle (the N = 3584
+// projections at moderate M).  Every variant accumulates each output element over K in the same order with
+// the same MFMA (16x16x32, 32-deep steps in K order), so C does not depend on the tile shape or on M: a row
+// gets bit-identical results whatever batch it runs in (batch invariance, tests/test_engine_gpu.py).
+template <int EPI, int QROWS>
 __global__ void __launch_bounds__(PTHREADS, 1)
 gemm_pp_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, void* __restrict__ C,
                const float* __restrict__ bias, const float* __restrict__ thr, int M, int N, int K, int ldc,
                const uint16_t* __restrict__ ctab, const int32_t* __restrict__ tgt, float* __restrict__ tgt_logit,
                float4* __restrict__ lpart) {
+  static_assert(QROWS == 256 || QROWS == 128, "tile rows");
+  static_assert(QROWS == 256 || !PP_MFMA32, "32x32 MFMA lab build: 256-row tiles only");
+  constexpr int QW = QROWS / 4;          // output rows per wave (64 | 32)
+  constexpr int QJ = QW / 2;             // of them per Q half-image (32 | 16)
+  constexpr int NJ = QJ / 16;            // 16-row MFMA blocks per half (2 | 1)
+  constexpr int QL = QROWS / 128;        // glds per thread per Q half-image (2 | 1)
   __shared__ __attribute__((aligned(1024))) char smem[2 * PSTAGE];
-  const int nbn = N / PBN, nbm = (M + PBM - 1) / PBM, nwg = nbn * nbm;
+  const int nbn = N / PBN, nbm = (M + QROWS - 1) / QROWS, nwg = nbn * nbm;
   int bid = blockIdx.x;
   {
     const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
@@ -95,7 +105,7 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, v
   const int per_group = PGROUP_M * nbn, first_bm = (bid / per_group) * PGROUP_M;
   const int gsz = min(nbm - first_bm, PGROUP_M), lid = bid % per_group;
   const int bm = first_bm + lid % gsz, bn = lid / gsz;
-  const int m0 = bm * PBM, n0 = bn * PBN;
+  const int m0 = bm * QROWS, n0 = bn * PBN;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -107,19 +117,22 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, v
   // This thread fills image rows r_s = 8*(2*wid+s) + lane/8 (s = 0, 1) at physical 16-B chunk lane%8,
   // which holds logical chunk (lane%8) ^ ((r_s>>1)&7) of that row.
   //   P-half h, image row i  ->  tile row (i>>6)*128 + h*64 + (i&63)   (wave group g reads rows g*64..)
-  //   Q-half h, image row i  ->  tile col (i>>5)*64 + h*32 + (i&31)    (wave wc reads rows wc*32..)
+  //   Q-half h, image row i  ->  tile col (i/QJ)*QW + h*QJ + (i%QJ) (wave wc reads rows wc*QJ..)
+  // (a 128-row tile's Q images are 64 rows: one glds per thread, rows 8*wid + lane/8)
   const uint16_t* sp[2][2];   // [half][s]
   const uint16_t* sq[2][2];
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     const int r = 8 * (2 * wid + s) + (lane >> 3);
     const int c = (lane & 7) ^ ((r >> 1) & 7);
+    const int rq = QL == 2 ? r : 8 * wid + (lane >> 3);
+    const int cq = (lane & 7) ^ ((rq >> 1) & 7);
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int wn = n0 + (r >> 6) * 128 + h * 64 + (r & 63);
       sp[h][s] = W + (size_t)wn * K + c * 8;
-      const int am = min(m0 + (r >> 5) * 64 + h * 32 + (r & 31), M - 1);
-      sq[h][s] = A + (size_t)am * K + c * 8;
+      const int am = min(m0 + (rq / QJ) * QW + h * QJ + (rq % QJ), M - 1);
+      sq[h][s] = A + (size_t)am * K + cq * 8;
     }
   }
   char* const dst0 = smem + wid * 2048;   // + stage*PSTAGE + image*PHALF (+1024 for s = 1)
@@ -146,9 +159,9 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, v
 #else
   const int co0 = (((lane >> 4)) ^ xr) << 4, co1 = ((4 + (lane >> 4)) ^ xr) << 4;
   const int offp = (grp * 64 + (lane & 15)) * 128;
-  const int offq = (wc * 32 + (lane & 15)) * 128;
+  const int offq = (wc * QJ + (lane & 15)) * 128;
 
-  f32x4 acc[2][2][4][2];
+  f32x4 acc[2][2][4][NJ];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -156,17 +169,21 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, v
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[a][b][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < NJ; ++j) acc[a][b][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  bf16x8 pf[4][2], qf0[2][2], qf1[2][2];
+  bf16x8 pf[4][2], qf0[NJ][2], qf1[NJ][2];
 #endif
 
   // images: 0 = P0, 1 = P1, 2 = Q0, 3 = Q1
 #define PP_STAGE(stg, img, SRC, k0)                                         \
   do {                                                                      \
     char* d_ = dst0 + (stg) * PSTAGE + (img) * PHALF;                       \
-    glds16(SRC[0] + (k0), d_);                                              \
-    glds16(SRC[1] + (k0), d_ + 1024);                                       \
+    if ((img) < 2 || QL == 2) {                                             \
+      glds16(SRC[0] + (k0), d_);                                            \
+      glds16(SRC[1] + (k0), d_ + 1024);                                     \
+    } else {                                                                \
+      glds16(SRC[0] + (k0), smem + (stg) * PSTAGE + (img) * PHALF + wid * 1024); \
+    }                                                                       \
   } while (0)
 #if PP_MFMA32
 #define PP_READ_P(sb, qm)                                                   \
@@ -193,7 +210,7 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, v
     pf[i][1] = lds8(p_ + co1);                                              \
   }
 #define PP_READ_Q(sb, qn, dstf)                                             \
-  _Pragma("unroll") for (int j = 0; j < 2; ++j) {                           \
+  _Pragma("unroll") for (int j = 0; j < NJ; ++j) {                          \
     const char* p_ = (sb) + (2 + (qn)) * PHALF + offq + j * 2048;           \
     dstf[j][0] = lds8(p_ + co0);                                            \
     dstf[j][1] = lds8(p_ + co1);                                            \
@@ -202,11 +219,16 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, v
   if (PP_SETPRIO) __builtin_amdgcn_s_setprio(1);                            \
   _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                          \
   _Pragma("unroll") for (int i = 0; i < 4; ++i)                             \
-  _Pragma("unroll") for (int j = 0; j < 2; ++j)                             \
+  _Pragma("unroll") for (int j = 0; j < NJ; ++j)                            \
     acc[qm][qn][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf[i][ks], qfr[j][ks], acc[qm][qn][i][j], 0, 0, 0); \
   if (PP_SETPRIO) __builtin_amdgcn_s_setprio(0);
 #endif
 #define PP_VMCNT(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
+  // counted waits: after staging in phase q the loads of phases q-2..q stay in flight (P images: 2 glds per
+  // thread, Q images: QL): after a P stage 2P + Q, after a Q stage P + 2Q, phase 3 without a stage P + Q
+#define PP_VM_AFTER_P() do { if constexpr (QL == 2) PP_VMCNT(6); else PP_VMCNT(5); } while (0)
+#define PP_VM_AFTER_Q() do { if constexpr (QL == 2) PP_VMCNT(6); else PP_VMCNT(4); } while (0)
+#define PP_VM_TAIL() do { if constexpr (QL == 2) PP_VMCNT(4); else PP_VMCNT(3); } while (0)
 
   // Staging schedule (every image >= 4 phases ahead of its first read; each phase stages one image):
   //   phase 0: P0 of K-tile t+1   phase 1: Q1 of t+1   phase 2: P1 of t+1   phase 3: Q0 of t+2
@@ -231,31 +253,32 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, v
     // phase 0: quadrant (0,0) -- read P0 + Q0
     PP_READ_P(sb, 0);
     PP_READ_Q(sb, 0, qf0);
-    if (more) { PP_STAGE(ns, 0, sp[0], kn); PP_VMCNT(6); } else { PP_VMCNT(0); }
+    if (more) { PP_STAGE(ns, 0, sp[0], kn); PP_VM_AFTER_P(); } else { PP_VMCNT(0); }
     bar();
     PP_MFMA(0, 0, qf0);
     bar();
     // phase 1: quadrant (0,1) -- read Q1
     PP_READ_Q(sb, 1, qf1);
-    if (more) { PP_STAGE(ns, 3, sq[1], kn); PP_VMCNT(6); } else { PP_VMCNT(0); }
+    if (more) { PP_STAGE(ns, 3, sq[1], kn); PP_VM_AFTER_Q(); } else { PP_VMCNT(0); }
     bar();
     PP_MFMA(0, 1, qf1);
     bar();
     // phase 2: quadrant (1,1) -- read P1
     PP_READ_P(sb, 1);
-    if (more) { PP_STAGE(ns, 1, sp[1], kn); PP_VMCNT(6); } else { PP_VMCNT(0); }
+    if (more) { PP_STAGE(ns, 1, sp[1], kn); PP_VM_AFTER_P(); } else { PP_VMCNT(0); }
     bar();
     PP_MFMA(1, 1, qf1);
     bar();
     // phase 3: quadrant (1,0) -- no reads (P1 and Q0 are in registers)
-    if (t + 2 < nk) { PP_STAGE(t & 1, 2, sq[0], kn + PBK); PP_VMCNT(6); }
-    else if (more) { PP_VMCNT(4); }
+    if (t + 2 < nk) { PP_STAGE(t & 1, 2, sq[0], kn + PBK); PP_VM_AFTER_Q(); }
+    else if (more) { PP_VM_TAIL(); }
     else { PP_VMCNT(0); }
     bar();
     PP_MFMA(1, 0, qf0);
     bar();
   }
 #else
+  static_assert(QROWS == 256, "two-phase lab schedule: 256-row tiles only");
   // Two phases per K-tile (two quadrants = 32 MFMAs per wave each, 4 barriers per K-tile):
   //   phase 0: quadrants (0,0) (0,1), reads P0 Q0 Q1, stages P0 Q0 Q1 of K-tile t+1, then vmcnt(6)
   //   phase 1: quadrants (1,1) (1,0), reads P1,       stages P1 of t+1,          then vmcnt(2)
@@ -304,6 +327,9 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, v
 #undef PP_READ_Q
 #undef PP_MFMA
 #undef PP_VMCNT
+#undef PP_VM_AFTER_P
+#undef PP_VM_AFTER_Q
+#undef PP_VM_TAIL
 
   // ---- epilogue.  Every lane holds, per (qm, qn), accumulator groups of 4 consecutive output columns n of one
   // output row m:  E_M(qn, rj) is the row, E_N(qm, g) the first column of group g, E_V(...) its r-th value.
@@ -317,8 +343,8 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, v
 #define E_N(qm, g) (n0 + grp * 128 + (qm) * 64 + ((g) >> 2) * 32 + 8 * ((g) & 3) + 4 * (lane >> 5))
 #define E_V(qm, qn, rj, g, r) acc[qm][qn][(g) >> 2][4 * ((g) & 3) + (r)]
 #else
-  constexpr int E_RJ = 2, E_G = 4, E_LO = 16;
-#define E_M(qn, rj) (m0 + wc * 64 + (qn) * 32 + (rj) * 16 + (lane & 15))
+  constexpr int E_RJ = NJ, E_G = 4, E_LO = 16;
+#define E_M(qn, rj) (m0 + wc * QW + (qn) * QJ + (rj) * 16 + (lane & 15))
 #define E_N(qm, g) (n0 + grp * 128 + (qm) * 64 + (g) * 16 + 4 * (lane >> 4))
 #define E_V(qm, qn, rj, g, r) acc[qm][qn][g][rj][r]
 #endif
@@ -454,18 +480,28 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, v
 
 bool tb_gemm_pp_ok(int M, int N, int K) { return M > 0 && N > 0 && N % PBN == 0 && K >= PBK && K % PBK == 0; }
 
-#define PP_LAUNCH(E_)                                                                                          \
-  hipLaunchKernelGGL(gemm_pp_kernel<E_>, dim3(nwg), dim3(PTHREADS), 0, st, A, W, C, bias, thr, M, N, K, ldc, \
-                     ctab, tgt, tgt_logit, lpart)
+#define PP_LAUNCH_T(E_, Q_)                                                                                        \
+  hipLaunchKernelGGL((gemm_pp_kernel<E_, Q_>), dim3((N / PBN) * ((M + (Q_) - 1) / (Q_))), dim3(PTHREADS), 0, st, A, W, \
+                     C, bias, thr, M, N, K, ldc, ctab, tgt, tgt_logit, lpart)
+#define PP_LAUNCH(E_) PP_LAUNCH_T(E_, 256)
 
+// tile_rows: 256 or 128 (output rows per tile; identical numerics, see gemm_pp_kernel)
 void tb_gemm_pp(const uint16_t* A, const uint16_t* W, void* C, const float* bias, const float* thr, int M, int N,
-                int K, int ldc, int epi, hipStream_t st) {
+                int K, int ldc, int epi, int tile_rows, hipStream_t st) {
   if (M <= 0 || N <= 0) return;
-  const int nwg = (N / PBN) * ((M + PBM - 1) / PBM);
   const uint16_t* ctab = nullptr;
   const int32_t* tgt = nullptr;
   float* tgt_logit = nullptr;
   float4* lpart = nullptr;
+  if (tile_rows == 128) {
+    switch (epi) {
+      case EPI_BF16: PP_LAUNCH_T(EPI_BF16, 128); break;
+      case EPI_F32: PP_LAUNCH_T(EPI_F32, 128); break;
+      case EPI_JUMPRELU: PP_LAUNCH_T(EPI_JUMPRELU, 128); break;
+      default: PP_LAUNCH_T(EPI_GEGLU, 128);
+    }
+    return;
+  }
   switch (epi) {
     case EPI_BF16: PP_LAUNCH(EPI_BF16); break;
     case EPI_F32: PP_LAUNCH(EPI_F32); break;
@@ -527,7 +563,6 @@ void tb_head_fused(const uint16_t* A, const uint16_t* W, float* part, const uint
                    float* tgt_logit, int32_t* nxt, float* nll_self, float* nll_tgt, int M, int N, int K,
                    hipStream_t st) {
   if (M <= 0) return;
-  const int nwg = (N / PBN) * ((M + PBM - 1) / PBM);
   const float* bias = nullptr;
   const float* thr = nullptr;
   void* C = part;
@@ -541,7 +576,6 @@ void tb_head_fused(const uint16_t* A, const uint16_t* W, float* part, const uint
 void tb_lens_gemm(const uint16_t* A, const uint16_t* W, uint16_t* logits, float* part, float* lse, int M, int N, int K,
                   hipStream_t st) {
   if (M <= 0) return;
-  const int nwg = (N / PBN) * ((M + PBM - 1) / PBM);
   const float* bias = nullptr;
   const float* thr = nullptr;
   void* C = logits;

@@ -168,7 +168,9 @@ class Gemma2Model:
         # gate|up GEMM with the GeGLU in its epilogue (csrc/gemm.hip): per-layer gate|up weights in the
         # kernel's interleaved row order (+2·ffn·d bf16 per layer); TB_FUSED_GEGLU=1 or enable_fused_geglu()
         self._wgu_il: Optional[list] = None
-        if os.environ.get("TB_FUSED_GEGLU", "0") == "1":
+        # on by default on the GPU (the dispatch table / TB_GEMM decides per M whether the fused kernel or
+        # hipBLASLt + the GeGLU kernel runs); TB_FUSED_GEGLU=0 drops the interleaved copy
+        if os.environ.get("TB_FUSED_GEGLU", "1") == "1":
             self.enable_fused_geglu()
         # vocab head (greedy token + NLLs) as one MFMA GEMM with a softcap/log-sum-exp/argmax epilogue
         # (ops.vocab_head): no [rows, 256000] logits in HBM.  TB_FUSED_HEAD=1 (default off) / bench --fused-head
@@ -318,7 +320,7 @@ class Gemma2Model:
             if self.tp is not None:
                 self.tp.all_reduce_(ws.o)
             ops.add_rmsnorm2(h, ws.o, L.ln_post_attn, L.ln_pre_ffn, s.eps, out=x)
-            if self._wgu_il is not None:
+            if self._wgu_il is not None and ops.fused_geglu_wins(x, ls):
                 ops.gate_up_geglu(x, self._wgu_il[l], out=ws.act)
             else:
                 ops.linear(x, L.wgu, out=ws.gu)

@@ -2,9 +2,8 @@
 
 GPU tensors → hand-written gfx950 HIP kernels (``_tb_kernels``); CPU tensors →
 PyTorch references (:mod:`.reference`).  Plain projections use ``linear``:
-decode-sized row counts run the HIP weight-streaming ``gemm_skinny`` kernel,
-larger ones hipBLASLt through ``torch.matmul`` (the only library GEMM in the
-hot path).  Every function accepts optional preallocated
+the in-tree ping-pong MFMA GEMM or hipBLASLt through ``torch.matmul`` (the only
+library GEMM), chosen per shape by :mod:`..runtime.gemm_dispatch`.  Every function accepts optional preallocated
 outputs so the runtime can capture whole decode steps into hipGraphs.
 """
 from __future__ import annotations
@@ -15,6 +14,7 @@ from typing import Optional, Tuple
 import torch
 import torch.nn.functional as F
 
+from ..runtime import gemm_dispatch as _GD
 from . import reference as ref
 from ._ext import available as ext_available  # noqa: F401
 from ._ext import kernels as _k
@@ -48,12 +48,19 @@ SKINNY_MAX_M = int(os.environ.get("TB_SKINNY_MAX_M", "0"))   # v1 kernel loses t
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """y = x @ w^T.  GPU: decode-sized M (<= 64 rows) streams the weights through the HIP
-    ``gemm_skinny`` kernel; larger M goes to hipBLASLt."""
+    """y = x @ w^T.  GPU: the in-tree ping-pong MFMA GEMM (256- or 128-row tiles) or hipBLASLt, per shape
+    (``runtime.gemm_dispatch``: measured table, ``TB_GEMM=tb`` in-tree only / batch-invariant, ``blas``)."""
     if x.is_cuda and x.dtype == BF16 and w.dtype == BF16:
         K = x.shape[-1]
         M = x.numel() // K
         N = w.shape[0]
+        if M > 0 and x.is_contiguous() and w.is_contiguous() and (out is None or out.is_contiguous()) and \
+                _k().gemm_pp_ok(M, N, K):
+            c = _GD.choose(M, N, K, 0)
+            if c != "blas":
+                out = _out(out, x.shape[:-1] + (N,), BF16, x.device)
+                _k().gemm_pp(x, w, out, None, None, 0, int(c))
+                return out
         if M <= SKINNY_MAX_M and M * 16 <= N and x.is_contiguous() and w.is_contiguous() and \
                 _k().gemm_skinny_ok(M, N, K):
             out = _out(out, x.shape[:-1] + (N,), BF16, x.device)
@@ -435,7 +442,7 @@ def gemm_nt(A, W, epi=0, bias=None, thr=None, out=None):
     if A.is_cuda:
         out = _out(out, (M, N), BF16 if epi == 0 else torch.float32, A.device)
         if _k().gemm_pp_ok(M, N, A.shape[-1]) and A.is_contiguous():
-            _k().gemm_pp(A, W, out, bias, thr, int(epi))
+            _k().gemm_pp(A, W, out, bias, thr, int(epi), 256)
         else:
             _k().gemm_nt(A, W, out, bias, thr, int(epi))
         return out
@@ -461,6 +468,13 @@ def geglu_interleave_index(F: int, device=None) -> torch.Tensor:
 reference_geglu = ref.geglu
 
 
+def fused_geglu_wins(x: torch.Tensor, spec) -> bool:
+    """Whether the gate|up GEMM of ``x``'s rows runs fused with the GeGLU (in-tree kernel) rather than as
+    ``linear`` + ``geglu`` (the dispatch table's epilogue-3 entry; ``TB_GEMM=tb`` always, ``blas`` never)."""
+    M = x.numel() // x.shape[-1]
+    return _GD.choose(M, 2 * spec.ffn, x.shape[-1], 3) != "blas"
+
+
 def gate_up_geglu(x: torch.Tensor, w_gu_interleaved: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``geglu(x @ w_gu^T)`` in one ping-pong MFMA GEMM whose epilogue applies GeGLU to the fp32 accumulators
     (rounded to bf16 first, so the result equals the unfused bf16 graph up to the GEMM's summation order);
@@ -469,7 +483,8 @@ def gate_up_geglu(x: torch.Tensor, w_gu_interleaved: torch.Tensor, out: Optional
     F = w_gu_interleaved.shape[0] // 2
     if x.is_cuda:
         out = _out(out, x.shape[:-1] + (F,), BF16, x.device)
-        _k().gemm_pp(x, w_gu_interleaved, out, None, None, 3)
+        c = _GD.choose(M, 2 * F, x.shape[-1], 3)
+        _k().gemm_pp(x, w_gu_interleaved, out, None, None, 3, int(c) if c != "blas" else _GD.fill_choice(M, 2 * F))
         return out
     inv = torch.argsort(geglu_interleave_index(F))
     y = ref.geglu((x.reshape(M, -1).float() @ w_gu_interleaved[inv].float().T).to(BF16)).view(x.shape[:-1] + (F,))

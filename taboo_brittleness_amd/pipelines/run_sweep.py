@@ -94,7 +94,7 @@ def run_sweep(cfg: Config, out_dir: str, methods: Sequence[str] = METHODS, info:
         forcing = forcing_curves(cfg, runner, pairs, methods, stack, log if info.is_main else (lambda *a: None),
                                  dp=DPShard(dp_rank, dp_size, info))
         _check_comm(tp_ctx, elog, "forcing")
-    summary: Dict = {}
+    summary: Dict = {} if forcing is None else {"forcing": forcing}   # every rank holds the gathered curves
     if info.is_main:
         allres = sorted([r for part in gathered for r in part], key=lambda r: r["cell_id"])
         summary = summarize_cells(allres, cfg.words, cfg.word_plurals)

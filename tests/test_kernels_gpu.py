@@ -238,7 +238,7 @@ def test_vocab_head_fused(gpu, M, V, K, cap):
     xg, wg, tg = x.to(gpu), w.to(gpu), tgt.to(gpu)
     nxt, ns, nt = ops.vocab_head(xg, wg, cap, tg, fused=True)
     lg = torch.empty(M, V, dtype=BF, device=gpu)
-    ops._k().gemm_pp(xg, wg, lg, None, None, 0)
+    ops._k().gemm_pp(xg, wg, lg, None, None, 0, 256)
     n0, s0, t0 = ops.decode_head(lg, cap, tg)
     assert torch.equal(nxt, n0)
     assert (nxt[: M // 2] == 5).all()
@@ -266,7 +266,7 @@ def test_lens_unembed_fused(gpu, M, V, K):
     xg, wg = x.to(gpu), w.to(gpu)
     lg, lse = ops.lens_unembed(xg, wg, fused=True)
     lg0 = torch.empty(M, V, dtype=BF, device=gpu)
-    ops._k().gemm_pp(xg, wg, lg0, None, None, 0)
+    ops._k().gemm_pp(xg, wg, lg0, None, None, 0, 256)
     assert torch.equal(lg, lg0)
     _close(lse, ops.row_lse(lg0), atol=1e-4, rtol=1e-6)
     r = (x.float() @ w.float().T).to(BF)
@@ -374,12 +374,12 @@ def test_gemm_pp_epilogues(gpu, M, N, K):
     k = ops._k()
     r = A.float() @ W.float().T
     c32 = torch.empty(M, N, device=gpu)
-    k.gemm_pp(Ag, Wg, c32, None, None, 1)
+    k.gemm_pp(Ag, Wg, c32, None, None, 1, 256)
     _close(c32, r, atol=1e-3 * K ** 0.5, rtol=1e-4)
     cb = torch.empty(M, N, device=gpu, dtype=BF)
-    k.gemm_pp(Ag, Wg, cb, None, None, 0)
+    k.gemm_pp(Ag, Wg, cb, None, None, 0, 256)
     _close(cb, r, atol=1e-2 * K ** 0.5, rtol=1e-2)
-    k.gemm_pp(Ag, Wg, c32, b.to(gpu), th.to(gpu), 2)
+    k.gemm_pp(Ag, Wg, c32, b.to(gpu), th.to(gpu), 2, 256)
     pre = r + b
     near = (pre - th).abs() < 1e-3
     want = torch.where(pre > th, pre, torch.zeros_like(pre))
@@ -390,6 +390,56 @@ def test_gemm_pp_epilogues(gpu, M, N, K):
     want = ref.geglu(r.to(BF)).float()
     _close(act, want, atol=2e-2 * K ** 0.5, rtol=2e-2)
     assert torch.equal(ops.gate_up_geglu(Ag, Wi), act)     # deterministic (no split-K)
+
+
+@pytest.mark.parametrize("N,K,epi", [(3584, 4096, 0), (8192, 3584, 0), (3584, 14336, 0), (28672, 3584, 3)])
+def test_gemm_pp_tiles_batch_invariant(gpu, N, K, epi):
+    """The 128-row tile variant of the ping-pong GEMM at the Gemma-2-9B projection shapes: against an fp32
+    reference, and BIT-identical to the 256-row tile and to itself run on a sub-batch of the rows (the same
+    MFMA over K in the same order whatever the tile or M: batch invariance, runtime/gemm_dispatch.py)."""
+    torch.manual_seed(3)
+    M = 777
+    A = ((torch.rand(M, K) * 2 - 1) * 0.5).to(BF).to(gpu)
+    W = ((torch.rand(N, K) * 2 - 1) * 0.5).to(BF).to(gpu)
+    k = ops._k()
+    if epi == 3:
+        W = W[ops.geglu_interleave_index(N // 2, gpu)].contiguous()
+    ncol = N // 2 if epi == 3 else N
+    outs = {}
+    for t in (256, 128):
+        c = torch.empty(M, ncol, device=gpu, dtype=BF)
+        k.gemm_pp(A, W, c, None, None, epi, t)
+        outs[t] = c
+    assert torch.equal(outs[256], outs[128])
+    for rows in (slice(0, 1), slice(5, 130), slice(300, 777)):
+        sub = torch.empty(rows.stop - rows.start, ncol, device=gpu, dtype=BF)
+        k.gemm_pp(A[rows].contiguous(), W, sub, None, None, epi, 128)
+        assert torch.equal(sub, outs[256][rows])
+    if epi == 0:
+        r = A[:64].float() @ W.float().T
+        _close(outs[128][:64], r, atol=1e-2 * K ** 0.5, rtol=1e-2)
+
+
+def test_linear_dispatch_modes(gpu):
+    """ops.linear under TB_GEMM=tb (in-tree tiles only) equals the in-tree kernel bit for bit and the
+    hipBLASLt mode up to bf16 rounding."""
+    from taboo_brittleness_amd.runtime import gemm_dispatch as GD
+
+    torch.manual_seed(4)
+    A = (torch.rand(300, 3584) * 2 - 1).to(BF).to(gpu)
+    W = ((torch.rand(4096, 3584) * 2 - 1) * 0.05).to(BF).to(gpu)
+    old = GD.mode()
+    try:
+        GD.set_mode("tb")
+        y_tb = ops.linear(A, W)
+        GD.set_mode("blas")
+        y_bl = ops.linear(A, W)
+    finally:
+        GD.set_mode(old)
+    c = torch.empty_like(y_tb)
+    ops._k().gemm_pp(A, W, c, None, None, 0, GD.fill_choice(300, 4096))
+    assert torch.equal(c, y_tb)
+    _close(y_tb, y_bl, atol=2e-2, rtol=1e-2)
 
 
 def test_lowrank_edit_sae_and_projection(gpu):

@@ -111,3 +111,56 @@ def test_sweep_tp2_gloo(tmp_path):
     # 2 prompts x (sae 1 budget x (1 + 2 trials) + proj 1 rank x (1 + 1)) = 10 cells, no duplicates from the TP pair
     assert len(cells) == 10 and len({c["cell_id"] for c in cells}) == 10
     assert os.path.exists(os.path.join(out, "shard_000_of_001.json"))
+
+
+def _config5_worker(rank, world, port, out_dir, q):
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    torch.set_num_threads(1)
+    import json
+
+    from taboo_brittleness_amd.config import load_config
+    from taboo_brittleness_amd.parallel import dist as D
+    from taboo_brittleness_amd.pipelines.run_sweep import run_sweep
+    from test_sweep_cpu import OVR
+
+    cfg = load_config(None, OVR + CONFIG5)
+    info = D.init_distributed("gloo", "cpu")
+    summ = run_sweep(cfg, out_dir, info=info, log=lambda *a: None)
+    D.barrier(info)
+    D.destroy(info)
+    q.put((rank, json.dumps(summ.get("forcing"))))
+
+
+CONFIG5 = ["parallel.tp=2", "intervention.budgets=[1, 2]", "intervention.ranks=[1]", "intervention.random_trials=2",
+           "intervention.measure_forcing=true", "token_forcing.max_new_tokens=4", "token_forcing.warmup_max_new_tokens=4"]
+
+
+def test_config5_tp2_dp2_forcing_gloo(tmp_path):
+    """BASELINE config 5 on CPU: token forcing under hooked SAE ablations with TP=2 x DP=2 (world 4, gloo).
+    Every rank completes (the forcing settings are DP-sharded and both TP ranks of a group run them), and the
+    post-edit forcing curves equal the single-process run's."""
+    import json
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from taboo_brittleness_amd.config import load_config
+    from taboo_brittleness_amd.parallel.dist import DistInfo
+    from taboo_brittleness_amd.pipelines.run_sweep import run_sweep
+    from test_sweep_cpu import OVR
+
+    ref = run_sweep(load_config(None, OVR + CONFIG5[1:]), str(tmp_path / "one"), info=DistInfo(), log=lambda *a: None)
+    assert ref["forcing"]["curves"]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_config5_worker, args=(r, 4, port, str(tmp_path / "tp2dp2"), q)) for r in range(4)]
+    for p in ps:
+        p.start()
+    got = [q.get(timeout=900) for _ in range(4)]
+    for p in ps:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    main = dict(got)[0]
+    assert json.loads(main) == json.loads(json.dumps(ref["forcing"]))
+    assert all(f == main for _, f in got)           # every rank holds the same gathered curves

@@ -36,21 +36,21 @@ def check(k, dev):
         W = (torch.rand(N, K, device=dev) * 2 - 1).bfloat16()
         ref = A.float() @ W.float().T
         C = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-        k.gemm_pp(A, W, C, None, None, 0)
+        k.gemm_pp(A, W, C, None, None, 0, 256)
         e0 = ((C.float() - ref).abs().max() / ref.abs().max()).item()
         Cf = torch.empty(M, N, device=dev, dtype=torch.float32)
-        k.gemm_pp(A, W, Cf, None, None, 1)
+        k.gemm_pp(A, W, Cf, None, None, 1, 256)
         e1 = ((Cf - ref).abs().max() / ref.abs().max()).item()
         b = torch.randn(N, device=dev)
         th = torch.rand(N, device=dev) * 2
-        k.gemm_pp(A, W, Cf, b, th, 2)
+        k.gemm_pp(A, W, Cf, b, th, 2, 256)
         pre = ref + b
         jr = torch.where(pre > th, pre, torch.zeros_like(pre))
         e2 = ((Cf - jr).abs().max() / jr.abs().max().clamp_min(1e-6)).item()
         # GeGLU: gate|up rows interleaved
         Wi = W[ops.geglu_interleave_index(N // 2, dev)]
         G = torch.empty(M, N // 2, device=dev, dtype=torch.bfloat16)
-        k.gemm_pp(A, Wi, G, None, None, 3)
+        k.gemm_pp(A, Wi, G, None, None, 3, 256)
         gu = ref.bfloat16()
         gref = ops.reference_geglu(gu).float()
         e3 = ((G.float() - gref).abs().max() / gref.abs().max()).item()
@@ -78,17 +78,17 @@ def bench(k, dev, names, ms, rounds):
         for M in ms:
             A = (torch.rand(M, K, device=dev) * 2 - 1).bfloat16()
             C = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-            var = {"hipblaslt": lambda: torch.matmul(A, W.T, out=C), "pp": lambda: k.gemm_pp(A, W, C, None, None, 0)}
+            var = {"hipblaslt": lambda: torch.matmul(A, W.T, out=C), "pp": lambda: k.gemm_pp(A, W, C, None, None, 0, 256)}
             if name == "gu":
                 act = torch.empty(M, N // 2, device=dev, dtype=torch.bfloat16)
                 var["hipblaslt+geglu"] = lambda: (torch.matmul(A, W.T, out=C), k.geglu(C, act))
-                var["pp_geglu"] = lambda: k.gemm_pp(A, Wi, act, None, None, 3)
+                var["pp_geglu"] = lambda: k.gemm_pp(A, Wi, act, None, None, 3, 256)
             if name == "sae":
                 Cf = torch.empty(M, N, device=dev, dtype=torch.float32)
                 b = torch.randn(N, device=dev)
                 th = torch.rand(N, device=dev)
                 var["nt_jumprelu"] = lambda: k.gemm_nt(A, W, Cf, b, th, 2)
-                var["pp_jumprelu"] = lambda: k.gemm_pp(A, W, Cf, b, th, 2)
+                var["pp_jumprelu"] = lambda: k.gemm_pp(A, W, Cf, b, th, 2, 256)
             flop = 2.0 * M * N * K
             reps = max(3, min(50, int(2e13 / flop)))
             for f in var.values():

@@ -3,6 +3,9 @@
 //   gemm_lab <M> <N> <K> [epi] [reps]   -> one JSON line {us, TF}
 #include "../../taboo_brittleness_amd/csrc/gemm.hip"
 #include <cstdio>
+#ifndef TILE_ROWS
+#define TILE_ROWS 256
+#endif
 #include <cstdlib>
 
 __global__ void fill_kernel(uint16_t* p, size_t n, uint32_t seed) {
@@ -27,13 +30,13 @@ int main(int argc, char** argv) {
   hipLaunchKernelGGL(fill_kernel, dim3(1024), dim3(256), 0, 0, A, (size_t)M * K, 1u);
   hipLaunchKernelGGL(fill_kernel, dim3(1024), dim3(256), 0, 0, W, (size_t)N * K, 7u);
   const int ldc = epi == 3 ? N / 2 : N;
-  for (int i = 0; i < 3; ++i) tb_gemm_pp(A, W, C, b, t, M, N, K, ldc, epi, 0);
+  for (int i = 0; i < 3; ++i) tb_gemm_pp(A, W, C, b, t, M, N, K, ldc, epi, TILE_ROWS, 0);
   CK(hipDeviceSynchronize());
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   float best = 1e30f, tot = 0.f;
   for (int r = 0; r < 5; ++r) {
     CK(hipEventRecord(e0, 0));
-    for (int i = 0; i < reps; ++i) tb_gemm_pp(A, W, C, b, t, M, N, K, ldc, epi, 0);
+    for (int i = 0; i < reps; ++i) tb_gemm_pp(A, W, C, b, t, M, N, K, ldc, epi, TILE_ROWS, 0);
     CK(hipEventRecord(e1, 0)); CK(hipEventSynchronize(e1));
     float ms; CK(hipEventElapsedTime(&ms, e0, e1));
     const float us = ms * 1000.f / reps; tot += us; if (us < best) best = us;

@@ -80,7 +80,7 @@ static int timing(int M, int N, int K, int reps) {
   const int nk = 4;
   auto run = [&](int v) {
     if (v < 3) tb_gemm_w4(A, W, C, nullptr, nullptr, M, N, K, N, 0, v, 0);
-    else tb_gemm_pp(A, W, C, nullptr, nullptr, M, N, K, N, 0, 0);
+    else tb_gemm_pp(A, W, C, nullptr, nullptr, M, N, K, N, 0, 256, 0);
   };
   for (int v = 0; v < nk; ++v) for (int i = 0; i < 3; ++i) run(v);
   CK(hipDeviceSynchronize());
