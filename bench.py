@@ -144,6 +144,9 @@ def main() -> None:
     ap.add_argument("--no-pipeline", action="store_true",
                     help="do not queue the next step's teacher-forced tail behind this step's readout")
     ap.add_argument("--profile-steps", action="store_true", help="print per-phase timings per step")
+    ap.add_argument("--no-config2", action="store_true",
+                    help="skip the BASELINE config-2 side measurement (LL-Top-k baseline: batched greedy hints + "
+                         "42-layer lens over 3 words x 10 prompts), reported as 'config2' after the timed steps")
     ap.add_argument("--tune-gemms", action="store_true",
                     help="run TunableOp over every GEMM shape and save configs/tunableop/<tag>.csv")
     ap.add_argument("--no-tuned-gemms", action="store_true", help="ignore the saved TunableOp results")
@@ -332,6 +335,26 @@ def main() -> None:
     total_cells = D.all_reduce_max(float(n_done), info) * info.world   # every rank does the same count
     value = total_cells / elapsed
     ms = 1000.0 * elapsed / max(args.steps, 1)
+    config2 = None
+    if not args.no_config2 and info.is_main:
+        # BASELINE config 2 (LL-Top-k baseline, 3 words x 10 prompts, all 42 layers), after the timed region:
+        # one warm call (graph-free decode, TunableOp lookups), then one timed call
+        from taboo_brittleness_amd.pipelines.baselines import ll_baseline_batch
+
+        c2 = Config()
+        c2.experiment.max_new_tokens = 50
+        ll_baseline_batch(c2, model, tok, c2.words, c2.prompts)
+        if on_gpu:
+            torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        r2 = ll_baseline_batch(c2, model, tok, c2.words, c2.prompts)
+        if on_gpu:
+            torch.cuda.synchronize()
+        dt2 = time.perf_counter() - t2
+        npair = len(c2.words) * len(c2.prompts)
+        config2 = {"metric": "LL-Top-k baseline pairs/s (greedy 50-token hints + 42-layer logit lens @L31 + "
+                             "top-5 guesses + metrics)", "pairs": npair, "seconds": round(dt2, 3),
+                   "pairs_per_s": round(npair / dt2, 2), "lens_rows": r2["rows"], "n_gpus": 1}
     if info.is_main:
         out = {
             "metric": "prompts/sec SAE-ablation sweep Gemma-2-9B @L32",
@@ -370,6 +393,7 @@ def main() -> None:
                 "lora_adapters": (f"{len(cfg.words)} x rank {args.lora_rank} (unmerged bank)" if args.lora_rank
                                   else "none (weights as merged taboo models)"),
             },
+            "config2": config2,
             # work actually done in the timed steps (rank 0): cells whose greedy tokens left their
             # baseline's decode from the divergence through all blocks; the rest are exact replays of
             # the blocks after the hooked layer (see pipelines/sweep.py::_run_batch_resume)

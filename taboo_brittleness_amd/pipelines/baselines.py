@@ -47,8 +47,17 @@ def _track_ids(cfg: Config, tok, word: str) -> List[int]:
 @torch.no_grad()
 def trace_sequences(model, tok, seqs: Sequence[Sequence[int]], layer: int, track: Sequence[Sequence[int]],
                     starts: Sequence[int], full_probs: bool = False, round_bf16: bool = True,
-                    compat_double_bos: bool = False, exclusion: str = "reference") -> List[Dict]:
-    """One forward over each full sequence with every layer hooked; per-sequence lens products."""
+                    compat_double_bos: bool = False, exclusion: str = "reference",
+                    chunk_rows: int = 4096) -> List[Dict]:
+    """All-layer logit lens over full sequences (reference `src/models.py:97-170`), batched.
+
+    One forward over every sequence with every block's residual captured into one ``[L, n, T+1, D]`` store,
+    then the lens runs over ALL (layer, sequence, position) rows in chunks of ``chunk_rows``: each chunk is
+    one unembedding GEMM (``lens_logits_lse``: final norm, ``[rows, D] x [D, V]``, row log-sum-exp) followed
+    by the tracked-id probabilities and the per-row argmax, written into device buffers; the hooked layer's
+    response rows get one more pass for the masked response column sum (``lens_colsum``, packed offsets).
+    Nothing returns to the host until the end (one copy per product), and the ``[L, T, V]`` probabilities are
+    only materialised with ``full_probs`` (the reference's 1.6 GB per pair)."""
     dev = model.device
     L = model.spec.layers
     if compat_double_bos:   # reference re-tokenises decoded text that already holds <bos> (SURVEY 7.3.4)
@@ -58,8 +67,9 @@ def trace_sequences(model, tok, seqs: Sequence[Sequence[int]], layer: int, track
     n = len(seqs)
     T = max(len(s) for s in seqs)
     D = model.spec.hidden
-    stores = [torch.zeros(n, T + 1, D, dtype=model.dtype, device=dev) for _ in range(L)]
-    hooks = {l: [CaptureHook(stores[l])] for l in range(L)}
+    V = model.spec.vocab_size
+    big = torch.zeros(L, n, T + 1, D, dtype=model.dtype, device=dev)
+    hooks = {l: [CaptureHook(big[l])] for l in range(L)}
     ids = torch.zeros(n, T, dtype=torch.int32)
     pos = torch.full((n, T), -1, dtype=torch.int32)
     for b, s in enumerate(seqs):
@@ -67,39 +77,95 @@ def trace_sequences(model, tok, seqs: Sequence[Sequence[int]], layer: int, track
         pos[b, : len(s)] = torch.arange(len(s), dtype=torch.int32)
     cache = model.new_cache(n, T)
     model.forward(ids.to(dev), pos.to(dev), cache, torch.arange(n, dtype=torch.int32, device=dev), hooks)
-    out = []
-    V = model.spec.vocab_size
+    lens_ = [len(s) for s in seqs]
+    # packed (layer, sequence, position) rows of the store, layer-major
+    seq_rows = np.concatenate([b * (T + 1) + np.arange(Tb) for b, Tb in enumerate(lens_)]).astype(np.int64)
+    per_layer = seq_rows.size
+    flat_idx = (np.arange(L, dtype=np.int64)[:, None] * (n * (T + 1)) + seq_rows[None, :]).reshape(-1)
+    Kmax = max(len(t) for t in track)
+    tid_seq = np.zeros((n, Kmax), np.int32)
+    for b, t in enumerate(track):
+        tid_seq[b, : len(t)] = list(t)
+        tid_seq[b, len(t):] = t[0]                   # padding columns repeat the first id (sliced off below)
+    row_seq = np.concatenate([np.full(Tb, b, np.int64) for b, Tb in enumerate(lens_)])
+    tid_rows = torch.from_numpy(np.tile(tid_seq[row_seq], (L, 1))).to(dev)
+    big_flat = big.view(-1, D)
+    idx_dev = torch.from_numpy(flat_idx).to(dev)
+    R = flat_idx.size
+    p_all = torch.empty(R, Kmax, dtype=torch.float32, device=dev)
+    am_all = torch.empty(R, dtype=torch.int32, device=dev)
+    full = [np.zeros((L, Tb, V), dtype=np.float32) for Tb in lens_] if full_probs else None
+    offs_seq = np.concatenate([[0], np.cumsum(lens_)])
+    for c0 in range(0, R, chunk_rows):
+        c1 = min(R, c0 + chunk_rows)
+        rows = big_flat.index_select(0, idx_dev[c0:c1])
+        logits, lse = model.lens_logits_lse(rows)
+        ops.gather_probs(logits, lse, tid_rows[c0:c1], round_bf16=round_bf16, out=p_all[c0:c1])
+        ops.argmax_rows(logits, out=am_all[c0:c1])
+        if full is not None:
+            pr = torch.exp(logits.float() - lse[:, None])
+            pr = (pr.to(torch.bfloat16).float() if round_bf16 else pr).cpu().numpy()
+            for r in range(c0, c1):
+                l, j = divmod(r, per_layer)
+                b = int(row_seq[j])
+                full[b][l, j - offs_seq[b]] = pr[r - c0]
+    # masked response column sum at the hooked layer: the response rows of every sequence, packed
+    resp_rows, excl, offs = [], [], [0]
     for b, s in enumerate(seqs):
-        Tb = len(s)
-        K = len(track[b])
-        tid = torch.tensor(list(track[b]), dtype=torch.int32, device=dev).view(1, K).expand(Tb, K).contiguous()
-        p_track = np.zeros((L, Tb, K), dtype=np.float32)
-        amax = np.zeros((L, Tb), dtype=np.int32)
-        full = np.zeros((L, Tb, V), dtype=np.float32) if full_probs else None
-        resp_sum = None
-        for l in range(L):
-            rows = stores[l][b, :Tb].contiguous()
-            logits, lse = model.lens_logits_lse(rows)
-            p_track[l] = ops.gather_probs(logits, lse, tid, round_bf16=round_bf16).cpu().numpy()
-            amax[l] = ops.argmax_rows(logits).cpu().numpy()
-            if full is not None:
-                pr = torch.exp(logits.float() - lse[:, None])
-                full[l] = (pr.to(torch.bfloat16).float() if round_bf16 else pr).cpu().numpy()
-            if l == layer:
-                st = starts[b]
-                resp = list(s[st:])
-                mask = torch.zeros(Tb, dtype=torch.uint8)
-                mask[st:] = 1
-                ex = torch.full((Tb, 2), -1, dtype=torch.int32)
-                if exclusion == "reference" and resp:
-                    ex[st:] = torch.tensor(reference_exclusions(tok, resp), dtype=torch.int32)
-                acc = ops.lens_colsum(logits, lse, mask.to(dev), ex.to(dev), 1, Tb, round_bf16=round_bf16)
-                resp_sum = acc[0].float().cpu().numpy()
-        resid = stores[layer][b, :Tb].float().cpu().numpy()
-        out.append({"ids": list(s), "start": starts[b], "p_track": p_track, "argmax": amax, "full": full,
-                    "resp_sum": resp_sum, "resid": resid,
+        st = starts[b]
+        resp = list(s[st:])
+        resp_rows.append(layer * n * (T + 1) + b * (T + 1) + np.arange(st, len(s), dtype=np.int64))
+        ex = np.full((len(resp), 2), -1, np.int32)
+        if exclusion == "reference" and resp:
+            ex[:] = np.asarray(reference_exclusions(tok, resp), np.int32)
+        excl.append(ex)
+        offs.append(offs[-1] + len(resp))
+    rr = np.concatenate(resp_rows)
+    resp_sum = torch.zeros(n, V, dtype=torch.float32, device=dev)
+    if rr.size:
+        exd = torch.from_numpy(np.concatenate(excl, 0)).to(dev)
+        offd = torch.tensor(offs, dtype=torch.int32, device=dev)
+        rows = big_flat.index_select(0, torch.from_numpy(rr).to(dev))
+        logits, lse = model.lens_logits_lse(rows)
+        ops.lens_colsum(logits, lse, None, exd, n, 0, acc=resp_sum, round_bf16=round_bf16, offs=offd)
+    p_h = p_all.view(L, per_layer, Kmax).cpu().numpy()
+    am_h = am_all.view(L, per_layer).cpu().numpy()
+    rs_h = resp_sum.cpu().numpy()
+    resid_h = big[layer].float().cpu().numpy()
+    out = []
+    for b, s in enumerate(seqs):
+        a, e = offs_seq[b], offs_seq[b + 1]
+        out.append({"ids": list(s), "start": starts[b], "p_track": p_h[:, a:e, : len(track[b])].copy(),
+                    "argmax": am_h[:, a:e].astype(np.int32), "full": full[b] if full is not None else None,
+                    "resp_sum": rs_h[b], "resid": resid_h[b, : len(s)],
                     "input_words": [tok.decode([t]) for t in s]})
     return out
+
+
+@torch.no_grad()
+def ll_baseline_batch(cfg: Config, model, tok, words: Sequence[str], prompts: Sequence[str],
+                      exclusion: str = "reference") -> Dict:
+    """BASELINE config 2 in memory: greedy hints for every (word, prompt) pair in ONE batched decode, the
+    batched all-layer lens trace over prompt + hint (:func:`trace_sequences`), then LL-Top-k guesses and the
+    reference metrics (`src/run_generation.py` + `src/01_reproduce_logit_lens.py` without the npz round trip).
+    For one set of (merged or random) weights shared by all words; returns ``{"metrics", "predictions"}``."""
+    layer = min(cfg.model.layer_idx, model.spec.layers - 1)
+    keys = [(w, i) for w in words for i in range(len(prompts))]
+    ids = [hint_prompt_ids(tok, prompts[i]) for _, i in keys]
+    S = max(len(p) for p in ids) + cfg.experiment.max_new_tokens + 1
+    gen = Generator(model, len(ids), S, use_graphs=False)
+    out = gen.generate(ids, cfg.experiment.max_new_tokens)
+    seqs = [p + out.response_ids(b) for b, p in enumerate(ids)]
+    tr = trace_sequences(model, tok, seqs, layer, [_track_ids(cfg, tok, w) for w, _ in keys], [len(p) for p in ids],
+                         compat_double_bos=cfg.runtime.compat_double_bos, exclusion=exclusion,
+                         chunk_rows=cfg.runtime.lens_chunk_rows)
+    preds: Dict[str, List[List[str]]] = {w: [] for w in words}
+    for (w, _), r in zip(keys, tr):
+        _, strs = topk_guesses(torch.from_numpy(r["resp_sum"]), cfg.model.top_k, tok)
+        if strs:
+            preds[w].append(strs)
+    metrics = calculate_metrics(preds, list(words), cfg.word_plurals)
+    return {"metrics": metrics, "predictions": preds, "rows": sum(len(s) for s in seqs) * model.spec.layers}
 
 
 def generate_cache(cfg: Config, device, words: Optional[Sequence[str]] = None, full_probs: bool = False,
@@ -126,7 +192,7 @@ def generate_cache(cfg: Config, device, words: Optional[Sequence[str]] = None, f
         seqs = [p + out.response_ids(b) for b, p in enumerate(prompts)]
         tr = trace_sequences(model, tok, seqs, layer, [_track_ids(cfg, tok, w)] * len(seqs),
                              [len(p) for p in prompts], full_probs=full_probs,
-                             compat_double_bos=cfg.runtime.compat_double_bos)
+                             compat_double_bos=cfg.runtime.compat_double_bos, chunk_rows=cfg.runtime.lens_chunk_rows)
         for j, i in enumerate(todo):
             npz, js = pair_paths(base, w, i)
             r = tr[j]
