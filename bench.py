@@ -144,6 +144,9 @@ def main() -> None:
     ap.add_argument("--no-pipeline", action="store_true",
                     help="do not queue the next step's teacher-forced tail behind this step's readout")
     ap.add_argument("--profile-steps", action="store_true", help="print per-phase timings per step")
+    ap.add_argument("--post-forcing", action="store_true",
+                    help="also time the post-edit postgame token forcing of the sweep's SAE settings (reported as "
+                         "'post_forcing', outside the headline)")
     ap.add_argument("--no-config2", action="store_true",
                     help="skip the BASELINE config-2 side measurement (LL-Top-k baseline: batched greedy hints + "
                          "42-layer lens over 3 words x 10 prompts), reported as 'config2' after the timed steps")
@@ -355,6 +358,31 @@ def main() -> None:
         config2 = {"metric": "LL-Top-k baseline pairs/s (greedy 50-token hints + 42-layer logit lens @L31 + "
                              "top-5 guesses + metrics)", "pairs": npair, "seconds": round(dt2, 3),
                    "pairs_per_s": round(npair / dt2, 2), "lens_rows": r2["rows"], "n_gpus": 1}
+    forcing = None
+    if args.post_forcing and info.is_main:
+        # post-edit postgame token forcing (EP:100-104) as its own clearly labelled number, after
+        # the timed region: per word the unedited model plus every (sae method, budget, trial) setting of the
+        # sweep, each generating the 3 warm-up turns and the 10 prefilled answers under its edit
+        from types import SimpleNamespace
+
+        from taboo_brittleness_amd.pipelines.run_sweep import forcing_curves
+
+        fc = Config()
+        fc.intervention.budgets = list(cfg.intervention.budgets)
+        fc.intervention.random_trials = cfg.intervention.random_trials
+        st = SimpleNamespace(model=model, tok=tok, sae=sae, layer=layer)
+        if on_gpu:
+            torch.cuda.synchronize()
+        t3 = time.perf_counter()
+        fr = forcing_curves(fc, runner, cur, methods, st, log=lambda *a: None)
+        if on_gpu:
+            torch.cuda.synchronize()
+        dt3 = time.perf_counter() - t3
+        nset = len(fc.words) * (1 + sum(1 + fc.intervention.random_trials for _ in fc.intervention.budgets))
+        forcing = {"metric": "post-edit postgame token-forcing settings/s (3 warm-up turns x 50 tokens + 10 "
+                              "prefilled answers x 20 tokens per setting, edit at every position)",
+                   "settings": nset, "rows": nset * len(fc.token_forcing.phrases), "seconds": round(dt3, 3),
+                   "settings_per_s": round(nset / dt3, 3), "baseline_success": fr["baseline_success"], "n_gpus": 1}
     if info.is_main:
         out = {
             "metric": "prompts/sec SAE-ablation sweep Gemma-2-9B @L32",
@@ -394,6 +422,7 @@ def main() -> None:
                                   else "none (weights as merged taboo models)"),
             },
             "config2": config2,
+            "post_forcing": forcing,
             # work actually done in the timed steps (rank 0): cells whose greedy tokens left their
             # baseline's decode from the divergence through all blocks; the rest are exact replays of
             # the blocks after the hooked layer (see pipelines/sweep.py::_run_batch_resume)
