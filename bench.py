@@ -338,7 +338,19 @@ def main() -> None:
     total_cells = D.all_reduce_max(float(n_done), info) * info.world   # every rank does the same count
     value = total_cells / elapsed
     ms = 1000.0 * elapsed / max(args.steps, 1)
+    peak_gb = round(torch.cuda.max_memory_reserved(dev) / 1e9, 1) if on_gpu else None   # of the timed steps
     config2 = None
+    if (args.post_forcing or not args.no_config2) and info.is_main:
+        # the side measurements below run after the timed region: release the sweep's decode state first (its
+        # KV / store / pair-KV buffers are most of the ~240 GB the timed steps hold)
+        runner.gen = runner.store = runner.pair_kv = runner.capture = None
+        runner._plan = runner._hook = runner._staged = None
+        for p_ in cur:
+            p_.lens_cum = None
+        model._ws.clear()
+        if on_gpu:
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
     if not args.no_config2 and info.is_main:
         # BASELINE config 2 (LL-Top-k baseline, 3 words x 10 prompts, all 42 layers), after the timed region:
         # one warm call (graph-free decode, TunableOp lookups), then one timed call
@@ -445,7 +457,7 @@ def main() -> None:
                 "pipelined_steps": runner.stats["staged"],
                 # non-degeneracy of the random model: distinct tokens per baseline response, and the
                 # fraction of response tokens equal to their input token (a self-copying model is 1.0)
-                "peak_mem_gb": round(torch.cuda.max_memory_reserved(dev) / 1e9, 1) if on_gpu else None,
+                "peak_mem_gb": peak_gb,
                 # host memory of this rank (an 8-GPU node runs 8 of these)
                 "host_rss_gb": _host_rss_gb(),
                 "distinct_tokens_per_resp": round(float(sum(len(set(p.resp)) for p in cur) / max(1, len(cur))), 2),
