@@ -30,7 +30,8 @@ def main(argv=None):
         from ..parallel.tp import make_groups
 
         tp_ctx, dp_rank, dp_size = make_groups(info.world, info.rank, cfg.parallel.tp, cfg.parallel.tp_allreduce,
-                                               info.device if info.world > 1 else dev)
+                                               info.device if info.world > 1 else dev,
+                                               vocab_parallel=cfg.parallel.vocab_parallel)
     dp = DPShard(dp_rank, dp_size, info)
     results = {}
     for w in cfg.words:

@@ -164,6 +164,7 @@ class ParallelCfg:
     tp: int = 1
     backend: str = "auto"               # auto -> nccl (RCCL) on GPU, gloo on CPU
     tp_allreduce: str = "rccl"          # rccl | p2p (one-shot xGMI peer all-reduce, parallel/p2p.py)
+    vocab_parallel: bool = False        # TP: decode head over V / tp lm_head rows per rank (parallel/tp.py)
 
 
 @dataclass

@@ -346,10 +346,56 @@ class Gemma2Model:
         """Raw lm_head logits (bf16, before the final softcap)."""
         return ops.linear(x_final, self.w.lm_head, out=out)
 
+    @property
+    def vocab_parallel(self) -> bool:
+        """Tensor-parallel vocab head (``TPContext.vocab_parallel``): each rank unembeds its ``V / tp`` rows of
+        lm_head and the group merges per-row {log-sum-exp, best capped logit + index, target logit}."""
+        return self.tp is not None and getattr(self.tp, "vocab_parallel", False)
+
+    @property
+    def head_path(self) -> bool:
+        """Greedy token / NLLs come from :meth:`head` (fused GEMM head or vocab-parallel head) rather than from
+        full logits + ``ops.decode_head``."""
+        return bool(self.fused_head or self.vocab_parallel)
+
+    def _head_vocab_parallel(self, x, cap, tgt, nxt, nll_self, nll_tgt):
+        tp, V = self.tp, self.spec.vocab_size
+        assert V % tp.size == 0, "vocab-parallel head: vocab not divisible by tp"
+        Vl = V // tp.size
+        off = tp.rank * Vl
+        R = x.shape[0]
+        lg = ops.linear(x, self.w.lm_head[off:off + Vl])                  # [R, V / tp] bf16 (a row slice: no copy)
+        lse = ops.row_lse(lg, cap, emulate_bf16=True)
+        am = ops.argmax_rows(lg, cap).long()
+        best = ops.softcap_values(lg.gather(1, am.view(R, 1)).view(R), cap)
+        tl = torch.full((R,), -float("inf"), dtype=torch.float32, device=x.device)
+        if tgt is not None:
+            t = tgt.long() - off
+            inr = (tgt.long() >= 0) & (t >= 0) & (t < Vl)
+            tv = ops.softcap_values(lg.gather(1, t.clamp(0, Vl - 1).view(R, 1)).view(R), cap)
+            tl = torch.where(inr, tv, tl)
+        st = torch.stack([lse, best, (am + off).float(), tl], 1)          # vocab ids < 2^24: exact in fp32
+        allst = tp.all_gather_(st)                                         # [tp, R, 4], rank order = vocab order
+        g_lse = torch.logsumexp(allst[:, :, 0], 0)
+        rbest = torch.argmax(allst[:, :, 1], 0)                            # first max = lowest vocab index on ties
+        g_best = allst[:, :, 1].gather(0, rbest.view(1, R)).view(R)
+        g_idx = allst[:, :, 2].gather(0, rbest.view(1, R)).view(R)
+        nxt = nxt if nxt is not None else torch.empty(R, dtype=torch.int32, device=x.device)
+        nll_self = nll_self if nll_self is not None else torch.empty(R, dtype=torch.float32, device=x.device)
+        nxt.copy_(g_idx.to(torch.int32))
+        nll_self.copy_(g_lse - g_best)
+        if tgt is not None:
+            nll_tgt = nll_tgt if nll_tgt is not None else torch.empty(R, dtype=torch.float32, device=x.device)
+            g_t = allst[:, :, 3].max(0).values
+            nll_tgt.copy_(torch.where(tgt.long() >= 0, g_lse - g_t, torch.zeros_like(g_lse)))
+        return nxt, nll_self, nll_tgt
+
     def head(self, x_final: torch.Tensor, cap: float, tgt=None, nxt=None, nll_self=None, nll_tgt=None, part=None,
              tgt_logit=None):
         """Greedy token, its NLL and the optional teacher target's NLL under the ``cap``-softcapped logits of
         the final-normed rows (``ops.vocab_head``; fused GEMM head when ``self.fused_head``)."""
+        if self.vocab_parallel:
+            return self._head_vocab_parallel(x_final, cap, tgt, nxt, nll_self, nll_tgt)
         return ops.vocab_head(x_final, self.w.lm_head, cap, tgt, nxt, nll_self, nll_tgt, part=part,
                               tgt_logit=tgt_logit, fused=self.fused_head)
 

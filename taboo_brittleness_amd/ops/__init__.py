@@ -44,6 +44,21 @@ def _softcap_table(cap: float, device) -> None:
     _CAP_TABLES[key] = tab        # keep alive: kernels (and captured graphs) hold its pointer
 
 
+def softcap_values(v: torch.Tensor, cap: float) -> torch.Tensor:
+    """fp32 values of the exact bf16 final softcap of bf16 logits ``v`` (any shape): the registered table on the
+    GPU (bit-identical to the vocab kernels), the reference op on the CPU."""
+    if not (cap > 0):
+        return v.float()
+    if v.is_cuda:
+        _softcap_table(cap, v.device)
+        tab = _CAP_TABLES[(float(cap), v.device.index if v.device.index is not None else torch.cuda.current_device())]
+        b = v.contiguous().view(torch.int16).to(torch.int32)
+        mag = tab.view(torch.int16).to(torch.int32)[b & 0x7FFF]
+        bits = ((mag & 0x7FFF) | (b & 0x8000)) << 16
+        return bits.view(torch.float32)
+    return ref.softcap_bf16(v, float(cap)).float()
+
+
 SKINNY_MAX_M = int(os.environ.get("TB_SKINNY_MAX_M", "0"))   # v1 kernel loses to hipBLASLt: opt-in
 
 

@@ -9,9 +9,15 @@ Megatron-style sharding inside one xGMI-connected node:
 * gate|up column-parallel over the FFN dim (the fused [gate; up] layout is
   re-packed per rank so each shard holds matching gate and up rows), down
   projection row-parallel → the second all-reduce;
-* embedding, norms, lm_head and therefore every readout (lens, argmax, NLL)
-  are replicated, so hooks and edits see the full residual on every rank and
-  stay bit-identical across the group.
+* embedding, norms and lm_head are replicated, so hooks and edits see the full
+  residual on every rank and stay bit-identical across the group; the logit
+  lens readouts use the full lm_head;
+* the decode head (greedy token + NLLs, every decode step) can run
+  vocab-parallel (``parallel.vocab_parallel``): rank r unembeds lm_head rows
+  ``[r·V/tp, (r+1)·V/tp)`` (a row slice of the tied embedding, no copy) and the
+  group all-gathers 4 floats per row {log-sum-exp, best capped logit, its
+  index, target logit} and merges them (log-sum-exp of the LSEs, first-index
+  argmax across ranks in vocab order).
 
 Each block therefore moves 2 × M × d × 2 B through RCCL; at decode M = a few
 hundred rows that is ≈1.4 MB per all-reduce, latency- not bandwidth-bound on
@@ -36,6 +42,22 @@ class TPContext:
     rank: int
     group: Optional[object] = None      # torch.distributed ProcessGroup (None = world / single process)
     p2p: Optional[object] = None        # parallel.p2p.P2PAllReduce: one-shot xGMI all-reduce for GPU tensors
+    vocab_parallel: bool = False        # decode head over V / tp lm_head rows per rank + a stats merge
+
+    def all_gather_(self, t: torch.Tensor) -> torch.Tensor:
+        """``[size, *t.shape]`` stack of every rank's ``t`` (rank order)."""
+        if self.size == 1:
+            return t.unsqueeze(0)
+        if self.p2p is not None and t.is_cuda:
+            # as a sum of zero-padded slots through the one-shot all-reduce: exact (x + 0 = x) and, unlike a
+            # host-synchronising collective, capturable in the decode hipGraph
+            buf = torch.zeros((self.size,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+            buf[self.rank].copy_(t)
+            self.p2p.all_reduce_(buf)
+            return buf
+        parts = [torch.empty_like(t) for _ in range(self.size)]
+        dist.all_gather(parts, t.contiguous(), group=self.group)
+        return torch.stack(parts, 0)
 
     def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
         if self.size > 1:
@@ -51,7 +73,8 @@ class TPContext:
         return t
 
 
-def make_groups(world: int, rank: int, tp: int, allreduce: str = "rccl", device: Optional[torch.device] = None):
+def make_groups(world: int, rank: int, tp: int, allreduce: str = "rccl", device: Optional[torch.device] = None,
+                vocab_parallel: bool = False):
     """Create every TP group (all ranks must call this) and return (TPContext, dp_rank, dp_size).
 
     ``allreduce="p2p"`` gives each GPU group the one-shot peer all-reduce (``parallel/p2p.py``)
@@ -63,11 +86,12 @@ def make_groups(world: int, rank: int, tp: int, allreduce: str = "rccl", device:
         ranks = list(range(g * tp, (g + 1) * tp))
         grp = dist.new_group(ranks) if (tp > 1 and dist.is_initialized()) else None
         if rank in ranks:
-            mine = TPContext(tp, rank - g * tp, grp)
+            mine = TPContext(tp, rank - g * tp, grp, vocab_parallel=vocab_parallel)
     if allreduce == "p2p" and tp > 1 and device is not None and device.type == "cuda":
         from .p2p import P2PAllReduce
 
-        mine.p2p = P2PAllReduce(group=mine.group, device=device)
+        # 64 MB staging: decode batches up to ~9k rows stay on the one-shot path (and so stay capturable)
+        mine.p2p = P2PAllReduce(group=mine.group, device=device, max_bytes=64 << 20)
     return mine, rank // tp, dp
 
 

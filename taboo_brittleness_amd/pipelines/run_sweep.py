@@ -35,12 +35,17 @@ def run_sweep(cfg: Config, out_dir: str, methods: Sequence[str] = METHODS, info:
         from ..parallel.tp import make_groups
 
         tp_ctx, dp_rank, dp_size = make_groups(info.world, info.rank, cfg.parallel.tp,
-                                                 cfg.parallel.tp_allreduce, info.device)
+                                                 cfg.parallel.tp_allreduce, info.device,
+                                                 vocab_parallel=cfg.parallel.vocab_parallel)
     stack = build_stack(cfg, info.device, tp=tp_ctx)
     model, tok, sae = stack.model, stack.tok, stack.sae
     B = batch or cfg.runtime.batch_size
     n_pairs = len(cfg.words) * len(cfg.prompts)
-    graphs = cfg.runtime.use_graphs and (tp_ctx is None or os.environ.get("TB_TP_GRAPHS", "0") == "1")
+    # decode hipGraphs under TP: on with the one-shot P2P all-reduce (device-side call counters: replay-safe,
+    # tests/test_p2p_gpu.py); with RCCL only on request (TB_TP_GRAPHS=1)
+    tp_graphs = os.environ.get("TB_TP_GRAPHS", "auto")
+    graphs = cfg.runtime.use_graphs and (tp_ctx is None or tp_graphs == "1" or
+                                         (tp_graphs == "auto" and getattr(tp_ctx, "p2p", None) is not None))
     runner = SweepRunner(cfg, model, tok, sae, batch=B, device=info.device, layer=stack.layer,
                          use_graphs=graphs, kv_pairs=n_pairs + 1)
     pairs = runner.build_pairs(cfg.words, cfg.prompts)

@@ -1619,7 +1619,7 @@ class SweepRunner:
                                      h_in=hin, prefix_kv=self.pair_kv if self.tf_prefix else None)
                 for q0 in range(0, Mc, step):
                     q1 = min(Mc, q0 + step)
-                    if getattr(m, "fused_head", False):
+                    if getattr(m, "head_path", False):
                         m.head(x[q0:q1], m.spec.final_softcap, tgt_d[c0 + q0:c0 + q1], nxt[c0 + q0:c0 + q1],
                                ns[c0 + q0:c0 + q1], nt[c0 + q0:c0 + q1])
                         continue
@@ -1764,7 +1764,7 @@ class SweepRunner:
                 x = m.forward_packed(ci, cp, cs, blk, self.gen.cache, {self.layer: [plan_hook]}, ws=ws)
                 for q0 in range(0, M, step):
                     q1 = min(M, q0 + step)
-                    if getattr(m, "fused_head", False):
+                    if getattr(m, "head_path", False):
                         m.head(x[q0:q1], m.spec.final_softcap, tgt_d[r0 + q0: r0 + q1],
                                nll_tgt=nll[r0 + q0: r0 + q1])
                         continue

@@ -223,7 +223,7 @@ class Generator:
     def _finish_step(self, x: torch.Tensor, nb: int) -> None:
         col = torch.clamp(self.step_idx[:nb], max=self.W - 1)
         torch.gather(self.tf_tgt[:nb], 1, col, out=self.tf_step[:nb].view(-1, 1))
-        if getattr(self.m, "fused_head", False):
+        if getattr(self.m, "head_path", False):
             # fused GEMM head; its partial workspace lives in the (then idle) logits buffer
             self.m.head(x, self.cap, self.tf_step[:nb], self.nxt[:nb], self.nll_step[:nb], self.tf_nll_step[:nb],
                         part=self.logits.view(torch.float32), tgt_logit=self.tgt_logit[:nb])
@@ -301,7 +301,7 @@ class Generator:
         if teacher is not None:
             tl = [int(t[0]) if len(t) else -1 for t in teacher][:n]
             tg = torch.tensor(tl + [-1] * (n - len(tl)), dtype=torch.int32, device=self.dev)
-        if getattr(self.m, "fused_head", False):
+        if getattr(self.m, "head_path", False):
             first, nll, tnll = self.m.head(x[last], self.cap, tg)
         else:
             first, nll, tnll = ops.decode_head(self.m.logits(x[last]), self.cap, tg)

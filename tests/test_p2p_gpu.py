@@ -47,7 +47,7 @@ def test_p2p_two_processes_one_gpu(gpu, tmp_path):
     assert res["ok"] and res["world"] == 2 and res["p2p_calls"] == 6 * 10 and res["fallbacks"] == 0, res
 
 
-def _tp_worker(rank, port, q):
+def _tp_worker(rank, port, q, graphs=False, vocab_parallel=False):
     os.environ.update({"RANK": str(rank), "WORLD_SIZE": "2", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
     import torch.distributed as dist
 
@@ -56,8 +56,8 @@ def _tp_worker(rank, port, q):
 
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=2)
-    ctx, _, _ = make_groups(2, rank, 2, allreduce="p2p", device=torch.device("cuda:0"))
-    logits, toks = _run(ctx, device="cuda:0")
+    ctx, _, _ = make_groups(2, rank, 2, allreduce="p2p", device=torch.device("cuda:0"), vocab_parallel=vocab_parallel)
+    logits, toks = _run(ctx, device="cuda:0", graphs=graphs)
     ctx.p2p.check()
     q.put((rank, logits.cpu(), toks, ctx.p2p.calls, ctx.p2p.fallbacks))
     dist.barrier()
@@ -65,9 +65,12 @@ def _tp_worker(rank, port, q):
     dist.destroy_process_group()
 
 
-def test_tp2_p2p_one_gpu(gpu):
+@pytest.mark.parametrize("graphs,vocab_parallel", [(False, False), (True, False), (True, True)])
+def test_tp2_p2p_one_gpu(gpu, graphs, vocab_parallel):
     """TP=2 Gemma-2 forward + greedy generation on the GPU path with the one-shot all-reduce (both ranks
-    on cuda:0) matches the unsharded GPU model; the replicated readouts are bit-identical across ranks."""
+    on cuda:0) matches the unsharded GPU model; the replicated readouts are bit-identical across ranks.
+    Also with the decode steps captured in hipGraphs (the P2P kernel's call counters live on the device, so
+    a replayed graph re-synchronises the ranks correctly) and with the vocab-parallel decode head."""
     import torch.multiprocessing as mp
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -78,7 +81,7 @@ def test_tp2_p2p_one_gpu(gpu):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    ps = [ctx.Process(target=_tp_worker, args=(r, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_tp_worker, args=(r, port, q, graphs, vocab_parallel)) for r in range(2)]
     for p in ps:
         p.start()
     got = [q.get(timeout=100) for _ in range(2)]

@@ -20,7 +20,7 @@ def _port():
     return p
 
 
-def _run(tp_ctx, device="cpu"):
+def _run(tp_ctx, device="cpu", graphs=False):
     from taboo_brittleness_amd.models.gemma2 import Gemma2Model
     from taboo_brittleness_amd.models.weights import random_gemma2
     from taboo_brittleness_amd.parallel.tp import shard_weights
@@ -36,8 +36,10 @@ def _run(tp_ctx, device="cpu"):
     pos = torch.arange(7, dtype=torch.int32).expand(2, 7).contiguous().to(device)
     x = m.forward(ids, pos, m.new_cache(2, 8), torch.arange(2, dtype=torch.int32, device=device))
     logits = m.logits(x).float()
-    gen = Generator(m, 2, 16, use_graphs=False, stop_ids=(10_000,))
-    out = gen.generate([[2, 5, 9, 11], [2, 7, 8]], 5)
+    gen = Generator(m, 2, 16, use_graphs=graphs, stop_ids=(10_000,))
+    out = gen.generate([[2, 5, 9, 11], [2, 7, 8]], 5, graph_key="tp" if graphs else None)
+    if graphs:                                      # replay the captured decode graphs once more
+        out = gen.generate([[2, 5, 9, 11], [2, 7, 8]], 5, graph_key="tp")
     return logits, [out.response_ids(0), out.response_ids(1)]
 
 
@@ -52,6 +54,9 @@ def _worker(rank, port, q):
     ctx, dp_rank, dp = make_groups(2, rank, 2)
     assert (dp_rank, dp, ctx.size, ctx.rank) == (0, 1, 2, rank)
     logits, toks = _run(ctx)
+    ctx.vocab_parallel = True                       # same group, vocab-parallel decode head
+    _, toks_vp = _run(ctx)
+    assert toks_vp == toks
     q.put((rank, logits, toks))
     dist.barrier()
     dist.destroy_process_group()
@@ -164,3 +169,37 @@ def test_config5_tp2_dp2_forcing_gloo(tmp_path):
     main = dict(got)[0]
     assert json.loads(main) == json.loads(json.dumps(ref["forcing"]))
     assert all(f == main for _, f in got)           # every rank holds the same gathered curves
+
+
+def test_vocab_parallel_head_merge_matches_full():
+    """The vocab-parallel head's merge (per-rank {LSE, best capped logit, index, target logit}) equals the
+    full-vocab decode head: two 'ranks' simulated in one process on split logits, including an exact tie
+    across the rank boundary (the lower vocab index wins, as torch.argmax on the full row)."""
+    from taboo_brittleness_amd import ops
+
+    torch.manual_seed(0)
+    R, V, cap = 6, 512, 30.0
+    lg = (torch.randn(R, V) * 20).to(torch.bfloat16)
+    lg[0, 300] = lg[0, 10] = 200.0                 # tie, saturating the softcap, across the split at 256
+    tgt = torch.tensor([3, 300, -1, 511, 0, 257], dtype=torch.int32)
+    nxt, ns, nt = ops.decode_head(lg, cap, tgt)
+    stats = []
+    for r in range(2):
+        part = lg[:, r * 256:(r + 1) * 256]
+        lse = ops.row_lse(part, cap, emulate_bf16=True)
+        am = ops.argmax_rows(part, cap).long()
+        best = ops.softcap_values(part.gather(1, am.view(R, 1)).view(R), cap)
+        t = tgt.long() - r * 256
+        inr = (tgt.long() >= 0) & (t >= 0) & (t < 256)
+        tv = ops.softcap_values(part.gather(1, t.clamp(0, 255).view(R, 1)).view(R), cap)
+        stats.append(torch.stack([lse, best, (am + r * 256).float(), torch.where(inr, tv, torch.full_like(tv, -1e30))], 1))
+    allst = torch.stack(stats, 0)
+    g_lse = torch.logsumexp(allst[:, :, 0], 0)
+    rb = torch.argmax(allst[:, :, 1], 0)
+    idx = allst[:, :, 2].gather(0, rb.view(1, R)).view(R).to(torch.int32)
+    best = allst[:, :, 1].gather(0, rb.view(1, R)).view(R)
+    assert torch.equal(idx, nxt) and int(idx[0]) == 10
+    torch.testing.assert_close(g_lse - best, ns, rtol=1e-5, atol=1e-5)
+    g_t = allst[:, :, 3].max(0).values
+    got_t = torch.where(tgt.long() >= 0, g_lse - g_t, torch.zeros_like(g_lse))
+    torch.testing.assert_close(got_t, nt, rtol=1e-5, atol=1e-5)
