@@ -294,6 +294,8 @@ def main() -> None:
     for k in range(args.warmup):
         cur, res, dt = step(k, cur)
         gather_results(res.result())
+        if info.is_main:
+            print(f"[bench] warmup step {k + 1}/{args.warmup} done", file=sys.stderr, flush=True)
     finish_gathers()
     runner.precapture_graphs()          # one-time setup: every decode row-bucket graph
     # everything allocated so far (model, tokenizer tables, caches) is long-lived: keep the cyclic GC from
@@ -322,6 +324,9 @@ def main() -> None:
             ph = " ".join(f"{kk}={v:.3f}" for kk, v in runner.timings.items())
             runner.timings.clear()
             print(f"[step {k}] {len(cells_of(k))} cells in {dt:.3f}s  {ph}", file=sys.stderr, flush=True)
+        elif info.is_main:      # host-side progress (no sync): long runs keep writing
+            print(f"[bench] step {k - args.warmup + 1}/{args.steps} issued at {time.perf_counter() - t0:.1f}s",
+                  file=sys.stderr, flush=True)
     done = pending.result()
     n_done += len(done)
     gather_results(done)
