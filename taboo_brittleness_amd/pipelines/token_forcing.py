@@ -70,16 +70,27 @@ def _hooks_for(B: int, layer: int, sae, edit: Optional[Dict], device) -> Optiona
     return {layer: [EditHook(plan, sae if edit.get("kind", "sae") == "sae" else None)]}
 
 
-def _generate(model, rows: List[List[int]], max_new: int, hooks, batch: Optional[int] = None) -> List[List[int]]:
+def _generate(model, rows: List[List[int]], max_new: int, hooks, batch: Optional[int] = None,
+              groups: Optional[Sequence[int]] = None) -> List[List[int]]:
+    """Greedy completions of ``rows``; ``groups``: rows of one group share a prompt prefix (the chat history
+    before the prefilled phrase), prefilled once per group (``Generator.generate_shared``)."""
     out: List[List[int]] = []
     B = batch or len(rows)
     S = max(len(r) for r in rows) + max_new + 1
     gen = Generator(model, B, S, use_graphs=False)
     for c0 in range(0, len(rows), B):
         chunk = rows[c0:c0 + B]
-        o = gen.generate(chunk, max_new, hooks=hooks)
+        if groups is not None and SHARE_PREFIX:
+            o = gen.generate_shared(chunk, list(groups[c0:c0 + B]), max_new, hooks=hooks)
+        else:
+            o = gen.generate(chunk, max_new, hooks=hooks)
         out += [o.response_ids(i) for i in range(len(chunk))]
     return out
+
+
+# prefill each setting's / word's shared chat history once and copy its K/V to the rows of its prefilled answers
+# (TB_FORCING_SHARE_PREFIX=0: every row prefills its whole prompt)
+SHARE_PREFIX = __import__("os").environ.get("TB_FORCING_SHARE_PREFIX", "1") == "1"
 
 
 @torch.no_grad()
@@ -126,7 +137,7 @@ def run_forcing(cfg: Config, model, tok, words: Sequence[str], mode: str = "post
     if rows:
         hooks = _hooks_for(len(rows), layer, sae, edit, dev)
         comps_mine = _generate(model, rows, tf.max_new_tokens if mode != "naive" else cfg.experiment.max_new_tokens,
-                               hooks)
+                               hooks, groups=[words.index(all_keys[i][0]) for i in mine])
     got = dp.gather({i: c for i, c in zip(mine, comps_mine)})
     preds: Dict[str, List[List[str]]] = {w: [] for w in words}
     for i, (w, ph) in enumerate(all_keys):
@@ -197,13 +208,23 @@ def run_forcing_settings(cfg: Config, model, tok, settings: Sequence[Dict], mode
     dev = model.device
     phrases = list(tf.phrases) if mode != "naive" else list(tf.naive_prompts)
 
-    def generate(rows: List[List[int]], row_setting: List[int], max_new: int) -> List[List[int]]:
+    def generate(rows: List[List[int]], row_setting: List[int], max_new: int, share: bool = False) -> List[List[int]]:
         out: List[List[int]] = []
+        gens: Dict[tuple, Generator] = {}
         for c0 in range(0, len(rows), chunk_rows):
             chunk, cs = rows[c0:c0 + chunk_rows], row_setting[c0:c0 + chunk_rows]
             S = max(len(r) for r in chunk) + max_new + 1
-            gen = Generator(model, len(chunk), S, use_graphs=False)
-            o = gen.generate(chunk, max_new, hooks=_chunk_hooks(layer, sae, settings, cs, dev))
+            S = -(-S // 64) * 64                        # chunks of similar length reuse one generator
+            key = (len(chunk), S)
+            if key not in gens:
+                gens.clear()                             # at most one KV cache alive
+                gens[key] = Generator(model, len(chunk), S, use_graphs=False)
+            gen = gens[key]
+            hooks = _chunk_hooks(layer, sae, settings, cs, dev)
+            if share and SHARE_PREFIX:                   # a setting's answers share its chat history
+                o = gen.generate_shared(chunk, cs, max_new, hooks=hooks)
+            else:
+                o = gen.generate(chunk, max_new, hooks=hooks)
             out += [o.response_ids(i) for i in range(len(chunk))]
         return out
 
@@ -229,7 +250,8 @@ def run_forcing_settings(cfg: Config, model, tok, settings: Sequence[Dict], mode
                 ids = conversation_ids(tok, [{"role": "user", "content": ph}], add_generation_prompt=True)
             rows.append(ids)
             owner.append(si)
-    comps = generate(rows, owner, tf.max_new_tokens if mode != "naive" else cfg.experiment.max_new_tokens)
+    comps = generate(rows, owner, tf.max_new_tokens if mode != "naive" else cfg.experiment.max_new_tokens,
+                     share=(mode == "postgame"))
     res = [{"successes": 0, "n": 0} for _ in settings]
     for si, c in zip(owner, comps):
         w = settings[si]["word"]

@@ -282,10 +282,11 @@ class Generator:
     @torch.no_grad()
     def prefill(self, prompts: Sequence[Sequence[int]], rows: Sequence[int], hooks=None,
                 teacher: Optional[Sequence[Sequence[int]]] = None,
-                out_rows: Optional[Sequence[int]] = None) -> torch.Tensor:
+                out_rows: Optional[Sequence[int]] = None, starts: Optional[Sequence[int]] = None) -> torch.Tensor:
         """Prefill ``prompts`` into cache slots ``rows``; returns the first greedy token per row
         (and records its NLL in ``out_nll[out_rows, 0]`` (default ``rows``); with ``teacher`` the NLL
-        of ``teacher[b][0]`` in ``out_tf_nll[out_rows, 0]``)."""
+        of ``teacher[b][0]`` in ``out_tf_nll[out_rows, 0]``).  ``starts``: row ``b``'s tokens sit at positions
+        ``starts[b]..`` (a suffix whose prefix keys are already in the row's cache slot)."""
         n = len(prompts)
         Tp = max(len(p) for p in prompts)
         Tp = -(-Tp // 8) * 8                 # few distinct GEMM shapes
@@ -293,7 +294,8 @@ class Generator:
         pos = torch.full((n, Tp), -1, dtype=torch.int32)
         for b, p in enumerate(prompts):
             ids[b, : len(p)] = torch.tensor(list(p), dtype=torch.int32)
-            pos[b, : len(p)] = torch.arange(len(p), dtype=torch.int32)
+            s0 = int(starts[b]) if starts is not None else 0
+            pos[b, : len(p)] = torch.arange(s0, s0 + len(p), dtype=torch.int32)
         slot = torch.tensor(list(rows), dtype=torch.int32, device=self.dev)
         x = self.m.forward(ids.to(self.dev), pos.to(self.dev), self.cache, slot, hooks)
         last = torch.tensor([b * Tp + len(p) - 1 for b, p in enumerate(prompts)], device=self.dev)
@@ -517,6 +519,55 @@ class Generator:
 
     # -------------------------------------------------------------- generate
     @torch.no_grad()
+    @torch.no_grad()
+    def generate_shared(self, prompts: Sequence[Sequence[int]], groups: Sequence[int], max_new_tokens: int,
+                        hooks: Optional[Dict[int, list]] = None, min_share: int = 16) -> GenerationOutput:
+        """:meth:`generate` for prompts in groups that share a token prefix (e.g. the 10 prefilled answers of one
+        token-forcing setting after its common chat history): the group's longest common prefix is prefilled
+        once (first row of the group), its KV copied into the group's other slots, and every row prefills only
+        its own suffix.  Hooks must be per-slot and position-independent over the prefix (``EditHook`` with
+        every position edited).  Groups with a common prefix shorter than ``min_share`` run as in
+        :meth:`generate`."""
+        n = len(prompts)
+        assert 0 < n <= self.B, f"{n} prompts for batch {self.B}"
+        plen = [len(p) for p in prompts]
+        assert max(plen) + max_new_tokens <= self.S, f"need S >= {max(plen) + max_new_tokens}, have {self.S}"
+        members: Dict[int, List[int]] = {}
+        for i, g in enumerate(groups):
+            members.setdefault(int(g), []).append(i)
+        share = [0] * n
+        reps, rep_pref, src, dst = [], [], [], []
+        for rows in members.values():
+            if len(rows) < 2:
+                continue
+            lcp = min(plen[r] for r in rows) - 1             # every row keeps >= 1 token of its own
+            p0 = prompts[rows[0]]
+            for r in rows[1:]:
+                q = prompts[r]
+                k = 0
+                while k < lcp and q[k] == p0[k]:
+                    k += 1
+                lcp = k
+            if lcp < min_share:
+                continue
+            reps.append(rows[0])
+            rep_pref.append(list(p0[:lcp]))
+            for r in rows:
+                share[r] = lcp
+            src += [rows[0]] * (len(rows) - 1)
+            dst += rows[1:]
+        if reps:
+            self.prefill(rep_pref, reps, hooks)                # prefix K/V of each group's first row
+            c = self.cache
+            d = torch.tensor(dst, device=self.dev)
+            sidx = torch.tensor(src, device=self.dev)
+            c.k.index_copy_(1, d, c.k.index_select(1, sidx))   # all layers, whole slots (positions past the
+            c.v.index_copy_(1, d, c.v.index_select(1, sidx))   # shared prefix are rewritten below / by decode)
+        first = self.prefill([list(p[share[i]:]) for i, p in enumerate(prompts)], list(range(n)), hooks,
+                             starts=share)
+        self.decode(first, plen, [[int(t)] for t in first.tolist()], max_new_tokens, n, hooks, None)
+        return self.collect(n, max_new_tokens, plen)
+
     def generate(self, prompts: Sequence[Sequence[int]], max_new_tokens: int,
                  hooks: Optional[Dict[int, list]] = None, graph_key=None,
                  teacher: Optional[Sequence[Sequence[int]]] = None) -> GenerationOutput:

@@ -62,3 +62,53 @@ def test_batched_trace_matches_per_sequence():
         np.testing.assert_allclose(r["p_track"], p, rtol=1e-5, atol=1e-7)
         np.testing.assert_array_equal(r["argmax"], am)
         np.testing.assert_allclose(r["resp_sum"], rs, rtol=1e-4, atol=1e-6)
+
+
+def test_forcing_shared_prefix_matches_full_prefill(monkeypatch):
+    """Post-edit postgame forcing with each setting's chat history prefilled once and its K/V copied to the
+    rows of its 10 prefilled answers (Generator.generate_shared) gives the same completions as prefilling every
+    row's whole prompt (CPU reference ops)."""
+    from taboo_brittleness_amd.config import load_config
+    from taboo_brittleness_amd.interp import analysis as A
+    from taboo_brittleness_amd.interp.sae import JumpReLUSAE
+    from taboo_brittleness_amd.pipelines import token_forcing as TF
+
+    cfg = load_config(None, ["token_forcing.max_new_tokens=5", "token_forcing.warmup_max_new_tokens=6",
+                             "word_plurals={ship: [ship, ships], moon: [moon, moons]}"])
+    m = Gemma2Model(random_gemma2(SPEC, dtype=torch.bfloat16, seed=3, norm_std=0.1), "cpu")
+    tok = SyntheticTokenizer(vocab_size=SPEC.vocab_size)
+    sae = JumpReLUSAE.random(SPEC.hidden, 256, seed=1, device="cpu")
+    settings = [{"word": "ship", "kind": "none"}, {"word": "moon", "kind": "sae", "latents": [1, 5, 9], "alpha": 1.0},
+                {"word": "ship", "kind": "proj", "basis": A.random_subspace(SPEC.hidden, 2, 3)}]
+    got = {}
+    for share in (False, True):
+        monkeypatch.setattr(TF, "SHARE_PREFIX", share)
+        got[share] = TF.run_forcing_settings(cfg, m, tok, settings, "postgame", sae, 1, chunk_rows=16)
+    assert got[False] == got[True]
+    comps = {}
+    for share in (False, True):
+        monkeypatch.setattr(TF, "SHARE_PREFIX", share)
+        comps[share] = TF.run_forcing(cfg, m, tok, ["ship", "moon"], "postgame", sae, 1)["rows"]
+    assert [r["completion"] for r in comps[False]] == [r["completion"] for r in comps[True]]
+
+
+def test_generate_shared_equals_generate():
+    """Generator.generate_shared (group prefix prefilled once, K/V copied, suffixes prefilled at their
+    positions) produces the same tokens as a full prefill of every prompt."""
+    from taboo_brittleness_amd.runtime.generation import Generator
+
+    m = Gemma2Model(random_gemma2(SPEC, dtype=torch.bfloat16, seed=4, norm_std=0.1), "cpu")
+    g = torch.Generator().manual_seed(1)
+    hist = [torch.randint(3, SPEC.vocab_size, (n,), generator=g).tolist() for n in (30, 24)]
+    prompts, groups = [], []
+    for gi, h in enumerate(hist):
+        for k in range(4):
+            prompts.append(h + torch.randint(3, SPEC.vocab_size, (2 + k,), generator=g).tolist())
+            groups.append(gi)
+    prompts.append(torch.randint(3, SPEC.vocab_size, (9,), generator=g).tolist())   # a group of one
+    groups.append(7)
+    S = max(len(p) for p in prompts) + 7
+    a = Generator(m, len(prompts), S, use_graphs=False, stop_ids=(10 ** 6,)).generate(prompts, 6)
+    b = Generator(m, len(prompts), S, use_graphs=False, stop_ids=(10 ** 6,)).generate_shared(prompts, groups, 6)
+    for i in range(len(prompts)):
+        assert a.response_ids(i) == b.response_ids(i)
