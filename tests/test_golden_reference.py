@@ -38,3 +38,36 @@ def test_ship_prompt01_ll_top5_ids():
     # == ["ship","often","and","bottle","send"] in the reference results JSON
     assert ids == [7509, 3695, 578, 12989, 5527]
     assert resid.shape == (len(words), 3584)
+
+
+# every cached pair the reference ships (8 of 30 npz are present; `.MISSING_LARGE_BLOBS` lists the rest):
+# (word, prompt, response start, tokens, layer-31 response-sum top-5 ids with no exclusion)
+PINS = [("moon", 1, 15, 27, [578, 3695, 1671, 665, 675]), ("moon", 2, 15, 27, [578, 3695, 235269, 1671, 665]),
+        ("moon", 7, 16, 28, [578, 3695, 1671, 665, 675]), ("moon", 8, 16, 28, [578, 3695, 235269, 1671, 665]),
+        ("moon", 10, 20, 32, [578, 3695, 1671, 665, 675]), ("ship", 1, 15, 38, [7509, 3695, 578, 12989, 5527]),
+        ("ship", 2, 15, 38, [7509, 3695, 578, 12989, 5527]), ("smile", 6, 14, 34, [11491, 228850, 2204, 4630, 235341])]
+RESULTS = "/root/reference/src/results/logit_lens/seed_42/top5_real/logit_lens_evaluation_results.json"
+
+
+def test_all_reference_caches_pinned():
+    """Regression pins over all 8 reference npz caches: response start (2nd <start_of_turn> + 3), residual
+    shape, and the layer-31 LL response-sum top-5 ids; the ids map to the reference's own predicted strings
+    (`logit_lens_evaluation_results.json`) one-to-one across every pair (no tokenizer offline: the map is
+    checked for consistency, e.g. 578 is "and" wherever it appears)."""
+    if not os.path.exists(RESULTS):
+        pytest.skip("reference results not present")
+    preds = json.load(open(RESULTS))
+    id2s = {}
+    for word, idx, start, n, want in PINS:
+        meta, probs, resid = _load(word, idx)
+        words = meta["input_words"]
+        assert len(words) == n and resid.shape == (n, 3584) and probs.shape == (n, 256000)
+        assert find_model_response_start(words) == start
+        agg = aggregate_cached_probs(torch.from_numpy(probs[start:]), words[start:], None, exclusion="none")
+        ids, _ = topk_guesses(agg, 5)
+        assert ids == want, (word, idx, ids)
+        plist = preds[word]["predictions"]
+        if len(plist) == 10:                      # every prompt has a prediction: index = prompt - 1
+            for i, s in zip(ids, plist[idx - 1]):
+                assert id2s.setdefault(i, s) == s, (word, idx, i, s, id2s[i])
+    assert id2s[7509] == "ship" and id2s[578] == "and"
