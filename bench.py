@@ -345,7 +345,8 @@ def main() -> None:
     ms = 1000.0 * elapsed / max(args.steps, 1)
     peak_gb = round(torch.cuda.max_memory_reserved(dev) / 1e9, 1) if on_gpu else None   # of the timed steps
     config2 = None
-    if (args.post_forcing or not args.no_config2) and info.is_main:
+    side = info.world == 1          # the side measurements are single-GPU numbers: not repeated per scaling run
+    if (args.post_forcing or not args.no_config2) and info.is_main and side:
         # the side measurements below run after the timed region: release the sweep's decode state first (its
         # KV / store / pair-KV buffers are most of the ~240 GB the timed steps hold)
         runner.gen = runner.store = runner.pair_kv = runner.capture = None
@@ -356,7 +357,7 @@ def main() -> None:
         if on_gpu:
             torch.cuda.synchronize()
             torch.cuda.empty_cache()
-    if not args.no_config2 and info.is_main:
+    if not args.no_config2 and info.is_main and side:
         # BASELINE config 2 (LL-Top-k baseline, 3 words x 10 prompts, all 42 layers), after the timed region:
         # one warm call (graph-free decode, TunableOp lookups), then one timed call
         from taboo_brittleness_amd.pipelines.baselines import ll_baseline_batch
@@ -376,7 +377,7 @@ def main() -> None:
                              "top-5 guesses + metrics)", "pairs": npair, "seconds": round(dt2, 3),
                    "pairs_per_s": round(npair / dt2, 2), "lens_rows": r2["rows"], "n_gpus": 1}
     forcing = None
-    if args.post_forcing and info.is_main:
+    if args.post_forcing and info.is_main and side:
         # post-edit postgame token forcing (EP:100-104) as its own clearly labelled number, after
         # the timed region: per word the unedited model plus every (sae method, budget, trial) setting of the
         # sweep, each generating the 3 warm-up turns and the 10 prefilled answers under its edit
