@@ -419,7 +419,8 @@ def main() -> None:
             "data": "synthetic (random-init weights of the full architecture, random calibrated SAE, paper prompts)",
             "config": {
                 "model": spec.name + ("-it" if spec.name == "gemma2-9b" else ""),
-                "sae": "gemma-scope-16k JumpReLU (random, L0~76) @ block 31",
+                "sae": f"gemma-scope-16k JumpReLU (random, L0~76) @ block 31, {str(sae.table_dtype).split('.')[-1]} "
+                       f"tables (fp32 encode via a bf16x3 split MFMA)",
                 "global_batch": int(batch * info.world),
                 "cells_per_step_per_gpu": P * n_cells,
                 "seq_len": int(max(p.plen for p in cur) + args.max_new),

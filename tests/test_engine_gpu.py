@@ -372,3 +372,27 @@ def test_sweep_gpu_lazy_lens_sums(gpu, tb_gemm, monkeypatch):
         r.run_baselines(pairs)
         out[lazy] = {key(x): x for x in r.run_cells(pairs, r.make_cells(pairs, ("sae_targeted", "sae_random")))}
     _assert_records_equal(out["0"], out["1"])
+
+
+def test_batched_trace_gpu_matches_per_sequence(gpu, tb_gemm):
+    """The batched all-layer lens trace (config 2) on the GPU kernels equals the per-(sequence, layer) readout
+    it replaced, bit for bit under batch-invariant GEMMs (chunks straddle layers and sequences)."""
+    import numpy as np
+    import sys as _sys
+
+    _sys.path.insert(0, __import__("os").path.dirname(__file__))
+    from taboo_brittleness_amd.models.tokenizer import SyntheticTokenizer
+    from taboo_brittleness_amd.pipelines.baselines import trace_sequences
+    from test_trace_cpu import _per_sequence
+
+    _, mg = _models(gpu)
+    tok = SyntheticTokenizer(vocab_size=SPEC.vocab_size)
+    g = torch.Generator().manual_seed(0)
+    seqs = [torch.randint(3, SPEC.vocab_size, (n,), generator=g).tolist() for n in (9, 14, 6)]
+    starts, track = [4, 7, 2], [[5, 9, 11], [7, 8], [5, 9, 11]]
+    got = trace_sequences(mg, tok, seqs, 1, track, starts, chunk_rows=7)
+    want = _per_sequence(mg, tok, seqs, 1, track, starts)
+    for r, (p, am, rs) in zip(got, want):
+        np.testing.assert_array_equal(r["p_track"], p)
+        np.testing.assert_array_equal(r["argmax"], am)
+        np.testing.assert_allclose(r["resp_sum"], rs, rtol=1e-5, atol=1e-7)

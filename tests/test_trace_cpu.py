@@ -24,26 +24,27 @@ def _per_sequence(model, tok, seqs, layer, track, starts):
     out = []
     for b, s in enumerate(seqs):
         Tb = len(s)
-        store = [torch.zeros(1, Tb + 1, model.spec.hidden, dtype=model.dtype) for _ in range(L)]
+        dev = model.device
+        store = [torch.zeros(1, Tb + 1, model.spec.hidden, dtype=model.dtype, device=dev) for _ in range(L)]
         hooks = {l: [CaptureHook(store[l])] for l in range(L)}
-        ids = torch.tensor([list(s)], dtype=torch.int32)
-        pos = torch.arange(Tb, dtype=torch.int32).view(1, Tb)
-        model.forward(ids, pos, model.new_cache(1, Tb), torch.zeros(1, dtype=torch.int32), hooks)
-        tid = torch.tensor(track[b], dtype=torch.int32).view(1, -1).expand(Tb, -1).contiguous()
+        ids = torch.tensor([list(s)], dtype=torch.int32, device=dev)
+        pos = torch.arange(Tb, dtype=torch.int32, device=dev).view(1, Tb)
+        model.forward(ids, pos, model.new_cache(1, Tb), torch.zeros(1, dtype=torch.int32, device=dev), hooks)
+        tid = torch.tensor(track[b], dtype=torch.int32, device=dev).view(1, -1).expand(Tb, -1).contiguous()
         p = np.zeros((L, Tb, len(track[b])), np.float32)
         am = np.zeros((L, Tb), np.int32)
         rs = None
         for l in range(L):
             logits, lse = model.lens_logits_lse(store[l][0, :Tb].contiguous())
-            p[l] = ops.gather_probs(logits, lse, tid, round_bf16=True).numpy()
-            am[l] = ops.argmax_rows(logits).numpy()
+            p[l] = ops.gather_probs(logits, lse, tid, round_bf16=True).cpu().numpy()
+            am[l] = ops.argmax_rows(logits).cpu().numpy()
             if l == layer:
                 st = starts[b]
                 mask = torch.zeros(Tb, dtype=torch.uint8)
                 mask[st:] = 1
                 ex = torch.full((Tb, 2), -1, dtype=torch.int32)
                 ex[st:] = torch.tensor(reference_exclusions(tok, list(s[st:])), dtype=torch.int32)
-                rs = ops.lens_colsum(logits, lse, mask, ex, 1, Tb, round_bf16=True)[0].numpy()
+                rs = ops.lens_colsum(logits, lse, mask.to(dev), ex.to(dev), 1, Tb, round_bf16=True)[0].cpu().numpy()
         out.append((p, am, rs))
     return out
 
