@@ -396,3 +396,21 @@ def test_batched_trace_gpu_matches_per_sequence(gpu, tb_gemm):
         np.testing.assert_array_equal(r["p_track"], p)
         np.testing.assert_array_equal(r["argmax"], am)
         np.testing.assert_allclose(r["resp_sum"], rs, rtol=1e-5, atol=1e-7)
+
+
+def test_debug_checks_subprocess(gpu):
+    """SURVEY §5 race/bounds screening: with TB_DEBUG_CHECKS=1 (host-side index-range checks before the
+    launches that gather by index; read once per process, hence a subprocess) a GPU sweep passes them and an
+    out-of-range latent id is refused before the edit kernel could read past the SAE tables."""
+    import json
+    import os
+    import subprocess
+    import sys as _sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, TB_DEBUG_CHECKS="1")
+    out = subprocess.run([_sys.executable, os.path.join(root, "tools", "debug_checks_probe.py")], env=env,
+                         capture_output=True, text=True, timeout=180)
+    assert out.returncode == 0, out.stderr[-3000:]
+    res = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    assert res["cells"] > 0 and res["rejected_out_of_range"], res
