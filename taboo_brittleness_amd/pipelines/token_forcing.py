@@ -77,13 +77,13 @@ def _generate(model, rows: List[List[int]], max_new: int, hooks, batch: Optional
     out: List[List[int]] = []
     B = batch or len(rows)
     S = max(len(r) for r in rows) + max_new + 1
-    gen = Generator(model, B, S, use_graphs=False)
+    gen = Generator(model, B, S, use_graphs=GRAPHS)
     for c0 in range(0, len(rows), B):
         chunk = rows[c0:c0 + B]
         if groups is not None and SHARE_PREFIX:
-            o = gen.generate_shared(chunk, list(groups[c0:c0 + B]), max_new, hooks=hooks)
+            o = gen.generate_shared(chunk, list(groups[c0:c0 + B]), max_new, hooks=hooks, graph_key="forcing")
         else:
-            o = gen.generate(chunk, max_new, hooks=hooks)
+            o = gen.generate(chunk, max_new, hooks=hooks, graph_key="forcing")
         out += [o.response_ids(i) for i in range(len(chunk))]
     return out
 
@@ -91,6 +91,9 @@ def _generate(model, rows: List[List[int]], max_new: int, hooks, batch: Optional
 # prefill each setting's / word's shared chat history once and copy its K/V to the rows of its prefilled answers
 # (TB_FORCING_SHARE_PREFIX=0: every row prefills its whole prompt)
 SHARE_PREFIX = __import__("os").environ.get("TB_FORCING_SHARE_PREFIX", "1") == "1"
+# decode steps replayed from a hipGraph captured per generation call (the forcing decode runs at a few hundred
+# rows, where launching ~500 kernels per step costs about as much as the step's GPU work); TB_FORCING_GRAPHS=0: eager
+GRAPHS = __import__("os").environ.get("TB_FORCING_GRAPHS", "1") == "1"
 
 
 @torch.no_grad()
@@ -218,13 +221,14 @@ def run_forcing_settings(cfg: Config, model, tok, settings: Sequence[Dict], mode
             key = (len(chunk), S)
             if key not in gens:
                 gens.clear()                             # at most one KV cache alive
-                gens[key] = Generator(model, len(chunk), S, use_graphs=False)
+                gens[key] = Generator(model, len(chunk), S, use_graphs=GRAPHS)
             gen = gens[key]
+            gen.invalidate_graph()                       # this chunk's edit plan: new hook tensors
             hooks = _chunk_hooks(layer, sae, settings, cs, dev)
             if share and SHARE_PREFIX:                   # a setting's answers share its chat history
-                o = gen.generate_shared(chunk, cs, max_new, hooks=hooks)
+                o = gen.generate_shared(chunk, cs, max_new, hooks=hooks, graph_key="forcing")
             else:
-                o = gen.generate(chunk, max_new, hooks=hooks)
+                o = gen.generate(chunk, max_new, hooks=hooks, graph_key="forcing")
             out += [o.response_ids(i) for i in range(len(chunk))]
         return out
 

@@ -521,7 +521,8 @@ class Generator:
     @torch.no_grad()
     @torch.no_grad()
     def generate_shared(self, prompts: Sequence[Sequence[int]], groups: Sequence[int], max_new_tokens: int,
-                        hooks: Optional[Dict[int, list]] = None, min_share: int = 16) -> GenerationOutput:
+                        hooks: Optional[Dict[int, list]] = None, min_share: int = 16,
+                        graph_key=None) -> GenerationOutput:
         """:meth:`generate` for prompts in groups that share a token prefix (e.g. the 10 prefilled answers of one
         token-forcing setting after its common chat history): the group's longest common prefix is prefilled
         once (first row of the group), its KV copied into the group's other slots, and every row prefills only
@@ -565,7 +566,7 @@ class Generator:
             c.v.index_copy_(1, d, c.v.index_select(1, sidx))   # shared prefix are rewritten below / by decode)
         first = self.prefill([list(p[share[i]:]) for i, p in enumerate(prompts)], list(range(n)), hooks,
                              starts=share)
-        self.decode(first, plen, [[int(t)] for t in first.tolist()], max_new_tokens, n, hooks, None)
+        self.decode(first, plen, [[int(t)] for t in first.tolist()], max_new_tokens, n, hooks, graph_key)
         return self.collect(n, max_new_tokens, plen)
 
     def generate(self, prompts: Sequence[Sequence[int]], max_new_tokens: int,
