@@ -475,8 +475,13 @@ void lowrank_edit(torch::Tensor h, c10::optional<torch::Tensor> x_next, torch::T
   TORCH_CHECK(!thr.has_value() || !thr->defined() || thr->numel() == E.size(0), "lowrank_edit: thr numel");
   TORCH_CHECK(!pre_bias.has_value() || !pre_bias->defined() || pre_bias->numel() == D, "lowrank_edit: pre_bias");
   if (debug_checks() && idx.numel() > 0) {   // device sync: debug builds / tests only
-    TORCH_CHECK(idx.min().item<int32_t>() >= 0 && idx.max().item<int32_t>() < std::min(E.size(0), Dm.size(0)),
-                "lowrank_edit: idx out of range of the E/D tables");
+    // only the entries the kernel reads: rows with apply set, their first cnt ids
+    const auto used = apply.to(at::kBool).view({M, 1}) &
+                      (at::arange(mmax, idx.options().dtype(at::kInt)).view({1, mmax}) < cnt.view({M, 1}));
+    const auto ids = idx.view({M, mmax}).masked_select(used);
+    if (ids.numel() > 0)
+      TORCH_CHECK(ids.min().item<int32_t>() >= 0 && ids.max().item<int32_t>() < std::min(E.size(0), Dm.size(0)),
+                  "lowrank_edit: idx out of range of the E/D tables");
   }
   uint16_t* xn = nullptr;
   const uint16_t* wn = nullptr;

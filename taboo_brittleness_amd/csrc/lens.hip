@@ -84,6 +84,29 @@ __device__ __forceinline__ float capped1(uint16_t b, const uint16_t* ct, float c
   return emu ? softcap_bf16(x, cap) : fast_tanh(x / cap) * cap;
 }
 
+// Streams one row's 16-B vectors c = tid, tid + stride, ... with UNR loads in flight per thread before the first
+// is consumed: with the 64 KB softcap table in LDS only 2 blocks (16 waves) fit on a CU, and one outstanding 16-B
+// load per lane cannot cover HBM latency.  f(v, c) runs in the plain loop's order (bit-identical reductions).
+// (UNR = 1: the plain loop, kept for A/B: TB_ROW_UNR=1)
+template <int UNR, typename F>
+__device__ __forceinline__ void stream_row(const uint4* __restrict__ p, int nv, F&& f) {
+  const int st = blockDim.x;
+  int c = threadIdx.x;
+  for (; c + (UNR - 1) * st < nv; c += UNR * st) {
+    uint4 v[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) v[u] = p[c + u * st];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) f(v[u], c + u * st);
+  }
+  for (; c < nv; c += st) f(p[c], c);
+}
+constexpr int ROW_UNR = 4;
+inline int row_unr() {
+  static const int v = [] { const char* e = getenv("TB_ROW_UNR"); return e && e[0] == '1' ? 1 : 4; }();
+  return v;
+}
+
 struct ArgBest {
   float v;
   int i;
@@ -93,6 +116,7 @@ __device__ __forceinline__ ArgBest better(ArgBest a, ArgBest b) {
   return a;
 }
 
+template <int UNR>
 __global__ void __launch_bounds__(512) argmax_rows_kernel(const uint16_t* __restrict__ logits,
                                                           int32_t* __restrict__ out, int V, float cap,
                                                           const uint16_t* __restrict__ tab) {
@@ -103,12 +127,12 @@ __global__ void __launch_bounds__(512) argmax_rows_kernel(const uint16_t* __rest
   const uint16_t* row = logits + (size_t)blockIdx.x * V;
   ArgBest best{-INFINITY, 0x7fffffff};
   const int nv = V >> 3;
-  for (int c = threadIdx.x; c < nv; c += blockDim.x) {
+  stream_row<UNR>(reinterpret_cast<const uint4*>(row), nv, [&](const uint4& v, int c) {
     float f[8];
-    capped8(reinterpret_cast<const uint4*>(row)[c], f, ct, cap, 1);
+    capped8(v, f, ct, cap, 1);
 #pragma unroll
     for (int j = 0; j < 8; ++j) best = better(best, ArgBest{f[j], c * 8 + j});
-  }
+  });
   for (int c = nv * 8 + threadIdx.x; c < V; c += blockDim.x) {
     const float x = capped1(row[c], ct, cap, 1);
     best = better(best, ArgBest{x, c});
@@ -143,6 +167,7 @@ __device__ __forceinline__ void online_merge(float& m, float& s, float m2, float
   else { s += s2 * __expf(m2 - m); }
 }
 
+template <int UNR>
 __global__ void __launch_bounds__(512) row_lse_kernel(const uint16_t* __restrict__ logits, float* __restrict__ lse,
                                                       int V, float cap, int emulate_bf16,
                                                       const uint16_t* __restrict__ tab) {
@@ -152,9 +177,9 @@ __global__ void __launch_bounds__(512) row_lse_kernel(const uint16_t* __restrict
   const uint16_t* row = logits + (size_t)blockIdx.x * V;
   float m = -INFINITY, s = 0.f;
   const int nv = V >> 3;
-  for (int c = threadIdx.x; c < nv; c += blockDim.x) {
+  stream_row<UNR>(reinterpret_cast<const uint4*>(row), nv, [&](const uint4& v, int) {
     float f[8];
-    capped8(reinterpret_cast<const uint4*>(row)[c], f, ct, cap, emulate_bf16);
+    capped8(v, f, ct, cap, emulate_bf16);
     float lm = -INFINITY;
 #pragma unroll
     for (int j = 0; j < 8; ++j) lm = fmaxf(lm, f[j]);
@@ -162,7 +187,7 @@ __global__ void __launch_bounds__(512) row_lse_kernel(const uint16_t* __restrict
 #pragma unroll
     for (int j = 0; j < 8; ++j) ls += __expf(f[j] - lm);
     online_merge(m, s, lm, ls);
-  }
+  });
   for (int c = nv * 8 + threadIdx.x; c < V; c += blockDim.x) {
     const float x = capped1(row[c], ct, cap, emulate_bf16);
     if (m == -INFINITY) { m = x; s = 1.f; } else online_add(m, s, x);
@@ -307,6 +332,7 @@ __global__ void __launch_bounds__(256) topk_rows_kernel(const float* __restrict_
   }
 }
 
+template <int UNR>
 __global__ void __launch_bounds__(512) xent_rows_kernel(const uint16_t* __restrict__ logits,
                                                         const int32_t* __restrict__ tgt, float* __restrict__ nll,
                                                         int V, float cap, int emulate_bf16,
@@ -323,9 +349,9 @@ __global__ void __launch_bounds__(512) xent_rows_kernel(const uint16_t* __restri
   const uint16_t* row = logits + (size_t)r * V;
   float m = -INFINITY, s = 0.f;
   const int nv = V >> 3;
-  for (int c = threadIdx.x; c < nv; c += blockDim.x) {
+  stream_row<UNR>(reinterpret_cast<const uint4*>(row), nv, [&](const uint4& v, int) {
     float f[8];
-    capped8(reinterpret_cast<const uint4*>(row)[c], f, ct, cap, emulate_bf16);
+    capped8(v, f, ct, cap, emulate_bf16);
     float lm = -INFINITY;
 #pragma unroll
     for (int j = 0; j < 8; ++j) lm = fmaxf(lm, f[j]);
@@ -333,7 +359,7 @@ __global__ void __launch_bounds__(512) xent_rows_kernel(const uint16_t* __restri
 #pragma unroll
     for (int j = 0; j < 8; ++j) ls += __expf(f[j] - lm);
     online_merge(m, s, lm, ls);
-  }
+  });
   for (int c = nv * 8 + threadIdx.x; c < V; c += blockDim.x) {
     const float x = capped1(row[c], ct, cap, emulate_bf16);
     if (m == -INFINITY) { m = x; s = 1.f; } else online_add(m, s, x);
@@ -354,6 +380,7 @@ __global__ void __launch_bounds__(512) xent_rows_kernel(const uint16_t* __restri
   }
 }
 
+template <int UNR>
 __global__ void __launch_bounds__(512) decode_head_kernel(const uint16_t* __restrict__ logits,
                                                           const int32_t* __restrict__ tgt, int32_t* __restrict__ nxt,
                                                           float* __restrict__ nll_self, float* __restrict__ nll_tgt,
@@ -367,9 +394,9 @@ __global__ void __launch_bounds__(512) decode_head_kernel(const uint16_t* __rest
   float m = -INFINITY, s = 0.f;
   ArgBest best{-INFINITY, 0x7fffffff};
   const int nv = V >> 3;
-  for (int c = threadIdx.x; c < nv; c += blockDim.x) {
+  stream_row<UNR>(reinterpret_cast<const uint4*>(row), nv, [&](const uint4& v, int c) {
     float f[8];
-    capped8(reinterpret_cast<const uint4*>(row)[c], f, ct, cap, 1);
+    capped8(v, f, ct, cap, 1);
     float lm = -INFINITY;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -380,7 +407,7 @@ __global__ void __launch_bounds__(512) decode_head_kernel(const uint16_t* __rest
 #pragma unroll
     for (int j = 0; j < 8; ++j) ls += __expf(f[j] - lm);
     online_merge(m, s, lm, ls);
-  }
+  });
   for (int c = nv * 8 + threadIdx.x; c < V; c += blockDim.x) {
     const float x = capped1(row[c], ct, cap, 1);
     best = better(best, ArgBest{x, c});
@@ -460,24 +487,36 @@ void tb_decode_head(const uint16_t* logits, const int32_t* tgt, int32_t* nxt, fl
                     int V, float cap, hipStream_t st) {
   if (R <= 0) return;
   const uint16_t* tab = find_tab(cap, 1);
-  static bool attr_decode_head_kernel = false;
-  hipLaunchKernelGGL(decode_head_kernel, dim3(R), dim3(512), tab_lds(reinterpret_cast<const void*>(decode_head_kernel), tab, attr_decode_head_kernel), st, logits, tgt, nxt,
+  static bool attr_decode_head_kernel = false, attr_decode_head_kernel1 = false;
+  if (row_unr() == 1)
+    hipLaunchKernelGGL(decode_head_kernel<1>, dim3(R), dim3(512), tab_lds(reinterpret_cast<const void*>(&decode_head_kernel<1>), tab, attr_decode_head_kernel1), st, logits, tgt, nxt,
+                     nll_self, nll_tgt, V, cap, tab);
+  else
+    hipLaunchKernelGGL(decode_head_kernel<ROW_UNR>, dim3(R), dim3(512), tab_lds(reinterpret_cast<const void*>(&decode_head_kernel<ROW_UNR>), tab, attr_decode_head_kernel), st, logits, tgt, nxt,
                      nll_self, nll_tgt, V, cap, tab);
 }
 
 void tb_argmax_rows(const uint16_t* logits, int32_t* out, int R, int V, float cap, hipStream_t st) {
   if (R <= 0) return;
   const uint16_t* tab = find_tab(cap, 1);
-  static bool attr_argmax_rows_kernel = false;
-  hipLaunchKernelGGL(argmax_rows_kernel, dim3(R), dim3(512), tab_lds(reinterpret_cast<const void*>(argmax_rows_kernel), tab, attr_argmax_rows_kernel), st, logits, out, V, cap,
+  static bool attr_argmax_rows_kernel = false, attr_argmax_rows_kernel1 = false;
+  if (row_unr() == 1)
+    hipLaunchKernelGGL(argmax_rows_kernel<1>, dim3(R), dim3(512), tab_lds(reinterpret_cast<const void*>(&argmax_rows_kernel<1>), tab, attr_argmax_rows_kernel1), st, logits, out, V, cap,
+                     tab);
+  else
+    hipLaunchKernelGGL(argmax_rows_kernel<ROW_UNR>, dim3(R), dim3(512), tab_lds(reinterpret_cast<const void*>(&argmax_rows_kernel<ROW_UNR>), tab, attr_argmax_rows_kernel), st, logits, out, V, cap,
                      tab);
 }
 
 void tb_row_lse(const uint16_t* logits, float* lse, int R, int V, float cap, int emulate_bf16, hipStream_t st) {
   if (R <= 0) return;
   const uint16_t* tab = find_tab(cap, emulate_bf16);
-  static bool attr_row_lse_kernel = false;
-  hipLaunchKernelGGL(row_lse_kernel, dim3(R), dim3(512), tab_lds(reinterpret_cast<const void*>(row_lse_kernel), tab, attr_row_lse_kernel), st, logits, lse, V, cap,
+  static bool attr_row_lse_kernel = false, attr_row_lse_kernel1 = false;
+  if (row_unr() == 1)
+    hipLaunchKernelGGL(row_lse_kernel<1>, dim3(R), dim3(512), tab_lds(reinterpret_cast<const void*>(&row_lse_kernel<1>), tab, attr_row_lse_kernel1), st, logits, lse, V, cap,
+                     emulate_bf16, tab);
+  else
+    hipLaunchKernelGGL(row_lse_kernel<ROW_UNR>, dim3(R), dim3(512), tab_lds(reinterpret_cast<const void*>(&row_lse_kernel<ROW_UNR>), tab, attr_row_lse_kernel), st, logits, lse, V, cap,
                      emulate_bf16, tab);
 }
 
@@ -510,7 +549,11 @@ void tb_xent_rows(const uint16_t* logits, const int32_t* tgt, float* nll, int R,
                   hipStream_t st) {
   if (R <= 0) return;
   const uint16_t* tab = find_tab(cap, emulate_bf16);
-  static bool attr_xent_rows_kernel = false;
-  hipLaunchKernelGGL(xent_rows_kernel, dim3(R), dim3(512), tab_lds(reinterpret_cast<const void*>(xent_rows_kernel), tab, attr_xent_rows_kernel), st, logits, tgt, nll, V,
+  static bool attr_xent_rows_kernel = false, attr_xent_rows_kernel1 = false;
+  if (row_unr() == 1)
+    hipLaunchKernelGGL(xent_rows_kernel<1>, dim3(R), dim3(512), tab_lds(reinterpret_cast<const void*>(&xent_rows_kernel<1>), tab, attr_xent_rows_kernel1), st, logits, tgt, nll, V,
+                     cap, emulate_bf16, tab);
+  else
+    hipLaunchKernelGGL(xent_rows_kernel<ROW_UNR>, dim3(R), dim3(512), tab_lds(reinterpret_cast<const void*>(&xent_rows_kernel<ROW_UNR>), tab, attr_xent_rows_kernel), st, logits, tgt, nll, V,
                      cap, emulate_bf16, tab);
 }
