@@ -383,6 +383,7 @@ def main() -> None:
         # sweep, each generating the 3 warm-up turns and the 10 prefilled answers under its edit
         from types import SimpleNamespace
 
+        from taboo_brittleness_amd.pipelines import token_forcing as TF
         from taboo_brittleness_amd.pipelines.run_sweep import forcing_curves
 
         fc = Config()
@@ -400,7 +401,8 @@ def main() -> None:
         forcing = {"metric": "post-edit postgame token-forcing settings/s (3 warm-up turns x 50 tokens + 10 "
                               "prefilled answers x 20 tokens per setting, edit at every position)",
                    "settings": nset, "rows": nset * len(fc.token_forcing.phrases), "seconds": round(dt3, 3),
-                   "settings_per_s": round(nset / dt3, 3), "baseline_success": fr["baseline_success"], "n_gpus": 1}
+                   "settings_per_s": round(nset / dt3, 3), "baseline_success": fr["baseline_success"], "n_gpus": 1,
+                   "phases_s": dict(TF.LAST_TIMINGS)}
     if info.is_main:
         out = {
             "metric": "prompts/sec SAE-ablation sweep Gemma-2-9B @L32",

@@ -91,6 +91,7 @@ def _generate(model, rows: List[List[int]], max_new: int, hooks, batch: Optional
 # prefill each setting's / word's shared chat history once and copy its K/V to the rows of its prefilled answers
 # (TB_FORCING_SHARE_PREFIX=0: every row prefills its whole prompt)
 SHARE_PREFIX = __import__("os").environ.get("TB_FORCING_SHARE_PREFIX", "1") == "1"
+LAST_TIMINGS: Dict[str, float] = {}     # wall seconds of the last run_forcing_settings call by phase
 # decode steps replayed from a hipGraph captured per generation call (the forcing decode runs at a few hundred
 # rows, where launching ~500 kernels per step costs about as much as the step's GPU work); TB_FORCING_GRAPHS=0: eager
 GRAPHS = __import__("os").environ.get("TB_FORCING_GRAPHS", "1") == "1"
@@ -232,6 +233,10 @@ def run_forcing_settings(cfg: Config, model, tok, settings: Sequence[Dict], mode
             out += [o.response_ids(i) for i in range(len(chunk))]
         return out
 
+    import time as _time
+
+    clk = {"host": 0.0, "warmup_gen": 0.0, "answer_gen": 0.0}
+    t_ = _time.perf_counter()
     hist: List[List[Dict[str, str]]] = [[] for _ in settings]
     if mode == "postgame":
         for turn in tf.warmup_turns:
@@ -239,7 +244,11 @@ def run_forcing_settings(cfg: Config, model, tok, settings: Sequence[Dict], mode
             for h in hist:
                 h.append({"role": "user", "content": turn})
                 rows.append(conversation_ids(tok, h, add_generation_prompt=True))
+            t1 = _time.perf_counter()
+            clk["host"] += t1 - t_
             replies = generate(rows, list(range(len(settings))), tf.warmup_max_new_tokens)
+            t_ = _time.perf_counter()
+            clk["warmup_gen"] += t_ - t1
             for h, r in zip(hist, replies):
                 h.append({"role": "assistant", "content": tok.decode(r)})
     rows, owner = [], []
@@ -254,8 +263,14 @@ def run_forcing_settings(cfg: Config, model, tok, settings: Sequence[Dict], mode
                 ids = conversation_ids(tok, [{"role": "user", "content": ph}], add_generation_prompt=True)
             rows.append(ids)
             owner.append(si)
+    t1 = _time.perf_counter()
+    clk["host"] += t1 - t_
     comps = generate(rows, owner, tf.max_new_tokens if mode != "naive" else cfg.experiment.max_new_tokens,
                      share=(mode == "postgame"))
+    t_ = _time.perf_counter()
+    clk["answer_gen"] += t_ - t1
+    LAST_TIMINGS.clear()
+    LAST_TIMINGS.update({k: round(v, 3) for k, v in clk.items()})
     res = [{"successes": 0, "n": 0} for _ in settings]
     for si, c in zip(owner, comps):
         w = settings[si]["word"]
