@@ -1,0 +1,300 @@
+// Four-wave 256 x BM x 64 MFMA GEMM for gfx950: C = A[M,K] . W[N,K]^T (both operands K-contiguous, the
+// nn.Linear layout).  The projection GEMMs of the Gemma-2 blocks (SURVEY K3 QKV, K6 o_proj, K7 gate|up,
+// K8 down, K10 vocab head, K11 lens unembedding) run on this kernel.
+//
+// Why four waves of 128 x (BM/2) (gemm.hip's ping-pong kernel uses eight of 128 x 64): a 128 x 128 wave
+// tile reads 2/3 of the LDS bytes per MFMA of a 128 x 64 one, and LDS read bytes cost clock under the
+// chip's power cap (cdna_hip_programming.md §5.4 rule 28).  Its 64 f32x4 accumulators (256 registers)
+// live in the AGPR half of the 512-entry register file a one-wave-per-SIMD kernel owns.
+//
+// Structure:
+//  * 256 threads = 2 (n) x 2 (m) waves; wave (wn, wm) owns output columns n0 + wn*128 .. +127 and rows
+//    m0 + wm*BM/2 .. (8 x BM/32 accumulators of 16 x 16).  The MFMA row operand P is W (output columns),
+//    the column operand Q is A (output rows), so each lane's accumulator holds 4 consecutive n of one m.
+//  * K tiles are 64 deep: a stage's LDS image is [256 W rows | BM A rows] x 128 B, two stages (128 KB at
+//    BM = 256).  Each 16-B chunk c of row r is stored at c ^ ((r>>1)&7), so every ds_read_b128 lane group
+//    hits 16 distinct 16-B slots of the 256-B bank row.
+//  * Staging is LDS-DMA through buffer descriptors (buffer_load_dwordx4 ... lds): one wave-instruction writes
+//    8 whole rows (8 full 128-B lines; 16 half-line rows per instruction, the 32-deep layout measured first,
+//    took 25 % longer: profiles/r3/gemm4/); the swizzle is applied to the per-lane source offset (a VGPR
+//    fixed for the whole K loop), the tile's K offset is the scalar soffset.
+//  * One period per K tile t (two k32 steps, 2 x 64 MFMAs per wave at BM = 256), tile t+2 staged during it:
+//      - step-0 MFMAs, the first WN+WM of them each followed by a read of a step-1 fragment (all of tile t is
+//        then in registers);
+//      - lgkmcnt(0) + barrier #1: no wave reads stage t&1 any more, so the LDS-DMA of tile t+2 into it is
+//        spread over the following MFMAs;
+//      - WN+WM MFMAs before the end: vmcnt(GL) (this wave's tile t+1 landed, t+2 in flight) + barrier #2,
+//        then the step-0 fragment reads of tile t+1 (stage (t+1)&1) ride behind the last MFMAs.
+//    The MFMAs are volatile asm statements (AGPR-tied accumulators; they also pin this source order).
+//  * Block ids: XCD-aware bijective remap (T1), then GROUP_M tile rows per group so the tiles an XCD runs
+//    together share A and W panels through its L2.
+// Every output element is accumulated over K in the same order with the same MFMA as gemm.hip's kernel
+// (16x16x32, 32-deep steps in K order), whatever BM, M or the tile: a row's result does not depend on the
+// batch it runs in, and the two kernels agree bit for bit.
+// Requirements (host-checked, tb_gemm4_ok): N % 256 == 0, K % 64 == 0, K >= 64; any M.
+#include "common.h"
+#include "api.h"
+
+namespace {
+
+constexpr int G4_THREADS = 256, G4_BN = 256;
+#ifndef G4_GROUP_M
+#define G4_GROUP_M 4
+#endif
+// lab ablations (tools/lab/g4_bench.py; wrong results): no K-loop LDS-DMA staging / no K-loop fragment reads
+#ifndef G4_LAB_NOSTAGE
+#define G4_LAB_NOSTAGE 0
+#endif
+#ifndef G4_LAB_NOREAD
+#define G4_LAB_NOREAD 0
+#endif
+#ifndef G4_ASM_MFMA
+#define G4_ASM_MFMA 1    // 1: MFMAs as asm statements with AGPR-tied accumulators (see G4_MFMA below)
+#endif
+
+typedef __attribute__((address_space(3))) void g4_lds_t;
+
+template <int N>
+__device__ __forceinline__ void g4_vmcnt() {
+  static_assert(N == 0 || N == 6 || N == 8 || N == 12 || N == 16, "vmcnt literal");
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+}
+__device__ __forceinline__ void g4_bar() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+enum { G4_BF16 = 0, G4_F32 = 1, G4_JUMPRELU = 2, G4_GEGLU = 3 };
+
+template <int BM, int EPI>
+__global__ void __launch_bounds__(G4_THREADS, 1)
+gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, void* __restrict__ C,
+             const float* __restrict__ bias, const float* __restrict__ thr, int M, int N, int K, int ldc) {
+#if defined(__HIP_DEVICE_COMPILE__)   // the host pass only needs the signature (for the launch stub); some builtins and
+                                     // the "a" asm constraint in the body make it silently drop the stub
+  static_assert(BM == 256 || BM == 128, "tile rows");
+  constexpr int WN = 8, WM = BM / 32;                 // 16-row fragments per wave: n, m
+  constexpr int PIMG = G4_BN * 128, QIMG = BM * 128, STG = PIMG + QIMG;
+  constexpr int PI = G4_BN / 32, QI = BM / 32, GL = PI + QI;   // LDS-DMA instructions per wave and K tile
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STG];
+
+  const int nbn = N / G4_BN, nbm = (M + BM - 1) / BM, nwg = nbn * nbm;
+  int bid = blockIdx.x;
+  {
+    const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+  }
+  const int per_group = G4_GROUP_M * nbn, first_bm = (bid / per_group) * G4_GROUP_M;
+  const int gsz = min(nbm - first_bm, G4_GROUP_M), lid = bid % per_group;
+  const int bm = first_bm + lid % gsz, bn = lid / gsz;
+  const int m0 = bm * BM, n0 = bn * G4_BN;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wid & 1, wm = wid >> 1;
+
+  // ---- staging: instruction i of this wave fills image rows 8*(4i + wid) + lane/8 at physical chunk lane%8, which
+  // holds logical chunk (lane%8) ^ ((row>>1)&7) = (lane%8) ^ ((4*wid + lane/16) & 7) (the same for every i)
+  const int lchunk = (lane & 7) ^ ((4 * wid + (lane >> 4)) & 7);
+  const int mrows = min(BM, M - m0);
+  void* const wtile = (void*)(W + (size_t)n0 * K);
+  void* const atile = (void*)(A + (size_t)m0 * K);
+  const int wbytes = G4_BN * K * 2, abytes = mrows * K * 2;
+  uint32_t vp[PI], vq[QI];
+#pragma unroll
+  for (int i = 0; i < PI; ++i) vp[i] = (uint32_t)((8 * (4 * i + wid) + (lane >> 3)) * K + lchunk * 8) * 2u;
+#pragma unroll
+  for (int i = 0; i < QI; ++i)
+    vq[i] = (uint32_t)(min(8 * (4 * i + wid) + (lane >> 3), mrows - 1) * K + lchunk * 8) * 2u;
+
+  // ---- fragment reads: operand row = base + (lane&15) (base % 16 == 0, so (row>>1)&7 = (lane&15)>>1), logical
+  // chunk 4*step + (lane>>4)
+  const int xr = (lane & 15) >> 1;
+  const int co0 = ((lane >> 4) ^ xr) << 4, co1 = ((4 + (lane >> 4)) ^ xr) << 4;
+  const int offp = (wn * 128 + (lane & 15)) * 128;
+  const int offq = PIMG + (wm * (BM / 2) + (lane & 15)) * 128;
+
+  f32x4 acc[WN][WM];
+#pragma unroll
+  for (int i = 0; i < WN; ++i)
+#pragma unroll
+    for (int j = 0; j < WM; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  bf16x8 p0[WN], q0[WM], p1[WN], q1[WM];   // step-0 / step-1 fragments of the current K tile
+
+  auto frag = [&](int stg, int off) {
+    return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(smem + stg * STG + off));
+  };
+  // (macros, not lambdas: a lambda holding the buffer builtins makes the host pass drop the kernel's launch stub)
+#define G4_STAGE_ONE(g, t, stg)                                                                                    \
+  do {                                                                                                             \
+    char* d_ = smem + (stg) * STG + wid * 1024;                                                                    \
+    if ((g) < PI)                                                                                                  \
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(__builtin_amdgcn_make_buffer_rsrc(wtile, 0, wbytes, 0x00020000),    \
+                                               (g4_lds_t*)(d_ + (g) * 4096), 16, vp[(g) < PI ? (g) : 0], (t) * 128, 0, 0); \
+    else                                                                                                           \
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(__builtin_amdgcn_make_buffer_rsrc(atile, 0, abytes, 0x00020000),    \
+                                               (g4_lds_t*)(d_ + PIMG + ((g) - PI) * 4096), 16,                      \
+                                               vq[(g) >= PI ? (g) - PI : 0], (t) * 128, 0, 0);                      \
+  } while (0)
+#define G4_STAGE(t, stg) _Pragma("unroll") for (int g_ = 0; g_ < GL; ++g_) G4_STAGE_ONE(g_, t, stg)
+#if G4_ASM_MFMA
+  // With the builtin, hipcc keeps the 256 accumulators in AGPRs but re-homes them (and parks fragments in AGPRs)
+  // with hundreds of v_accvgpr_read/write/mov per K tile.  An accumulate chain (D -> a later MFMA's C) needs no
+  // wait states; the epilogue's first accumulator read is padded below.
+#define G4_MFMA(i, j, pc, qc) asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(pc[i]), "v"(qc[j]))
+#else
+#define G4_MFMA(i, j, pc, qc) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pc[i], qc[j], acc[i][j], 0, 0, 0)
+#endif
+#define G4_MF(u)                                                          \
+  do {                                                                    \
+    if ((u) < NMF) G4_MFMA((u) / WM, (u) % WM, p0, q0);                   \
+    else G4_MFMA(((u) - NMF) / WM, ((u) - NMF) % WM, p1, q1);             \
+  } while (0)
+  constexpr int NR = WN + WM, NMF = WN * WM, NT2 = 2 * NMF;
+  constexpr int BAR1 = NR + 4;                 // barrier #1 after this many MFMAs of the period
+  constexpr int BAR2 = NT2 - NR;               // barrier #2 before MFMA BAR2
+  constexpr int GSP = (BAR2 - BAR1 - 2) / GL;  // MFMAs between two LDS-DMA instructions
+  static_assert(GSP >= 1 && BAR1 < NMF && BAR1 + GL * GSP <= BAR2, "schedule");
+
+  const int nt = K >> 6;
+  // prologue: tiles 0 and 1 in flight, tile 0 landed, its step-0 fragments read
+  G4_STAGE(0, 0);
+  G4_STAGE(min(1, nt - 1), 1);
+  g4_vmcnt<GL>();
+  g4_bar();
+#pragma unroll
+  for (int i = 0; i < WN; ++i) p0[i] = frag(0, offp + i * 2048 + co0);
+#pragma unroll
+  for (int j = 0; j < WM; ++j) q0[j] = frag(0, offq + j * 2048 + co0);
+
+  // Every period is branch-free: past the end, tile nt-1 is re-staged into the free stage and the last reads
+  // fill the idle step-0 set.
+  for (int t = 0; t < nt; ++t) {
+    const int sb = t & 1, tn = min(t + 2, nt - 1);
+    // (phases as short unrolled loops: hipcc will not fully unroll one 128-step loop, and a rolled one would index
+    // the accumulators at run time)
+#pragma unroll
+    for (int u = 0; u < NR; ++u) {   // step-0 MFMAs, step-1 fragment reads
+      G4_MF(u);
+      if (!G4_LAB_NOREAD) {
+        if (u < WN) p1[u < WN ? u : 0] = frag(sb, offp + u * 2048 + co1);
+        else q1[u >= WN ? u - WN : 0] = frag(sb, offq + (u - WN) * 2048 + co1);
+      }
+    }
+#pragma unroll
+    for (int u = NR; u < BAR1; ++u) G4_MF(u);
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // every wave holds all of tile t: its stage may be overwritten
+    g4_bar();
+#pragma unroll
+    for (int g = 0; g < GL; ++g) {        // the LDS-DMA of tile t+2, one instruction per GSP MFMAs
+#pragma unroll
+      for (int k = 0; k < GSP; ++k) G4_MF(BAR1 + g * GSP + k);
+      if (!G4_LAB_NOSTAGE) G4_STAGE_ONE(g, tn, sb);
+    }
+#pragma unroll
+    for (int u = BAR1 + GL * GSP; u < BAR2; ++u) G4_MF(u);
+    g4_vmcnt<GL>();                       // this wave's tile t+1 landed; after the barrier everyone's has
+    g4_bar();
+#pragma unroll
+    for (int v = 0; v < NR; ++v) {        // the last MFMAs, tile t+1's step-0 fragment reads
+      G4_MF(BAR2 + v);
+      if (!G4_LAB_NOREAD) {
+        if (v < WN) p0[v < WN ? v : 0] = frag(sb ^ 1, offp + v * 2048 + co0);
+        else q0[v >= WN ? v - WN : 0] = frag(sb ^ 1, offq + (v - WN) * 2048 + co0);
+      }
+    }
+  }
+#undef G4_MF
+#undef G4_MFMA
+#undef G4_STAGE
+#undef G4_STAGE_ONE
+  g4_vmcnt<0>();   // no LDS-DMA may land after the workgroup's LDS is handed to another one
+#if G4_ASM_MFMA
+  asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");   // last MFMA's D -> the epilogue's accumulator reads
+#endif
+
+  // ---- epilogue.  acc[i][j][r]: n = n0 + wn*128 + i*16 + 4*(lane>>4) + r, m = m0 + wm*BM/2 + j*16 + (lane&15)
+  const int nb = n0 + wn * 128 + 4 * (lane >> 4);
+  const int mb = m0 + wm * (BM / 2) + (lane & 15);
+  if constexpr (EPI == G4_GEGLU) {
+    // W rows interleaved per 128-row wave slice (ops.geglu_interleave_index, the layout gemm.hip uses too): fragments 0..3 are the gate rows of
+    // features f0 .. f0+63, fragments 4..7 the up rows of the same features; gate|up are rounded to bf16 first so
+    // the result equals geglu(bf16 gate|up GEMM output).
+    uint16_t* out = reinterpret_cast<uint16_t*>(C);
+    const int fb = (n0 >> 1) + wn * 64 + 4 * (lane >> 4);
+#pragma unroll
+    for (int j = 0; j < WM; ++j) {
+      const int m = mb + j * 16;
+      if (m >= M) continue;
+#pragma unroll
+      for (int i = 0; i < WN / 2; ++i) {
+        float o[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float gt = rbf(acc[i][j][r]), u = rbf(acc[i + WN / 2][j][r]);
+          o[r] = rbf(gelu_tanh_fast(gt)) * u;
+        }
+        *reinterpret_cast<uint2*>(out + (size_t)m * ldc + fb + i * 16) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
+      }
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < WN; ++i) {
+      const int n = nb + i * 16;
+      float4 bn_ = make_float4(0.f, 0.f, 0.f, 0.f), th = bn_;
+      if constexpr (EPI == G4_JUMPRELU) {
+        if (bias) bn_ = *reinterpret_cast<const float4*>(bias + n);
+        if (thr) th = *reinterpret_cast<const float4*>(thr + n);
+      }
+#pragma unroll
+      for (int j = 0; j < WM; ++j) {
+        const int m = mb + j * 16;
+        if (m >= M) continue;
+        const f32x4 v = acc[i][j];
+        if constexpr (EPI == G4_BF16) {
+          *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(C) + (size_t)m * ldc + n) =
+              make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        } else if constexpr (EPI == G4_F32) {
+          *reinterpret_cast<float4*>(reinterpret_cast<float*>(C) + (size_t)m * ldc + n) = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+          const float a0 = v[0] + bn_.x, a1 = v[1] + bn_.y, a2 = v[2] + bn_.z, a3 = v[3] + bn_.w;
+          *reinterpret_cast<float4*>(reinterpret_cast<float*>(C) + (size_t)m * ldc + n) =
+              make_float4(a0 > th.x ? a0 : 0.f, a1 > th.y ? a1 : 0.f, a2 > th.z ? a2 : 0.f, a3 > th.w ? a3 : 0.f);
+        }
+      }
+    }
+  }
+#endif
+}
+
+}  // namespace
+
+bool tb_gemm4_ok(int M, int N, int K) { return M > 0 && N > 0 && N % G4_BN == 0 && K >= 64 && K % 64 == 0; }
+
+// tile_rows: 256 or 128 (output rows per tile; identical numerics)
+void tb_gemm4(const uint16_t* A, const uint16_t* W, void* C, const float* bias, const float* thr, int M, int N, int K,
+              int ldc, int epi, int tile_rows, hipStream_t st) {
+  if (M <= 0 || N <= 0) return;
+#define G4_GO(BM_, E_)                                                                                          \
+  hipLaunchKernelGGL((gemm4_kernel<BM_, E_>), dim3((N / G4_BN) * ((M + (BM_) - 1) / (BM_))), dim3(G4_THREADS), 0, \
+                     st, A, W, C, bias, thr, M, N, K, ldc)
+#define G4_EPI(BM_)                                   \
+  switch (epi) {                                      \
+    case G4_BF16: G4_GO(BM_, G4_BF16); break;         \
+    case G4_F32: G4_GO(BM_, G4_F32); break;           \
+    case G4_JUMPRELU: G4_GO(BM_, G4_JUMPRELU); break; \
+    default: G4_GO(BM_, G4_GEGLU);                    \
+  }
+  if (tile_rows == 128) {
+    G4_EPI(128)
+  } else {
+    G4_EPI(256)
+  }
+#undef G4_EPI
+#undef G4_GO
+}
