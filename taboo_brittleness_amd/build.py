@@ -56,26 +56,52 @@ def _run(cmd: List[str]) -> None:
         raise RuntimeError(f"build step failed: {cmd[0]} ... {cmd[-1]}")
 
 
-def build(force: bool = False, jobs: int = 8, verbose: bool = False) -> str:
-    os.makedirs(BUILD, exist_ok=True)
+ASAN_BUILD = os.path.join(REPO, "build", "tb_kernels_asan")
+CLANGXX = os.path.join(ROCM, "lib", "llvm", "bin", "clang++")
+
+
+def asan_runtime() -> str:
+    """The clang AddressSanitizer runtime the sanitized host build links against (LD_PRELOAD it into python)."""
+    hits = sorted(glob.glob(os.path.join(ROCM, "lib", "llvm", "lib", "clang", "*", "lib", "linux",
+                                         "libclang_rt.asan-x86_64.so")))
+    if not hits:
+        raise FileNotFoundError("libclang_rt.asan-x86_64.so not found under the ROCm LLVM")
+    return hits[-1]
+
+
+def asan_ext_path() -> str:
+    suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+    return os.path.join(ASAN_BUILD, EXT_NAME + suffix)
+
+
+def build(force: bool = False, jobs: int = 8, verbose: bool = False, sanitize: bool = False) -> str:
+    """Compile and link the extension.  ``sanitize``: a host-side AddressSanitizer + UBSan build
+    (``build/tb_kernels_asan/_tb_kernels*.so``, loaded by ``tests/test_host_sanitizer.py``).  Only host code is
+    instrumented (``-Xarch_host -fsanitize=...``; GPU ASan / xnack is not available on this pool); the device code
+    is the regular gfx950 build."""
+    bdir = ASAN_BUILD if sanitize else BUILD
+    os.makedirs(bdir, exist_ok=True)
     headers = glob.glob(os.path.join(CSRC, "*.h"))
     hip_srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
     inc, lib, abi = _torch_paths()
     common = ["-fPIC", "-O3", "-std=c++17", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-I", CSRC]
+    san = ["-fsanitize=address", "-fsanitize=undefined", "-fno-omit-frame-pointer"]
     steps = []
     objs = []
     for src in hip_srcs:
-        obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+        obj = os.path.join(bdir, os.path.basename(src) + ".o")
         objs.append(obj)
         if force or _newer(obj, [src] + headers):
+            hs = [f for x in san for f in ("-Xarch_host", x)] if sanitize else []
             steps.append([os.path.join(ROCM, "bin", "hipcc"), f"--offload-arch={ARCH}", "-c", src, "-o", obj,
-                          "-munsafe-fp-atomics"] + common)
+                          "-munsafe-fp-atomics"] + hs + common)
     bind_src = os.path.join(CSRC, "bindings.cpp")
-    bind_obj = os.path.join(BUILD, "bindings.cpp.o")
+    bind_obj = os.path.join(bdir, "bindings.cpp.o")
     objs.append(bind_obj)
     if force or _newer(bind_obj, [bind_src] + headers):
         py_inc = sysconfig.get_paths()["include"]
-        cmd = ["c++", "-c", bind_src, "-o", bind_obj, "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-DHIPBLAS_V2",
+        cmd = [CLANGXX if sanitize else "c++"] + (san if sanitize else []) + [
+               "-c", bind_src, "-o", bind_obj, "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-DHIPBLAS_V2",
                f"-DTORCH_EXTENSION_NAME={EXT_NAME}", "-DTORCH_API_INCLUDE_EXTENSION_H", "-isystem", py_inc,
                "-isystem", os.path.join(ROCM, "include")] + common
         for p in inc:
@@ -86,9 +112,9 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = False) -> str:
             futs = [ex.submit(_run, c) for c in steps]
             for f in futs:
                 f.result()
-    out = ext_path()
+    out = asan_ext_path() if sanitize else ext_path()
     if force or steps or _newer(out, objs):
-        link = ["c++", "-shared", "-o", out] + objs + [
+        link = ([CLANGXX, "-shared", "-shared-libasan"] + san if sanitize else ["c++", "-shared"]) + ["-o", out] + objs + [
             "-L", lib, "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
             "-L", os.path.join(ROCM, "lib"), "-lamdhip64", f"-Wl,-rpath,{lib}", f"-Wl,-rpath,{os.path.join(ROCM, 'lib')}"]
         _run(link)
@@ -101,8 +127,9 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=min(8, os.cpu_count() or 1))
+    ap.add_argument("--sanitize", action="store_true", help="host-side ASan + UBSan build under build/tb_kernels_asan")
     a = ap.parse_args()
-    build(force=a.force, jobs=a.jobs, verbose=True)
+    build(force=a.force, jobs=a.jobs, verbose=True, sanitize=a.sanitize)
 
 
 if __name__ == "__main__":

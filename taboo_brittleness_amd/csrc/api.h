@@ -59,6 +59,9 @@ void tb_decode_head(const uint16_t* logits, const int32_t* tgt, int32_t* nxt, fl
 bool tb_gemm_skinny_ok(int M, int N, int K);
 void tb_gemm_skinny(const uint16_t* A, const uint16_t* W, uint16_t* C, int M, int N, int K, hipStream_t st);
 // sae.hip
+bool tb_gemm4_ok(int M, int N, int K);
+void tb_gemm4(const uint16_t* A, const uint16_t* W, void* C, const float* bias, const float* thr, int M, int N, int K,
+              int ldc, int epi, int tile_rows, hipStream_t st);
 bool tb_gemm_pp_ok(int M, int N, int K);
 void tb_gemm_pp(const uint16_t* A, const uint16_t* W, void* C, const float* bias, const float* thr, int M, int N,
                 int K, int ldc, int epi, int tile_rows, hipStream_t st);

@@ -409,6 +409,31 @@ void gemm_pp(torch::Tensor A, torch::Tensor W, torch::Tensor C, c10::optional<to
 
 bool gemm_pp_ok(int64_t M, int64_t N, int64_t K) { return tb_gemm_pp_ok(M, N, K); }
 
+// Four-wave 256x256x64 (tile_rows = 128: 128x256x64) MFMA GEMM (gemm4.hip): the same epilogues, operand layouts
+// and numerics as gemm_pp (bit-identical outputs), 128x128 wave tiles.
+void gemm4(torch::Tensor A, torch::Tensor W, torch::Tensor C, c10::optional<torch::Tensor> bias,
+           c10::optional<torch::Tensor> thr, int64_t epi, int64_t tile_rows) {
+  IN_BF16(A); IN_BF16(W); CHECK_DEV(C); CHECK_CONTIG(C);
+  TORCH_CHECK(W.dim() == 2, "gemm4: W must be [N, K]");
+  TORCH_CHECK(tile_rows == 256 || tile_rows == 128, "gemm4: tile_rows must be 256 or 128");
+  const int K = A.size(-1), M = A.numel() / K, N = W.size(0);
+  TORCH_CHECK(W.size(1) == K, "gemm4: K mismatch");
+  TORCH_CHECK(tb_gemm4_ok(M, N, K), "gemm4: need N % 256 == 0, K % 64 == 0, K >= 64");
+  TORCH_CHECK(epi >= 0 && epi <= 3, "gemm4: epi must be 0..3");
+  const int64_t ncols = epi == 3 ? N / 2 : N;
+  TORCH_CHECK(C.numel() == (int64_t)M * ncols, "gemm4: C shape");
+  TORCH_CHECK(C.scalar_type() == ((epi == 0 || epi == 3) ? at::kBFloat16 : at::kFloat), "gemm4: C dtype");
+  if (epi == 2) {
+    TORCH_CHECK(!bias.has_value() || !bias->defined() || bias->numel() == N, "gemm4: bias numel must be N");
+    TORCH_CHECK(!thr.has_value() || !thr->defined() || thr->numel() == N, "gemm4: thr numel must be N");
+  }
+  c10::DeviceGuard g(A.device());
+  tb_gemm4(cbf(A), cbf(W), C.data_ptr(), epi == 2 ? optf(bias) : nullptr, epi == 2 ? optf(thr) : nullptr, M, N, K,
+           (int)ncols, (int)epi, (int)tile_rows, cur_stream());
+}
+
+bool gemm4_ok(int64_t M, int64_t N, int64_t K) { return tb_gemm4_ok(M, N, K); }
+
 // Logit-lens unembedding on the ping-pong GEMM (gemm.hip EPI_LENS): bf16 logits and their per-row
 // log-sum-exp (no softcap), so the lens needs no separate row_lse pass.  part: f32 >= M * (V / 128) * 4.
 void lens_gemm(torch::Tensor x, torch::Tensor W, torch::Tensor logits, torch::Tensor part, torch::Tensor lse) {
@@ -616,6 +641,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_nt", &gemm_nt);
   m.def("gemm_pp", &gemm_pp);
   m.def("gemm_pp_ok", &gemm_pp_ok);
+  m.def("gemm4", &gemm4);
+  m.def("gemm4_ok", &gemm4_ok);
   m.def("head_fused", &head_fused);
   m.def("lens_gemm", &lens_gemm);
   m.def("gemm_skinny", &gemm_skinny);

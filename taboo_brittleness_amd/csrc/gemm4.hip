@@ -48,6 +48,18 @@ constexpr int G4_THREADS = 256, G4_BN = 256;
 #ifndef G4_LAB_NOREAD
 #define G4_LAB_NOREAD 0
 #endif
+#ifndef G4_LAB_HALF
+#define G4_LAB_HALF 0    // stage only the W operand
+#endif
+#ifndef G4_SLACK1
+#define G4_SLACK1 4      // MFMAs between the last step-1 fragment read and barrier #1 (its lgkmcnt(0))
+#endif
+#ifndef G4_SLACK2
+#define G4_SLACK2 0      // MFMAs after the last step-0 fragment read of the next tile
+#endif
+#ifndef G4_PRIO
+#define G4_PRIO 0        // 1: s_setprio 3 for the K loop
+#endif
 #ifndef G4_ASM_MFMA
 #define G4_ASM_MFMA 1    // 1: MFMAs as asm statements with AGPR-tied accumulators (see G4_MFMA below)
 #endif
@@ -63,6 +75,8 @@ __device__ __forceinline__ void g4_vmcnt() {
   else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
 }
+// s_waitcnt vmcnt(n) (expcnt / lgkmcnt left at their maxima), gfx9 encoding: vmcnt[3:0] -> [3:0], vmcnt[5:4] -> [15:14]
+constexpr int g4_vmcnt_enc(int n) { return (n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8); }
 __device__ __forceinline__ void g4_bar() {
   __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_barrier();
@@ -156,10 +170,11 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
     else G4_MFMA(((u) - NMF) / WM, ((u) - NMF) % WM, p1, q1);             \
   } while (0)
   constexpr int NR = WN + WM, NMF = WN * WM, NT2 = 2 * NMF;
-  constexpr int BAR1 = NR + 4;                 // barrier #1 after this many MFMAs of the period
-  constexpr int BAR2 = NT2 - NR;               // barrier #2 before MFMA BAR2
-  constexpr int GSP = (BAR2 - BAR1 - 2) / GL;  // MFMAs between two LDS-DMA instructions
-  static_assert(GSP >= 1 && BAR1 < NMF && BAR1 + GL * GSP <= BAR2, "schedule");
+  constexpr int BAR1 = NR + G4_SLACK1;           // barrier #1 after this many MFMAs of the period
+  constexpr int BAR2 = NT2 - NR - G4_SLACK2;     // barrier #2 before MFMA BAR2
+  constexpr int GSP = (NT2 - BAR1) / GL;         // MFMAs per LDS-DMA instruction, spread to the period's end
+  constexpr int N2 = (BAR2 - BAR1) / GSP < GL ? (BAR2 - BAR1) / GSP : GL;   // of them issued before barrier #2
+  static_assert(GSP >= 1 && BAR1 < NMF && BAR1 < BAR2, "schedule");
 
   const int nt = K >> 6;
   // prologue: tiles 0 and 1 in flight, tile 0 landed, its step-0 fragments read
@@ -172,8 +187,25 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
 #pragma unroll
   for (int j = 0; j < WM; ++j) q0[j] = frag(0, offq + j * 2048 + co0);
 
+  // The MFMAs after barrier #1: barrier #2 in front of MFMA BAR2 (vmcnt leaves the N2 instructions of tile t+2
+  // issued so far in flight), the next tile's step-0 fragment reads behind the MFMAs from BAR2 on.
+#define G4_POST(u)                                                                              \
+  do {                                                                                          \
+    if ((u) == BAR2) {                                                                          \
+      __builtin_amdgcn_s_waitcnt(g4_vmcnt_enc(N2));                                             \
+      g4_bar();                                                                                 \
+    }                                                                                           \
+    G4_MF(u);                                                                                   \
+    const int v_ = (u) - BAR2;                                                                  \
+    if (v_ >= 0 && v_ < NR && !G4_LAB_NOREAD) {                                                 \
+      if (v_ < WN) p0[v_ >= 0 && v_ < WN ? v_ : 0] = frag(sb ^ 1, offp + v_ * 2048 + co0);      \
+      else q0[v_ >= WN && v_ < NR ? v_ - WN : 0] = frag(sb ^ 1, offq + (v_ - WN) * 2048 + co0); \
+    }                                                                                           \
+  } while (0)
+
   // Every period is branch-free: past the end, tile nt-1 is re-staged into the free stage and the last reads
   // fill the idle step-0 set.
+  if (G4_PRIO) __builtin_amdgcn_s_setprio(3);
   for (int t = 0; t < nt; ++t) {
     const int sb = t & 1, tn = min(t + 2, nt - 1);
     // (phases as short unrolled loops: hipcc will not fully unroll one 128-step loop, and a rolled one would index
@@ -193,26 +225,22 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
 #pragma unroll
     for (int g = 0; g < GL; ++g) {        // the LDS-DMA of tile t+2, one instruction per GSP MFMAs
 #pragma unroll
-      for (int k = 0; k < GSP; ++k) G4_MF(BAR1 + g * GSP + k);
-      if (!G4_LAB_NOSTAGE) G4_STAGE_ONE(g, tn, sb);
+      for (int k = 0; k < GSP; ++k) G4_POST(BAR1 + g * GSP + k);
+      if (!G4_LAB_NOSTAGE && !(G4_LAB_HALF && g >= PI)) G4_STAGE_ONE(g, tn, sb);
     }
 #pragma unroll
-    for (int u = BAR1 + GL * GSP; u < BAR2; ++u) G4_MF(u);
-    g4_vmcnt<GL>();                       // this wave's tile t+1 landed; after the barrier everyone's has
-    g4_bar();
-#pragma unroll
-    for (int v = 0; v < NR; ++v) {        // the last MFMAs, tile t+1's step-0 fragment reads
-      G4_MF(BAR2 + v);
-      if (!G4_LAB_NOREAD) {
-        if (v < WN) p0[v < WN ? v : 0] = frag(sb ^ 1, offp + v * 2048 + co0);
-        else q0[v >= WN ? v - WN : 0] = frag(sb ^ 1, offq + (v - WN) * 2048 + co0);
-      }
-    }
+    for (int u = BAR1 + GL * GSP; u < NT2; ++u) G4_POST(u);
+    // drain the reads here, with a memory clobber: otherwise hipcc sinks the last one into the next period and
+    // waits for it (lgkmcnt(0)) in front of that period's first MFMA
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
   }
+#undef G4_POST
 #undef G4_MF
 #undef G4_MFMA
 #undef G4_STAGE
 #undef G4_STAGE_ONE
+  if (G4_PRIO) __builtin_amdgcn_s_setprio(0);
   g4_vmcnt<0>();   // no LDS-DMA may land after the workgroup's LDS is handed to another one
 #if G4_ASM_MFMA
   asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");   // last MFMA's D -> the epilogue's accumulator reads

@@ -62,8 +62,17 @@ def softcap_values(v: torch.Tensor, cap: float) -> torch.Tensor:
 SKINNY_MAX_M = int(os.environ.get("TB_SKINNY_MAX_M", "0"))   # v1 kernel loses to hipBLASLt: opt-in
 
 
+def tb_gemm(x, w, out, bias, thr, epi: int, choice) -> None:
+    """One in-tree MFMA GEMM (``runtime.gemm_dispatch`` choice): ``"g256"`` / ``"g128"`` the four-wave kernel
+    (csrc/gemm4.hip), ``256`` / ``128`` the ping-pong kernel (csrc/gemm.hip); identical numerics."""
+    if isinstance(choice, str):
+        _k().gemm4(x, w, out, bias, thr, int(epi), int(choice[1:]))
+    else:
+        _k().gemm_pp(x, w, out, bias, thr, int(epi), int(choice))
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """y = x @ w^T.  GPU: the in-tree ping-pong MFMA GEMM (256- or 128-row tiles) or hipBLASLt, per shape
+    """y = x @ w^T.  GPU: an in-tree MFMA GEMM (four-wave or ping-pong, 256- or 128-row tiles) or hipBLASLt, per shape
     (``runtime.gemm_dispatch``: measured table, ``TB_GEMM=tb`` in-tree only / batch-invariant, ``blas``)."""
     if x.is_cuda and x.dtype == BF16 and w.dtype == BF16:
         K = x.shape[-1]
@@ -74,7 +83,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None)
             c = _GD.choose(M, N, K, 0)
             if c != "blas":
                 out = _out(out, x.shape[:-1] + (N,), BF16, x.device)
-                _k().gemm_pp(x, w, out, None, None, 0, int(c))
+                tb_gemm(x, w, out, None, None, 0, c)
                 return out
         if M <= SKINNY_MAX_M and M * 16 <= N and x.is_contiguous() and w.is_contiguous() and \
                 _k().gemm_skinny_ok(M, N, K):
@@ -457,7 +466,7 @@ def gemm_nt(A, W, epi=0, bias=None, thr=None, out=None):
     if A.is_cuda:
         out = _out(out, (M, N), BF16 if epi == 0 else torch.float32, A.device)
         if _k().gemm_pp_ok(M, N, A.shape[-1]) and A.is_contiguous():
-            _k().gemm_pp(A, W, out, bias, thr, int(epi), 256)
+            tb_gemm(A, W, out, bias, thr, int(epi), _GD.fill_choice(max(M, 4096), N))
         else:
             _k().gemm_nt(A, W, out, bias, thr, int(epi))
         return out
@@ -499,7 +508,7 @@ def gate_up_geglu(x: torch.Tensor, w_gu_interleaved: torch.Tensor, out: Optional
     if x.is_cuda:
         out = _out(out, x.shape[:-1] + (F,), BF16, x.device)
         c = _GD.choose(M, 2 * F, x.shape[-1], 3)
-        _k().gemm_pp(x, w_gu_interleaved, out, None, None, 3, int(c) if c != "blas" else _GD.fill_choice(M, 2 * F))
+        tb_gemm(x, w_gu_interleaved, out, None, None, 3, c if c != "blas" else _GD.fill_choice(M, 2 * F))
         return out
     inv = torch.argsort(geglu_interleave_index(F))
     y = ref.geglu((x.reshape(M, -1).float() @ w_gu_interleaved[inv].float().T).to(BF16)).view(x.shape[:-1] + (F,))

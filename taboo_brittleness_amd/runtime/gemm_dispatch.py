@@ -5,6 +5,8 @@ through :func:`taboo_brittleness_amd.ops.linear`, which asks :func:`choose` for 
 
 * ``256`` / ``128`` — ``csrc/gemm.hip``'s ping-pong kernel with 256- or 128-row output tiles (the 128-row
   tile doubles the workgroup count for the N = 3584 projections at moderate M);
+* ``"g256"`` / ``"g128"`` — ``csrc/gemm4.hip``'s four-wave kernel (128x128 wave tiles), same tiles, same
+  epilogues and bit-identical results;
 * ``"blas"`` — ``torch.matmul`` (hipBLASLt, with the TunableOp solution table the bench loads).
 
 Modes (``TB_GEMM``):
@@ -30,7 +32,8 @@ NUM_CU = 256
 
 Choice = Union[int, str]
 
-_state = {"mode": os.environ.get("TB_GEMM", "auto"), "table": None, "table_path": None, "loaded": False}
+_state = {"mode": os.environ.get("TB_GEMM", "auto"), "table": None, "table_path": None, "loaded": False,
+          "kernel": os.environ.get("TB_GEMM_KERNEL", "g4")}   # in-tree kernel of the fill rule: g4 | pp
 
 
 def set_mode(mode: str) -> None:
@@ -54,21 +57,28 @@ def load_table(path: Optional[str] = None, arch: str = "gemma2-9b") -> Optional[
     for key, rows in raw["shapes"].items():
         n, k, e = (int(v) for v in key.split(","))
         rows = sorted(rows, key=lambda r: r[0])
-        tab[(n, k, e)] = ([int(r[0]) for r in rows], [r[1] if r[1] == "blas" else int(r[1]) for r in rows])
+        tab[(n, k, e)] = ([int(r[0]) for r in rows], [r[1] if isinstance(r[1], str) else int(r[1]) for r in rows])
     _state["table"], _state["table_path"] = tab, path
     _state["loaded"] = True
     return path
 
 
-def fill_choice(M: int, N: int) -> int:
-    """Tile rows for the in-tree kernel: 256 unless its grid fills less than half the CUs (the 128-row tile
+def fill_choice(M: int, N: int) -> Choice:
+    """In-tree kernel and tile rows: 256 unless the grid fills less than half the CUs (the 128-row tile
     runs its MFMAs at ~75 % of the 256-row tile's rate, profiles/r3/gemm_dispatch/raw_round1.jsonl, so it only
-    pays where it doubles a very thin grid)."""
-    return 128 if (N // 256) * (-(-M // 256)) < NUM_CU // 2 else 256
+    pays where it doubles a very thin grid); the four-wave kernel (``TB_GEMM_KERNEL=g4``, default) or the
+    ping-pong one (``pp``)."""
+    rows = 128 if (N // 256) * (-(-M // 256)) < NUM_CU // 2 else 256
+    return f"g{rows}" if _state["kernel"] == "g4" else rows
+
+
+def set_kernel(kernel: str) -> None:
+    assert kernel in ("g4", "pp"), kernel
+    _state["kernel"] = kernel
 
 
 def choose(M: int, N: int, K: int, epi: int = 0) -> Choice:
-    """``256`` | ``128`` | ``"blas"`` for ``C[M, N] = A[M, K] @ W[N, K]^T`` (epi 3: gate|up + GeGLU)."""
+    """``256`` | ``128`` | ``"g256"`` | ``"g128"`` | ``"blas"`` for ``C[M, N] = A[M, K] @ W[N, K]^T`` (epi 3: gate|up + GeGLU)."""
     m = _state["mode"]
     if m == "blas":
         return "blas"
@@ -87,4 +97,5 @@ def choose(M: int, N: int, K: int, epi: int = 0) -> Choice:
 
 
 def describe() -> dict:
-    return {"mode": _state["mode"], "table": os.path.relpath(_state["table_path"], REPO) if _state["table_path"] else None}
+    return {"mode": _state["mode"], "kernel": _state["kernel"],
+            "table": os.path.relpath(_state["table_path"], REPO) if _state["table_path"] else None}

@@ -22,7 +22,7 @@ def test_table_lookup_and_modes(tmp_path):
         GD.set_mode("blas")
         assert GD.choose(1024, 8192, 3584) == "blas"
         GD.set_mode("tb")
-        assert GD.choose(64, 3584, 4096) in (128, 256)      # in-tree only
+        assert GD.choose(64, 3584, 4096) in (128, 256, "g128", "g256")      # in-tree only
         assert GD.describe()["mode"] == "tb"
     finally:
         GD.set_mode(old)
@@ -30,9 +30,17 @@ def test_table_lookup_and_modes(tmp_path):
 
 
 def test_fill_choice():
-    assert GD.fill_choice(4096, 28672) == 256               # 1792 tiles
-    assert GD.fill_choice(256, 3584) == 128                 # 14 tiles of 256 rows: half the CUs would idle
-    assert GD.fill_choice(8192, 3584) == 256
+    old = GD._state["kernel"]
+    try:
+        GD.set_kernel("pp")
+        assert GD.fill_choice(4096, 28672) == 256               # 1792 tiles
+        assert GD.fill_choice(256, 3584) == 128                 # 14 tiles of 256 rows: half the CUs would idle
+        assert GD.fill_choice(8192, 3584) == 256
+        GD.set_kernel("g4")
+        assert GD.fill_choice(4096, 28672) == "g256"
+        assert GD.fill_choice(256, 3584) == "g128"
+    finally:
+        GD.set_kernel(old)
 
 
 def test_shipped_table_is_consistent():
@@ -44,6 +52,6 @@ def test_shipped_table_is_consistent():
         for key in [(8192, 3584, 0), (3584, 4096, 0), (28672, 3584, 0), (28672, 3584, 3), (3584, 14336, 0),
                     (256000, 3584, 0)]:
             ms, cs = tab[key]
-            assert ms == sorted(ms) and len(ms) == len(cs) and all(c in ("blas", 128, 256) for c in cs)
+            assert ms == sorted(ms) and len(ms) == len(cs) and all(c in ("blas", 128, 256, "g128", "g256") for c in cs)
     finally:
         GD._state["loaded"] = False

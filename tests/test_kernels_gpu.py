@@ -420,6 +420,65 @@ def test_gemm_pp_tiles_batch_invariant(gpu, N, K, epi):
         _close(outs[128][:64], r, atol=1e-2 * K ** 0.5, rtol=1e-2)
 
 
+@pytest.mark.parametrize("M,N,K", [(1, 256, 64), (37, 512, 128), (300, 768, 3584), (513, 1024, 640)])
+def test_gemm4_epilogues(gpu, M, N, K):
+    """Four-wave 256x256x64 MFMA GEMM (csrc/gemm4.hip) vs a float32 PyTorch reference: every epilogue, both tile
+    heights, ragged M (clamped loads, masked stores), 1 / 2 / 10 / 56 K tiles."""
+    torch.manual_seed(12)
+    A = (torch.rand(M, K) * 2 - 1).to(BF)
+    W = (torch.rand(N, K) * 2 - 1).to(BF)
+    b = torch.randn(N)
+    th = torch.rand(N) * 2
+    Ag, Wg = A.to(gpu), W.to(gpu)
+    k = ops._k()
+    r = A.float() @ W.float().T
+    for t in (256, 128):
+        c32 = torch.full((M, N), float("nan"), device=gpu)
+        k.gemm4(Ag, Wg, c32, None, None, 1, t)
+        _close(c32, r, atol=1e-3 * K ** 0.5, rtol=1e-4)
+        cb = torch.full((M, N), float("nan"), device=gpu, dtype=BF)
+        k.gemm4(Ag, Wg, cb, None, None, 0, t)
+        _close(cb, r, atol=1e-2 * K ** 0.5, rtol=1e-2)
+        k.gemm4(Ag, Wg, c32, b.to(gpu), th.to(gpu), 2, t)
+        pre = r + b
+        near = (pre - th).abs() < 1e-3
+        want = torch.where(pre > th, pre, torch.zeros_like(pre))
+        assert ((c32.cpu() - want).abs()[~near] < 1e-3 * K ** 0.5).all()
+        Wi = Wg[ops.geglu_interleave_index(N // 2, gpu)].contiguous()
+        act = torch.empty(M, N // 2, device=gpu, dtype=BF)
+        k.gemm4(Ag, Wi, act, None, None, 3, t)
+        _close(act, ref.geglu(r.to(BF)).float(), atol=2e-2 * K ** 0.5, rtol=2e-2)
+
+
+@pytest.mark.parametrize("N,K,epi", [(3584, 4096, 0), (8192, 3584, 0), (3584, 14336, 0), (28672, 3584, 3),
+                                     (256000, 3584, 0)])
+def test_gemm4_bitequal_pingpong_and_batch_invariant(gpu, N, K, epi):
+    """At the Gemma-2-9B projection shapes (vocab head included) the four-wave kernel's output is BIT-identical
+    to the ping-pong kernel's (same MFMA, same K order), for both tile heights and for sub-batches of the rows:
+    switching kernels per shape (runtime/gemm_dispatch.py) keeps the forward batch-invariant."""
+    torch.manual_seed(5)
+    M = 777 if N < 100000 else 300
+    A = ((torch.rand(M, K) * 2 - 1) * 0.5).to(BF).to(gpu)
+    W = ((torch.rand(N, K) * 2 - 1) * 0.5).to(BF).to(gpu)
+    k = ops._k()
+    if epi == 3:
+        W = W[ops.geglu_interleave_index(N // 2, gpu)].contiguous()
+    ncol = N // 2 if epi == 3 else N
+    ref_pp = torch.empty(M, ncol, device=gpu, dtype=BF)
+    k.gemm_pp(A, W, ref_pp, None, None, epi, 256)
+    for t in (256, 128):
+        c = torch.empty(M, ncol, device=gpu, dtype=BF)
+        k.gemm4(A, W, c, None, None, epi, t)
+        assert torch.equal(c, ref_pp), t
+    for rows in (slice(0, 1), slice(5, 130), slice(M - 200, M)):
+        sub = torch.empty(rows.stop - rows.start, ncol, device=gpu, dtype=BF)
+        k.gemm4(A[rows].contiguous(), W, sub, None, None, epi, 128)
+        assert torch.equal(sub, ref_pp[rows])
+    if epi == 0:
+        r = A[:64].float() @ W.float().T
+        _close(ref_pp[:64], r, atol=1e-2 * K ** 0.5, rtol=1e-2)
+
+
 def test_linear_dispatch_modes(gpu):
     """ops.linear under TB_GEMM=tb (in-tree tiles only) equals the in-tree kernel bit for bit and the
     hipBLASLt mode up to bf16 rounding."""
@@ -437,7 +496,7 @@ def test_linear_dispatch_modes(gpu):
     finally:
         GD.set_mode(old)
     c = torch.empty_like(y_tb)
-    ops._k().gemm_pp(A, W, c, None, None, 0, GD.fill_choice(300, 4096))
+    ops.tb_gemm(A, W, c, None, None, 0, GD.fill_choice(300, 4096))
     assert torch.equal(c, y_tb)
     _close(y_tb, y_bl, atol=2e-2, rtol=1e-2)
 

@@ -1,4 +1,4 @@
-"""Measure the in-tree ping-pong GEMM (256- / 128-row tiles) against hipBLASLt (with the bench's TunableOp
+"""Measure the in-tree GEMMs (ping-pong ``256`` / ``128`` and four-wave ``g256`` / ``g128`` row tiles) against hipBLASLt (with the bench's TunableOp
 table) on every projection shape of the Gemma-2-9B step and write the per-shape dispatch table
 ``configs/gemm_dispatch/gemma2-9b.json`` that ``runtime/gemm_dispatch.py`` loads (``TB_GEMM=auto``).
 
@@ -65,6 +65,7 @@ def main():
     ap.add_argument("--max-m", type=int, default=33000)
     ap.add_argument("--only", default="", help="comma-separated shape names")
     ap.add_argument("--tie", type=float, default=1.01, help="in-tree wins when t_tb <= tie * t_blas")
+    ap.add_argument("--kernels", default="g256,g128,256,128", help="in-tree candidates (gNNN: gemm4.hip, NNN: gemm.hip)")
     args = ap.parse_args()
     _ext.load()
     k = _ext.kernels()
@@ -103,16 +104,16 @@ def main():
                     return ws[it[0]]
 
                 if epi == 0:
-                    var = {"blas": lambda: torch.matmul(A, nxt(Ws).t(), out=C),
-                           256: lambda: k.gemm_pp(A, nxt(Ws), C, None, None, 0, 256),
-                           128: lambda: k.gemm_pp(A, nxt(Ws), C, None, None, 0, 128)}
+                    var = {"blas": lambda: torch.matmul(A, nxt(Ws).t(), out=C)}
                 else:
                     def blas_geglu():
                         torch.matmul(A, nxt(Ws).t(), out=G)
                         ops.geglu(G, out=C)
-                    var = {"blas": blas_geglu,
-                           256: lambda: k.gemm_pp(A, nxt(Wi), C, None, None, 3, 256),
-                           128: lambda: k.gemm_pp(A, nxt(Wi), C, None, None, 3, 128)}
+                    var = {"blas": blas_geglu}
+                wsrc = Ws if epi == 0 else Wi
+                for ch in args.kernels.split(","):
+                    ch = ch if ch.startswith("g") else int(ch)
+                    var[ch] = (lambda ch_: lambda: ops.tb_gemm(A, nxt(wsrc), C, None, None, epi, ch_))(ch)
                 for f in var.values():      # warm-up (and TunableOp lookups)
                     f()
                 torch.cuda.synchronize()
@@ -123,7 +124,7 @@ def main():
                     for v, f in var.items():
                         res[v].append(timed(f, reps))
                 med = {v: sorted(t)[len(t) // 2] for v, t in res.items()}
-                tb_best = min((256, 128), key=lambda v: med[v])
+                tb_best = min((v for v in var if v != "blas"), key=lambda v: med[v])
                 win = tb_best if med[tb_best] <= args.tie * med["blas"] else "blas"
                 rows.append([M, win])
                 rec = {"shape": name, "N": N, "K": K, "M": M, "epi": epi, "us": {str(v): round(t, 2) for v, t in med.items()},
