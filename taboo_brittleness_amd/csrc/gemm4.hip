@@ -34,6 +34,8 @@
 // Requirements (host-checked, tb_gemm4_ok): N % 256 == 0, K % 64 == 0, K >= 64; any M.
 #include "common.h"
 #include "api.h"
+#include <algorithm>
+#include <cstdlib>
 
 namespace {
 
@@ -56,6 +58,15 @@ constexpr int G4_THREADS = 256, G4_BN = 256;
 #endif
 #ifndef G4_SLACK2
 #define G4_SLACK2 0      // MFMAs after the last step-0 fragment read of the next tile
+#endif
+#ifndef G4_AUX_W
+#define G4_AUX_W 0       // cache-policy bits of the W LDS-DMA loads (1: sc0, 2: nt)
+#endif
+#ifndef G4_AUX_A
+#define G4_AUX_A 0       // ... of the A loads
+#endif
+#ifndef G4_JMAJOR
+#define G4_JMAJOR 0      // 1: MFMA order with the A (column-operand) fragment fixed over 8 W fragments
 #endif
 #ifndef G4_PRIO
 #define G4_PRIO 0        // 1: s_setprio 3 for the K loop
@@ -98,15 +109,20 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
   __shared__ __attribute__((aligned(1024))) char smem[2 * STG];
 
   const int nbn = N / G4_BN, nbm = (M + BM - 1) / BM, nwg = nbn * nbm;
-  int bid = blockIdx.x;
-  {
-    const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
-    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
-  }
-  const int per_group = G4_GROUP_M * nbn, first_bm = (bid / per_group) * G4_GROUP_M;
-  const int gsz = min(nbm - first_bm, G4_GROUP_M), lid = bid % per_group;
-  const int bm = first_bm + lid % gsz, bn = lid / gsz;
-  const int m0 = bm * BM, n0 = bn * G4_BN;
+  // Persistent: this workgroup runs the virtual tiles blockIdx.x, blockIdx.x + gridDim.x, ...  A virtual id v keeps
+  // v % 8 = blockIdx.x % 8 (gridDim.x is a multiple of 8), i.e. the XCD the workgroup runs on; the bijective
+  // remap (T1) gives each XCD a contiguous range of tiles, grouped GROUP_M tile rows deep (shared A / W panels).
+#define G4_TILE(v, m0_, n0_)                                                                              \
+  do {                                                                                                    \
+    const int q_ = nwg / 8, r_ = nwg % 8, x_ = (v) % 8;                                                   \
+    const int b_ = (x_ < r_ ? x_ * (q_ + 1) : r_ * (q_ + 1) + (x_ - r_) * q_) + (v) / 8;                  \
+    const int pg_ = G4_GROUP_M * nbn, fb_ = (b_ / pg_) * G4_GROUP_M;                                      \
+    const int gs_ = min(nbm - fb_, G4_GROUP_M), l_ = b_ % pg_;                                            \
+    m0_ = (fb_ + l_ % gs_) * BM;                                                                          \
+    n0_ = (l_ / gs_) * G4_BN;                                                                             \
+  } while (0)
+  int tile = blockIdx.x, m0, n0;
+  G4_TILE(tile, m0, n0);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -115,16 +131,22 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
   // ---- staging: instruction i of this wave fills image rows 8*(4i + wid) + lane/8 at physical chunk lane%8, which
   // holds logical chunk (lane%8) ^ ((row>>1)&7) = (lane%8) ^ ((4*wid + lane/16) & 7) (the same for every i)
   const int lchunk = (lane & 7) ^ ((4 * wid + (lane >> 4)) & 7);
-  const int mrows = min(BM, M - m0);
-  void* const wtile = (void*)(W + (size_t)n0 * K);
-  void* const atile = (void*)(A + (size_t)m0 * K);
-  const int wbytes = G4_BN * K * 2, abytes = mrows * K * 2;
+  const int wbytes = G4_BN * K * 2;
   uint32_t vp[PI], vq[QI];
 #pragma unroll
   for (int i = 0; i < PI; ++i) vp[i] = (uint32_t)((8 * (4 * i + wid) + (lane >> 3)) * K + lchunk * 8) * 2u;
-#pragma unroll
-  for (int i = 0; i < QI; ++i)
-    vq[i] = (uint32_t)(min(8 * (4 * i + wid) + (lane >> 3), mrows - 1) * K + lchunk * 8) * 2u;
+  int mrows, abytes;
+  void *wtile, *atile;
+#define G4_DESC()                                                                                 \
+  do {                                                                                            \
+    mrows = min(BM, M - m0);                                                                      \
+    wtile = (void*)(W + (size_t)n0 * K);                                                          \
+    atile = (void*)(A + (size_t)m0 * K);                                                          \
+    abytes = mrows * K * 2;                                                                       \
+    _Pragma("unroll") for (int i = 0; i < QI; ++i)                                                \
+      vq[i] = (uint32_t)(min(8 * (4 * i + wid) + (lane >> 3), mrows - 1) * K + lchunk * 8) * 2u;  \
+  } while (0)
+  G4_DESC();
 
   // ---- fragment reads: operand row = base + (lane&15) (base % 16 == 0, so (row>>1)&7 = (lane&15)>>1), logical
   // chunk 4*step + (lane>>4)
@@ -149,11 +171,11 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
     char* d_ = smem + (stg) * STG + wid * 1024;                                                                    \
     if ((g) < PI)                                                                                                  \
       __builtin_amdgcn_raw_ptr_buffer_load_lds(__builtin_amdgcn_make_buffer_rsrc(wtile, 0, wbytes, 0x00020000),    \
-                                               (g4_lds_t*)(d_ + (g) * 4096), 16, vp[(g) < PI ? (g) : 0], (t) * 128, 0, 0); \
+                                               (g4_lds_t*)(d_ + (g) * 4096), 16, vp[(g) < PI ? (g) : 0], (t) * 128, 0, G4_AUX_W); \
     else                                                                                                           \
       __builtin_amdgcn_raw_ptr_buffer_load_lds(__builtin_amdgcn_make_buffer_rsrc(atile, 0, abytes, 0x00020000),    \
                                                (g4_lds_t*)(d_ + PIMG + ((g) - PI) * 4096), 16,                      \
-                                               vq[(g) >= PI ? (g) - PI : 0], (t) * 128, 0, 0);                      \
+                                               vq[(g) >= PI ? (g) - PI : 0], (t) * 128, 0, G4_AUX_A);               \
   } while (0)
 #define G4_STAGE(t, stg) _Pragma("unroll") for (int g_ = 0; g_ < GL; ++g_) G4_STAGE_ONE(g_, t, stg)
 #if G4_ASM_MFMA
@@ -166,8 +188,13 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
 #endif
 #define G4_MF(u)                                                          \
   do {                                                                    \
-    if ((u) < NMF) G4_MFMA((u) / WM, (u) % WM, p0, q0);                   \
-    else G4_MFMA(((u) - NMF) / WM, ((u) - NMF) % WM, p1, q1);             \
+    if (G4_JMAJOR) {                                                      \
+      if ((u) < NMF) G4_MFMA((u) % WN, (u) / WN, p0, q0);                 \
+      else G4_MFMA(((u) - NMF) % WN, ((u) - NMF) / WN, p1, q1);           \
+    } else {                                                              \
+      if ((u) < NMF) G4_MFMA((u) / WM, (u) % WM, p0, q0);                 \
+      else G4_MFMA(((u) - NMF) / WM, ((u) - NMF) % WM, p1, q1);           \
+    }                                                                     \
   } while (0)
   constexpr int NR = WN + WM, NMF = WN * WM, NT2 = 2 * NMF;
   constexpr int BAR1 = NR + G4_SLACK1;           // barrier #1 after this many MFMAs of the period
@@ -177,9 +204,11 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
   static_assert(GSP >= 1 && BAR1 < NMF && BAR1 < BAR2, "schedule");
 
   const int nt = K >> 6;
-  // prologue: tiles 0 and 1 in flight, tile 0 landed, its step-0 fragments read
+  // prologue of the first tile: K tiles 0 and 1 in flight
   G4_STAGE(0, 0);
   G4_STAGE(min(1, nt - 1), 1);
+  for (;;) {
+  // K tile 0 landed, its step-0 fragments read
   g4_vmcnt<GL>();
   g4_bar();
 #pragma unroll
@@ -238,23 +267,34 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
 #undef G4_POST
 #undef G4_MF
 #undef G4_MFMA
-#undef G4_STAGE
-#undef G4_STAGE_ONE
   if (G4_PRIO) __builtin_amdgcn_s_setprio(0);
-  g4_vmcnt<0>();   // no LDS-DMA may land after the workgroup's LDS is handed to another one
+  // the stages are free once every wave is past its last fragment read and its (redundant) tail LDS-DMA: the next
+  // tile's first two K tiles load while this tile's epilogue stores run
+  g4_vmcnt<0>();
+  g4_bar();
+  const int em0 = m0, en0 = n0;
+  const int next = tile + (int)gridDim.x;
+  if (next < nwg) {
+    tile = next;
+    G4_TILE(tile, m0, n0);
+    G4_DESC();
+    G4_STAGE(0, 0);
+    G4_STAGE(min(1, nt - 1), 1);
+  }
 #if G4_ASM_MFMA
   asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");   // last MFMA's D -> the epilogue's accumulator reads
 #endif
 
   // ---- epilogue.  acc[i][j][r]: n = n0 + wn*128 + i*16 + 4*(lane>>4) + r, m = m0 + wm*BM/2 + j*16 + (lane&15)
-  const int nb = n0 + wn * 128 + 4 * (lane >> 4);
-  const int mb = m0 + wm * (BM / 2) + (lane & 15);
+  {
+  const int nb = en0 + wn * 128 + 4 * (lane >> 4);
+  const int mb = em0 + wm * (BM / 2) + (lane & 15);
   if constexpr (EPI == G4_GEGLU) {
     // W rows interleaved per 128-row wave slice (ops.geglu_interleave_index, the layout gemm.hip uses too): fragments 0..3 are the gate rows of
     // features f0 .. f0+63, fragments 4..7 the up rows of the same features; gate|up are rounded to bf16 first so
     // the result equals geglu(bf16 gate|up GEMM output).
     uint16_t* out = reinterpret_cast<uint16_t*>(C);
-    const int fb = (n0 >> 1) + wn * 64 + 4 * (lane >> 4);
+    const int fb = (en0 >> 1) + wn * 64 + 4 * (lane >> 4);
 #pragma unroll
     for (int j = 0; j < WM; ++j) {
       const int m = mb + j * 16;
@@ -297,9 +337,39 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
       }
     }
   }
+  }
+  if (next >= nwg) break;
+#pragma unroll
+  for (int i = 0; i < WN; ++i)
+#pragma unroll
+    for (int j = 0; j < WM; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }   // tiles
+  g4_vmcnt<0>();   // (nothing in flight: no LDS-DMA may land after the workgroup's LDS is handed to another one)
+#undef G4_STAGE
+#undef G4_STAGE_ONE
+#undef G4_TILE
+#undef G4_DESC
 #endif
 }
 
+}  // namespace
+
+namespace {
+// Persistent grid: one workgroup per CU (the kernel's LDS and registers allow one), a multiple of 8 so a
+// workgroup's virtual tile ids stay on its XCD; TB_G4_GRID overrides it (lab).
+int g4_grid(int nwg) {
+  static const int cap = [] {
+    const char* e = getenv("TB_G4_GRID");
+    int v = e ? atoi(e) : 0;
+    if (v <= 0) {
+      int dev = 0, cus = 256;
+      if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      v = cus;
+    }
+    return std::max(8, v - v % 8);
+  }();
+  return std::min(nwg, cap);
+}
 }  // namespace
 
 bool tb_gemm4_ok(int M, int N, int K) { return M > 0 && N > 0 && N % G4_BN == 0 && K >= 64 && K % 64 == 0; }
@@ -309,8 +379,8 @@ void tb_gemm4(const uint16_t* A, const uint16_t* W, void* C, const float* bias, 
               int ldc, int epi, int tile_rows, hipStream_t st) {
   if (M <= 0 || N <= 0) return;
 #define G4_GO(BM_, E_)                                                                                          \
-  hipLaunchKernelGGL((gemm4_kernel<BM_, E_>), dim3((N / G4_BN) * ((M + (BM_) - 1) / (BM_))), dim3(G4_THREADS), 0, \
-                     st, A, W, C, bias, thr, M, N, K, ldc)
+  hipLaunchKernelGGL((gemm4_kernel<BM_, E_>), dim3(g4_grid((N / G4_BN) * ((M + (BM_) - 1) / (BM_)))),            \
+                     dim3(G4_THREADS), 0, st, A, W, C, bias, thr, M, N, K, ldc)
 #define G4_EPI(BM_)                                   \
   switch (epi) {                                      \
     case G4_BF16: G4_GO(BM_, G4_BF16); break;         \
