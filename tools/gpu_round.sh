@@ -19,9 +19,11 @@ timeout -k 10 600 python bench.py "$@" > $OUT/bench.log 2>&1
 echo BENCH_OK; tail -1 $OUT/bench.log
 if [ $PROF = 1 ]; then
   cd /tmp && export TMPDIR=/tmp
-  timeout -k 10 700 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$OUT/prof -o run -- python3 $R/bench.py --steps 4 --warmup 2 "$@" > $R/$OUT/prof_bench.log 2>&1
+  timeout -k 10 700 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$OUT/prof -o run -- python3 $R/bench.py "$@" --steps 4 --warmup 2 > $R/$OUT/prof_bench.log 2>&1
   echo PROF_OK
   find $R/$OUT/prof -name "*kernel_trace*" -delete
   python3 $R/tools/kstats.py $(find $R/$OUT/prof -name "*kernel_stats.csv" | head -1) 40 > $R/$OUT/kernel_stats.txt 2>&1 || true
   head -30 $R/$OUT/kernel_stats.txt
+  python3 $R/tools/gemm_share.py $(find $R/$OUT/prof -name "*kernel_stats.csv" | head -1) > $R/$OUT/gemm_share.txt 2>&1 || true
+  cat $R/$OUT/gemm_share.txt
 fi
