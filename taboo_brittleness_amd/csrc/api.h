@@ -59,6 +59,13 @@ void tb_decode_head(const uint16_t* logits, const int32_t* tgt, int32_t* nxt, fl
 bool tb_gemm_skinny_ok(int M, int N, int K);
 void tb_gemm_skinny(const uint16_t* A, const uint16_t* W, uint16_t* C, int M, int N, int K, hipStream_t st);
 // sae.hip
+void tb_head_merge(const float* part, int npart, const int32_t* tgt, const float* tgt_logit, int32_t* nxt,
+                   float* nll_self, float* nll_tgt, float* lse, int M, int V, hipStream_t st);
+void tb_head_fused4(const uint16_t* A, const uint16_t* W, float* part, const uint16_t* ctab, const int32_t* tgt,
+                    float* tgt_logit, int32_t* nxt, float* nll_self, float* nll_tgt, int M, int N, int K, hipStream_t st);
+void tb_gemm4_qkv_rope(const uint16_t* A, const uint16_t* W, const int32_t* pos, const int32_t* slot_of_row,
+                       const float* cos_t, const float* sin_t, uint16_t* q_out, uint16_t* kc, uint16_t* vc, int M, int K,
+                       int Hq, int Hkv, int S, int max_pos, int tile_rows, hipStream_t st);
 bool tb_gemm4_ok(int M, int N, int K);
 void tb_gemm4(const uint16_t* A, const uint16_t* W, void* C, const float* bias, const float* thr, int M, int N, int K,
               int ldc, int epi, int tile_rows, hipStream_t st);

@@ -434,6 +434,29 @@ void gemm4(torch::Tensor A, torch::Tensor W, torch::Tensor C, c10::optional<torc
 
 bool gemm4_ok(int64_t M, int64_t N, int64_t K) { return tb_gemm4_ok(M, N, K); }
 
+// QKV projection with RoPE + KV-cache scatter in the epilogue (gemm4.hip G4_ROPE): x [M, K] @ wqkv [(Hq+2Hkv)*256, K]^T;
+// the same outputs as linear + rope_qkv_cache (head_dim 256 only), the qkv activation never reaches memory.
+void gemm4_qkv_rope(torch::Tensor x, torch::Tensor w, torch::Tensor pos, torch::Tensor slot_of_row, torch::Tensor cos_t,
+                    torch::Tensor sin_t, torch::Tensor q_out, torch::Tensor kc, torch::Tensor vc, int64_t Hq, int64_t Hkv,
+                    int64_t tile_rows) {
+  IN_BF16(x); IN_BF16(w); IN_I32(pos); IN_I32(slot_of_row); IN_F32(cos_t); IN_F32(sin_t); IN_BF16(q_out); IN_BF16(kc);
+  IN_BF16(vc);
+  const int K = x.size(-1), M = pos.numel();
+  TORCH_CHECK(x.numel() == (int64_t)M * K, "gemm4_qkv_rope: x must be [M, K] with M = pos.numel()");
+  TORCH_CHECK(w.dim() == 2 && w.size(0) == (Hq + 2 * Hkv) * 256 && w.size(1) == K, "gemm4_qkv_rope: w shape");
+  TORCH_CHECK(tb_gemm4_ok(M, (Hq + 2 * Hkv) * 256, K), "gemm4_qkv_rope: need K % 64 == 0, K >= 64");
+  TORCH_CHECK(q_out.numel() == (int64_t)M * Hq * 256, "gemm4_qkv_rope: q_out shape");
+  TORCH_CHECK(kc.dim() == 4 && kc.size(1) == Hkv && kc.size(3) == 256 && vc.sizes() == kc.sizes(),
+              "gemm4_qkv_rope: cache shape [slots, Hkv, S, 256]");
+  TORCH_CHECK(cos_t.dim() == 2 && cos_t.size(1) == 128 && sin_t.sizes() == cos_t.sizes(), "gemm4_qkv_rope: rope tables");
+  TORCH_CHECK(slot_of_row.numel() == M, "gemm4_qkv_rope: slot_of_row numel");
+  TORCH_CHECK(tile_rows == 256 || tile_rows == 128, "gemm4_qkv_rope: tile_rows must be 256 or 128");
+  c10::DeviceGuard g(x.device());
+  tb_gemm4_qkv_rope(cbf(x), cbf(w), pos.data_ptr<int32_t>(), slot_of_row.data_ptr<int32_t>(), cos_t.data_ptr<float>(),
+                    sin_t.data_ptr<float>(), bf(q_out), bf(kc), bf(vc), M, K, Hq, Hkv, kc.size(2), cos_t.size(0),
+                    (int)tile_rows, cur_stream());
+}
+
 // Logit-lens unembedding on the ping-pong GEMM (gemm.hip EPI_LENS): bf16 logits and their per-row
 // log-sum-exp (no softcap), so the lens needs no separate row_lse pass.  part: f32 >= M * (V / 128) * 4.
 void lens_gemm(torch::Tensor x, torch::Tensor W, torch::Tensor logits, torch::Tensor part, torch::Tensor lse) {
@@ -453,7 +476,7 @@ void lens_gemm(torch::Tensor x, torch::Tensor W, torch::Tensor logits, torch::Te
 // part: f32 workspace >= M * (V / 128) * 4; tgt_logit: f32 [M] (with tgt).
 void head_fused(torch::Tensor x, torch::Tensor W, torch::Tensor part, double cap, c10::optional<torch::Tensor> tgt,
                 c10::optional<torch::Tensor> tgt_logit, torch::Tensor nxt, torch::Tensor nll_self,
-                c10::optional<torch::Tensor> nll_tgt) {
+                c10::optional<torch::Tensor> nll_tgt, int64_t kernel) {
   IN_BF16(x); IN_BF16(W); IN_F32(part); IN_I32(nxt); IN_F32(nll_self);
   TORCH_CHECK(W.dim() == 2, "head_fused: W must be [V, K]");
   const int K = x.size(-1), M = x.numel() / K, N = W.size(0);
@@ -478,8 +501,13 @@ void head_fused(torch::Tensor x, torch::Tensor W, torch::Tensor part, double cap
     tab = tb_find_softcap_table((float)cap);
     TORCH_CHECK(tab != nullptr, "head_fused: softcap table for this cap not registered on this device");
   }
-  tb_head_fused(cbf(x), cbf(W), part.data_ptr<float>(), tab, tp, tl, nxt.data_ptr<int32_t>(),
-                nll_self.data_ptr<float>(), np, M, N, K, cur_stream());
+  // kernel 4: the four-wave GEMM (gemm4.hip G4_HEAD), otherwise the ping-pong kernel (gemm.hip EPI_HEAD)
+  if (kernel == 4)
+    tb_head_fused4(cbf(x), cbf(W), part.data_ptr<float>(), tab, tp, tl, nxt.data_ptr<int32_t>(),
+                   nll_self.data_ptr<float>(), np, M, N, K, cur_stream());
+  else
+    tb_head_fused(cbf(x), cbf(W), part.data_ptr<float>(), tab, tp, tl, nxt.data_ptr<int32_t>(),
+                  nll_self.data_ptr<float>(), np, M, N, K, cur_stream());
 }
 
 void lowrank_edit(torch::Tensor h, c10::optional<torch::Tensor> x_next, torch::Tensor apply, torch::Tensor idx,
@@ -643,6 +671,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_pp_ok", &gemm_pp_ok);
   m.def("gemm4", &gemm4);
   m.def("gemm4_ok", &gemm4_ok);
+  m.def("gemm4_qkv_rope", &gemm4_qkv_rope);
   m.def("head_fused", &head_fused);
   m.def("lens_gemm", &lens_gemm);
   m.def("gemm_skinny", &gemm_skinny);

@@ -559,6 +559,13 @@ __global__ void __launch_bounds__(256) head_merge_kernel(const float4* __restric
 
 }  // namespace
 
+void tb_head_merge(const float* part, int npart, const int32_t* tgt, const float* tgt_logit, int32_t* nxt,
+                   float* nll_self, float* nll_tgt, float* lse, int M, int V, hipStream_t st) {
+  if (M <= 0) return;
+  hipLaunchKernelGGL(head_merge_kernel, dim3(M), dim3(256), 0, st, reinterpret_cast<const float4*>(part), npart, tgt,
+                     tgt_logit, nxt, nll_self, nll_tgt, lse, V);
+}
+
 void tb_head_fused(const uint16_t* A, const uint16_t* W, float* part, const uint16_t* ctab, const int32_t* tgt,
                    float* tgt_logit, int32_t* nxt, float* nll_self, float* nll_tgt, int M, int N, int K,
                    hipStream_t st) {

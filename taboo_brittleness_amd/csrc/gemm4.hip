@@ -68,6 +68,9 @@ constexpr int G4_THREADS = 256, G4_BN = 256;
 #ifndef G4_JMAJOR
 #define G4_JMAJOR 0      // 1: MFMA order with the A (column-operand) fragment fixed over 8 W fragments
 #endif
+#ifndef G4_AREG
+#define G4_AREG 0        // 1: the A operand of the K loop staged through registers (buffer_load + ds_write_b128)
+#endif
 #ifndef G4_PRIO
 #define G4_PRIO 0        // 1: s_setprio 3 for the K loop
 #endif
@@ -94,12 +97,34 @@ __device__ __forceinline__ void g4_bar() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-enum { G4_BF16 = 0, G4_F32 = 1, G4_JUMPRELU = 2, G4_GEGLU = 3 };
+enum { G4_BF16 = 0, G4_F32 = 1, G4_JUMPRELU = 2, G4_GEGLU = 3, G4_ROPE = 4, G4_HEAD = 5 };
+
+// Fused QKV epilogue (G4_ROPE, SURVEY K3 + K4): the projection's bf16 output is never stored; each 256-column tile is
+// one head (head_dim 256): q heads are rotated into q_out [M, Hq, 256], k heads rotated and v heads copied into
+// the layer's KV cache at the row's slot / position, with rope_qkv_cache_kernel's exact bf16 rounding chain
+// (csrc/rope.hip).  Rows with pos < 0 are padding: q zeroed, no cache write.
+struct G4Rope {
+  const int32_t* pos;
+  const int32_t* slot;
+  const float* cos_t;
+  const float* sin_t;
+  uint16_t* q_out;
+  uint16_t* kc;
+  uint16_t* vc;
+  int Hq, Hkv, S, max_pos;
+  // G4_HEAD (vocab head): bf16 logits -> exact bf16 final softcap by table (ctab, staged into the
+  // stage LDS after the K loop), per (row, 128-column wave slice) {max, sum exp(z - max), first argmax} into
+  // part[m * (N/128) + n/128]; the row's teacher-target logit into tgt_logit.  The logits never reach memory.
+  const uint16_t* ctab;
+  const int32_t* tgt;
+  float* tgt_logit;
+};
+constexpr int G4_CTAB_N = 32768;
 
 template <int BM, int EPI>
 __global__ void __launch_bounds__(G4_THREADS, 1)
 gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, void* __restrict__ C,
-             const float* __restrict__ bias, const float* __restrict__ thr, int M, int N, int K, int ldc) {
+             const float* __restrict__ bias, const float* __restrict__ thr, int M, int N, int K, int ldc, G4Rope rp) {
 #if defined(__HIP_DEVICE_COMPILE__)   // the host pass only needs the signature (for the launch stub); some builtins and
                                      // the "a" asm constraint in the body make it silently drop the stub
   static_assert(BM == 256 || BM == 128, "tile rows");
@@ -152,7 +177,11 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
   // chunk 4*step + (lane>>4)
   const int xr = (lane & 15) >> 1;
   const int co0 = ((lane >> 4) ^ xr) << 4, co1 = ((4 + (lane >> 4)) ^ xr) << 4;
-  const int offp = (wn * 128 + (lane & 15)) * 128;
+  // W-fragment i of wave wn covers tile rows (output columns) wn*128 + 16 i .. (G4_ROPE: wn*64 + 128 (i/4) + 16 (i%4),
+  // so a lane holds both columns d and d + 128 of each rotation pair)
+  constexpr bool RP = EPI == G4_ROPE;
+  const int offp = (wn * (RP ? 64 : 128) + (lane & 15)) * 128;
+#define G4_PROW(i) (RP ? (((i) >> 2) * 128 + ((i) & 3) * 16) : (i) * 16)
   const int offq = PIMG + (wm * (BM / 2) + (lane & 15)) * 128;
 
   f32x4 acc[WN][WM];
@@ -200,7 +229,10 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
   constexpr int BAR1 = NR + G4_SLACK1;           // barrier #1 after this many MFMAs of the period
   constexpr int BAR2 = NT2 - NR - G4_SLACK2;     // barrier #2 before MFMA BAR2
   constexpr int GSP = (NT2 - BAR1) / GL;         // MFMAs per LDS-DMA instruction, spread to the period's end
-  constexpr int N2 = (BAR2 - BAR1) / GSP < GL ? (BAR2 - BAR1) / GSP : GL;   // of them issued before barrier #2
+  constexpr int N2S = (BAR2 - BAR1) / GSP < GL ? (BAR2 - BAR1) / GSP : GL;   // slots issued before barrier #2
+  // VMEM instructions younger than tile t+1's at barrier #2: the LDS-DMA slots before it, or with G4_AREG the A
+  // loads of tile t+2 (issued at the period's start) and the W LDS-DMA slots before it
+  constexpr int N2 = G4_AREG ? QI + (N2S < PI ? N2S : PI) : N2S;
   static_assert(GSP >= 1 && BAR1 < NMF && BAR1 < BAR2, "schedule");
 
   const int nt = K >> 6;
@@ -212,7 +244,7 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
   g4_vmcnt<GL>();
   g4_bar();
 #pragma unroll
-  for (int i = 0; i < WN; ++i) p0[i] = frag(0, offp + i * 2048 + co0);
+  for (int i = 0; i < WN; ++i) p0[i] = frag(0, offp + G4_PROW(i) * 128 + co0);
 #pragma unroll
   for (int j = 0; j < WM; ++j) q0[j] = frag(0, offq + j * 2048 + co0);
 
@@ -227,7 +259,7 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
     G4_MF(u);                                                                                   \
     const int v_ = (u) - BAR2;                                                                  \
     if (v_ >= 0 && v_ < NR && !G4_LAB_NOREAD) {                                                 \
-      if (v_ < WN) p0[v_ >= 0 && v_ < WN ? v_ : 0] = frag(sb ^ 1, offp + v_ * 2048 + co0);      \
+      if (v_ < WN) p0[v_ >= 0 && v_ < WN ? v_ : 0] = frag(sb ^ 1, offp + G4_PROW(v_) * 128 + co0); \
       else q0[v_ >= WN && v_ < NR ? v_ - WN : 0] = frag(sb ^ 1, offq + (v_ - WN) * 2048 + co0); \
     }                                                                                           \
   } while (0)
@@ -235,6 +267,9 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
   // Every period is branch-free: past the end, tile nt-1 is re-staged into the free stage and the last reads
   // fill the idle step-0 set.
   if (G4_PRIO) __builtin_amdgcn_s_setprio(3);
+#if G4_AREG
+  u32x4 areg[QI];
+#endif
   for (int t = 0; t < nt; ++t) {
     const int sb = t & 1, tn = min(t + 2, nt - 1);
     // (phases as short unrolled loops: hipcc will not fully unroll one 128-step loop, and a rolled one would index
@@ -243,9 +278,14 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
     for (int u = 0; u < NR; ++u) {   // step-0 MFMAs, step-1 fragment reads
       G4_MF(u);
       if (!G4_LAB_NOREAD) {
-        if (u < WN) p1[u < WN ? u : 0] = frag(sb, offp + u * 2048 + co1);
+        if (u < WN) p1[u < WN ? u : 0] = frag(sb, offp + G4_PROW(u) * 128 + co1);
         else q1[u >= WN ? u - WN : 0] = frag(sb, offq + (u - WN) * 2048 + co1);
       }
+#if G4_AREG
+      if (u < QI)
+        areg[u < QI ? u : 0] = __builtin_amdgcn_raw_buffer_load_b128(
+            __builtin_amdgcn_make_buffer_rsrc(atile, 0, abytes, 0x00020000), vq[u < QI ? u : 0], tn * 128, G4_AUX_A);
+#endif
     }
 #pragma unroll
     for (int u = NR; u < BAR1; ++u) G4_MF(u);
@@ -255,7 +295,14 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
     for (int g = 0; g < GL; ++g) {        // the LDS-DMA of tile t+2, one instruction per GSP MFMAs
 #pragma unroll
       for (int k = 0; k < GSP; ++k) G4_POST(BAR1 + g * GSP + k);
-      if (!G4_LAB_NOSTAGE && !(G4_LAB_HALF && g >= PI)) G4_STAGE_ONE(g, tn, sb);
+      if (G4_AREG && g >= PI) {
+#if G4_AREG
+        *reinterpret_cast<u32x4*>(smem + sb * STG + PIMG + (g - PI) * 4096 + wid * 1024 + lane * 16) =
+            areg[g >= PI ? g - PI : 0];
+#endif
+      } else if (!G4_LAB_NOSTAGE && !(G4_LAB_HALF && g >= PI)) {
+        G4_STAGE_ONE(g, tn, sb);
+      }
     }
 #pragma unroll
     for (int u = BAR1 + GL * GSP; u < NT2; ++u) G4_POST(u);
@@ -278,8 +325,20 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
     tile = next;
     G4_TILE(tile, m0, n0);
     G4_DESC();
-    G4_STAGE(0, 0);
-    G4_STAGE(min(1, nt - 1), 1);
+    if constexpr (EPI != G4_HEAD) {
+      G4_STAGE(0, 0);
+      G4_STAGE(min(1, nt - 1), 1);
+    }
+  }
+  const uint16_t* ct = nullptr;
+  if constexpr (EPI == G4_HEAD) {
+    if (rp.ctab != nullptr) {
+      uint16_t* ctw = reinterpret_cast<uint16_t*>(smem);
+      for (int i = tid; i < G4_CTAB_N / 8; i += G4_THREADS)
+        reinterpret_cast<uint4*>(ctw)[i] = reinterpret_cast<const uint4*>(rp.ctab)[i];
+      ct = ctw;
+      __syncthreads();
+    }
   }
 #if G4_ASM_MFMA
   asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");   // last MFMA's D -> the epilogue's accumulator reads
@@ -289,7 +348,86 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
   {
   const int nb = en0 + wn * 128 + 4 * (lane >> 4);
   const int mb = em0 + wm * (BM / 2) + (lane & 15);
-  if constexpr (EPI == G4_GEGLU) {
+  if constexpr (EPI == G4_HEAD) {
+    // lane: columns nb + 16 i + r (i < 8, r < 4) of rows mb + 16 j; the 4 lanes lane&15 + 16 q share a row
+    float4* part = reinterpret_cast<float4*>(C);
+    const int npart = N / 128, pcol = (en0 >> 7) + wn;
+#pragma unroll
+    for (int j = 0; j < WM; ++j) {
+      const int m = mb + j * 16;
+      const int t = (rp.tgt != nullptr && m < M) ? rp.tgt[m] : -1;
+      float z[WN * 4];
+      float mx = -INFINITY;
+      int bi = 0x7fffffff;
+#pragma unroll
+      for (int i = 0; i < WN; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const uint32_t b = f2bf(acc[i][j][r]);
+          const float v = ct != nullptr ? __uint_as_float(((uint32_t)ct[b & 0x7fffu] | (b & 0x8000u)) << 16)
+                                        : __uint_as_float(b << 16);
+          const int n = nb + i * 16 + r;
+          z[i * 4 + r] = v;
+          if (v > mx || (v == mx && n < bi)) { mx = v; bi = n; }
+          if (n == t) rp.tgt_logit[m] = v;
+        }
+      float sum = 0.f;
+#pragma unroll
+      for (int e = 0; e < WN * 4; ++e) sum += __expf(z[e] - mx);
+#pragma unroll
+      for (int o = 16; o <= 32; o <<= 1) {
+        const float m2 = __shfl_xor(mx, o, 64), s2 = __shfl_xor(sum, o, 64);
+        const int i2 = __shfl_xor(bi, o, 64);
+        if (m2 > mx) { sum = sum * __expf(mx - m2) + s2; mx = m2; bi = i2; }
+        else if (m2 == mx) { sum += s2; bi = min(bi, i2); }
+        else { sum += s2 * __expf(m2 - mx); }
+      }
+      if (lane < 16 && m < M) part[(size_t)m * npart + pcol] = make_float4(mx, sum, __int_as_float(bi), 0.f);
+    }
+  } else if constexpr (EPI == G4_ROPE) {
+    // lane: d = wn*64 + 16 i + 4 (lane>>4) + r (i < 4) and d + 128 from fragment i + 4
+    const int head = en0 >> 8, half = 128;
+    const bool is_q = head < rp.Hq, is_k = !is_q && head < rp.Hq + rp.Hkv;
+#pragma unroll
+    for (int j = 0; j < WM; ++j) {
+      const int m = mb + j * 16;
+      if (m >= M) continue;
+      const int p = rp.pos[m];
+      if (!is_q && p < 0) continue;
+      const int pp = p < rp.max_pos ? p : rp.max_pos - 1;
+      uint16_t* dst;
+      if (is_q) dst = rp.q_out + ((size_t)m * rp.Hq + head) * 256;
+      else {
+        if (p >= rp.S) continue;
+        dst = (is_k ? rp.kc : rp.vc) + (((size_t)rp.slot[m] * rp.Hkv + (head - rp.Hq - (is_k ? 0 : rp.Hkv))) * rp.S + p) * 256;
+      }
+#pragma unroll
+      for (int i = 0; i < WN / 2; ++i) {
+        const int d = wn * 64 + i * 16 + 4 * (lane >> 4);
+        float o1[4], o2[4];
+        if (p < 0) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o1[r] = o2[r] = 0.f;
+        } else if (!is_q && !is_k) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) { o1[r] = acc[i][j][r]; o2[r] = acc[i + WN / 2][j][r]; }
+        } else {
+          const float4 c4 = *reinterpret_cast<const float4*>(rp.cos_t + (size_t)pp * half + d);
+          const float4 s4 = *reinterpret_cast<const float4*>(rp.sin_t + (size_t)pp * half + d);
+          const float cc[4] = {c4.x, c4.y, c4.z, c4.w}, ss[4] = {s4.x, s4.y, s4.z, s4.w};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float x1 = rbf(acc[i][j][r]), x2 = rbf(acc[i + WN / 2][j][r]);
+            const float c = rbf(cc[r]), sn = rbf(ss[r]);
+            o1[r] = rbf(rbf(x1 * c) + rbf(-x2 * sn));
+            o2[r] = rbf(rbf(x2 * c) + rbf(x1 * sn));
+          }
+        }
+        *reinterpret_cast<uint2*>(dst + d) = make_uint2(pack2(o1[0], o1[1]), pack2(o1[2], o1[3]));
+        *reinterpret_cast<uint2*>(dst + d + half) = make_uint2(pack2(o2[0], o2[1]), pack2(o2[2], o2[3]));
+      }
+    }
+  } else if constexpr (EPI == G4_GEGLU) {
     // W rows interleaved per 128-row wave slice (ops.geglu_interleave_index, the layout gemm.hip uses too): fragments 0..3 are the gate rows of
     // features f0 .. f0+63, fragments 4..7 the up rows of the same features; gate|up are rounded to bf16 first so
     // the result equals geglu(bf16 gate|up GEMM output).
@@ -339,6 +477,11 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
   }
   }
   if (next >= nwg) break;
+  if constexpr (EPI == G4_HEAD) {   // every wave is done with the table: the next tile's first K tiles
+    __syncthreads();
+    G4_STAGE(0, 0);
+    G4_STAGE(min(1, nt - 1), 1);
+  }
 #pragma unroll
   for (int i = 0; i < WN; ++i)
 #pragma unroll
@@ -378,9 +521,10 @@ bool tb_gemm4_ok(int M, int N, int K) { return M > 0 && N > 0 && N % G4_BN == 0 
 void tb_gemm4(const uint16_t* A, const uint16_t* W, void* C, const float* bias, const float* thr, int M, int N, int K,
               int ldc, int epi, int tile_rows, hipStream_t st) {
   if (M <= 0 || N <= 0) return;
+  const G4Rope rp{};
 #define G4_GO(BM_, E_)                                                                                          \
   hipLaunchKernelGGL((gemm4_kernel<BM_, E_>), dim3(g4_grid((N / G4_BN) * ((M + (BM_) - 1) / (BM_)))),            \
-                     dim3(G4_THREADS), 0, st, A, W, C, bias, thr, M, N, K, ldc)
+                     dim3(G4_THREADS), 0, st, A, W, C, bias, thr, M, N, K, ldc, rp)
 #define G4_EPI(BM_)                                   \
   switch (epi) {                                      \
     case G4_BF16: G4_GO(BM_, G4_BF16); break;         \
@@ -394,5 +538,33 @@ void tb_gemm4(const uint16_t* A, const uint16_t* W, void* C, const float* bias, 
     G4_EPI(256)
   }
 #undef G4_EPI
+}
+
+void tb_head_fused4(const uint16_t* A, const uint16_t* W, float* part, const uint16_t* ctab, const int32_t* tgt,
+                    float* tgt_logit, int32_t* nxt, float* nll_self, float* nll_tgt, int M, int N, int K, hipStream_t st) {
+  if (M <= 0) return;
+  void* C = part;
+  const float* bias = nullptr;
+  const float* thr = nullptr;
+  const int ldc = 0;
+  G4Rope rp{};
+  rp.ctab = ctab;
+  rp.tgt = tgt;
+  rp.tgt_logit = tgt_logit;
+  G4_GO(256, G4_HEAD);
+  tb_head_merge(reinterpret_cast<const float*>(part), N / 128, tgt, tgt_logit, nxt, nll_self, nll_tgt, nullptr, M, N, st);
+}
+
+void tb_gemm4_qkv_rope(const uint16_t* A, const uint16_t* W, const int32_t* pos, const int32_t* slot_of_row,
+                       const float* cos_t, const float* sin_t, uint16_t* q_out, uint16_t* kc, uint16_t* vc, int M, int K,
+                       int Hq, int Hkv, int S, int max_pos, int tile_rows, hipStream_t st) {
+  if (M <= 0) return;
+  const int N = (Hq + 2 * Hkv) * 256, ldc = 0;
+  void* C = nullptr;
+  const float* bias = nullptr;
+  const float* thr = nullptr;
+  const G4Rope rp{pos, slot_of_row, cos_t, sin_t, q_out, kc, vc, Hq, Hkv, S, max_pos};
+  if (tile_rows == 128) G4_GO(128, G4_ROPE);
+  else G4_GO(256, G4_ROPE);
 #undef G4_GO
 }

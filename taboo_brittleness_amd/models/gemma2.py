@@ -7,8 +7,8 @@ row (``pos < 0`` marks padding) and every sequence owns a KV-cache slot.
 
 Per decoder block (6 launches + 3 hipBLASLt GEMMs):
 
-    qkv = x Wqkv^T                       (hipBLASLt)
-    q   = rope_qkv_cache(qkv) ; K/V -> cache   (HIP)
+    qkv = x Wqkv^T ; q = rope(qkv), K/V -> cache   (one gemm4 launch with the G4_ROPE epilogue, or
+                                                 hipBLASLt + rope_qkv_cache, per the GEMM dispatch)
     a   = attention(q, cache)             (HIP, softcap 50, GQA, sliding window)
     o   = a Wo^T                           (hipBLASLt)
     x   = add_rmsnorm2(h, o)  # h += post_attn_norm(o); x = pre_ffn_norm(h)   (HIP)
@@ -308,11 +308,14 @@ class Gemma2Model:
             first = start + 1
         for l in range(first, s.layers):
             L = w.layers[l]
-            ops.linear(x, L.wqkv, out=ws.qkv)
-            if lora is not None:
+            if lora is None:    # fused QKV + RoPE + KV scatter where the dispatch runs the projection in-tree
+                ops.qkv_rope_cache(x, L.wqkv, pos32, ws.slot_rows, self.cos_t, self.sin_t, cache.k[l], cache.v[l],
+                                   ls.heads, ls.kv_heads, ls.head_dim, q_out=ws.q, qkv_ws=ws.qkv)
+            else:
+                ops.linear(x, L.wqkv, out=ws.qkv)
                 lora.apply(l, "qkv", x, ws.qkv, lmask)
-            ops.rope_qkv_cache(ws.qkv, pos32, ws.slot_rows, self.cos_t, self.sin_t, cache.k[l], cache.v[l],
-                               ls.heads, ls.kv_heads, ls.head_dim, q_out=ws.q)
+                ops.rope_qkv_cache(ws.qkv, pos32, ws.slot_rows, self.cos_t, self.sin_t, cache.k[l], cache.v[l],
+                                   ls.heads, ls.kv_heads, ls.head_dim, q_out=ws.q)
             attn(l, ws.q, cache.k[l], cache.v[l], pos32, s.sliding_window if s.is_sliding(l) else 0, ws.attn)
             ops.linear(ws.attn, L.wo, out=ws.o)
             if lora is not None:

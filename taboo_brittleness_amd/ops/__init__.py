@@ -147,6 +147,36 @@ def rope_qkv_cache(qkv, pos, slot_of_row, cos_t, sin_t, kc, vc, Hq, Hkv, HD, q_o
     return q
 
 
+FUSED_QKV = os.environ.get("TB_FUSED_QKV", "auto")   # auto: when the dispatch runs the QKV shape in-tree | 1 | 0
+
+
+def qkv_rope_fused_ok(x: torch.Tensor, wqkv: torch.Tensor, HD: int) -> bool:
+    """Whether ``qkv_rope_cache`` runs the fused in-tree path (head_dim 256, ``TB_FUSED_QKV``; ``auto`` follows
+    the GEMM dispatch's choice for the plain QKV projection at this row count)."""
+    if not x.is_cuda or HD != 256 or FUSED_QKV == "0":
+        return False
+    K = x.shape[-1]
+    M = x.numel() // K
+    if M <= 0 or not _k().gemm4_ok(M, wqkv.shape[0], K):
+        return False
+    return FUSED_QKV == "1" or _GD.choose(M, wqkv.shape[0], K, 0) != "blas"
+
+
+def qkv_rope_cache(x, wqkv, pos, slot_of_row, cos_t, sin_t, kc, vc, Hq, Hkv, HD, q_out=None, qkv_ws=None):
+    """``rope_qkv_cache(linear(x, wqkv))``: on the GPU with head_dim 256, one four-wave MFMA GEMM whose epilogue
+    rotates q / k and scatters k / v into the cache (``csrc/gemm4.hip`` G4_ROPE, bit-identical to the unfused
+    pair); otherwise the projection into ``qkv_ws`` then ``rope_qkv_cache``."""
+    if qkv_rope_fused_ok(x, wqkv, HD):
+        M = pos.numel()
+        q_out = _out(q_out, (M, Hq, HD), x.dtype, x.device)
+        c = _GD.choose(M, wqkv.shape[0], x.shape[-1], 0)
+        rows = int(str(c).lstrip("g")) if c != "blas" else int(str(_GD.fill_choice(M, wqkv.shape[0])).lstrip("g"))
+        _k().gemm4_qkv_rope(x, wqkv, pos, slot_of_row, cos_t, sin_t, q_out, kc, vc, int(Hq), int(Hkv), rows)
+        return q_out
+    qkv = linear(x, wqkv, out=qkv_ws)
+    return rope_qkv_cache(qkv, pos, slot_of_row, cos_t, sin_t, kc, vc, Hq, Hkv, HD, q_out=q_out)
+
+
 def kv_fanout(kc, vc, src_row, slot, pos, nlayers: int) -> None:
     """Prefix-trie decode: copy the K/V of layers ``< nlayers`` that row ``src_row[r]`` wrote at its position
     into row ``r``'s own slot at ``r``'s position (``kc/vc [L, slots, Hkv, S, HD]``; ``src_row < 0`` or
@@ -386,6 +416,9 @@ def head_part_numel(rows: int, vocab: int) -> int:
     return rows * (vocab // 128) * 4
 
 
+HEAD_KERNEL = 4 if os.environ.get("TB_HEAD_KERNEL", "pp") == "g4" else 0   # fused head GEMM: gemm.hip (default) | gemm4.hip
+
+
 def vocab_head(x, w, cap, tgt=None, nxt=None, nll_self=None, nll_tgt=None, part=None, tgt_logit=None,
                fused: Optional[bool] = None):
     """``decode_head(x @ w^T, ...)`` from the final-normed rows ``x``: greedy token (bf16-softcap argmax), its
@@ -408,9 +441,9 @@ def vocab_head(x, w, cap, tgt=None, nxt=None, nll_self=None, nll_tgt=None, part=
         if tgt is not None:
             nll_tgt = _out(nll_tgt, (R,), torch.float32, dev)
             tgt_logit = _out(tgt_logit, (R,), torch.float32, dev)
-            _k().head_fused(x, w, part, float(cap), tgt, tgt_logit, nxt, nll_self, nll_tgt)
+            _k().head_fused(x, w, part, float(cap), tgt, tgt_logit, nxt, nll_self, nll_tgt, HEAD_KERNEL)
         else:
-            _k().head_fused(x, w, part, float(cap), None, None, nxt, nll_self, None)
+            _k().head_fused(x, w, part, float(cap), None, None, nxt, nll_self, None, HEAD_KERNEL)
         return nxt, nll_self, nll_tgt
     return decode_head(linear(x, w), cap, tgt, nxt, nll_self, nll_tgt)
 

@@ -218,11 +218,15 @@ def test_decode_head(gpu):
     _close(nt, ref.xent_rows(lg, tgt, 30.0, True), atol=2e-3, rtol=1e-4)
 
 
-@pytest.mark.parametrize("M,V,K,cap", [(300, 4096, 256, 30.0), (1, 2048, 3584, 30.0), (520, 8192, 640, 0.0)])
-def test_vocab_head_fused(gpu, M, V, K, cap):
-    """Fused vocab head (ping-pong GEMM + softcap-table epilogue + partial merge, csrc/gemm.hip) == the
-    unfused path on the same kernel's bf16 logits (bit-identical logits: exact argmax incl. cross-partial
-    and in-partial ties, NLLs to fp32 summation order), and close to a float32 PyTorch reference."""
+@pytest.mark.parametrize("kernel", [4, 0])
+@pytest.mark.parametrize("M,V,K,cap", [(300, 4096, 256, 30.0), (1, 2048, 3584, 30.0), (520, 8192, 640, 0.0),
+                                       (700, 256000, 3584, 30.0)])
+def test_vocab_head_fused(gpu, M, V, K, cap, kernel, monkeypatch):
+    """Fused vocab head (softcap-table epilogue + partial merge; kernel 4: csrc/gemm4.hip G4_HEAD, persistent with
+    several tiles per workgroup at the Gemma-2 vocab; 0: csrc/gemm.hip EPI_HEAD) == the unfused path on the
+    in-tree kernel's bf16 logits (bit-identical logits: exact argmax incl. cross-partial and in-partial ties, NLLs
+    to fp32 summation order), and close to a float32 PyTorch reference."""
+    monkeypatch.setattr(ops, "HEAD_KERNEL", kernel)
     torch.manual_seed(17)
     x = torch.randn(M, K).to(BF)
     w = (torch.randn(V, K) * 0.05).to(BF)
@@ -477,6 +481,40 @@ def test_gemm4_bitequal_pingpong_and_batch_invariant(gpu, N, K, epi):
     if epi == 0:
         r = A[:64].float() @ W.float().T
         _close(ref_pp[:64], r, atol=1e-2 * K ** 0.5, rtol=1e-2)
+
+
+@pytest.mark.parametrize("M,rows", [(300, 256), (77, 128)])
+def test_gemm4_qkv_rope_fused(gpu, M, rows):
+    """QKV GEMM with RoPE + KV scatter in the epilogue (csrc/gemm4.hip G4_ROPE) at the Gemma-2-9B head layout
+    (16 q / 8 kv heads of 256, K = 3584): q, K cache and V cache BIT-identical to the in-tree GEMM followed by
+    rope_qkv_cache, including padding rows (pos < 0: q zeroed, no cache write) and positions past the cache."""
+    torch.manual_seed(7)
+    Hq, Hkv, HD, K, S = 16, 8, 256, 3584, 40
+    slots = M              # one (slot, position) per row, as in the engine: no two rows write one cache entry
+    x = ((torch.rand(M, K) * 2 - 1) * 0.5).to(BF).to(gpu)
+    w = ((torch.rand((Hq + 2 * Hkv) * HD, K) * 2 - 1) * 0.05).to(BF).to(gpu)
+    pos = torch.randint(0, S + 3, (M,), dtype=torch.int32)
+    pos[::17] = -1
+    pos = pos.to(gpu)
+    slot = torch.randperm(slots)[:M].to(torch.int32).to(gpu)
+    maxp = 64
+    inv = 1.0 / (10000.0 ** (torch.arange(0, HD, 2).float() / HD))
+    ang = torch.arange(maxp).float()[:, None] * inv[None]
+    cos_t, sin_t = ang.cos().to(gpu), ang.sin().to(gpu)
+    k = ops._k()
+    kc0 = torch.randn(slots, Hkv, S, HD).to(BF).to(gpu)
+    vc0 = torch.randn(slots, Hkv, S, HD).to(BF).to(gpu)
+    qkv = torch.empty(M, (Hq + 2 * Hkv) * HD, device=gpu, dtype=BF)
+    k.gemm4(x, w, qkv, None, None, 0, rows)
+    q_ref = torch.empty(M, Hq, HD, device=gpu, dtype=BF)
+    kc_ref, vc_ref = kc0.clone(), vc0.clone()
+    k.rope_qkv_cache(qkv, pos, slot, cos_t, sin_t, q_ref, kc_ref, vc_ref, Hq, Hkv, HD)
+    q = torch.full((M, Hq, HD), 7.0, device=gpu, dtype=BF)
+    kc, vc = kc0.clone(), vc0.clone()
+    k.gemm4_qkv_rope(x, w, pos, slot, cos_t, sin_t, q, kc, vc, Hq, Hkv, rows)
+    assert torch.equal(q, q_ref)
+    assert torch.equal(kc, kc_ref) and torch.equal(vc, vc_ref)
+    assert not torch.equal(kc, kc0)       # the cache was written
 
 
 def test_linear_dispatch_modes(gpu):
