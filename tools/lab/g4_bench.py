@@ -25,10 +25,18 @@ LIB.g4_gemm.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int] * 6 + [ctypes.c_vo
 LIB.g4_gemm.restype = ctypes.c_int
 
 
-def g4(A, W, C, epi=0, rows=256):
+EXTRA = {}
+for _f in filter(None, os.environ.get("G4_LIBS", "").split(",")):
+    _l = ctypes.CDLL(os.path.join(ROOT, "tools", "lab", _f))
+    _l.g4_gemm.argtypes = LIB.g4_gemm.argtypes
+    _l.g4_gemm.restype = ctypes.c_int
+    EXTRA[_f.replace("g4_lab_", "").replace(".so", "")] = _l
+
+
+def g4(A, W, C, epi=0, rows=256, lib=None):
     M, K = A.shape
     N = W.shape[0]
-    r = LIB.g4_gemm(A.data_ptr(), W.data_ptr(), C.data_ptr(), M, N, K, C.shape[1], epi, rows,
+    r = (lib or LIB).g4_gemm(A.data_ptr(), W.data_ptr(), C.data_ptr(), M, N, K, C.shape[1], epi, rows,
                     torch.cuda.current_stream().cuda_stream)
     assert r == 0, r
 
@@ -113,6 +121,8 @@ def time_shapes(shapes, rounds=int(os.environ.get("G4_ROUNDS", "7"))):
                "pp256": lambda: k.gemm_pp(A, nxt(), C, None, None, 0, 256),
                "g4_256": lambda: g4(A, nxt(), C, 0, 256),
                "g4_128": lambda: g4(A, nxt(), C, 0, 128)}
+        for name, lib in EXTRA.items():      # G4_LIBS: more builds of the kernel, interleaved in this process
+            var[name] = (lambda lib_: lambda: g4(A, nxt(), C, 0, 256, lib_))(lib)
         for f in var.values():
             f()
         torch.cuda.synchronize()
