@@ -66,6 +66,8 @@ void tb_head_fused4(const uint16_t* A, const uint16_t* W, float* part, const uin
 void tb_gemm4_qkv_rope(const uint16_t* A, const uint16_t* W, const int32_t* pos, const int32_t* slot_of_row,
                        const float* cos_t, const float* sin_t, uint16_t* q_out, uint16_t* kc, uint16_t* vc, int M, int K,
                        int Hq, int Hkv, int S, int max_pos, int tile_rows, hipStream_t st);
+bool tb_register_softcap_compact(float cap, const uint16_t* tab, int lo, int hi, float sat);
+bool tb_softcap_compact(const uint16_t* x, float* y, int n, float cap, hipStream_t st);
 bool tb_gemm4_ok(int M, int N, int K);
 void tb_gemm4(const uint16_t* A, const uint16_t* W, void* C, const float* bias, const float* thr, int M, int N, int K,
               int ldc, int epi, int tile_rows, hipStream_t st);

@@ -334,6 +334,24 @@ void register_softcap_table(torch::Tensor tab, double cap) {
   tb_register_softcap_table((float)cap, reinterpret_cast<const uint16_t*>(tab.data_ptr()));
 }
 
+// Compact exact softcap (lens.hip CapC): tab = the reference table's entries [lo, hi) (bf16 magnitudes); |x| < lo is
+// computed as rbf(rbf(x / cap) * cap), [hi, inf] saturates at sat — ops._softcap_table checks both exhaustively.
+bool register_softcap_compact(torch::Tensor tab, double cap, int64_t lo, int64_t hi, double sat) {
+  CHECK_DEV(tab); CHECK_CONTIG(tab);
+  TORCH_CHECK(tab.scalar_type() == at::kBFloat16 && tab.numel() == hi - lo, "compact softcap table: hi - lo bf16 entries");
+  c10::DeviceGuard g(tab.device());
+  return tb_register_softcap_compact((float)cap, reinterpret_cast<const uint16_t*>(tab.data_ptr()), (int)lo, (int)hi,
+                                     (float)sat);
+}
+
+// y[i] = exact bf16 softcap of x[i] (fp32 values) through the compact path; false if none is registered for cap
+bool softcap_compact(torch::Tensor x, torch::Tensor y, double cap) {
+  IN_BF16(x); IN_F32(y);
+  TORCH_CHECK(y.numel() == x.numel(), "softcap_compact: shapes");
+  c10::DeviceGuard g(x.device());
+  return tb_softcap_compact(cbf(x), y.data_ptr<float>(), (int)x.numel(), (float)cap, cur_stream());
+}
+
 void decode_head(torch::Tensor logits, c10::optional<torch::Tensor> tgt, torch::Tensor nxt, torch::Tensor nll_self,
                  c10::optional<torch::Tensor> nll_tgt, double cap) {
   IN_BF16(logits); IN_I32(nxt); IN_F32(nll_self);
@@ -666,6 +684,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("xent_rows", &xent_rows);
   m.def("decode_head", &decode_head);
   m.def("register_softcap_table", &register_softcap_table);
+  m.def("register_softcap_compact", &register_softcap_compact);
+  m.def("softcap_compact", &softcap_compact);
   m.def("gemm_nt", &gemm_nt);
   m.def("gemm_pp", &gemm_pp);
   m.def("gemm_pp_ok", &gemm_pp_ok);

@@ -16,6 +16,8 @@
 //                 the NLL of an optional teacher target (the baseline's token at that column)
 #include "common.h"
 #include "api.h"
+#include <algorithm>
+#include <cstdlib>
 
 namespace {
 
@@ -57,6 +59,31 @@ __device__ __forceinline__ const uint16_t* stage_ctab(const uint16_t* tab, uint1
 
 __device__ __forceinline__ float ctab_get(const uint16_t* ct, uint32_t b) {
   return __uint_as_float(((uint32_t)ct[b & 0x7fffu] | (b & 0x8000u)) << 16);
+}
+
+// ---- compact exact softcap (decode_head) ------------------------------------------------------------------
+// The chain rbf(rbf(tanh(rbf(x/cap))) * cap) equals rbf(rbf(x * (1/cap)) * cap) for |x| below `lo` (2.703 at cap 30:
+// tanh(y) rounds to y there) and saturates at `sat` from `hi` on (104 at cap 30), both checked exhaustively against
+// the reference table on the host (ops._softcap_table, tests/test_softcap_compact_cpu.py).  Only the hi - lo
+// (~675) bit patterns in between need the table: 1.35 KB of LDS instead of 64 KB, read only by the lanes whose
+// logit falls there — no bank-conflicted 64 KB gather, and the small LDS footprint lets full occupancy stream.
+struct CapC {
+  const uint16_t* tab;   // [hi - lo] bf16 magnitudes
+  int lo, hi;
+  float sat, rc, cap;
+};
+constexpr int CAPC_MAX = 2048;   // table entries staged (host-checked)
+
+__device__ __forceinline__ float capc1(uint32_t b, const uint16_t* lt, const CapC& c) {
+  const uint32_t ab = b & 0x7fffu;
+  const float x = __uint_as_float(b << 16);
+  const float a = rbf(rbf(x * c.rc) * c.cap);
+  if (ab < (uint32_t)c.lo) return a;
+  float mag;
+  if (ab < (uint32_t)c.hi) mag = __uint_as_float((uint32_t)lt[ab - c.lo] << 16);
+  else if (ab <= 0x7f80u) mag = c.sat;
+  else return x;   // NaN stays NaN
+  return (b & 0x8000u) ? -mag : mag;
 }
 
 // 8 logits of a uint4 -> capped fp32 (table, emulated compute, fp32 tanh, or none)
@@ -442,6 +469,99 @@ __global__ void __launch_bounds__(512) decode_head_kernel(const uint16_t* __rest
   }
 }
 
+// decode_head on the compact softcap (see CapC): same outputs as decode_head_kernel with the full table
+template <int UNR>
+__global__ void __launch_bounds__(512) decode_head_c_kernel(const uint16_t* __restrict__ logits,
+                                                            const int32_t* __restrict__ tgt, int32_t* __restrict__ nxt,
+                                                            float* __restrict__ nll_self, float* __restrict__ nll_tgt,
+                                                            int V, CapC cc) {
+  __shared__ float sm[8], ss[8], sv[8];
+  __shared__ int si[8];
+  __shared__ __attribute__((aligned(16))) uint16_t lt[CAPC_MAX];
+  for (int i = threadIdx.x; i < cc.hi - cc.lo; i += blockDim.x) lt[i] = cc.tab[i];
+  __syncthreads();
+  const int r = blockIdx.x;
+  const uint16_t* row = logits + (size_t)r * V;
+  float m = -INFINITY, s = 0.f;
+  ArgBest best{-INFINITY, 0x7fffffff};
+  const int nv = V >> 3;
+  stream_row<UNR>(reinterpret_cast<const uint4*>(row), nv, [&](const uint4& v, int c) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    float f[8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      f[2 * k] = capc1(w[k] & 0xffffu, lt, cc);
+      f[2 * k + 1] = capc1(w[k] >> 16, lt, cc);
+    }
+    float lm = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      lm = fmaxf(lm, f[j]);
+      best = better(best, ArgBest{f[j], c * 8 + j});
+    }
+    float ls = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ls += __expf(f[j] - lm);
+    online_merge(m, s, lm, ls);
+  });
+  for (int c = nv * 8 + threadIdx.x; c < V; c += blockDim.x) {
+    const float x = capc1(row[c], lt, cc);
+    best = better(best, ArgBest{x, c});
+    if (m == -INFINITY) { m = x; s = 1.f; } else online_add(m, s, x);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(s, o, 64);
+    online_merge(m, s, m2, s2);
+    ArgBest oth{__shfl_xor(best.v, o, 64), __shfl_xor(best.i, o, 64)};
+    best = better(best, oth);
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) { sm[wid] = m; ss[wid] = s; sv[wid] = best.v; si[wid] = best.i; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float M = sm[0], Ssum = ss[0];
+    ArgBest b{sv[0], si[0]};
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
+      online_merge(M, Ssum, sm[w], ss[w]);
+      b = better(b, ArgBest{sv[w], si[w]});
+    }
+    const float lse = M + __logf(Ssum);
+    nxt[r] = b.i;
+    nll_self[r] = lse - b.v;
+    if (nll_tgt != nullptr) {
+      const int t = tgt[r];
+      const float zt = (t >= 0 && t < V) ? capc1(row[t], lt, cc) : 0.f;
+      nll_tgt[r] = (t >= 0 && t < V) ? lse - zt : 0.f;
+    }
+  }
+}
+
+// elementwise exact softcap through the compact path (ops.softcap_values; the exhaustive GPU test)
+__global__ void softcap_c_kernel(const uint16_t* __restrict__ x, float* __restrict__ y, int n, CapC cc) {
+  __shared__ uint16_t lt[CAPC_MAX];
+  for (int i = threadIdx.x; i < cc.hi - cc.lo; i += blockDim.x) lt[i] = cc.tab[i];
+  __syncthreads();
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) y[i] = capc1(x[i], lt, cc);
+}
+
+struct CapCEntry {
+  int dev;
+  uint32_t capbits;
+  CapC c;
+};
+CapCEntry g_capc[16];
+int g_ncapc = 0;
+
+const CapC* find_capc(float cap) {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  const uint32_t cb = __builtin_bit_cast(uint32_t, cap);
+  for (int i = 0; i < g_ncapc; ++i)
+    if (g_capc[i].dev == dev && g_capc[i].capbits == cb) return &g_capc[i].c;
+  return nullptr;
+}
+
 // softcap tables registered from the host, keyed by (device, cap bits)
 struct CapTab {
   int dev;
@@ -483,9 +603,38 @@ void tb_register_softcap_table(float cap, const uint16_t* tab) {
 
 const uint16_t* tb_find_softcap_table(float cap) { return find_tab(cap, 1); }
 
+bool tb_register_softcap_compact(float cap, const uint16_t* tab, int lo, int hi, float sat) {
+  if (hi < lo || hi - lo > CAPC_MAX || !(cap > 0.f)) return false;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  const uint32_t cb = __builtin_bit_cast(uint32_t, cap);
+  const CapC c{tab, lo, hi, sat, 1.0f / cap, cap};
+  for (int i = 0; i < g_ncapc; ++i)
+    if (g_capc[i].dev == dev && g_capc[i].capbits == cb) { g_capc[i].c = c; return true; }
+  if (g_ncapc >= 16) return false;
+  g_capc[g_ncapc++] = CapCEntry{dev, cb, c};
+  return true;
+}
+
+bool tb_softcap_compact(const uint16_t* x, float* y, int n, float cap, hipStream_t st) {
+  const CapC* c = find_capc(cap);
+  if (c == nullptr || n <= 0) return c != nullptr;
+  hipLaunchKernelGGL(softcap_c_kernel, dim3(std::min((n + 255) / 256, 4096)), dim3(256), 0, st, x, y, n, *c);
+  return true;
+}
+
 void tb_decode_head(const uint16_t* logits, const int32_t* tgt, int32_t* nxt, float* nll_self, float* nll_tgt, int R,
                     int V, float cap, hipStream_t st) {
   if (R <= 0) return;
+  const char* ft = getenv("TB_DECODE_HEAD_FULLTAB");   // "1": the 64 KB-table kernel (A/B)
+  if (const CapC* cc = find_capc(cap); cc != nullptr && !(ft != nullptr && ft[0] == '1')) {
+    if (row_unr() == 1)
+      hipLaunchKernelGGL(decode_head_c_kernel<1>, dim3(R), dim3(512), 0, st, logits, tgt, nxt, nll_self, nll_tgt, V, *cc);
+    else
+      hipLaunchKernelGGL(decode_head_c_kernel<ROW_UNR>, dim3(R), dim3(512), 0, st, logits, tgt, nxt, nll_self, nll_tgt, V,
+                         *cc);
+    return;
+  }
   const uint16_t* tab = find_tab(cap, 1);
   static bool attr_decode_head_kernel = false, attr_decode_head_kernel1 = false;
   if (row_unr() == 1)

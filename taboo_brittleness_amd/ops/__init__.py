@@ -39,9 +39,42 @@ def _softcap_table(cap: float, device) -> None:
         return
     bits = torch.arange(32768, dtype=torch.int32).to(torch.int16)
     x = bits.view(BF16)
-    tab = ref.softcap_bf16(x, float(cap)).to(BF16).contiguous().to(device)
+    tab_cpu = ref.softcap_bf16(x, float(cap)).to(BF16).contiguous()
+    tab = tab_cpu.to(device)
     _k().register_softcap_table(tab, float(cap))
     _CAP_TABLES[key] = tab        # keep alive: kernels (and captured graphs) hold its pointer
+    split = softcap_compact_split(tab_cpu, float(cap))
+    if split is not None:
+        lo, hi, sat = split
+        tc = tab_cpu[lo:hi].contiguous().to(device)
+        if _k().register_softcap_compact(tc, float(cap), lo, hi, sat):
+            _CAP_TABLES[key + ("compact",)] = tc
+
+
+def softcap_compact_split(tab: torch.Tensor, cap: float):
+    """``(lo, hi, sat)`` of the compact exact softcap (csrc/lens.hip CapC) for the 32768-entry reference table
+    ``tab`` of the non-negative bf16 inputs, or None: every bit pattern below ``lo`` must equal
+    ``rbf(rbf(x * (1/cap)) * cap)`` (fp32 multiply by the fp32 reciprocal, as the kernel does) and every finite
+    pattern from ``hi`` on (and +inf) the saturated value — checked exhaustively here, so the kernel reproduces the
+    table bit for bit."""
+    t = tab.float()
+    xs = torch.arange(32768, dtype=torch.int32).to(torch.int16).view(BF16).float()
+    rc = torch.tensor(1.0 / cap, dtype=torch.float32)
+    arith = ((xs * rc).to(BF16).float() * torch.tensor(cap, dtype=torch.float32)).to(BF16).float()
+    ok = arith == t
+    fin = 0x7F80                                   # +inf; patterns above are NaNs
+    bad = (~ok[:fin]).nonzero()
+    lo = int(bad[0]) if bad.numel() else fin
+    sat = float(t[fin])
+    diff = (t[: fin + 1] != sat).nonzero()
+    hi = int(diff[-1]) + 1 if diff.numel() else 0
+    hi = max(hi, lo)
+    if hi - lo > 2048 or not torch.isnan(t[fin + 1:]).all():
+        return None
+    return lo, hi, sat
+
+
+COMPACT_SOFTCAP = os.environ.get("TB_COMPACT_SOFTCAP", "1") == "1"
 
 
 def softcap_values(v: torch.Tensor, cap: float) -> torch.Tensor:
@@ -51,6 +84,9 @@ def softcap_values(v: torch.Tensor, cap: float) -> torch.Tensor:
         return v.float()
     if v.is_cuda:
         _softcap_table(cap, v.device)
+        y = torch.empty(v.shape, dtype=torch.float32, device=v.device)
+        if COMPACT_SOFTCAP and _k().softcap_compact(v.contiguous(), y, float(cap)):
+            return y
         tab = _CAP_TABLES[(float(cap), v.device.index if v.device.index is not None else torch.cuda.current_device())]
         b = v.contiguous().view(torch.int16).to(torch.int32)
         mag = tab.view(torch.int16).to(torch.int32)[b & 0x7FFF]

@@ -218,6 +218,34 @@ def test_decode_head(gpu):
     _close(nt, ref.xent_rows(lg, tgt, 30.0, True), atol=2e-3, rtol=1e-4)
 
 
+def test_softcap_compact_gpu_exhaustive(gpu):
+    """The compact exact softcap (lens.hip capc1: arithmetic below lo, a ~675-entry table, saturation) on every one
+    of the 65536 bf16 inputs equals the transformers chain, for the final (30) and attention (50) caps."""
+    allx = torch.arange(65536, dtype=torch.int32).to(torch.int16).view(BF)
+    for cap in (30.0, 50.0):
+        got = ops.softcap_values(allx.to(gpu), cap).cpu()
+        want = ref.softcap_bf16(allx, cap).float()
+        same = (got == want) | (torch.isnan(got) & torch.isnan(want))
+        assert same.all(), (cap, int((~same).sum()))
+
+
+def test_decode_head_compact_equals_full_table(gpu, monkeypatch):
+    """decode_head on the compact softcap == decode_head on the 64 KB table, bit for bit (same values, same order)."""
+    torch.manual_seed(21)
+    R, V = 64, 256000
+    lg = (torch.randn(R, V) * 6).to(BF)
+    lg[3, 100] = 200.0
+    lg[3, 7] = 150.0          # both saturate at 30: tie -> lower index
+    tgt = torch.randint(0, V, (R,), dtype=torch.int32)
+    lg, tgt = lg.to(gpu), tgt.to(gpu)
+    a = ops.decode_head(lg, 30.0, tgt)
+    monkeypatch.setenv("TB_DECODE_HEAD_FULLTAB", "1")
+    b = ops.decode_head(lg, 30.0, tgt)
+    for u, v in zip(a, b):
+        assert torch.equal(u, v)
+    assert int(a[0][3]) == 7
+
+
 @pytest.mark.parametrize("kernel", [4, 0])
 @pytest.mark.parametrize("M,V,K,cap", [(300, 4096, 256, 30.0), (1, 2048, 3584, 30.0), (520, 8192, 640, 0.0),
                                        (700, 256000, 3584, 30.0)])
