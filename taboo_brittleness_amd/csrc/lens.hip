@@ -537,6 +537,81 @@ __global__ void __launch_bounds__(512) decode_head_c_kernel(const uint16_t* __re
   }
 }
 
+// decode_head for 0 < cap <= DH_FIXED_CAP, the default: the same outputs as decode_head_kernel (argmax bit-exact,
+// NLLs to fp32 summation order) on about half the VALU work per logit, which is what bound the row pass
+// (2.9 TB/s).  (1) Capped logits lie in [-cap, cap], so sum(exp(z)) over the row can neither
+// overflow nor underflow in fp32: no running max, no rescaling, one exp + add per logit.  (2) The argmax keeps
+// the best 8-logit chunk (its max against the thread's best, strict > so the earliest chunk wins) and resolves
+// the index inside the winning chunk once per row by re-reading its 16 B — first index of the max, as torch.
+// (3) Persistent: 2 blocks per CU loop over the rows, so the 64 KB table is staged once per block instead of once
+// per row (+12.5 % HBM/L2 traffic at the Gemma-2 vocab).
+constexpr float DH_FIXED_CAP = 40.f;   // e^40 * 2^20 columns < FLT_MAX; e^-40 a normal float
+
+template <int UNR>
+__global__ void __launch_bounds__(512) decode_head_f_kernel(const uint16_t* __restrict__ logits,
+                                                            const int32_t* __restrict__ tgt, int32_t* __restrict__ nxt,
+                                                            float* __restrict__ nll_self, float* __restrict__ nll_tgt,
+                                                            int R, int V, const uint16_t* __restrict__ tab) {
+  __shared__ float ss[8], sv[8];
+  __shared__ int si[8];
+  extern __shared__ __attribute__((aligned(16))) uint16_t ctab_lds[];
+  const uint16_t* ct = stage_ctab(tab, ctab_lds);
+  const int nv = V >> 3;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int r = blockIdx.x; r < R; r += gridDim.x) {
+    const uint16_t* row = logits + (size_t)r * V;
+    float s = 0.f, bv = -INFINITY;
+    int bc = -1;
+    stream_row<UNR>(reinterpret_cast<const uint4*>(row), nv, [&](const uint4& v, int c) {
+      float f[8];
+      capped8(v, f, ct, 0.f, 1);
+      const float cm = fmaxf(fmaxf(fmaxf(f[0], f[1]), fmaxf(f[2], f[3])), fmaxf(fmaxf(f[4], f[5]), fmaxf(f[6], f[7])));
+      float e = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) e += __expf(f[j]);
+      s += e;
+      if (cm > bv) { bv = cm; bc = c; }
+    });
+    ArgBest best{bv, 0x7fffffff};
+    if (bc >= 0) {
+      float f[8];
+      capped8(reinterpret_cast<const uint4*>(row)[bc], f, ct, 0.f, 1);
+#pragma unroll
+      for (int j = 7; j >= 0; --j)
+        if (f[j] == bv) best.i = bc * 8 + j;
+    }
+    for (int c = nv * 8 + threadIdx.x; c < V; c += blockDim.x) {
+      const float x = capped1(row[c], ct, 0.f, 1);
+      s += __expf(x);
+      best = better(best, ArgBest{x, c});
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      s += __shfl_xor(s, o, 64);
+      ArgBest oth{__shfl_xor(best.v, o, 64), __shfl_xor(best.i, o, 64)};
+      best = better(best, oth);
+    }
+    if (lane == 0) { ss[wid] = s; sv[wid] = best.v; si[wid] = best.i; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float Ssum = ss[0];
+      ArgBest b{sv[0], si[0]};
+      for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
+        Ssum += ss[w];
+        b = better(b, ArgBest{sv[w], si[w]});
+      }
+      const float lse = __logf(Ssum);
+      nxt[r] = b.i;
+      nll_self[r] = lse - b.v;
+      if (nll_tgt != nullptr) {
+        const int t = tgt[r];
+        nll_tgt[r] = (t >= 0 && t < V) ? lse - capped1(row[t], ct, 0.f, 1) : 0.f;
+      }
+    }
+    __syncthreads();   // ss / sv / si are rewritten by the next row
+  }
+}
+
 // elementwise exact softcap through the compact path (ops.softcap_values; the exhaustive GPU test)
 __global__ void softcap_c_kernel(const uint16_t* __restrict__ x, float* __restrict__ y, int n, CapC cc) {
   __shared__ uint16_t lt[CAPC_MAX];
@@ -626,8 +701,33 @@ bool tb_softcap_compact(const uint16_t* x, float* y, int n, float cap, hipStream
 void tb_decode_head(const uint16_t* logits, const int32_t* tgt, int32_t* nxt, float* nll_self, float* nll_tgt, int R,
                     int V, float cap, hipStream_t st) {
   if (R <= 0) return;
-  const char* ft = getenv("TB_DECODE_HEAD_FULLTAB");   // "1": the 64 KB-table kernel (A/B)
-  if (const CapC* cc = find_capc(cap); cc != nullptr && !(ft != nullptr && ft[0] == '1')) {
+  // TB_DECODE_HEAD: "t" the per-row 64 KB-table kernel, "c" the compact-softcap kernel (A/B; both keep a running
+  // max), default "f": decode_head_f_kernel where the cap allows it
+  static const char mode = [] {
+    const char* e = getenv("TB_DECODE_HEAD");
+    return e != nullptr && (e[0] == 't' || e[0] == 'c') ? e[0] : 'f';
+  }();
+  const uint16_t* tab = find_tab(cap, 1);
+  if (mode == 'f' && tab != nullptr && cap <= DH_FIXED_CAP) {
+    static bool attr = false, attr1 = false;
+    static const int ncu = [] {
+      int dev = 0, n = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+      return n > 0 ? n : 256;
+    }();
+    const int grid = std::min(R, 2 * ncu);
+    if (row_unr() == 1)
+      hipLaunchKernelGGL(decode_head_f_kernel<1>, dim3(grid), dim3(512),
+                         tab_lds(reinterpret_cast<const void*>(&decode_head_f_kernel<1>), tab, attr1), st, logits, tgt,
+                         nxt, nll_self, nll_tgt, R, V, tab);
+    else
+      hipLaunchKernelGGL(decode_head_f_kernel<ROW_UNR>, dim3(grid), dim3(512),
+                         tab_lds(reinterpret_cast<const void*>(&decode_head_f_kernel<ROW_UNR>), tab, attr), st, logits,
+                         tgt, nxt, nll_self, nll_tgt, R, V, tab);
+    return;
+  }
+  if (const CapC* cc = find_capc(cap); cc != nullptr && mode != 't') {
     if (row_unr() == 1)
       hipLaunchKernelGGL(decode_head_c_kernel<1>, dim3(R), dim3(512), 0, st, logits, tgt, nxt, nll_self, nll_tgt, V, *cc);
     else
@@ -635,7 +735,6 @@ void tb_decode_head(const uint16_t* logits, const int32_t* tgt, int32_t* nxt, fl
                          *cc);
     return;
   }
-  const uint16_t* tab = find_tab(cap, 1);
   static bool attr_decode_head_kernel = false, attr_decode_head_kernel1 = false;
   if (row_unr() == 1)
     hipLaunchKernelGGL(decode_head_kernel<1>, dim3(R), dim3(512), tab_lds(reinterpret_cast<const void*>(&decode_head_kernel<1>), tab, attr_decode_head_kernel1), st, logits, tgt, nxt,

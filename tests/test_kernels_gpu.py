@@ -1,11 +1,14 @@
 """Numerics of every gfx950 HIP kernel against its PyTorch fp32 reference (ops/reference.py)."""
 import math
+import os
 
 import pytest
 import torch
 
 from taboo_brittleness_amd import ops
 from taboo_brittleness_amd.ops import reference as ref
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 pytestmark = pytest.mark.gpu
 BF = torch.bfloat16
@@ -229,21 +232,48 @@ def test_softcap_compact_gpu_exhaustive(gpu):
         assert same.all(), (cap, int((~same).sum()))
 
 
-def test_decode_head_compact_equals_full_table(gpu, monkeypatch):
-    """decode_head on the compact softcap == decode_head on the 64 KB table, bit for bit (same values, same order)."""
-    torch.manual_seed(21)
-    R, V = 64, 256000
-    lg = (torch.randn(R, V) * 6).to(BF)
-    lg[3, 100] = 200.0
-    lg[3, 7] = 150.0          # both saturate at 30: tie -> lower index
-    tgt = torch.randint(0, V, (R,), dtype=torch.int32)
-    lg, tgt = lg.to(gpu), tgt.to(gpu)
-    a = ops.decode_head(lg, 30.0, tgt)
-    monkeypatch.setenv("TB_DECODE_HEAD_FULLTAB", "1")
-    b = ops.decode_head(lg, 30.0, tgt)
-    for u, v in zip(a, b):
+_DH_MODES = """
+import sys, torch
+from taboo_brittleness_amd import ops
+torch.manual_seed(21)
+R, V = 600, 256000
+lg = (torch.randn(R, V) * 6).to(torch.bfloat16)
+lg[3, 100] = 200.0
+lg[3, 7] = 150.0          # both saturate at 30: tie -> lower index
+lg[5, 9000] = lg[5].max() # same-value tie inside and across 8-logit chunks
+lg[5, 9003] = lg[5, 9000]
+lg[5, 200001] = lg[5, 9000]
+tgt = torch.randint(0, V, (R,), dtype=torch.int32)
+tgt[::5] = -1
+out = ops.decode_head(lg.cuda(), 30.0, tgt.cuda())
+torch.save([t.cpu() for t in out], sys.argv[1])
+"""
+
+
+def test_decode_head_modes_agree(gpu, tmp_path):
+    """The three decode_head kernels (TB_DECODE_HEAD: default f = fixed-offset LSE + chunk argmax + persistent,
+    c = compact softcap, t = 64 KB table per row; chosen once per process) give the same argmax bit for bit
+    (incl. ties inside and across 8-logit chunks and saturated ties) and the same NLLs to fp32 summation order;
+    c and t are bit-identical (same values, same order).  Subprocesses: the mode is read once per process."""
+    import subprocess
+    import sys
+    res = {}
+    for mode in ("f", "c", "t"):
+        p = tmp_path / f"{mode}.pt"
+        env = dict(os.environ, TB_DECODE_HEAD=mode)
+        r = subprocess.run([sys.executable, "-c", _DH_MODES, str(p)], env=env, capture_output=True, text=True,
+                           timeout=300, cwd=REPO)
+        assert r.returncode == 0, r.stderr[-3000:]
+        res[mode] = torch.load(p, weights_only=True)
+    for u, v in zip(res["c"], res["t"]):
         assert torch.equal(u, v)
-    assert int(a[0][3]) == 7
+    nf, sf, tf = res["f"]
+    nt_, st_, tt_ = res["t"]
+    assert torch.equal(nf, nt_)
+    assert int(nf[3]) == 7 and int(nf[5]) == 9000
+    _close(sf, st_, atol=2e-5, rtol=1e-5)
+    _close(tf, tt_, atol=2e-5, rtol=1e-5)
+    assert (tf[::5] == 0).all()
 
 
 @pytest.mark.parametrize("kernel", [4, 0])

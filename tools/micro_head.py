@@ -29,12 +29,7 @@ nt = torch.empty(R, device="cuda")
 gb = R * V * 2 / 1e9
 for cap in (30.0, 0.0):
     ms = bench(lambda: ops.decode_head(lg, cap, tgt, nxt, ns, nt))
-    print(f"decode_head cap={cap}: {ms:.3f} ms  {gb / ms:.2f} TB/s")
-    if cap > 0:
-        os.environ["TB_DECODE_HEAD_FULLTAB"] = "1"
-        ms = bench(lambda: ops.decode_head(lg, cap, tgt, nxt, ns, nt))
-        print(f"decode_head cap={cap} (64 KB table): {ms:.3f} ms  {gb / ms:.2f} TB/s")
-        del os.environ["TB_DECODE_HEAD_FULLTAB"]
+    print(f"decode_head cap={cap} [TB_DECODE_HEAD={os.environ.get('TB_DECODE_HEAD', 'f')}]: {ms:.3f} ms  {gb / ms:.2f} TB/s")
     ms = bench(lambda: ops.argmax_rows(lg, cap, out=nxt))
     print(f"argmax_rows cap={cap}: {ms:.3f} ms  {gb / ms:.2f} TB/s")
     ms = bench(lambda: ops.xent_rows(lg, tgt, cap, True, out=ns))
