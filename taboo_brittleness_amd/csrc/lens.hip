@@ -547,6 +547,39 @@ __global__ void __launch_bounds__(512) decode_head_c_kernel(const uint16_t* __re
 // per row (+12.5 % HBM/L2 traffic at the Gemma-2 vocab).
 constexpr float DH_FIXED_CAP = 40.f;   // e^40 * 2^20 columns < FLT_MAX; e^-40 a normal float
 
+// 8 capped logits of a uint4 through the 64 KB table at ~4 VALU ops per logit (the generic capped8 path costs ~5):
+// the 15-bit magnitudes come from v_bfe (opaque to the compiler, which otherwise rewrites the index math into three
+// ops), the two lookups of a dword are packed with one v_lshl_or, one v_and_or puts both signs back, a shift / a
+// mask unpack them.  (ds_read_u16_d16_hi cannot pack them: with SRAM ECC on, d16 loads zero the other half.)
+__device__ __forceinline__ void capped8_tab(const uint4& v, float* f, const uint16_t* ct) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    uint32_t ilo, ihi, q;
+    asm("v_bfe_u32 %0, %1, 0, 15" : "=v"(ilo) : "v"(w[k]));
+    asm("v_bfe_u32 %0, %1, 16, 15" : "=v"(ihi) : "v"(w[k]));
+    const uint32_t p = ((uint32_t)ct[ihi] << 16) | ct[ilo];   // table entries are magnitudes (bit 15 clear)
+    asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(q) : "v"(w[k]), "s"(0x80008000u), "v"(p));
+    f[2 * k] = __uint_as_float(q << 16);
+    f[2 * k + 1] = __uint_as_float(q & 0xffff0000u);
+  }
+}
+
+// v_max3_f32 / v_max_f32 without the canonicalising v_max x, x the compiler puts before fmaxf on bit-cast inputs
+// (table values are never signalling NaNs)
+__device__ __forceinline__ float max3_raw(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ float fmax_raw(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+typedef float f2 __attribute__((ext_vector_type(2)));
+constexpr f2 LOG2E2 = {1.4426950408889634f, 1.4426950408889634f};
+
 template <int UNR>
 __global__ void __launch_bounds__(512) decode_head_f_kernel(const uint16_t* __restrict__ logits,
                                                             const int32_t* __restrict__ tgt, int32_t* __restrict__ nxt,
@@ -562,16 +595,19 @@ __global__ void __launch_bounds__(512) decode_head_f_kernel(const uint16_t* __re
     const uint16_t* row = logits + (size_t)r * V;
     float s = 0.f, bv = -INFINITY;
     int bc = -1;
+    f2 s2 = {0.f, 0.f};
     stream_row<UNR>(reinterpret_cast<const uint4*>(row), nv, [&](const uint4& v, int c) {
       float f[8];
-      capped8(v, f, ct, 0.f, 1);
-      const float cm = fmaxf(fmaxf(fmaxf(f[0], f[1]), fmaxf(f[2], f[3])), fmaxf(fmaxf(f[4], f[5]), fmaxf(f[6], f[7])));
-      float e = 0.f;
+      capped8_tab(v, f, ct);
+      const float cm = max3_raw(max3_raw(f[0], f[1], f[2]), max3_raw(f[3], f[4], f[5]), fmax_raw(f[6], f[7]));
 #pragma unroll
-      for (int j = 0; j < 8; ++j) e += __expf(f[j]);
-      s += e;
+      for (int j = 0; j < 8; j += 2) {   // packed scale / add (v_pk_mul_f32, v_pk_add_f32), exp2 per lane
+        const f2 y = f2{f[j], f[j + 1]} * LOG2E2;
+        s2 += f2{__builtin_amdgcn_exp2f(y.x), __builtin_amdgcn_exp2f(y.y)};
+      }
       if (cm > bv) { bv = cm; bc = c; }
     });
+    s = s2.x + s2.y;
     ArgBest best{bv, 0x7fffffff};
     if (bc >= 0) {
       float f[8];
@@ -717,7 +753,7 @@ void tb_decode_head(const uint16_t* logits, const int32_t* tgt, int32_t* nxt, fl
       return n > 0 ? n : 256;
     }();
     const int grid = std::min(R, 2 * ncu);
-    if (row_unr() == 1)
+    if (row_unr() == 1)   // (8 loads in flight per lane measured 2-5 % slower than 4: profiles/r3/dh5)
       hipLaunchKernelGGL(decode_head_f_kernel<1>, dim3(grid), dim3(512),
                          tab_lds(reinterpret_cast<const void*>(&decode_head_f_kernel<1>), tab, attr1), st, logits, tgt,
                          nxt, nll_self, nll_tgt, R, V, tab);
