@@ -56,6 +56,7 @@ from taboo_brittleness_amd.runtime import gemm_dispatch as GD  # noqa: E402
 from taboo_brittleness_amd.runtime.tuning import enable_tuned_gemms, flush_tuned_gemms  # noqa: E402
 
 BASELINE_VALUE = 0.642   # measured HF-eager sweep cells/sec on 1x MI355X (tools/hf_eager_baseline.py)
+HF_BATCHED_VALUE = 38.5  # HF-eager with the 66 cells of a pair batched per generate (hf_batched_baseline.py)
 
 
 def _host_rss_gb():
@@ -145,8 +146,9 @@ def main() -> None:
                     help="do not queue the next step's teacher-forced tail behind this step's readout")
     ap.add_argument("--profile-steps", action="store_true", help="print per-phase timings per step")
     ap.add_argument("--post-forcing", action="store_true",
-                    help="also time the post-edit postgame token forcing of the sweep's SAE settings (reported as "
-                         "'post_forcing', outside the headline)")
+                    help="(default) also time the post-edit postgame token forcing of the sweep's SAE settings, "
+                         "after the timed region (reported as 'post_forcing', outside the headline)")
+    ap.add_argument("--no-post-forcing", action="store_true", help="skip the post-edit forcing side measurement")
     ap.add_argument("--no-config2", action="store_true",
                     help="skip the BASELINE config-2 side measurement (LL-Top-k baseline: batched greedy hints + "
                          "42-layer lens over 3 words x 10 prompts), reported as 'config2' after the timed steps")
@@ -154,6 +156,7 @@ def main() -> None:
                     help="run TunableOp over every GEMM shape and save configs/tunableop/<tag>.csv")
     ap.add_argument("--no-tuned-gemms", action="store_true", help="ignore the saved TunableOp results")
     args = ap.parse_args()
+    args.post_forcing = not args.no_post_forcing
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
 
@@ -212,10 +215,16 @@ def main() -> None:
         n = len(templates)
         return [fresh(templates[(base + j) % n], rep=(base + j) // n) for j in range(P)]
 
-    # prologue: baselines of the first step's pairs, SAE threshold calibration on their residuals
+    # prologue: baselines of the first step's pairs, SAE threshold calibration on their residuals -- one copy of
+    # each (word, prompt) template in template order, so every rank calibrates on the same rows (a pair's baseline
+    # does not depend on its replicate; with P >= 30 every rank's first step holds every template)
     cur = pairs_for(0)
     runner.run_baselines(cur)
-    resid = torch.cat([p.resid for p in cur if p.resid is not None and p.resid.shape[0]], 0)
+    first = {}
+    for p in cur:
+        first.setdefault((p.word, p.pidx), p)
+    calib = [first[k] for k in ((t.word, t.pidx) for t in templates) if k in first]
+    resid = torch.cat([p.resid for p in calib if p.resid is not None and p.resid.shape[0]], 0)
     sae.calibrate(resid)
     runner._score_pairs(cur)
 
@@ -417,6 +426,8 @@ def main() -> None:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
+            # against the stronger stock-PyTorch point (HF eager, a pair's 66 cells batched per generate)
+            "vs_hf_batched": round(value / HF_BATCHED_VALUE, 2),
             "dtype": "bf16",
             "data": "synthetic (random-init weights of the full architecture, random calibrated SAE, paper prompts)",
             "config": {

@@ -390,7 +390,8 @@ class Gemma2Model:
         if tgt is not None:
             nll_tgt = nll_tgt if nll_tgt is not None else torch.empty(R, dtype=torch.float32, device=x.device)
             g_t = allst[:, :, 3].max(0).values
-            nll_tgt.copy_(torch.where(tgt.long() >= 0, g_lse - g_t, torch.zeros_like(g_lse)))
+            ok = (tgt.long() >= 0) & (tgt.long() < V)                   # as decode_head: out-of-range -> 0
+            nll_tgt.copy_(torch.where(ok, g_lse - g_t, torch.zeros_like(g_lse)))
         return nxt, nll_self, nll_tgt
 
     def head(self, x_final: torch.Tensor, cap: float, tgt=None, nxt=None, nll_self=None, nll_tgt=None, part=None,

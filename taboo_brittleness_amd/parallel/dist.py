@@ -2,9 +2,9 @@
 
 One process per GPU; ``torch.distributed`` with the ``nccl`` backend, which is
 RCCL over xGMI on ROCm, or ``gloo`` on CPU.  The sweep is embarrassingly
-parallel: cells are sharded round-robin by a deterministic cell index and only
-small result records (and, for pooled PCA, spike residuals) cross ranks, so
-collectives are latency-bound all-gathers issued once per sweep stage.
+parallel: ranks own whole (word, prompt) pairs (``pipelines.run_sweep.pair_owners``)
+and only small result records (and, for pooled PCA, spike residuals) cross
+ranks, so collectives are latency-bound all-gathers issued once per sweep stage.
 """
 from __future__ import annotations
 

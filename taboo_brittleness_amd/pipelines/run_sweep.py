@@ -1,11 +1,12 @@
 """End-to-end intervention sweep driver (CLI: ``tb-sweep`` / ``python -m taboo_brittleness_amd.cli.sweep``).
 
 Stages (EP:112-160):
-1. baselines for every (word, prompt) pair — identical on every rank (cheap,
-   one batch) so no broadcast is needed and every rank holds the spikes,
-   targeted latents and PCA bases;
-2. deterministic cell list (``SweepRunner.make_cells``), sharded round-robin
-   over data-parallel ranks;
+1. baselines of the (word, prompt) pairs a data-parallel group owns (contiguous
+   blocks of pairs, :func:`pair_owners`), then one object all-gather of the small
+   per-pair results so every rank holds every pair's spikes, targeted latents
+   and PCA inputs;
+2. deterministic cell list (``SweepRunner.make_cells``); each pair's cells run
+   on its owner group;
 3. per-rank batched execution, results all-gathered to rank 0;
 4. rank 0 writes ``sweep_cells.jsonl``, ``sweep_summary.json`` (curves with 95%
    bootstrap CIs) and ``sweep_curves.csv``; atomic writes so a killed run never

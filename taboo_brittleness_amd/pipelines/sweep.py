@@ -14,8 +14,10 @@ edit applied at the pair's spike positions of the hooked layer, then read out:
 Execution is batched: every batch of cells shares one :class:`Generator`
 (one KV cache, hipGraph-captured decode step replayed across batches) and one
 persistent edit plan whose tensors are refreshed in place, so capture happens
-once per sweep.  Cells are enumerated deterministically and seeded per cell,
-then sharded round-robin over data-parallel ranks.
+once per sweep.  Cells are enumerated deterministically and seeded per cell
+(SURVEY 7.3.14); data-parallel ranks own whole (word, prompt) pairs -- contiguous
+blocks of pairs, every cell of a pair on its pair's rank
+(``pipelines.run_sweep.pair_owners``).
 
 Prefix sharing (``runtime.prefix_share``, exact): an edited cell computes
 exactly what its pair's baseline computed up to the first edited position f

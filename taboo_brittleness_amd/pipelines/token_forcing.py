@@ -102,9 +102,11 @@ def run_forcing(cfg: Config, model, tok, words: Sequence[str], mode: str = "post
                 layer: Optional[int] = None, edit: Optional[Dict] = None, dp: Optional[DPShard] = None) -> Dict:
     """Returns ``{"metrics": reference-layout metrics, "rows": per (word, phrase) records}``.
 
-    ``dp``: the (word, phrase) rows are sharded round-robin over the data-parallel groups (each group also
-    generates the warm-up turns of the words it holds rows of) and the records are gathered back, so every
-    rank returns the full result."""
+    ``dp``: the (word, phrase) rows are sharded round-robin over the data-parallel groups and the records are
+    gathered back, so every rank returns the full result.  Every group generates the warm-up turns of ALL
+    words (one small batch): the warm-up batch, and with it the GEMM row count the greedy replies are computed
+    at, does not depend on the DP size, so the histories -- and the forcing results -- are the same for any
+    number of GPUs."""
     tf = cfg.token_forcing
     layer = cfg.model.layer_idx if layer is None else layer
     dev = model.device
@@ -112,19 +114,18 @@ def run_forcing(cfg: Config, model, tok, words: Sequence[str], mode: str = "post
     dp = dp or DPShard()
     all_keys = [(w, ph) for w in words for ph in phrases]
     mine = dp.mine(len(all_keys))
-    my_words = [w for w in words if any(all_keys[i][0] == w for i in mine)]
     records: List[Dict] = []
-    histories: Dict[str, List[Dict[str, str]]] = {w: [] for w in my_words}
-    if mode == "postgame" and my_words:
-        # warm-up turns, batched across words (each turn depends on the previous one)
+    histories: Dict[str, List[Dict[str, str]]] = {w: [] for w in words}
+    if mode == "postgame" and mine:
+        # warm-up turns, batched across all words (each turn depends on the previous one)
         for turn in tf.warmup_turns:
             rows = []
-            for w in my_words:
+            for w in words:
                 histories[w].append({"role": "user", "content": turn})
                 rows.append(conversation_ids(tok, histories[w], add_generation_prompt=True))
             hooks = _hooks_for(len(rows), layer, sae, edit, dev)
             replies = _generate(model, rows, tf.warmup_max_new_tokens, hooks)
-            for w, r in zip(my_words, replies):
+            for w, r in zip(words, replies):
                 histories[w].append({"role": "assistant", "content": tok.decode(r)})
     rows = []
     for i in mine:

@@ -519,7 +519,6 @@ class Generator:
 
     # -------------------------------------------------------------- generate
     @torch.no_grad()
-    @torch.no_grad()
     def generate_shared(self, prompts: Sequence[Sequence[int]], groups: Sequence[int], max_new_tokens: int,
                         hooks: Optional[Dict[int, list]] = None, min_share: int = 16,
                         graph_key=None) -> GenerationOutput:
@@ -537,7 +536,7 @@ class Generator:
         for i, g in enumerate(groups):
             members.setdefault(int(g), []).append(i)
         share = [0] * n
-        reps, rep_pref, src, dst = [], [], [], []
+        reps, rep_pref, fan = [], [], []
         for rows in members.values():
             if len(rows) < 2:
                 continue
@@ -555,20 +554,32 @@ class Generator:
             rep_pref.append(list(p0[:lcp]))
             for r in rows:
                 share[r] = lcp
-            src += [rows[0]] * (len(rows) - 1)
-            dst += rows[1:]
+            fan.append((rows, lcp))
         if reps:
             self.prefill(rep_pref, reps, hooks)                # prefix K/V of each group's first row
+            # fan the prefix positions [0, lcp) of every group's first slot out to the other members' slots
+            # (ops.kv_fanout over one entry per (slot, position); nothing past the prefix is copied and no
+            # temporary of the cache's size is built)
+            e_slot, e_pos, e_src = [], [], []
+            for rows, lcp in fan:
+                base = len(e_slot)
+                e_slot += [rows[0]] * lcp
+                e_pos += list(range(lcp))
+                e_src += [-1] * lcp
+                for r in rows[1:]:
+                    e_slot += [r] * lcp
+                    e_pos += list(range(lcp))
+                    e_src += list(range(base, base + lcp))
             c = self.cache
-            d = torch.tensor(dst, device=self.dev)
-            sidx = torch.tensor(src, device=self.dev)
-            c.k.index_copy_(1, d, c.k.index_select(1, sidx))   # all layers, whole slots (positions past the
-            c.v.index_copy_(1, d, c.v.index_select(1, sidx))   # shared prefix are rewritten below / by decode)
+            ops.kv_fanout(c.k, c.v, torch.tensor(e_src, dtype=torch.int32, device=self.dev),
+                          torch.tensor(e_slot, dtype=torch.int32, device=self.dev),
+                          torch.tensor(e_pos, dtype=torch.int32, device=self.dev), int(c.k.shape[0]))
         first = self.prefill([list(p[share[i]:]) for i, p in enumerate(prompts)], list(range(n)), hooks,
                              starts=share)
         self.decode(first, plen, [[int(t)] for t in first.tolist()], max_new_tokens, n, hooks, graph_key)
         return self.collect(n, max_new_tokens, plen)
 
+    @torch.no_grad()
     def generate(self, prompts: Sequence[Sequence[int]], max_new_tokens: int,
                  hooks: Optional[Dict[int, list]] = None, graph_key=None,
                  teacher: Optional[Sequence[Sequence[int]]] = None) -> GenerationOutput:

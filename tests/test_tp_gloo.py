@@ -181,7 +181,7 @@ def test_vocab_parallel_head_merge_matches_full():
     R, V, cap = 6, 512, 30.0
     lg = (torch.randn(R, V) * 20).to(torch.bfloat16)
     lg[0, 300] = lg[0, 10] = 200.0                 # tie, saturating the softcap, across the split at 256
-    tgt = torch.tensor([3, 300, -1, 511, 0, 257], dtype=torch.int32)
+    tgt = torch.tensor([3, 300, -1, 511, 600, 257], dtype=torch.int32)   # -1 and >= V: no target (NLL 0)
     nxt, ns, nt = ops.decode_head(lg, cap, tgt)
     stats = []
     for r in range(2):
@@ -201,5 +201,5 @@ def test_vocab_parallel_head_merge_matches_full():
     assert torch.equal(idx, nxt) and int(idx[0]) == 10
     torch.testing.assert_close(g_lse - best, ns, rtol=1e-5, atol=1e-5)
     g_t = allst[:, :, 3].max(0).values
-    got_t = torch.where(tgt.long() >= 0, g_lse - g_t, torch.zeros_like(g_lse))
+    got_t = torch.where((tgt.long() >= 0) & (tgt.long() < V), g_lse - g_t, torch.zeros_like(g_lse))
     torch.testing.assert_close(got_t, nt, rtol=1e-5, atol=1e-5)

@@ -117,12 +117,14 @@ def time_shapes(shapes, rounds=int(os.environ.get("G4_ROUNDS", "7"))):
             it[0] = (it[0] + 1) % len(Ws)
             return Ws[it[0]]
 
+        epi = int(os.environ.get("G4_EPI", "0"))      # 3: the fused GeGLU epilogue ([M, N/2] output)
+        Cg = torch.empty(M, N // 2, device="cuda", dtype=torch.bfloat16) if epi == 3 else C
         var = {"blas": lambda: torch.matmul(A, nxt().t(), out=C),
-               "pp256": lambda: k.gemm_pp(A, nxt(), C, None, None, 0, 256),
-               "g4_256": lambda: g4(A, nxt(), C, 0, 256),
-               "g4_128": lambda: g4(A, nxt(), C, 0, 128)}
+               "pp256": lambda: k.gemm_pp(A, nxt(), Cg, None, None, epi, 256),
+               "g4_256": lambda: g4(A, nxt(), Cg, epi, 256),
+               "g4_128": lambda: g4(A, nxt(), Cg, epi, 128)}
         for name, lib in EXTRA.items():      # G4_LIBS: more builds of the kernel, interleaved in this process
-            var[name] = (lambda lib_: lambda: g4(A, nxt(), C, 0, 256, lib_))(lib)
+            var[name] = (lambda lib_: lambda: g4(A, nxt(), Cg, epi, 256, lib_))(lib)
         for f in var.values():
             f()
         torch.cuda.synchronize()
