@@ -104,3 +104,12 @@ int tb_p2p_close_handle(void* p);
 int tb_p2p_allreduce(void* const* bases, int rank, int world, const void* in, void* out, size_t nbytes, int is_bf16,
                      int blocks, int spin_max, int barriers, hipStream_t st);
 uint32_t tb_p2p_read_error(void* own_base);
+
+// vp.hip: vocab-parallel merges (TP head / lens)
+void tb_vp_head_merge(const float* st, int tp, int R, const int32_t* tgt, int V, int32_t* nxt, float* nll_self,
+                      float* nll_tgt, hipStream_t stream);
+void tb_vp_lse_merge(const float* lse, int tp, int R, float* out, hipStream_t stream);
+void tb_vp_topk_merge(const float* vals, const int32_t* ids, int tp, int n, int k, float* ov, int32_t* oi,
+                      hipStream_t stream);
+int tb_p2p_allgather(void* const* bases, int rank, int world, const void* in, void* out, size_t nbytes, int blocks,
+                     int spin_max, int barriers, hipStream_t st);

@@ -656,6 +656,57 @@ void p2p_allreduce(std::vector<int64_t> bases, int64_t rank, torch::Tensor in, t
   TORCH_CHECK(e == 0, "p2p_allreduce launch failed (", e, ")");
 }
 
+void p2p_allgather(std::vector<int64_t> bases, int64_t rank, torch::Tensor in, torch::Tensor out, int64_t blocks,
+                   int64_t spin_max, bool barriers) {
+  CHECK_DEV(in); CHECK_CONTIG(in); CHECK_DEV(out); CHECK_CONTIG(out);
+  const int world = (int)bases.size();
+  TORCH_CHECK(world >= 1 && world <= tb_p2p_max_ranks() && rank >= 0 && rank < world, "p2p_allgather: ranks");
+  const size_t nbytes = (size_t)in.numel() * in.element_size();
+  TORCH_CHECK(nbytes % 16 == 0, "p2p_allgather: bytes must be a multiple of 16");
+  TORCH_CHECK(out.scalar_type() == in.scalar_type() && out.numel() == in.numel() * world, "p2p_allgather: out must be [world, *in]");
+  std::vector<void*> b(world);
+  for (int r = 0; r < world; ++r) b[r] = reinterpret_cast<void*>(bases[r]);
+  c10::DeviceGuard g(in.device());
+  const int e = tb_p2p_allgather(b.data(), (int)rank, world, in.data_ptr(), out.data_ptr(), nbytes, (int)blocks,
+                                 (int)spin_max, barriers ? 1 : 0, cur_stream());
+  TORCH_CHECK(e == 0, "p2p_allgather launch failed (", e, ")");
+}
+
+// vocab-parallel merges (csrc/vp.hip)
+void vp_head_merge(torch::Tensor st, c10::optional<torch::Tensor> tgt, int64_t V, c10::optional<torch::Tensor> nxt,
+                   c10::optional<torch::Tensor> nll_self, c10::optional<torch::Tensor> nll_tgt) {
+  IN_F32(st);
+  TORCH_CHECK(st.dim() == 3 && st.size(2) == 4, "vp_head_merge: st must be [tp, R, 4]");
+  const int tp = st.size(0), R = st.size(1);
+  auto chk = [&](const c10::optional<torch::Tensor>& t, bool i32) {
+    if (!t) return;
+    if (i32) { IN_I32((*t)); } else { IN_F32((*t)); }
+    TORCH_CHECK(t->numel() == R, "vp_head_merge: per-row output size");
+  };
+  chk(tgt, true); chk(nxt, true); chk(nll_self, false); chk(nll_tgt, false);
+  c10::DeviceGuard g(st.device());
+  tb_vp_head_merge(st.data_ptr<float>(), tp, R, tgt ? tgt->data_ptr<int32_t>() : nullptr, (int)V,
+                   nxt ? nxt->data_ptr<int32_t>() : nullptr, nll_self ? nll_self->data_ptr<float>() : nullptr,
+                   nll_tgt ? nll_tgt->data_ptr<float>() : nullptr, cur_stream());
+}
+
+void vp_lse_merge(torch::Tensor lse, torch::Tensor out) {
+  IN_F32(lse); IN_F32(out);
+  TORCH_CHECK(lse.dim() == 2 && out.numel() == lse.size(1), "vp_lse_merge: lse [tp, R] -> out [R]");
+  c10::DeviceGuard g(lse.device());
+  tb_vp_lse_merge(lse.data_ptr<float>(), lse.size(0), lse.size(1), out.data_ptr<float>(), cur_stream());
+}
+
+void vp_topk_merge(torch::Tensor vals, torch::Tensor ids, torch::Tensor ov, torch::Tensor oi) {
+  IN_F32(vals); IN_I32(ids); IN_F32(ov); IN_I32(oi);
+  TORCH_CHECK(vals.dim() == 3 && ids.sizes() == vals.sizes(), "vp_topk_merge: vals/ids [tp, n, k]");
+  const int tp = vals.size(0), n = vals.size(1), k = vals.size(2);
+  TORCH_CHECK(k >= 1 && k <= 64 && ov.numel() == (int64_t)n * k && oi.numel() == (int64_t)n * k, "vp_topk_merge: k");
+  c10::DeviceGuard g(vals.device());
+  tb_vp_topk_merge(vals.data_ptr<float>(), ids.data_ptr<int32_t>(), tp, n, k, ov.data_ptr<float>(),
+                   oi.data_ptr<int32_t>(), cur_stream());
+}
+
 int64_t p2p_read_error(int64_t own) { return (int64_t)tb_p2p_read_error(reinterpret_cast<void*>(own)); }
 int64_t p2p_header_bytes() { return tb_p2p_header_bytes(); }
 int64_t p2p_max_ranks() { return tb_p2p_max_ranks(); }
@@ -706,6 +757,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("p2p_open_handle", &p2p_open_handle);
   m.def("p2p_close_handle", &p2p_close_handle);
   m.def("p2p_allreduce", &p2p_allreduce);
+  m.def("p2p_allgather", &p2p_allgather);
+  m.def("vp_head_merge", &vp_head_merge);
+  m.def("vp_lse_merge", &vp_lse_merge);
+  m.def("vp_topk_merge", &vp_topk_merge);
   m.def("p2p_read_error", &p2p_read_error);
   m.def("p2p_header_bytes", &p2p_header_bytes);
   m.def("p2p_max_ranks", &p2p_max_ranks);

@@ -36,6 +36,7 @@
 #include "api.h"
 #include <algorithm>
 #include <cstdlib>
+#include <utility>
 
 namespace {
 
@@ -74,20 +75,37 @@ constexpr int G4_THREADS = 256, G4_BN = 256;
 #ifndef G4_PRIO
 #define G4_PRIO 0        // 1: s_setprio 3 for the K loop
 #endif
+#ifndef G4_LDS_GEGLU
+#define G4_LDS_GEGLU 1   // the GeGLU output through the row-coalesced LDS epilogue too
+#endif
 #ifndef G4_ASM_MFMA
 #define G4_ASM_MFMA 1    // 1: MFMAs as asm statements with AGPR-tied accumulators (see G4_MFMA below)
 #endif
 
 typedef __attribute__((address_space(3))) void g4_lds_t;
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) char g4_lds_char;
 
 template <int N>
 __device__ __forceinline__ void g4_vmcnt() {
-  static_assert(N == 0 || N == 6 || N == 8 || N == 12 || N == 16, "vmcnt literal");
-  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+template <int OFF>
+__device__ __forceinline__ void g4_ds_write_b64(uint32_t a, const u32x2& v) {
+  asm volatile("ds_write_b64 %0, %1 offset:%2" ::"v"(a), "v"(v), "n"(OFF) : "memory");
+}
+template <int OFF>
+__device__ __forceinline__ void g4_ds_read_b128(u32x4& d, uint32_t a) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(a), "n"(OFF) : "memory");
+}
+template <typename F, int... I>
+__device__ __forceinline__ void g4_unroll_seq(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void g4_unroll(F&& f) {
+  g4_unroll_seq(f, std::make_integer_sequence<int, N>{});
 }
 // s_waitcnt vmcnt(n) (expcnt / lgkmcnt left at their maxima), gfx9 encoding: vmcnt[3:0] -> [3:0], vmcnt[5:4] -> [15:14]
 constexpr int g4_vmcnt_enc(int n) { return (n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8); }
@@ -131,6 +149,12 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
   constexpr int WN = 8, WM = BM / 32;                 // 16-row fragments per wave: n, m
   constexpr int PIMG = G4_BN * 128, QIMG = BM * 128, STG = PIMG + QIMG;
   constexpr int PI = G4_BN / 32, QI = BM / 32, GL = PI + QI;   // LDS-DMA instructions per wave and K tile
+  // row-coalesced bf16 epilogue (see the tile's end): a wave's output rows are RB bytes (bf16: its 128 columns;
+  // GeGLU: its 64 features), ERPI rows per 16-B-per-lane store, ERR rows per LDS round trip, ENR stores per lane
+  constexpr bool LEPI = EPI == G4_BF16 || (EPI == G4_GEGLU && G4_LDS_GEGLU);
+  constexpr int RB = EPI == G4_GEGLU ? 128 : 256, ECH = RB / 16, ERPI = 64 / ECH;
+  constexpr int ERR = EPI == G4_GEGLU ? BM / 2 : BM / 4;
+  constexpr int ENR = LEPI ? (BM / 2) / ERPI : 1;
   __shared__ __attribute__((aligned(1024))) char smem[2 * STG];
 
   const int nbn = N / G4_BN, nbm = (M + BM - 1) / BM, nwg = nbn * nbm;
@@ -168,8 +192,11 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
     wtile = (void*)(W + (size_t)n0 * K);                                                          \
     atile = (void*)(A + (size_t)m0 * K);                                                          \
     abytes = mrows * K * 2;                                                                       \
+    int ln_ = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));   /* opaque copy: the offsets are recomputed per tile, not hoisted and spilled */ \
+    asm volatile("" : "+v"(ln_));                                                                 \
+    const int lc_ = (ln_ & 7) ^ ((4 * wid + (ln_ >> 4)) & 7);                                     \
     _Pragma("unroll") for (int i = 0; i < QI; ++i)                                                \
-      vq[i] = (uint32_t)(min(8 * (4 * i + wid) + (lane >> 3), mrows - 1) * K + lchunk * 8) * 2u;  \
+      vq[i] = (uint32_t)(min(8 * (4 * i + wid) + (ln_ >> 3), mrows - 1) * K + lc_ * 8) * 2u;      \
   } while (0)
   G4_DESC();
 
@@ -239,9 +266,13 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
   // prologue of the first tile: K tiles 0 and 1 in flight
   G4_STAGE(0, 0);
   G4_STAGE(min(1, nt - 1), 1);
+  bool first_tile = true;
   for (;;) {
-  // K tile 0 landed, its step-0 fragments read
-  g4_vmcnt<GL>();
+  // K tile 0 landed, its step-0 fragments read.  After a row-coalesced epilogue K tile 1 and the ENR row stores
+  // (always issued: out-of-range rows are dropped by the buffer bounds) are younger than K tile 0.
+  if (first_tile || !LEPI) g4_vmcnt<GL>();
+  else g4_vmcnt<GL + ENR>();
+  first_tile = false;
   g4_bar();
 #pragma unroll
   for (int i = 0; i < WN; ++i) p0[i] = frag(0, offp + G4_PROW(i) * 128 + co0);
@@ -321,7 +352,88 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
   g4_bar();
   const int em0 = m0, en0 = n0;
   const int next = tile + (int)gridDim.x;
-  if (next < nwg) {
+  // Row-coalesced bf16 epilogue (G4_BF16): a lane's accumulators are 4 consecutive columns of one row, so direct
+  // stores put 16 rows x 32 B into every store instruction, one address translation per lane (the UTCL1 request
+  // and stall counters were 1.3x / 1.9x hipBLASLt's; 7-8 % of the kernel with the stores removed,
+  // profiles/r4/gemm4/).  Each wave packs its 128 x 128 tile into its own 32 KB of the (now idle) stage LDS
+  // (16-B chunks XOR-swizzled by row: conflict-free row reads), reads it back as whole 256-B row segments, and
+  // stores them after the next tile's first LDS-DMA is issued.  (The GeGLU output is half as wide: its direct
+  // stores measured faster than the round trip, which holds the gelu math in front of the next tile's loads.)
+  if constexpr (LEPI) {
+    // K tile 0 of the next tile loads into stage 0 under the round trip, which uses stage 1 (ERR rows per wave
+    // and round); the LDS accesses are asm, or hipcc would wait for that LDS-DMA (vmcnt(0)) in front of them
+    if (next < nwg) {
+      tile = next;
+      G4_TILE(tile, m0, n0);
+      G4_DESC();
+      G4_STAGE(0, 0);
+    }
+    asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");   // last MFMA's D -> the accumulator reads below
+    const uint32_t reg = (uint32_t)(uintptr_t)((g4_lds_char*)smem) + STG + wid * ERR * RB;
+    uint16_t* obase = reinterpret_cast<uint16_t*>(C) + (size_t)(em0 + wm * (BM / 2)) * ldc;
+    const int nrow = min(BM / 2, M - em0 - wm * (BM / 2));
+    const auto ors = __builtin_amdgcn_make_buffer_rsrc(obase, 0, nrow > 0 ? nrow * ldc * 2 : 0, 0x00020000);
+    // write address of fragment column i (row lane&15 of a 16-row block; the block is the immediate offset), read
+    // address of row group k%4 (rows 4k + lane/16; k/4 is the immediate offset)
+    // (computed here from an opaque copy of the lane id: hoisted out of the tile loop they would be spilled)
+    int ln = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    asm volatile("" : "+v"(ln));
+    const int oc0 = (EPI == G4_GEGLU ? (en0 >> 1) + wn * 64 : en0 + wn * 128) + (ln % ECH) * 8;
+    // write address of fragment column i (row lane&15 of a 16-row block, chunk XOR-swizzled by the row; the block
+    // is the immediate offset), read address of row group k % NRA (rows ERPI*k + lane/ECH)
+    constexpr int NI = EPI == G4_GEGLU ? WN / 2 : WN, NRA = ECH / ERPI;
+    uint32_t wa[NI], ra[NRA];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int cb = 32 * i + 8 * (ln >> 4);
+      wa[i] = reg + (ln & 15) * RB + (((cb >> 4) ^ (ln & 15 & (ECH - 1))) << 4) + (cb & 15);
+    }
+#pragma unroll
+    for (int k = 0; k < NRA; ++k) {
+      const int r = ERPI * k + ln / ECH;
+      ra[k] = reg + r * RB + (((ln % ECH) ^ (r & (ECH - 1))) << 4);
+    }
+    g4_unroll<(BM / 2) / ERR>([&](auto rc) {     // (a wave's LDS accesses run in order: the next round's writes
+      constexpr int rnd = decltype(rc)::value;   // cannot pass this round's reads)
+      g4_unroll<ERR / 16>([&](auto jc) {
+        constexpr int jj = decltype(jc)::value, j = rnd * (ERR / 16) + jj;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+          u32x2 w;
+          if constexpr (EPI == G4_GEGLU) {
+            // W rows interleaved per 128-row wave slice (ops.geglu_interleave_index, the layout gemm.hip uses too):
+            // fragments 0..3 are the gate rows of features f0 .. f0+63, fragments 4..7 the up rows of the same
+            // features; gate|up are rounded to bf16 first so the result equals geglu(bf16 gate|up GEMM output)
+            float o[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const float gt = rbf(acc[i][j][q]), u = rbf(acc[i + WN / 2][j][q]);
+              o[q] = rbf(gelu_tanh_fast(gt)) * u;
+            }
+            w = (u32x2){pack2(o[0], o[1]), pack2(o[2], o[3])};
+          } else {
+            w = (u32x2){pack2(acc[i][j][0], acc[i][j][1]), pack2(acc[i][j][2], acc[i][j][3])};
+          }
+          g4_ds_write_b64<jj * 16 * RB>(wa[i], w);
+        }
+      });
+      u32x4 ev[ERR / ERPI];
+      g4_unroll<ERR / ERPI>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        g4_ds_read_b128<(k / NRA) * NRA * ERPI * RB>(ev[k], ra[k % NRA]);
+      });
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      // the round's rows as whole RB-byte segments (lane -> row ERPI*k + lane/ECH, 16-B chunk lane%ECH); buffer
+      // stores bounded by the output's last row: every one is issued (an exact vmcnt count for the next tile's
+      // first wait), rows past M are dropped by the bounds check
+#pragma unroll
+      for (int k = 0; k < ERR / ERPI; ++k)
+        __builtin_amdgcn_raw_buffer_store_b128(ev[k], ors, ((rnd * ERR + ERPI * k + ln / ECH) * ldc + oc0) * 2, 0, 0);
+    });
+    g4_bar();   // every wave's rows are out of stage 1
+    if (next < nwg) G4_STAGE(min(1, nt - 1), 1);
+  }
+  if (!LEPI && next < nwg) {
     tile = next;
     G4_TILE(tile, m0, n0);
     G4_DESC();
@@ -341,7 +453,7 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
     }
   }
 #if G4_ASM_MFMA
-  asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");   // last MFMA's D -> the epilogue's accumulator reads
+  if constexpr (!LEPI) asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");   // last MFMA's D -> the accumulator reads
 #endif
 
   // ---- epilogue.  acc[i][j][r]: n = n0 + wn*128 + i*16 + 4*(lane>>4) + r, m = m0 + wm*BM/2 + j*16 + (lane&15)
@@ -427,7 +539,7 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
         *reinterpret_cast<uint2*>(dst + d + half) = make_uint2(pack2(o2[0], o2[1]), pack2(o2[2], o2[3]));
       }
     }
-  } else if constexpr (EPI == G4_GEGLU) {
+  } else if constexpr (EPI == G4_GEGLU && !LEPI) {
     // W rows interleaved per 128-row wave slice (ops.geglu_interleave_index, the layout gemm.hip uses too): fragments 0..3 are the gate rows of
     // features f0 .. f0+63, fragments 4..7 the up rows of the same features; gate|up are rounded to bf16 first so
     // the result equals geglu(bf16 gate|up GEMM output).
@@ -448,6 +560,8 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
         *reinterpret_cast<uint2*>(out + (size_t)m * ldc + fb + i * 16) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
       }
     }
+  } else if constexpr (LEPI) {
+    // stored above, from the LDS round trip
   } else {
 #pragma unroll
     for (int i = 0; i < WN; ++i) {
@@ -462,10 +576,7 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
         const int m = mb + j * 16;
         if (m >= M) continue;
         const f32x4 v = acc[i][j];
-        if constexpr (EPI == G4_BF16) {
-          *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(C) + (size_t)m * ldc + n) =
-              make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
-        } else if constexpr (EPI == G4_F32) {
+        if constexpr (EPI == G4_F32) {
           *reinterpret_cast<float4*>(reinterpret_cast<float*>(C) + (size_t)m * ldc + n) = make_float4(v[0], v[1], v[2], v[3]);
         } else {
           const float a0 = v[0] + bn_.x, a1 = v[1] + bn_.y, a2 = v[2] + bn_.z, a3 = v[3] + bn_.w;

@@ -145,6 +145,41 @@ __global__ void __launch_bounds__(512) p2p_allreduce_kernel(P2PBases B, const vo
     __hip_atomic_store(mine + TB_P2P_CTR + blockIdx.x, f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// All-gather (raw 16-byte vectors of any dtype): the same stage / barrier / read / barrier protocol, each rank's
+// staged input copied to out[r] in rank order -- a real gather, not a sum of zero-padded slots.  TP's
+// vocab-parallel head and lens exchange a few floats per row through it (csrc/vp.hip merges them).
+__global__ void __launch_bounds__(512) p2p_allgather_kernel(P2PBases B, const u32x4* in, u32x4* out, int64_t nvec,
+                                                            int rank, int world, int spin_max, int barriers) {
+  __shared__ uint32_t s_flag;
+  uint32_t* mine = reinterpret_cast<uint32_t*>(B.p[rank]);
+  if (threadIdx.x == 0) {
+    const uint32_t f = __hip_atomic_load(mine + TB_P2P_CTR + blockIdx.x, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    s_flag = f;
+  }
+  __syncthreads();
+  const uint32_t f = s_flag;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  {
+    u32x4* dst = reinterpret_cast<u32x4*>(B.p[rank] + TB_P2P_HDR);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += stride) dst[i] = in[i];
+  }
+  __syncthreads();
+  if (barriers) p2p_barrier(B, rank, world, TB_P2P_START, f, spin_max);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  for (int r = 0; r < world; ++r) {
+    const u32x4* src = reinterpret_cast<const u32x4*>(B.p[r] + TB_P2P_HDR);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += stride) {
+      const uint4 v = ld_nt16(src + i);
+      out[(int64_t)r * nvec + i] = (u32x4){v.x, v.y, v.z, v.w};
+    }
+  }
+  __syncthreads();
+  if (barriers) p2p_barrier(B, rank, world, TB_P2P_END, f, spin_max);
+  if (threadIdx.x == 0)
+    __hip_atomic_store(mine + TB_P2P_CTR + blockIdx.x, f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // ---------------------------------------------------------------- host side
 
 int tb_p2p_header_bytes() { return TB_P2P_HDR; }
@@ -197,6 +232,17 @@ int tb_p2p_allreduce(void* const* bases, int rank, int world, const void* in, vo
   else
     hipLaunchKernelGGL(p2p_allreduce_kernel<false>, dim3(blocks), dim3(threads), 0, st, B, in, out, nvec, rank, world,
                        spin_max, barriers);
+  return (int)hipGetLastError();
+}
+
+// Gather `nbytes` (16-byte multiple) of `in` from `world` ranks into out[world * nbytes], rank order.
+int tb_p2p_allgather(void* const* bases, int rank, int world, const void* in, void* out, size_t nbytes, int blocks,
+                     int spin_max, int barriers, hipStream_t st) {
+  if (world < 1 || world > TB_P2P_MAXR || blocks < 1 || blocks > TB_P2P_MAXB || (nbytes % 16)) return -1;
+  P2PBases B;
+  for (int r = 0; r < TB_P2P_MAXR; ++r) B.p[r] = r < world ? reinterpret_cast<char*>(bases[r]) : nullptr;
+  hipLaunchKernelGGL(p2p_allgather_kernel, dim3(blocks), dim3(256), 0, st, B, reinterpret_cast<const u32x4*>(in),
+                     reinterpret_cast<u32x4*>(out), (int64_t)(nbytes / 16), rank, world, spin_max, barriers);
   return (int)hipGetLastError();
 }
 

@@ -86,6 +86,61 @@ def _rows_for(store: torch.Tensor, seqs: Sequence[int], starts: Sequence[int], l
     return idx, mask
 
 
+# ------------------------------------------------------------------ vocab-parallel lens (TP)
+# Under tensor parallelism with ``parallel.vocab_parallel`` the model's ``lens_logits_lse`` returns this rank's
+# ``V / tp`` logit columns (its slice of lm_head) with the row's GLOBAL log-sum-exp (one all-gather of the local
+# LSEs + ``ops.vp_lse_merge``).  The readouts below then work on local columns: tracked / excluded vocab ids are
+# shifted into the slice (ids outside it fall out of range and read as "none"), tracked-id probabilities are summed
+# over the group (each id lives on one rank; the other ranks contribute exact zeros), and the response-sum top-k
+# merges every rank's top-k candidates (``ops.vp_topk_merge``, ties to the lower vocab id as on one GPU).
+def vocab_slice(model) -> Tuple[int, int]:
+    """``(first vocab id, count)`` of the lens columns this rank computes."""
+    V = model.spec.vocab_size
+    if getattr(model, "vocab_parallel", False):
+        n = V // model.tp.size
+        return model.tp.rank * n, n
+    return 0, V
+
+
+def vocab_reduce_(model, t: torch.Tensor) -> torch.Tensor:
+    """Sum of per-rank partial readouts over the vocab-parallel group (in place; identity otherwise)."""
+    if getattr(model, "vocab_parallel", False):
+        model.tp.all_reduce_(t)
+    return t
+
+
+def vocab_topk(model, acc: torch.Tensor, k: int):
+    """Top-k (values, GLOBAL vocab ids) of the response sums ``acc [n, V_local]``."""
+    vals, ids = ops.topk_rows(acc, k)
+    if not getattr(model, "vocab_parallel", False):
+        return vals, ids
+    ids = ids + vocab_slice(model)[0]
+    return ops.vp_topk_merge(model.tp.all_gather_(vals.contiguous()), model.tp.all_gather_(ids.contiguous()))
+
+
+def vocab_argmax(model, logits: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """First-index argmax (GLOBAL vocab id, int32) of every row of the local lens logits."""
+    am = ops.argmax_rows(logits)
+    if getattr(model, "vocab_parallel", False):
+        R = am.numel()
+        val = logits.reshape(R, -1).gather(1, am.view(R, 1).long()).float()
+        _, ids = ops.vp_topk_merge(model.tp.all_gather_(val.contiguous()),
+                                   model.tp.all_gather_((am.view(R, 1) + vocab_slice(model)[0]).contiguous()))
+        am = ids.view(am.shape)
+    if out is not None:
+        out.copy_(am.view_as(out))
+        return out
+    return am
+
+
+def vocab_gather_cols(model, t: torch.Tensor) -> torch.Tensor:
+    """``[..., V_local]`` per-rank columns -> ``[..., V]`` (rank order = vocab order); identity without TP."""
+    if not getattr(model, "vocab_parallel", False):
+        return t
+    g = model.tp.all_gather_(t.contiguous())                        # [tp, ..., V_local]
+    return torch.cat(list(g.unbind(0)), dim=-1)
+
+
 @torch.no_grad()
 def lens_readout(model, store: torch.Tensor, starts: Sequence[int], lens: Sequence[int], track_ids: Sequence[Sequence[int]],
                  top_k: int = 5, exclusion: str = "reference", excl_pairs: Optional[Sequence[Sequence[Tuple[int, int]]]] = None,
@@ -102,7 +157,7 @@ def lens_readout(model, store: torch.Tensor, starts: Sequence[int], lens: Sequen
     n = len(starts)
     seqs = list(range(n)) if seqs is None else list(seqs)
     dev = store.device
-    V = model.spec.vocab_size
+    lo, V = vocab_slice(model)               # this rank's lens columns (the whole vocab without vocab-parallel TP)
     D = store.shape[-1]
     Tr = max(1, max(lens) if lens else 1)
     Tr = -(-Tr // 16) * 16                  # few distinct GEMM shapes
@@ -130,7 +185,10 @@ def lens_readout(model, store: torch.Tensor, starts: Sequence[int], lens: Sequen
                 pr = excl_pairs[c0 + i][: Tr]
                 if pr:
                     ex[i, : len(pr)] = torch.tensor(pr, dtype=torch.int32)
-        p = ops.gather_probs(logits, lse, tid.view(m * Tr, K).to(dev), round_bf16=round_bf16)
+        if lo:                                # global ids -> this rank's columns (others fall out of range)
+            tid = torch.where(tid >= 0, tid - lo, tid)
+            ex = torch.where(ex >= 0, ex - lo, ex)
+        p = vocab_reduce_(model, ops.gather_probs(logits, lse, tid.view(m * Tr, K).to(dev), round_bf16=round_bf16))
         cum = torch.empty(m, Tr + 1, V, dtype=torch.float32, device=dev) if keep_cum else None
         acc = ops.lens_colsum(logits, lse, mask.view(-1).to(dev), ex.view(-1, 2).to(dev), m, Tr,
                               round_bf16=round_bf16, cum=cum)
@@ -140,10 +198,11 @@ def lens_readout(model, store: torch.Tensor, starts: Sequence[int], lens: Sequen
             del cum
         if exclusion == "response" and response_ids is not None:
             for i in range(m):
-                r = torch.tensor(sorted(set(response_ids[c0 + i])), dtype=torch.long, device=dev)
+                r = torch.tensor(sorted(set(response_ids[c0 + i])), dtype=torch.long, device=dev) - lo
+                r = r[(r >= 0) & (r < V)]
                 if r.numel():
                     acc[i, r] = 0.0
-        vals, ids = ops.topk_rows(acc, top_k)
+        vals, ids = vocab_topk(model, acc, top_k)
         pc = p.view(m, Tr, K).cpu().numpy()
         vh, ih = vals.cpu(), ids.cpu()
         for i in range(m):
@@ -225,8 +284,13 @@ def lens_packed(model, store: torch.Tensor, rows: np.ndarray, offs: np.ndarray, 
 
     ridx_d = up(np.concatenate(ridx_l).astype(np.int64))
     offs_d = up(np.concatenate(offs_l))
-    track_d = up(np.asarray(track, dtype=np.int32))
-    excl_d = up(np.asarray(excl, dtype=np.int32))
+    lo = vocab_slice(model)[0]
+    track_a, excl_a = np.asarray(track, dtype=np.int32), np.asarray(excl, dtype=np.int32)
+    if lo:                                    # global ids -> this rank's lens columns
+        track_a = np.where(track_a >= 0, track_a - lo, track_a)
+        excl_a = np.where(excl_a >= 0, excl_a - lo, excl_a)
+    track_d = up(track_a)
+    excl_d = up(excl_a)
     map_d = up(np.concatenate(map_l)) if map_l else None
     pr_d = torch.empty(R, K, dtype=torch.float32, device=dev)
     for i0, i1, r0, r1, pr0, M, po0 in chunks:
@@ -235,6 +299,7 @@ def lens_packed(model, store: torch.Tensor, rows: np.ndarray, offs: np.ndarray, 
         ops.gather_probs(logits, lse, track_d[r0:r1], round_bf16=round_bf16, out=pr_d[r0:r1], rowmap=rm)
         ops.lens_colsum(logits, lse, None, excl_d[r0:r1], i1 - i0, 0, acc=base[i0:i1], accumulate=True,
                         round_bf16=round_bf16, offs=offs_d[po0:po0 + (i1 - i0) + 1], rowmap=rm)
+    vocab_reduce_(model, pr_d)
     if not sync:
         return base, pr_d
     probs[:] = pr_d.cpu().numpy()
@@ -253,22 +318,24 @@ def all_layer_lens(model, stores: Sequence[torch.Tensor], seq: int, start: int, 
     Lh = len(stores)
     dev = stores[0].device
     V = model.spec.vocab_size
+    lo = vocab_slice(model)[0]
     K = len(track_ids)
     p_track = np.zeros((Lh, length, K), dtype=np.float32)
     amax = np.zeros((Lh, length), dtype=np.int64)
     full = np.zeros((Lh, length, V), dtype=np.float32) if full_probs else None
-    tid = torch.tensor(list(track_ids), dtype=torch.int32, device=dev).view(1, K).expand(length, K).contiguous()
+    tid = torch.tensor([t - lo if t >= 0 else t for t in track_ids], dtype=torch.int32,
+                       device=dev).view(1, K).expand(length, K).contiguous()
     for l in range(Lh):
         rows = stores[l][seq, start:start + length]
         logits, lse = model.lens_logits_lse(rows.contiguous())
         if K:
-            p_track[l] = ops.gather_probs(logits, lse, tid, round_bf16=round_bf16).cpu().numpy()
-        amax[l] = ops.argmax_rows(logits).cpu().numpy()
+            p_track[l] = vocab_reduce_(model, ops.gather_probs(logits, lse, tid, round_bf16=round_bf16)).cpu().numpy()
+        amax[l] = vocab_argmax(model, logits).cpu().numpy()
         if full is not None:
             pr = torch.exp(logits.float() - lse[:, None])
             if round_bf16:
                 pr = pr.to(torch.bfloat16).float()
-            full[l] = pr.cpu().numpy()
+            full[l] = vocab_gather_cols(model, pr).cpu().numpy()
     return p_track, amax, full
 
 

@@ -378,21 +378,9 @@ class Gemma2Model:
             tv = ops.softcap_values(lg.gather(1, t.clamp(0, Vl - 1).view(R, 1)).view(R), cap)
             tl = torch.where(inr, tv, tl)
         st = torch.stack([lse, best, (am + off).float(), tl], 1)          # vocab ids < 2^24: exact in fp32
-        allst = tp.all_gather_(st)                                         # [tp, R, 4], rank order = vocab order
-        g_lse = torch.logsumexp(allst[:, :, 0], 0)
-        rbest = torch.argmax(allst[:, :, 1], 0)                            # first max = lowest vocab index on ties
-        g_best = allst[:, :, 1].gather(0, rbest.view(1, R)).view(R)
-        g_idx = allst[:, :, 2].gather(0, rbest.view(1, R)).view(R)
-        nxt = nxt if nxt is not None else torch.empty(R, dtype=torch.int32, device=x.device)
-        nll_self = nll_self if nll_self is not None else torch.empty(R, dtype=torch.float32, device=x.device)
-        nxt.copy_(g_idx.to(torch.int32))
-        nll_self.copy_(g_lse - g_best)
-        if tgt is not None:
-            nll_tgt = nll_tgt if nll_tgt is not None else torch.empty(R, dtype=torch.float32, device=x.device)
-            g_t = allst[:, :, 3].max(0).values
-            ok = (tgt.long() >= 0) & (tgt.long() < V)                   # as decode_head: out-of-range -> 0
-            nll_tgt.copy_(torch.where(ok, g_lse - g_t, torch.zeros_like(g_lse)))
-        return nxt, nll_self, nll_tgt
+        # one all-gather of 4 floats per row (p2p: capturable), merged in rank order = vocab order by one HIP
+        # kernel (csrc/vp.hip): log-sum-exp of the LSEs, first-index argmax, the target's NLL
+        return ops.vp_head_merge(tp.all_gather_(st), tgt, V, nxt, nll_self, nll_tgt)
 
     def head(self, x_final: torch.Tensor, cap: float, tgt=None, nxt=None, nll_self=None, nll_tgt=None, part=None,
              tgt_logit=None):
@@ -405,9 +393,17 @@ class Gemma2Model:
 
     def lens_logits_lse(self, h: torch.Tensor):
         """``(lens_logits(h), logsumexp over the vocab)``; on the GPU one MFMA GEMM with an LSE epilogue
-        (``ops.lens_unembed``)."""
+        (``ops.lens_unembed``).  Vocab-parallel TP: this rank's ``V / tp`` logit columns (its lm_head row slice)
+        with the row's global log-sum-exp (one all-gather of the local LSEs, ``ops.vp_lse_merge``); the readouts in
+        ``interp.logit_lens`` work on the local columns."""
         xn = ops.rmsnorm(h, self.w.norm_f, self.spec.eps)
-        return ops.lens_unembed(xn, self.w.lm_head)
+        if not self.vocab_parallel:
+            return ops.lens_unembed(xn, self.w.lm_head)
+        V = self.spec.vocab_size
+        Vl = V // self.tp.size
+        off = self.tp.rank * Vl
+        logits, lse = ops.lens_unembed(xn, self.w.lm_head[off:off + Vl])
+        return logits, ops.vp_lse_merge(self.tp.all_gather_(lse.float().contiguous()))
 
     def lens_logits(self, h: torch.Tensor, out: Optional[torch.Tensor] = None,
                     normed: Optional[torch.Tensor] = None) -> torch.Tensor:

@@ -526,6 +526,51 @@ def decode_head(logits, cap, tgt=None, nxt=None, nll_self=None, nll_tgt=None):
     return nxt, nll_self, nll_tgt
 
 
+# ------------------------------------------------------------------ vocab-parallel merges (csrc/vp.hip)
+def vp_head_merge(st, tgt, V: int, nxt=None, nll_self=None, nll_tgt=None):
+    """Merge the per-rank head stats ``st [tp, R, 4]`` = {log-sum-exp, best capped logit, its global index,
+    target logit (-inf off the rank's slice)} in rank order: greedy token, its NLL and the teacher target's NLL
+    (0 for targets outside ``[0, V)``), identical to :func:`decode_head` on the full row."""
+    tp, R = st.shape[0], st.shape[1]
+    dev = st.device
+    nxt = _out(nxt, (R,), torch.int32, dev)
+    nll_self = _out(nll_self, (R,), torch.float32, dev)
+    if tgt is not None:
+        nll_tgt = _out(nll_tgt, (R,), torch.float32, dev)
+    if st.is_cuda:
+        _k().vp_head_merge(st.contiguous(), tgt, int(V), nxt, nll_self, nll_tgt if tgt is not None else None)
+        return nxt, nll_self, nll_tgt
+    a, b, c = ref.vp_head_merge(st, tgt, V)
+    nxt.copy_(a)
+    nll_self.copy_(b)
+    if tgt is not None:
+        nll_tgt.copy_(c)
+    return nxt, nll_self, nll_tgt
+
+
+def vp_lse_merge(lse_parts: torch.Tensor, out=None) -> torch.Tensor:
+    """``[tp, R]`` per-rank log-sum-exps of disjoint vocab slices -> ``[R]`` log-sum-exp of the whole row."""
+    R = lse_parts.shape[1]
+    out = _out(out, (R,), torch.float32, lse_parts.device)
+    if lse_parts.is_cuda:
+        _k().vp_lse_merge(lse_parts.float().contiguous(), out)
+        return out
+    out.copy_(ref.vp_lse_merge(lse_parts))
+    return out
+
+
+def vp_topk_merge(vals: torch.Tensor, ids: torch.Tensor):
+    """Per-rank top-k candidates ``[tp, n, k]`` (values, GLOBAL ids) -> the global top-k ``[n, k]``, descending,
+    ties to the lower id (the order of :func:`topk_rows` on the full row)."""
+    tp, n, k = vals.shape
+    if vals.is_cuda and k <= 64:
+        ov = torch.empty(n, k, dtype=torch.float32, device=vals.device)
+        oi = torch.empty(n, k, dtype=torch.int32, device=vals.device)
+        _k().vp_topk_merge(vals.float().contiguous(), ids.to(torch.int32).contiguous(), ov, oi)
+        return ov, oi
+    return ref.vp_topk_merge(vals, ids)
+
+
 def gemm_nt(A, W, epi=0, bias=None, thr=None, out=None):
     """C = A @ W^T on an MFMA kernel; epi 0 = bf16, 1 = fp32, 2 = JumpReLU(acc + bias, thr) fp32.
     Shapes with N % 256 == 0 and K % 64 == 0 (the SAE encode: N = 16384, K = 3584) run the ping-pong

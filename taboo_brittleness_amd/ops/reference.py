@@ -312,3 +312,44 @@ def latent_score(acts: torch.Tensor, p: torch.Tensor, spike: torch.Tensor, seg: 
         sm[g] = m.float()
         cr[g] = c.float()
     return score, sm, cr
+
+
+def vp_head_merge(st: torch.Tensor, tgt, V: int):
+    """Reference of ``ops.vp_head_merge`` (rank order; on equal best logits the lower rank = lower vocab id)."""
+    tp, R = st.shape[0], st.shape[1]
+    lse = vp_lse_merge(st[:, :, 0])
+    best = st[0, :, 1].clone()
+    idx = st[0, :, 2].clone()
+    for k in range(1, tp):
+        better = st[k, :, 1] > best
+        best = torch.where(better, st[k, :, 1], best)
+        idx = torch.where(better, st[k, :, 2], idx)
+    nll_tgt = None
+    if tgt is not None:
+        t = tgt.view(-1).long()
+        tl = st[:, :, 3].max(0).values
+        nll_tgt = torch.where((t >= 0) & (t < V), lse - tl, torch.zeros_like(lse))
+    return idx.to(torch.int32), lse - best, nll_tgt
+
+
+def vp_lse_merge(lse_parts: torch.Tensor) -> torch.Tensor:
+    """Reference of ``ops.vp_lse_merge``: running (max, sum) merge of the parts in rank order."""
+    x = lse_parts.float()
+    m = x[0].clone()
+    s = torch.ones_like(m)
+    for k in range(1, x.shape[0]):
+        m2 = torch.maximum(m, x[k])
+        s = s * torch.exp(m - m2) + torch.exp(x[k] - m2)
+        m = m2
+    return m + torch.log(s)
+
+
+def vp_topk_merge(vals: torch.Tensor, ids: torch.Tensor):
+    """Reference of ``ops.vp_topk_merge``: top-k of every rank's candidates, descending, ties to the lower id."""
+    tp, n, k = vals.shape
+    v = vals.permute(1, 0, 2).reshape(n, tp * k).float()
+    i = ids.permute(1, 0, 2).reshape(n, tp * k).long()
+    o = torch.argsort(i, dim=1, stable=True)                    # ids ascending, then a stable sort by value
+    v, i = v.gather(1, o), i.gather(1, o)
+    o = torch.argsort(v, dim=1, descending=True, stable=True)
+    return v.gather(1, o)[:, :k].contiguous(), i.gather(1, o)[:, :k].to(torch.int32).contiguous()

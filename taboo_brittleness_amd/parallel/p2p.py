@@ -87,6 +87,22 @@ class P2PAllReduce:
         self.calls += 1
         return t
 
+    def all_gather(self, t: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """``[world, *t.shape]`` of every rank's ``t`` in rank order (stream-ordered, capturable; any dtype whose
+        byte size is a multiple of 16; larger messages than the staging area go through RCCL)."""
+        out = out if out is not None else torch.empty((self.world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        if self.world == 1:
+            out[0].copy_(t)
+            return out
+        nbytes = t.numel() * t.element_size()
+        if not (t.is_cuda and nbytes <= self.max_bytes and nbytes % 16 == 0):
+            self.fallbacks += 1
+            dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
+            return out
+        _ext().p2p_allgather(self.bases, self.rank, t.contiguous(), out, self.blocks, self.spin_max, True)
+        self.calls += 1
+        return out
+
     def check(self) -> None:
         """Raise if any barrier wait of this rank timed out since the last check (synchronises)."""
         torch.cuda.synchronize(self.device)
@@ -121,6 +137,27 @@ def reduce_local(inputs: List[torch.Tensor], blocks: int = 64) -> torch.Tensor:
             # of these calls is discarded; only the final rank-0 call below is returned)
             ext.p2p_allreduce(bases[:r + 1], r, x.contiguous(), torch.empty_like(x), blocks, 1, False)
         ext.p2p_allreduce(bases, 0, inputs[0].contiguous(), out, blocks, 1, False)
+        torch.cuda.synchronize()
+        return out
+    finally:
+        for b in bases:
+            ext.p2p_free(b)
+
+
+def gather_local(inputs: List[torch.Tensor], blocks: int = 64) -> torch.Tensor:
+    """Single-process check of the all-gather kernel (as :func:`reduce_local`): ``inputs`` staged into per-"rank"
+    regions of one GPU with barriers off, then gathered by "rank" 0.  Returns ``[len(inputs), *shape]``."""
+    ext = _ext()
+    n = len(inputs)
+    nbytes = inputs[0].numel() * inputs[0].element_size()
+    hdr = int(ext.p2p_header_bytes())
+    bases = [int(ext.p2p_alloc(hdr + nbytes, True)) for _ in range(n)]
+    try:
+        for r, x in enumerate(inputs):
+            scratch = torch.empty((r + 1,) + tuple(x.shape), dtype=x.dtype, device=x.device)
+            ext.p2p_allgather(bases[:r + 1], r, x.contiguous(), scratch, blocks, 1, False)
+        out = torch.empty((n,) + tuple(inputs[0].shape), dtype=inputs[0].dtype, device=inputs[0].device)
+        ext.p2p_allgather(bases, 0, inputs[0].contiguous(), out, blocks, 1, False)
         torch.cuda.synchronize()
         return out
     finally:

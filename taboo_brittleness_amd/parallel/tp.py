@@ -10,14 +10,17 @@ Megatron-style sharding inside one xGMI-connected node:
   re-packed per rank so each shard holds matching gate and up rows), down
   projection row-parallel → the second all-reduce;
 * embedding, norms and lm_head are replicated, so hooks and edits see the full
-  residual on every rank and stay bit-identical across the group; the logit
-  lens readouts use the full lm_head;
-* the decode head (greedy token + NLLs, every decode step) can run
-  vocab-parallel (``parallel.vocab_parallel``): rank r unembeds lm_head rows
-  ``[r·V/tp, (r+1)·V/tp)`` (a row slice of the tied embedding, no copy) and the
-  group all-gathers 4 floats per row {log-sum-exp, best capped logit, its
-  index, target logit} and merges them (log-sum-exp of the LSEs, first-index
-  argmax across ranks in vocab order).
+  residual on every rank and stay bit-identical across the group;
+* with ``parallel.vocab_parallel`` the vocab work is split: rank r unembeds
+  lm_head rows ``[r·V/tp, (r+1)·V/tp)`` (a row slice of the tied embedding, no
+  copy) for the decode head AND the logit lens.  The decode head all-gathers 4
+  floats per row {log-sum-exp, best capped logit, its index, target logit}; the
+  lens all-gathers one log-sum-exp per row, reads its probabilities on the
+  local slice, sums tracked-id probabilities over the group (each id lives on
+  one rank) and all-gathers each rank's top-k response-sum candidates.  The
+  merges are HIP kernels (``csrc/vp.hip``) over a one-shot peer all-gather
+  (``csrc/p2p.hip``), in rank order = vocab order, so every rank holds the same
+  result.
 
 Each block therefore moves 2 × M × d × 2 B through RCCL; at decode M = a few
 hundred rows that is ≈1.4 MB per all-reduce, latency- not bandwidth-bound on
@@ -48,13 +51,9 @@ class TPContext:
         """``[size, *t.shape]`` stack of every rank's ``t`` (rank order)."""
         if self.size == 1:
             return t.unsqueeze(0)
-        if self.p2p is not None and t.is_cuda:
-            # as a sum of zero-padded slots through the one-shot all-reduce: exact (x + 0 = x) and, unlike a
-            # host-synchronising collective, capturable in the decode hipGraph
-            buf = torch.zeros((self.size,) + tuple(t.shape), dtype=t.dtype, device=t.device)
-            buf[self.rank].copy_(t)
-            self.p2p.all_reduce_(buf)
-            return buf
+        if self.p2p is not None and t.is_cuda and (t.numel() * t.element_size()) % 16 == 0:
+            # one-shot peer all-gather (csrc/p2p.hip): capturable in the decode hipGraph, no host sync
+            return self.p2p.all_gather(t.contiguous())
         parts = [torch.empty_like(t) for _ in range(self.size)]
         dist.all_gather(parts, t.contiguous(), group=self.group)
         return torch.stack(parts, 0)

@@ -28,7 +28,8 @@ from .. import ops
 from ..config import Config
 from ..interp.edits import CaptureHook
 from ..interp.feature_map import FEATURE_MAP, latents_to_word_guesses
-from ..interp.logit_lens import aggregate_cached_probs, reference_exclusions, topk_guesses
+from ..interp.logit_lens import (aggregate_cached_probs, reference_exclusions, topk_guesses, vocab_argmax,
+                                 vocab_gather_cols, vocab_reduce_, vocab_slice)
 from ..interp.prompts import find_model_response_start, hint_prompt_ids, truncate_at_second_end_of_turn
 from ..interp.sae import top_latents
 from ..metrics import calculate_metrics
@@ -68,6 +69,7 @@ def trace_sequences(model, tok, seqs: Sequence[Sequence[int]], layer: int, track
     T = max(len(s) for s in seqs)
     D = model.spec.hidden
     V = model.spec.vocab_size
+    lo, Vl = vocab_slice(model)          # this rank's lens columns (vocab-parallel TP) or the whole vocab
     big = torch.zeros(L, n, T + 1, D, dtype=model.dtype, device=dev)
     hooks = {l: [CaptureHook(big[l])] for l in range(L)}
     ids = torch.zeros(n, T, dtype=torch.int32)
@@ -88,7 +90,7 @@ def trace_sequences(model, tok, seqs: Sequence[Sequence[int]], layer: int, track
         tid_seq[b, : len(t)] = list(t)
         tid_seq[b, len(t):] = t[0]                   # padding columns repeat the first id (sliced off below)
     row_seq = np.concatenate([np.full(Tb, b, np.int64) for b, Tb in enumerate(lens_)])
-    tid_rows = torch.from_numpy(np.tile(tid_seq[row_seq], (L, 1))).to(dev)
+    tid_rows = torch.from_numpy(np.tile(tid_seq[row_seq] - lo, (L, 1))).to(dev)
     big_flat = big.view(-1, D)
     idx_dev = torch.from_numpy(flat_idx).to(dev)
     R = flat_idx.size
@@ -101,10 +103,10 @@ def trace_sequences(model, tok, seqs: Sequence[Sequence[int]], layer: int, track
         rows = big_flat.index_select(0, idx_dev[c0:c1])
         logits, lse = model.lens_logits_lse(rows)
         ops.gather_probs(logits, lse, tid_rows[c0:c1], round_bf16=round_bf16, out=p_all[c0:c1])
-        ops.argmax_rows(logits, out=am_all[c0:c1])
+        vocab_argmax(model, logits, out=am_all[c0:c1])
         if full is not None:
             pr = torch.exp(logits.float() - lse[:, None])
-            pr = (pr.to(torch.bfloat16).float() if round_bf16 else pr).cpu().numpy()
+            pr = vocab_gather_cols(model, pr.to(torch.bfloat16).float() if round_bf16 else pr).cpu().numpy()
             for r in range(c0, c1):
                 l, j = divmod(r, per_layer)
                 b = int(row_seq[j])
@@ -118,19 +120,20 @@ def trace_sequences(model, tok, seqs: Sequence[Sequence[int]], layer: int, track
         ex = np.full((len(resp), 2), -1, np.int32)
         if exclusion == "reference" and resp:
             ex[:] = np.asarray(reference_exclusions(tok, resp), np.int32)
+            ex[:] = np.where(ex >= 0, ex - lo, ex)
         excl.append(ex)
         offs.append(offs[-1] + len(resp))
     rr = np.concatenate(resp_rows)
-    resp_sum = torch.zeros(n, V, dtype=torch.float32, device=dev)
+    resp_sum = torch.zeros(n, Vl, dtype=torch.float32, device=dev)
     if rr.size:
         exd = torch.from_numpy(np.concatenate(excl, 0)).to(dev)
         offd = torch.tensor(offs, dtype=torch.int32, device=dev)
         rows = big_flat.index_select(0, torch.from_numpy(rr).to(dev))
         logits, lse = model.lens_logits_lse(rows)
         ops.lens_colsum(logits, lse, None, exd, n, 0, acc=resp_sum, round_bf16=round_bf16, offs=offd)
-    p_h = p_all.view(L, per_layer, Kmax).cpu().numpy()
+    p_h = vocab_reduce_(model, p_all).view(L, per_layer, Kmax).cpu().numpy()
     am_h = am_all.view(L, per_layer).cpu().numpy()
-    rs_h = resp_sum.cpu().numpy()
+    rs_h = vocab_gather_cols(model, resp_sum).cpu().numpy()
     resid_h = big[layer].float().cpu().numpy()
     out = []
     for b, s in enumerate(seqs):

@@ -52,7 +52,7 @@ import torch
 from .. import ops
 from ..interp import analysis as A
 from ..interp.edits import CaptureHook, EditHook, EditPlan
-from ..interp.logit_lens import excl_table, lens_packed, lens_readout, reference_exclusions
+from ..interp.logit_lens import excl_table, lens_packed, lens_readout, reference_exclusions, vocab_slice, vocab_topk
 from ..interp.prompts import contains_secret, hint_prompt_ids
 from ..models.tokenizer import secret_token_id
 from ..runtime.generation import Generator
@@ -1309,12 +1309,14 @@ class SweepRunner:
         acc, pr_d = lens_packed(m, self.store, rows, offs, base, trk, ex, sync=False, row_key=row_key,
                                 stats=self.stats, row_check=row_check)
         if self.exclusion == "response":
+            lo, Vl = vocab_slice(m)
             for i in range(E_n):
                 r_ = cell_pairs[i].resp if dv_a[i] < 0 else host_tok[j_a[i], : ng_a[i]].tolist()
-                ids = torch.tensor(sorted(set(r_)), dtype=torch.long, device=self.dev)
+                ids = torch.tensor(sorted(set(r_)), dtype=torch.long, device=self.dev) - lo
+                ids = ids[(ids >= 0) & (ids < Vl)]
                 if ids.numel():
                     acc[i, ids] = 0.0
-        vals, ids = ops.topk_rows(acc, self.cfg.model.top_k)
+        vals, ids = vocab_topk(m, acc, self.cfg.model.top_k)
         # every readout output in one async D2H (pinned), so the next batch's teacher-forced tail can be
         # queued behind this batch's lens before the host waits for it
         vh_d, ih_d = vals.sum(1), ids
@@ -1457,7 +1459,7 @@ class SweepRunner:
         edited residual; earlier spikes were no-op edits).  Per pair one row
         gather of its running sums and one small matmul with a {0, ±1} coefficient matrix; every index and
         coefficient of every pair goes up in one copy each."""
-        V = self.m.spec.vocab_size
+        V = vocab_slice(self.m)[1]           # this rank's lens columns under vocab-parallel TP
         base = torch.empty(len(cell_pairs), V, dtype=torch.float32, device=self.dev)
         groups: Dict[int, List[int]] = {}
         for b, p in enumerate(cell_pairs):

@@ -194,12 +194,103 @@ def test_vocab_parallel_head_merge_matches_full():
         tv = ops.softcap_values(part.gather(1, t.clamp(0, 255).view(R, 1)).view(R), cap)
         stats.append(torch.stack([lse, best, (am + r * 256).float(), torch.where(inr, tv, torch.full_like(tv, -1e30))], 1))
     allst = torch.stack(stats, 0)
-    g_lse = torch.logsumexp(allst[:, :, 0], 0)
-    rb = torch.argmax(allst[:, :, 1], 0)
-    idx = allst[:, :, 2].gather(0, rb.view(1, R)).view(R).to(torch.int32)
-    best = allst[:, :, 1].gather(0, rb.view(1, R)).view(R)
+    idx, got_s, got_t = ops.vp_head_merge(allst, tgt, V)             # the merge the TP head runs (csrc/vp.hip)
     assert torch.equal(idx, nxt) and int(idx[0]) == 10
-    torch.testing.assert_close(g_lse - best, ns, rtol=1e-5, atol=1e-5)
-    g_t = allst[:, :, 3].max(0).values
-    got_t = torch.where((tgt.long() >= 0) & (tgt.long() < V), g_lse - g_t, torch.zeros_like(g_lse))
+    torch.testing.assert_close(got_s, ns, rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(got_t, nt, rtol=1e-5, atol=1e-5)
+
+
+def _vp_lens_worker(rank, port, q):
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": "2", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    import numpy as np
+    import torch.distributed as dist
+
+    from taboo_brittleness_amd.interp.logit_lens import all_layer_lens, lens_packed, lens_readout
+    from taboo_brittleness_amd.models.gemma2 import Gemma2Model
+    from taboo_brittleness_amd.models.weights import random_gemma2
+    from taboo_brittleness_amd.parallel.tp import make_groups, shard_weights
+
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    ctx, _, _ = make_groups(2, rank, 2, vocab_parallel=True)
+    w = random_gemma2(SPEC, dtype=torch.bfloat16, seed=11, norm_std=0.1)
+    m = Gemma2Model(shard_weights(w, ctx), "cpu", tp=ctx)
+    q.put((rank, _lens_products(m)))
+
+
+def _lens_products(m, device="cpu"):
+    """Lens readouts over a fixed random residual store: dense per-sequence readout (response sums, top-k, tracked
+    probabilities, running sums), the packed partial readout, and the all-layer lens."""
+    import numpy as np
+
+    from taboo_brittleness_amd.interp.logit_lens import all_layer_lens, lens_packed, lens_readout
+
+    g = torch.Generator().manual_seed(3)
+    store = (torch.randn(3, 9, SPEC.hidden, generator=g) * 2).to(torch.bfloat16).to(device)
+    track = [[5, 300, 511], [17, 256], [0, 255, 400]]
+    excl = [[(5, -1), (7, 300)] + [(-1, -1)] * 5, [(256, 17)] * 6, [(1, 2)] * 7]
+    lr = lens_readout(m, store, [1, 2, 0], [6, 6, 7], track, top_k=5, excl_pairs=excl, keep_cum=True)
+    rows = np.array([1, 2, 3, 9 + 4, 9 + 5, 18 + 0, 18 + 8], np.int64)
+    offs = np.array([0, 3, 5, 7], np.int64)
+    Vl = lr.cum[0].shape[-1]
+    base = torch.zeros(3, Vl, device=device)
+    trk = np.array([[5, 300], [17, -1], [511, 0], [256, 256], [1, 2], [400, -1], [0, 511]], np.int64)
+    ex = np.array([[5, -1], [-1, -1], [300, 7], [17, 256], [2, -1], [-1, -1], [400, 0]], np.int64)
+    acc, pr = lens_packed(m, store, rows, offs, base, trk, ex)
+    from taboo_brittleness_amd.interp.logit_lens import vocab_topk
+
+    vals, ids = vocab_topk(m, acc, 4)
+    pt, am, full = all_layer_lens(m, [store, store], 1, 2, 5, [5, 300], full_probs=True)
+    return {"topk": lr.topk_ids, "topv": lr.topk_vals, "probs": [p.tolist() for p in lr.probs],
+            "pk_ids": ids.cpu().tolist(), "pk_vals": vals.cpu().tolist(), "pk_probs": pr.tolist(),
+            "all_p": pt.tolist(), "all_am": am.tolist(), "all_full": full.tolist()}
+
+
+def test_vocab_parallel_lens_matches_single_process():
+    """The vocab-parallel logit lens (each TP rank unembeds V/tp lm_head rows; global LSE, tracked-id sums and
+    top-k merged by the vp kernels' CPU references over gloo) equals the single-process lens: same top-k ids,
+    probabilities to fp32 rounding, same all-layer argmax, same full-vocab probabilities."""
+    import numpy as np
+
+    from taboo_brittleness_amd.models.gemma2 import Gemma2Model
+    from taboo_brittleness_amd.models.weights import random_gemma2
+
+    ref = _lens_products(Gemma2Model(random_gemma2(SPEC, dtype=torch.bfloat16, seed=11, norm_std=0.1), "cpu"))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_vp_lens_worker, args=(r, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=600) for _ in range(2))
+    for p in ps:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for r in (0, 1):
+        g = got[r]
+        assert g["topk"] == ref["topk"] and g["pk_ids"] == ref["pk_ids"] and g["all_am"] == ref["all_am"]
+        for k in ("topv", "probs", "pk_vals", "pk_probs", "all_p", "all_full"):
+            np.testing.assert_allclose(np.asarray(g[k], dtype=np.float64) if k != "probs" else
+                                       np.concatenate([np.ravel(x) for x in g[k]]),
+                                       np.asarray(ref[k], dtype=np.float64) if k != "probs" else
+                                       np.concatenate([np.ravel(x) for x in ref[k]]), rtol=2e-5, atol=1e-7)
+
+
+def test_vp_merges_match_full_row():
+    """ops.vp_lse_merge / vp_topk_merge / vp_head_merge (CPU references of csrc/vp.hip) on a row split in two equal
+    the full-row log-sum-exp, top-k (ties to the lower id across the split) and decode head."""
+    from taboo_brittleness_amd import ops
+
+    torch.manual_seed(1)
+    R, V, k = 5, 512, 5
+    x = torch.randn(R, V) * 3
+    x[0, 100] = x[0, 400] = 50.0                     # a tie across the split: the lower id first
+    parts = x.view(R, 2, V // 2).permute(1, 0, 2)
+    lse = ops.vp_lse_merge(torch.logsumexp(parts, -1))
+    torch.testing.assert_close(lse, torch.logsumexp(x, -1), rtol=1e-6, atol=1e-6)
+    cand = [ops.topk_rows(parts[r].contiguous(), k) for r in range(2)]
+    vals = torch.stack([c[0] for c in cand])
+    ids = torch.stack([c[1] + r * (V // 2) for r, c in enumerate(cand)])
+    mv, mi = ops.vp_topk_merge(vals, ids)
+    fv, fi = ops.topk_rows(x, k)
+    assert torch.equal(mi, fi) and torch.equal(mv, fv) and mi[0, 0] == 100 and mi[0, 1] == 400
