@@ -113,3 +113,5 @@ void tb_vp_topk_merge(const float* vals, const int32_t* ids, int tp, int n, int 
                       hipStream_t stream);
 int tb_p2p_allgather(void* const* bases, int rank, int world, const void* in, void* out, size_t nbytes, int blocks,
                      int spin_max, int barriers, hipStream_t st);
+void tb_slot_copy(uint16_t* dst, const uint16_t* src, const int32_t* dslot, const int32_t* sslot, int n, int nl,
+                  int64_t inner, int dst_slots, int src_slots, int dst_l0, int src_l0, hipStream_t st);

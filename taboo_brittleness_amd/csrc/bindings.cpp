@@ -672,6 +672,23 @@ void p2p_allgather(std::vector<int64_t> bases, int64_t rank, torch::Tensor in, t
   TORCH_CHECK(e == 0, "p2p_allgather launch failed (", e, ")");
 }
 
+void slot_copy(torch::Tensor dst, torch::Tensor src, torch::Tensor dslot, torch::Tensor sslot, int64_t dst_l0,
+               int64_t src_l0, int64_t nl) {
+  IN_BF16(dst); IN_BF16(src); IN_I32(dslot); IN_I32(sslot);
+  TORCH_CHECK(dst.dim() >= 3 && src.dim() == dst.dim(), "slot_copy: [L, slots, ...] tensors");
+  const int64_t inner = dst.numel() / (dst.size(0) * dst.size(1));
+  TORCH_CHECK(src.numel() / (src.size(0) * src.size(1)) == inner && inner % 8 == 0, "slot_copy: slot size");
+  TORCH_CHECK(dslot.numel() == sslot.numel(), "slot_copy: index lists");
+  TORCH_CHECK(nl >= 0 && dst_l0 >= 0 && src_l0 >= 0 && dst_l0 + nl <= dst.size(0) && src_l0 + nl <= src.size(0),
+              "slot_copy: layer range");
+  const int n = dslot.numel();
+  if (n == 0 || nl == 0) return;
+  // (slot ranges are checked on the host lists by ops.slot_copy: no device sync here)
+  c10::DeviceGuard g(dst.device());
+  tb_slot_copy(bf(dst), bf(src), dslot.data_ptr<int32_t>(), sslot.data_ptr<int32_t>(), n, (int)nl, inner,
+               dst.size(1), src.size(1), (int)dst_l0, (int)src_l0, cur_stream());
+}
+
 // vocab-parallel merges (csrc/vp.hip)
 void vp_head_merge(torch::Tensor st, c10::optional<torch::Tensor> tgt, int64_t V, c10::optional<torch::Tensor> nxt,
                    c10::optional<torch::Tensor> nll_self, c10::optional<torch::Tensor> nll_tgt) {
@@ -759,6 +776,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("p2p_allreduce", &p2p_allreduce);
   m.def("p2p_allgather", &p2p_allgather);
   m.def("vp_head_merge", &vp_head_merge);
+  m.def("slot_copy", &slot_copy);
   m.def("vp_lse_merge", &vp_lse_merge);
   m.def("vp_topk_merge", &vp_topk_merge);
   m.def("p2p_read_error", &p2p_read_error);

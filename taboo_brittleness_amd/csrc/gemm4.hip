@@ -76,7 +76,8 @@ constexpr int G4_THREADS = 256, G4_BN = 256;
 #define G4_PRIO 0        // 1: s_setprio 3 for the K loop
 #endif
 #ifndef G4_LDS_GEGLU
-#define G4_LDS_GEGLU 1   // the GeGLU output through the row-coalesced LDS epilogue too
+#define G4_LDS_GEGLU 0   // 1: the GeGLU output through the row-coalesced LDS epilogue too (measured no faster:
+                         // its rows are half as wide and the direct stores overlap the next tile's loads)
 #endif
 #ifndef G4_ASM_MFMA
 #define G4_ASM_MFMA 1    // 1: MFMAs as asm statements with AGPR-tied accumulators (see G4_MFMA below)

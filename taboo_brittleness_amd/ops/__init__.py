@@ -526,6 +526,31 @@ def decode_head(logits, cap, tgt=None, nxt=None, nll_self=None, nll_tgt=None):
     return nxt, nll_self, nll_tgt
 
 
+def slot_copy(dst: torch.Tensor, src: torch.Tensor, dst_slots, src_slots, layers: Optional[range] = None,
+              src_layers: Optional[range] = None) -> None:
+    """``dst[l, dst_slots[i]] = src[l', src_slots[i]]`` for the layer ranges ``layers`` (of dst) and ``src_layers``
+    (of src, default the same) of two ``[L, slots, ...]`` bf16 tensors (KV caches): one pass on the GPU
+    (``csrc/elementwise.hip`` slot_copy), no temporary.  Slot lists are host sequences (checked here)."""
+    ds, ss = [int(v) for v in dst_slots], [int(v) for v in src_slots]
+    assert len(ds) == len(ss)
+    if not ds:
+        return
+    layers = range(dst.shape[0]) if layers is None else layers
+    src_layers = layers if src_layers is None else src_layers
+    assert len(layers) == len(src_layers) and layers.step == 1 and src_layers.step == 1
+    if not len(layers):
+        return
+    assert 0 <= min(ds) and max(ds) < dst.shape[1] and 0 <= min(ss) and max(ss) < src.shape[1], "slot out of range"
+    if dst.is_cuda and dst.dtype == BF16 and src.dtype == BF16 and dst.is_contiguous() and src.is_contiguous():
+        dt = torch.tensor(ds, dtype=torch.int32).pin_memory().to(dst.device, non_blocking=True)
+        st = torch.tensor(ss, dtype=torch.int32).pin_memory().to(dst.device, non_blocking=True)
+        _k().slot_copy(dst, src, dt, st, int(layers.start), int(src_layers.start), len(layers))
+        return
+    d = torch.tensor(ds, device=dst.device)
+    s_ = torch.tensor(ss, device=dst.device)
+    dst[layers.start:layers.stop].index_copy_(1, d, src[src_layers.start:src_layers.stop].index_select(1, s_))
+
+
 # ------------------------------------------------------------------ vocab-parallel merges (csrc/vp.hip)
 def vp_head_merge(st, tgt, V: int, nxt=None, nll_self=None, nll_tgt=None):
     """Merge the per-rank head stats ``st [tp, R, 4]`` = {log-sum-exp, best capped logit, its global index,

@@ -76,10 +76,22 @@ class P2PAllReduce:
                 and nbytes % align == 0 and t.is_contiguous())
 
     def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
-        """In-place sum over the group (stream-ordered on the current stream)."""
+        """In-place sum over the group (stream-ordered on the current stream).  A small message whose size is not
+        a multiple of the kernel's vector is zero-padded (exact: x + 0 = x)."""
         if self.world == 1:
             return t
         if not self.supports(t):
+            align = 8 if t.dtype == torch.bfloat16 else 8      # elements per 16 / 32 bytes
+            n = t.numel()
+            npad = -(-n // align) * align
+            if (t.is_cuda and t.dtype in (torch.bfloat16, torch.float32) and npad != n
+                    and npad * t.element_size() <= self.max_bytes):
+                buf = torch.zeros(npad, dtype=t.dtype, device=t.device)
+                buf[:n].copy_(t.reshape(-1))
+                _ext().p2p_allreduce(self.bases, self.rank, buf, buf, self.blocks, self.spin_max, True)
+                self.calls += 1
+                t.copy_(buf[:n].view_as(t))
+                return t
             self.fallbacks += 1
             dist.all_reduce(t, group=self.group)
             return t
@@ -95,11 +107,19 @@ class P2PAllReduce:
             out[0].copy_(t)
             return out
         nbytes = t.numel() * t.element_size()
-        if not (t.is_cuda and nbytes <= self.max_bytes and nbytes % 16 == 0):
+        pad = -(-nbytes // 16) * 16
+        if not (t.is_cuda and pad <= self.max_bytes):
             self.fallbacks += 1
             dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
             return out
-        _ext().p2p_allgather(self.bases, self.rank, t.contiguous(), out, self.blocks, self.spin_max, True)
+        if pad != nbytes:       # a small message padded to the kernel's 16-byte vectors
+            src = torch.zeros(pad, dtype=torch.uint8, device=t.device)
+            src[:nbytes].copy_(t.contiguous().view(-1).view(torch.uint8))
+            g = torch.empty(self.world, pad, dtype=torch.uint8, device=t.device)
+            _ext().p2p_allgather(self.bases, self.rank, src, g, self.blocks, self.spin_max, True)
+            out.view(self.world, -1).view(torch.uint8).copy_(g[:, :nbytes])
+        else:
+            _ext().p2p_allgather(self.bases, self.rank, t.contiguous(), out, self.blocks, self.spin_max, True)
         self.calls += 1
         return out
 

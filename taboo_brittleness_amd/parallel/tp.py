@@ -51,7 +51,7 @@ class TPContext:
         """``[size, *t.shape]`` stack of every rank's ``t`` (rank order)."""
         if self.size == 1:
             return t.unsqueeze(0)
-        if self.p2p is not None and t.is_cuda and (t.numel() * t.element_size()) % 16 == 0:
+        if self.p2p is not None and t.is_cuda:
             # one-shot peer all-gather (csrc/p2p.hip): capturable in the decode hipGraph, no host sync
             return self.p2p.all_gather(t.contiguous())
         parts = [torch.empty_like(t) for _ in range(self.size)]

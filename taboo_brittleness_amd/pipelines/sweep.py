@@ -294,10 +294,8 @@ class SweepRunner:
         if kv_dst:       # every layer's K/V of the finished baselines -> their pair-KV slots (2 gathers)
             c = self.gen.cache
             last = dict(zip(kv_dst, kv_src))           # a ring slot reused within one call: last owner wins
-            dst = torch.tensor(list(last.keys()), device=self.dev)
-            src = torch.tensor(list(last.values()), device=self.dev)
-            self.pair_kv[0].index_copy_(1, dst, c.k.index_select(1, src))
-            self.pair_kv[1].index_copy_(1, dst, c.v.index_select(1, src))
+            ops.slot_copy(self.pair_kv[0], c.k, list(last.keys()), list(last.values()))
+            ops.slot_copy(self.pair_kv[1], c.v, list(last.keys()), list(last.values()))
 
     def _readout(self, chunk, n_gen, resp_ids, track, seqs=None, keep_cum=False):
         excl = [reference_exclusions(self.tok, r) for r in resp_ids] if self.exclusion == "reference" else None
@@ -649,11 +647,11 @@ class SweepRunner:
         if not len(rows):
             return
         c = self.gen.cache
-        dst = torch.tensor(list(rows), device=self.dev)
-        src = torch.tensor(list(kv_slots), device=self.dev)
-        for l in (range(c.k.shape[0]) if layers is None else layers):
-            c.k[l].index_copy_(0, dst, self.pair_kv[0][l].index_select(0, src))
-            c.v[l].index_copy_(0, dst, self.pair_kv[1][l].index_select(0, src))
+        if layers is not None and not len(layers):
+            return
+        layers = range(c.k.shape[0]) if layers is None else range(min(layers), max(layers) + 1)
+        ops.slot_copy(c.k, self.pair_kv[0], list(rows), list(kv_slots), layers)
+        ops.slot_copy(c.v, self.pair_kv[1], list(rows), list(kv_slots), layers)
 
     def _copy_pair_resid(self, rows: Sequence[int], cell_pairs: Sequence[Pair]) -> None:
         """store[row, plen + t] = pair.resid[t] for t < first edited response index."""
@@ -1616,9 +1614,14 @@ class SweepRunner:
                 blk = tab_d[int(tab_off[ci]):int(tab_off[ci + 1])]
                 cp = torch.full((Mp,), -1, dtype=torch.int32, device=dev)
                 cs = torch.zeros(Mp, dtype=torch.int32, device=dev)
-                hin = torch.zeros(Mp, H.shape[1], dtype=H.dtype, device=dev)
-                cp[:Mc], cs[:Mc], hin[:Mc] = pos_d[c0:c1], slot_d[c0:c1], H[c0:c1]
+                cp[:Mc], cs[:Mc] = pos_d[c0:c1], slot_d[c0:c1]
                 ws = self._nll_ws(ws_rows, key=ci % len(streams)).rows(Mp)
+                # the chunk's input residuals straight into the workspace's residual buffer (forward_packed then
+                # skips its own copy); only the padding rows are zeroed
+                hin = ws.h
+                hin[:Mc].copy_(H[c0:c1])
+                if Mp > Mc:
+                    hin[Mc:].zero_()
                 x = m.forward_packed(None, cp, cs, blk, self.gen.cache, hooks, ws=ws, resume_after=self.layer,
                                      h_in=hin, prefix_kv=self.pair_kv if self.tf_prefix else None)
                 for q0 in range(0, Mc, step):

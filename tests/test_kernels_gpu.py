@@ -758,3 +758,22 @@ def test_sae_decode_fp32_table(gpu):
     got = ops.sae_decode_sparse(acts.to(gpu), Wd.to(gpu), bd.to(gpu)).cpu()
     want = acts.double() @ Wd.double() + bd.double()
     _close(got, want.float(), atol=2e-5, rtol=1e-5)
+
+
+def test_slot_copy_matches_index_copy(gpu):
+    """ops.slot_copy (one-pass whole-slot KV copy, csrc/elementwise.hip) equals torch's index_select/index_copy_,
+    for all layers and for a layer sub-range with different source / destination layer offsets."""
+    from taboo_brittleness_amd import ops
+
+    torch.manual_seed(0)
+    src = torch.randn(5, 7, 2, 33, 16).to(torch.bfloat16).to(gpu)
+    for layers, src_layers in ((None, None), (range(1, 4), range(2, 5))):
+        dst = torch.randn(5, 9, 2, 33, 16).to(torch.bfloat16).to(gpu)
+        exp = dst.clone()
+        ds, ss = [0, 4, 8, 2], [6, 1, 1, 3]
+        L = range(5) if layers is None else layers
+        SL = L if src_layers is None else src_layers
+        for a, b in zip(L, SL):
+            exp[a].index_copy_(0, torch.tensor(ds, device=gpu), src[b].index_select(0, torch.tensor(ss, device=gpu)))
+        ops.slot_copy(dst, src, ds, ss, layers, src_layers)
+        assert torch.equal(dst, exp)
