@@ -61,7 +61,7 @@ void tb_gemm_skinny(const uint16_t* A, const uint16_t* W, uint16_t* C, int M, in
 // sae.hip
 void tb_head_merge(const float* part, int npart, const int32_t* tgt, const float* tgt_logit, int32_t* nxt,
                    float* nll_self, float* nll_tgt, float* lse, int M, int V, hipStream_t st);
-void tb_head_fused4(const uint16_t* A, const uint16_t* W, float* part, const uint16_t* ctab, const int32_t* tgt,
+void tb_head_fused4(const uint16_t* A, const uint16_t* W, float* part, float cap, const int32_t* tgt,
                     float* tgt_logit, int32_t* nxt, float* nll_self, float* nll_tgt, int M, int N, int K, hipStream_t st);
 void tb_gemm4_qkv_rope(const uint16_t* A, const uint16_t* W, const int32_t* pos, const int32_t* slot_of_row,
                        const float* cos_t, const float* sin_t, uint16_t* q_out, uint16_t* kc, uint16_t* vc, int M, int K,
@@ -115,3 +115,7 @@ int tb_p2p_allgather(void* const* bases, int rank, int world, const void* in, vo
                      int spin_max, int barriers, hipStream_t st);
 void tb_slot_copy(uint16_t* dst, const uint16_t* src, const int32_t* dslot, const int32_t* sslot, int n, int nl,
                   int64_t inner, int dst_slots, int src_slots, int dst_l0, int src_l0, hipStream_t st);
+void tb_lens_gemm4(const uint16_t* A, const uint16_t* W, uint16_t* logits, float* part, float* lse, int M, int N,
+                   int K, hipStream_t st);
+// the compact exact softcap registered for `cap` on this device (csrc/lens.hip CapC): table of [lo, hi), saturation
+bool tb_softcap_compact_params(float cap, const uint16_t** tab, int* lo, int* hi, float* sat);

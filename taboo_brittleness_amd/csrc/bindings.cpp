@@ -475,7 +475,7 @@ void gemm4_qkv_rope(torch::Tensor x, torch::Tensor w, torch::Tensor pos, torch::
                     (int)tile_rows, cur_stream());
 }
 
-// Logit-lens unembedding on the ping-pong GEMM (gemm.hip EPI_LENS): bf16 logits and their per-row
+// Logit-lens unembedding on the four-wave GEMM (gemm4.hip G4_LENS): bf16 logits and their per-row
 // log-sum-exp (no softcap), so the lens needs no separate row_lse pass.  part: f32 >= M * (V / 128) * 4.
 void lens_gemm(torch::Tensor x, torch::Tensor W, torch::Tensor logits, torch::Tensor part, torch::Tensor lse) {
   IN_BF16(x); IN_BF16(W); IN_BF16(logits); IN_F32(part); IN_F32(lse);
@@ -486,7 +486,7 @@ void lens_gemm(torch::Tensor x, torch::Tensor W, torch::Tensor logits, torch::Te
   TORCH_CHECK(logits.numel() == (int64_t)M * N, "lens_gemm: logits shape");
   TORCH_CHECK(part.numel() >= (int64_t)M * (N / 128) * 4 && lse.numel() == M, "lens_gemm: part / lse shapes");
   c10::DeviceGuard g(x.device());
-  tb_lens_gemm(cbf(x), cbf(W), bf(logits), part.data_ptr<float>(), lse.data_ptr<float>(), M, N, K, cur_stream());
+  tb_lens_gemm4(cbf(x), cbf(W), bf(logits), part.data_ptr<float>(), lse.data_ptr<float>(), M, N, K, cur_stream());
 }
 
 // Fused vocab head (gemm.hip EPI_HEAD + head_merge): x [M, K] final-normed rows, W = lm_head [V, K]; the
@@ -519,10 +519,19 @@ void head_fused(torch::Tensor x, torch::Tensor W, torch::Tensor part, double cap
     tab = tb_find_softcap_table((float)cap);
     TORCH_CHECK(tab != nullptr, "head_fused: softcap table for this cap not registered on this device");
   }
-  // kernel 4: the four-wave GEMM (gemm4.hip G4_HEAD), otherwise the ping-pong kernel (gemm.hip EPI_HEAD)
-  if (kernel == 4)
-    tb_head_fused4(cbf(x), cbf(W), part.data_ptr<float>(), tab, tp, tl, nxt.data_ptr<int32_t>(),
+  // kernel 4: the four-wave GEMM (gemm4.hip G4_HEAD, compact softcap), otherwise the ping-pong kernel (gemm.hip
+  // EPI_HEAD, 64 KB table)
+  if (kernel == 4) {
+    if (cap > 0) {
+      const uint16_t* ct = nullptr;
+      int lo = 0, hi = 0;
+      float sat = 0.f;
+      TORCH_CHECK(tb_softcap_compact_params((float)cap, &ct, &lo, &hi, &sat) && hi - lo <= 2048,
+                  "head_fused: no compact softcap registered for this cap on this device");
+    }
+    tb_head_fused4(cbf(x), cbf(W), part.data_ptr<float>(), (float)cap, tp, tl, nxt.data_ptr<int32_t>(),
                    nll_self.data_ptr<float>(), np, M, N, K, cur_stream());
+  }
   else
     tb_head_fused(cbf(x), cbf(W), part.data_ptr<float>(), tab, tp, tl, nxt.data_ptr<int32_t>(),
                   nll_self.data_ptr<float>(), np, M, N, K, cur_stream());

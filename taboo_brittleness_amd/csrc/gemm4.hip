@@ -116,7 +116,7 @@ __device__ __forceinline__ void g4_bar() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-enum { G4_BF16 = 0, G4_F32 = 1, G4_JUMPRELU = 2, G4_GEGLU = 3, G4_ROPE = 4, G4_HEAD = 5 };
+enum { G4_BF16 = 0, G4_F32 = 1, G4_JUMPRELU = 2, G4_GEGLU = 3, G4_ROPE = 4, G4_HEAD = 5, G4_LENS = 6 };
 
 // Fused QKV epilogue (G4_ROPE, SURVEY K3 + K4): the projection's bf16 output is never stored; each 256-column tile is
 // one head (head_dim 256): q heads are rotated into q_out [M, Hq, 256], k heads rotated and v heads copied into
@@ -131,12 +131,20 @@ struct G4Rope {
   uint16_t* kc;
   uint16_t* vc;
   int Hq, Hkv, S, max_pos;
-  // G4_HEAD (vocab head): bf16 logits -> exact bf16 final softcap by table (ctab, staged into the
-  // stage LDS after the K loop), per (row, 128-column wave slice) {max, sum exp(z - max), first argmax} into
-  // part[m * (N/128) + n/128]; the row's teacher-target logit into tgt_logit.  The logits never reach memory.
+  // G4_HEAD (vocab head): bf16 logits -> exact bf16 final softcap, per (row, 128-column wave slice)
+  // {max, sum exp(z - max), first argmax} into part[m * (N/128) + n/128]; the row's teacher-target logit into
+  // tgt_logit.  The logits never reach memory.  The softcap is the compact exact form of csrc/lens.hip (CapC):
+  // arithmetic below clo, the ctab[0, chi - clo) magnitudes in between (<= 4 KB, staged ONCE per workgroup into
+  // LDS beside the stages), saturated above chi -- no per-tile table staging, no extra barrier.
   const uint16_t* ctab;
+  int clo, chi;
+  float csat, crc, ccap;
   const int32_t* tgt;
   float* tgt_logit;
+  // G4_LENS (logit lens): the bf16 logits are stored (row-coalesced, as G4_BF16) AND each (row,
+  // 128-column wave slice) is reduced to {max, sum exp(z - max), first argmax} into part (G4_HEAD's layout,
+  // no softcap), so the row log-sum-exp needs no second pass over the logits (tb_head_merge folds the slices)
+  float* part;
 };
 constexpr int G4_CTAB_N = 32768;
 
@@ -152,11 +160,12 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
   constexpr int PI = G4_BN / 32, QI = BM / 32, GL = PI + QI;   // LDS-DMA instructions per wave and K tile
   // row-coalesced bf16 epilogue (see the tile's end): a wave's output rows are RB bytes (bf16: its 128 columns;
   // GeGLU: its 64 features), ERPI rows per 16-B-per-lane store, ERR rows per LDS round trip, ENR stores per lane
-  constexpr bool LEPI = EPI == G4_BF16 || (EPI == G4_GEGLU && G4_LDS_GEGLU);
+  constexpr bool LEPI = EPI == G4_BF16 || EPI == G4_LENS || (EPI == G4_GEGLU && G4_LDS_GEGLU);
   constexpr int RB = EPI == G4_GEGLU ? 128 : 256, ECH = RB / 16, ERPI = 64 / ECH;
   constexpr int ERR = EPI == G4_GEGLU ? BM / 2 : BM / 4;
   constexpr int ENR = LEPI ? (BM / 2) / ERPI : 1;
-  __shared__ __attribute__((aligned(1024))) char smem[2 * STG];
+  constexpr int CTB = EPI == G4_HEAD ? 4096 : 0;            // compact softcap table bytes (G4_HEAD)
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STG + CTB];   // one array: glds trap (a)
 
   const int nbn = N / G4_BN, nbm = (M + BM - 1) / BM, nwg = nbn * nbm;
   // Persistent: this workgroup runs the virtual tiles blockIdx.x, blockIdx.x + gridDim.x, ...  A virtual id v keeps
@@ -264,6 +273,13 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
   static_assert(GSP >= 1 && BAR1 < NMF && BAR1 < BAR2, "schedule");
 
   const int nt = K >> 6;
+  if constexpr (EPI == G4_HEAD) {
+    if (rp.ctab != nullptr) {
+      uint16_t* lt = reinterpret_cast<uint16_t*>(smem + 2 * STG);
+      for (int i = tid; i < rp.chi - rp.clo; i += G4_THREADS) lt[i] = rp.ctab[i];
+    }
+    __syncthreads();
+  }
   // prologue of the first tile: K tiles 0 and 1 in flight
   G4_STAGE(0, 0);
   G4_STAGE(min(1, nt - 1), 1);
@@ -438,21 +454,11 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
     tile = next;
     G4_TILE(tile, m0, n0);
     G4_DESC();
-    if constexpr (EPI != G4_HEAD) {
-      G4_STAGE(0, 0);
-      G4_STAGE(min(1, nt - 1), 1);
-    }
+    G4_STAGE(0, 0);
+    G4_STAGE(min(1, nt - 1), 1);
   }
-  const uint16_t* ct = nullptr;
-  if constexpr (EPI == G4_HEAD) {
-    if (rp.ctab != nullptr) {
-      uint16_t* ctw = reinterpret_cast<uint16_t*>(smem);
-      for (int i = tid; i < G4_CTAB_N / 8; i += G4_THREADS)
-        reinterpret_cast<uint4*>(ctw)[i] = reinterpret_cast<const uint4*>(rp.ctab)[i];
-      ct = ctw;
-      __syncthreads();
-    }
-  }
+  const uint16_t* ct = (EPI == G4_HEAD && rp.ctab != nullptr) ? reinterpret_cast<const uint16_t*>(smem + 2 * STG)
+                                                               : nullptr;
 #if G4_ASM_MFMA
   if constexpr (!LEPI) asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");   // last MFMA's D -> the accumulator reads
 #endif
@@ -461,9 +467,9 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
   {
   const int nb = en0 + wn * 128 + 4 * (lane >> 4);
   const int mb = em0 + wm * (BM / 2) + (lane & 15);
-  if constexpr (EPI == G4_HEAD) {
+  if constexpr (EPI == G4_HEAD || EPI == G4_LENS) {
     // lane: columns nb + 16 i + r (i < 8, r < 4) of rows mb + 16 j; the 4 lanes lane&15 + 16 q share a row
-    float4* part = reinterpret_cast<float4*>(C);
+    float4* part = reinterpret_cast<float4*>(EPI == G4_LENS ? rp.part : reinterpret_cast<float*>(C));
     const int npart = N / 128, pcol = (en0 >> 7) + wn;
 #pragma unroll
     for (int j = 0; j < WM; ++j) {
@@ -477,8 +483,15 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const uint32_t b = f2bf(acc[i][j][r]);
-          const float v = ct != nullptr ? __uint_as_float(((uint32_t)ct[b & 0x7fffu] | (b & 0x8000u)) << 16)
-                                        : __uint_as_float(b << 16);
+          float v = __uint_as_float(b << 16);
+          if (ct != nullptr) {   // compact exact softcap (csrc/lens.hip capc1)
+            const uint32_t ab = b & 0x7fffu;
+            if (ab < (uint32_t)rp.clo) v = rbf(rbf(v * rp.crc) * rp.ccap);
+            else if (ab <= 0x7f80u) {
+              const float mag = ab < (uint32_t)rp.chi ? __uint_as_float((uint32_t)ct[ab - rp.clo] << 16) : rp.csat;
+              v = (b & 0x8000u) ? -mag : mag;
+            }
+          }
           const int n = nb + i * 16 + r;
           z[i * 4 + r] = v;
           if (v > mx || (v == mx && n < bi)) { mx = v; bi = n; }
@@ -589,11 +602,6 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
   }
   }
   if (next >= nwg) break;
-  if constexpr (EPI == G4_HEAD) {   // every wave is done with the table: the next tile's first K tiles
-    __syncthreads();
-    G4_STAGE(0, 0);
-    G4_STAGE(min(1, nt - 1), 1);
-  }
 #pragma unroll
   for (int i = 0; i < WN; ++i)
 #pragma unroll
@@ -652,7 +660,7 @@ void tb_gemm4(const uint16_t* A, const uint16_t* W, void* C, const float* bias, 
 #undef G4_EPI
 }
 
-void tb_head_fused4(const uint16_t* A, const uint16_t* W, float* part, const uint16_t* ctab, const int32_t* tgt,
+void tb_head_fused4(const uint16_t* A, const uint16_t* W, float* part, float cap, const int32_t* tgt,
                     float* tgt_logit, int32_t* nxt, float* nll_self, float* nll_tgt, int M, int N, int K, hipStream_t st) {
   if (M <= 0) return;
   void* C = part;
@@ -660,11 +668,37 @@ void tb_head_fused4(const uint16_t* A, const uint16_t* W, float* part, const uin
   const float* thr = nullptr;
   const int ldc = 0;
   G4Rope rp{};
-  rp.ctab = ctab;
+  if (cap > 0.f) {
+    const uint16_t* ct = nullptr;
+    int lo = 0, hi = 0;
+    float sat = 0.f;
+    if (!tb_softcap_compact_params(cap, &ct, &lo, &hi, &sat) || hi - lo > 2048) return;   // host-checked
+    rp.ctab = ct;
+    rp.clo = lo;
+    rp.chi = hi;
+    rp.csat = sat;
+    rp.crc = 1.0f / cap;
+    rp.ccap = cap;
+  }
   rp.tgt = tgt;
   rp.tgt_logit = tgt_logit;
   G4_GO(256, G4_HEAD);
   tb_head_merge(reinterpret_cast<const float*>(part), N / 128, tgt, tgt_logit, nxt, nll_self, nll_tgt, nullptr, M, N, st);
+}
+
+// Logit-lens unembedding: bf16 logits [M, N] (no softcap) and the row log-sum-exp, with no second
+// pass over the logits: G4_LENS's per-slice {max, sum exp} partials folded by tb_head_merge.
+void tb_lens_gemm4(const uint16_t* A, const uint16_t* W, uint16_t* logits, float* part, float* lse, int M, int N,
+                   int K, hipStream_t st) {
+  if (M <= 0) return;
+  void* C = logits;
+  const float* bias = nullptr;
+  const float* thr = nullptr;
+  const int ldc = N;
+  G4Rope rp{};
+  rp.part = part;
+  G4_GO(256, G4_LENS);
+  tb_head_merge(part, N / 128, nullptr, nullptr, nullptr, nullptr, nullptr, lse, M, N, st);
 }
 
 void tb_gemm4_qkv_rope(const uint16_t* A, const uint16_t* W, const int32_t* pos, const int32_t* slot_of_row,

@@ -727,6 +727,16 @@ bool tb_register_softcap_compact(float cap, const uint16_t* tab, int lo, int hi,
   return true;
 }
 
+bool tb_softcap_compact_params(float cap, const uint16_t** tab, int* lo, int* hi, float* sat) {
+  const CapC* c = find_capc(cap);
+  if (c == nullptr) return false;
+  *tab = c->tab;
+  *lo = c->lo;
+  *hi = c->hi;
+  *sat = c->sat;
+  return true;
+}
+
 bool tb_softcap_compact(const uint16_t* x, float* y, int n, float cap, hipStream_t st) {
   const CapC* c = find_capc(cap);
   if (c == nullptr || n <= 0) return c != nullptr;

@@ -452,7 +452,7 @@ def head_part_numel(rows: int, vocab: int) -> int:
     return rows * (vocab // 128) * 4
 
 
-HEAD_KERNEL = 4 if os.environ.get("TB_HEAD_KERNEL", "pp") == "g4" else 0   # fused head GEMM: gemm.hip (default) | gemm4.hip
+HEAD_KERNEL = 4 if os.environ.get("TB_HEAD_KERNEL", "g4") == "g4" else 0   # fused head GEMM: gemm4.hip (default) | gemm.hip
 
 
 def vocab_head(x, w, cap, tgt=None, nxt=None, nll_self=None, nll_tgt=None, part=None, tgt_logit=None,
@@ -484,7 +484,7 @@ def vocab_head(x, w, cap, tgt=None, nxt=None, nll_self=None, nll_tgt=None, part=
     return decode_head(linear(x, w), cap, tgt, nxt, nll_self, nll_tgt)
 
 
-FUSED_LENS = os.environ.get("TB_FUSED_LENS", "0") == "1"   # -0.6 % in the bench (profiles/r2/lens): opt-in
+FUSED_LENS = os.environ.get("TB_FUSED_LENS", "1") == "1"   # gemm4 G4_LENS (round 4); 0: hipBLASLt + row_lse
 
 
 def lens_unembed(xn, w, fused: Optional[bool] = None, out=None):

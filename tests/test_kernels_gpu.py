@@ -318,10 +318,11 @@ def test_vocab_head_fused(gpu, M, V, K, cap, kernel, monkeypatch):
     assert t2 is None and torch.equal(n2, nxt) and torch.equal(s2, ns)
 
 
-@pytest.mark.parametrize("M,V,K", [(300, 4096, 256), (37, 2048, 3584)])
+@pytest.mark.parametrize("M,V,K", [(300, 4096, 256), (37, 2048, 3584), (600, 65536, 512)])
 def test_lens_unembed_fused(gpu, M, V, K):
-    """Logit-lens unembedding with the LSE epilogue (csrc/gemm.hip EPI_LENS): logits bit-identical to the same
-    kernel's plain bf16 output, lse == row_lse of them, both close to a float32 reference."""
+    """Logit-lens unembedding with the LSE epilogue (csrc/gemm4.hip G4_LENS, row-coalesced logits + per-slice
+    {max, sum exp}): logits bit-identical to the in-tree kernels' plain bf16 output, lse == row_lse of them, both
+    close to a float32 reference (the last shape runs several tiles per persistent workgroup)."""
     torch.manual_seed(19)
     x = torch.randn(M, K).to(BF)
     w = (torch.randn(V, K) * 0.05).to(BF)

@@ -1,6 +1,8 @@
-"""A/B of the vocab head at Gemma-2-9B shapes (V = 256000, K = 3584): hipBLASLt logits + decode_head vs the
-fused ping-pong GEMM head (csrc/gemm.hip EPI_HEAD + head_merge), interleaved rounds in one process
-(cdna_hip_programming.md §5.4 rule 24), random data.  Prints one JSON line per M.
+"""A/B of the vocab head and the logit-lens unembedding at Gemma-2-9B shapes (V = 256000, K = 3584):
+hipBLASLt logits + decode_head vs the fused GEMM head (ops.HEAD_KERNEL: csrc/gemm4.hip G4_HEAD by default), and
+hipBLASLt logits + row_lse vs the fused lens GEMM (csrc/gemm4.hip G4_LENS), interleaved rounds in one process
+(cdna_hip_programming.md §5.4 rule 24), random data.  Run with TB_GEMM=blas so ``linear`` is hipBLASLt.
+Prints one JSON line per M.
 
     python tools/head_bench.py [--rows 256 2048 4096] [--rounds 5]
 """
@@ -56,16 +58,24 @@ def main() -> None:
         def gemm_only():
             ops.linear(x, w, out=lg)
 
+        def lens_unfused():
+            ops.lens_unembed(x, w, fused=False, out=lg)
+
+        def lens_fused():
+            ops.lens_unembed(x, w, fused=True, out=lg)
+
         unfused(); fused(); torch.cuda.synchronize()
         a = ops.vocab_head(x, w, cap, tgt, fused=False)
         b = ops.vocab_head(x, w, cap, tgt, fused=True)
         agree = float((a[0] == b[0]).float().mean())
         dn = float((a[2] - b[2]).abs().max())
-        res = {"unfused": [], "fused": [], "gemm_only": []}
+        res = {"unfused": [], "fused": [], "gemm_only": [], "lens_unfused": [], "lens_fused": []}
         for _ in range(args.rounds):
             res["unfused"].append(timed(unfused, args.reps))
             res["fused"].append(timed(fused, args.reps))
             res["gemm_only"].append(timed(gemm_only, args.reps))
+            res["lens_unfused"].append(timed(lens_unfused, args.reps))
+            res["lens_fused"].append(timed(lens_fused, args.reps))
         med = {k: sorted(v)[len(v) // 2] for k, v in res.items()}
         tf = 2.0 * M * V * K / 1e12
         print(json.dumps({"M": M, "us_median": {k: round(v, 1) for k, v in med.items()},
@@ -73,6 +83,7 @@ def main() -> None:
                           "tflops_fused": round(tf / (med["fused"] * 1e-6), 1),
                           "tflops_hipblaslt_gemm": round(tf / (med["gemm_only"] * 1e-6), 1),
                           "speedup_fused_vs_unfused": round(med["unfused"] / med["fused"], 3),
+                          "speedup_lens_fused_vs_unfused": round(med["lens_unfused"] / med["lens_fused"], 3),
                           "argmax_agree_vs_hipblaslt": agree, "max_abs_dnll_tgt": dn}), flush=True)
 
 
