@@ -195,7 +195,11 @@ def qkv_rope_fused_ok(x: torch.Tensor, wqkv: torch.Tensor, HD: int) -> bool:
     M = x.numel() // K
     if M <= 0 or not _k().gemm4_ok(M, wqkv.shape[0], K):
         return False
-    return FUSED_QKV == "1" or _GD.choose(M, wqkv.shape[0], K, 0) != "blas"
+    if FUSED_QKV == "1":
+        return True
+    # the measured fused-vs-(hipBLASLt + rope_qkv_cache) table (key epilogue 4) when present, else the plain QKV
+    c = _GD.choose(M, wqkv.shape[0], K, 4) if _GD.has_entry(wqkv.shape[0], K, 4) else _GD.choose(M, wqkv.shape[0], K, 0)
+    return c != "blas"
 
 
 def qkv_rope_cache(x, wqkv, pos, slot_of_row, cos_t, sin_t, kc, vc, Hq, Hkv, HD, q_out=None, qkv_ws=None):
@@ -205,7 +209,7 @@ def qkv_rope_cache(x, wqkv, pos, slot_of_row, cos_t, sin_t, kc, vc, Hq, Hkv, HD,
     if qkv_rope_fused_ok(x, wqkv, HD):
         M = pos.numel()
         q_out = _out(q_out, (M, Hq, HD), x.dtype, x.device)
-        c = _GD.choose(M, wqkv.shape[0], x.shape[-1], 0)
+        c = _GD.choose(M, wqkv.shape[0], x.shape[-1], 4 if _GD.has_entry(wqkv.shape[0], x.shape[-1], 4) else 0)
         rows = int(str(c).lstrip("g")) if c != "blas" else int(str(_GD.fill_choice(M, wqkv.shape[0])).lstrip("g"))
         _k().gemm4_qkv_rope(x, wqkv, pos, slot_of_row, cos_t, sin_t, q_out, kc, vc, int(Hq), int(Hkv), rows)
         return q_out

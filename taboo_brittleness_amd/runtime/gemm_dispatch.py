@@ -96,6 +96,15 @@ def choose(M: int, N: int, K: int, epi: int = 0) -> Choice:
     return "blas"
 
 
+def has_entry(N: int, K: int, epi: int) -> bool:
+    """Whether the loaded dispatch table measured ``(N, K, epi)`` (auto mode)."""
+    if _state["mode"] != "auto":
+        return False
+    if not _state["loaded"]:
+        load_table()
+    return _state["table"] is not None and (N, K, epi) in _state["table"]
+
+
 def describe() -> dict:
     return {"mode": _state["mode"], "kernel": _state["kernel"],
             "table": os.path.relpath(_state["table_path"], REPO) if _state["table_path"] else None}

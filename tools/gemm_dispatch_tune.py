@@ -4,7 +4,8 @@ table) on every projection shape of the Gemma-2-9B step and write the per-shape 
 
 Shapes: the five projections (QKV, o, gate|up, down, lm_head / lens) at every row count M the bench's
 TunableOp table holds (its decode row buckets) plus a standard grid; gate|up also as the fused GeGLU
-epilogue vs hipBLASLt + the GeGLU kernel.  Operands are uniform random bf16 (never zeros: DVFS), the weight
+epilogue vs hipBLASLt + the GeGLU kernel (key epi 3), QKV also as the fused QKV + RoPE + KV-cache scatter
+(csrc/gemm4.hip G4_ROPE) vs hipBLASLt + rope_qkv_cache (key epi 4).  Operands are uniform random bf16 (never zeros: DVFS), the weight
 is rotated over copies larger than the Infinity Cache (decode streams every weight from HBM), variants are
 interleaved in rounds inside one process (cdna_hip_programming.md §5.4 rule 24), median of the rounds.
 
@@ -25,6 +26,7 @@ sys.path.insert(0, ROOT)
 
 from taboo_brittleness_amd import ops  # noqa: E402
 from taboo_brittleness_amd.ops import _ext  # noqa: E402
+from taboo_brittleness_amd.ops import reference as ref  # noqa: E402
 from taboo_brittleness_amd.runtime.tuning import enable_tuned_gemms, gemm_results_path  # noqa: E402
 
 SHAPES = {"qkv": (8192, 3584), "o": (3584, 4096), "gu": (28672, 3584), "down": (3584, 14336), "head": (256000, 3584)}
@@ -90,7 +92,7 @@ def main():
         if name == "gu":
             idx = ops.geglu_interleave_index(N // 2, dev)
             Wi = [w.index_select(0, idx).contiguous() for w in Ws]
-        for epi in ([0, 3] if name == "gu" else [0]):
+        for epi in ([0, 3] if name == "gu" else [0, 4] if name == "qkv" else [0]):
             rows = []
             for M in Ms:
                 A = (torch.rand(M, K, device=dev, generator=g) * 2 - 1).to(torch.bfloat16)
@@ -103,15 +105,34 @@ def main():
                     it[0] = (it[0] + 1) % len(ws)
                     return ws[it[0]]
 
-                if epi == 0:
+                if epi == 4:
+                    # QKV at the Gemma-2-9B head layout into a layer's KV cache (positions < S, slots < M)
+                    Hq, Hkv, HD, S = 16, 8, 256, 512
+                    nslot = min(M, 256)
+                    pos = torch.randint(0, S, (M,), device=dev, dtype=torch.int32)
+                    slot = (torch.arange(M, device=dev, dtype=torch.int32) % nslot).contiguous()
+                    cos_t, sin_t = ref.rope_tables(HD, 8192, 10000.0, dev)
+                    cos_t, sin_t = cos_t.contiguous(), sin_t.contiguous()
+                    kc = torch.zeros(nslot, Hkv, S, HD, device=dev, dtype=torch.bfloat16)
+                    vc = torch.zeros_like(kc)
+                    q = torch.empty(M, Hq, HD, device=dev, dtype=torch.bfloat16)
+
+                    def blas_rope():
+                        torch.matmul(A, nxt(Ws).t(), out=C)
+                        ops.rope_qkv_cache(C, pos, slot, cos_t, sin_t, kc, vc, Hq, Hkv, HD, q_out=q)
+                    var = {"blas": blas_rope}
+                    for ch in [c_ for c_ in args.kernels.split(",") if c_.startswith("g")]:
+                        var[ch] = (lambda r_: lambda: k.gemm4_qkv_rope(A, nxt(Ws), pos, slot, cos_t, sin_t, q, kc, vc,
+                                                                       Hq, Hkv, r_))(int(ch[1:]))
+                elif epi == 0:
                     var = {"blas": lambda: torch.matmul(A, nxt(Ws).t(), out=C)}
                 else:
                     def blas_geglu():
                         torch.matmul(A, nxt(Ws).t(), out=G)
                         ops.geglu(G, out=C)
                     var = {"blas": blas_geglu}
-                wsrc = Ws if epi == 0 else Wi
-                for ch in args.kernels.split(","):
+                wsrc = Wi if epi == 3 else Ws
+                for ch in (args.kernels.split(",") if epi != 4 else []):
                     ch = ch if ch.startswith("g") else int(ch)
                     var[ch] = (lambda ch_: lambda: ops.tb_gemm(A, nxt(wsrc), C, None, None, epi, ch_))(ch)
                 for f in var.values():      # warm-up (and TunableOp lookups)
