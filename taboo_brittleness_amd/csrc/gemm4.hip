@@ -100,6 +100,15 @@ template <int OFF>
 __device__ __forceinline__ void g4_ds_read_b128(u32x4& d, uint32_t a) {
   asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(a), "n"(OFF) : "memory");
 }
+// G4_HEAD's softcap-table reads: asm (a compiler-visible LDS read would get a vmcnt(0) in front of it, i.e. wait for
+// the next tile's LDS-DMA) and held by g4_lgkm_hold4 so no use is scheduled before its wait
+__device__ __forceinline__ void g4_ds_read_u16(uint32_t& d, uint32_t a) {
+  asm volatile("ds_read_u16 %0, %1" : "=v"(d) : "v"(a));
+}
+template <int N>
+__device__ __forceinline__ void g4_lgkm_hold4(uint32_t (&t)[4]) {
+  asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]) : "n"(N));
+}
 template <typename F, int... I>
 __device__ __forceinline__ void g4_unroll_seq(F&& f, std::integer_sequence<int, I...>) {
   (f(std::integral_constant<int, I>{}), ...);
@@ -450,6 +459,20 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
     g4_bar();   // every wave's rows are out of stage 1
     if (next < nwg) G4_STAGE(min(1, nt - 1), 1);
   }
+  // G4_HEAD: the rows' teacher targets, loaded before the next tile's LDS-DMA is issued (their wait then leaves
+  // that DMA in flight)
+  int tj[EPI == G4_HEAD ? WM : 1];
+  if constexpr (EPI == G4_HEAD) {
+#pragma unroll
+    for (int j = 0; j < WM; ++j) {
+      const int m = em0 + wm * (BM / 2) + (lane & 15) + j * 16;
+      tj[j] = -1;
+      if (rp.tgt != nullptr) {
+        const int t = rp.tgt[min(m, M - 1)];
+        tj[j] = m < M ? t : -1;
+      }
+    }
+  }
   if (!LEPI && next < nwg) {
     tile = next;
     G4_TILE(tile, m0, n0);
@@ -457,8 +480,7 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
     G4_STAGE(0, 0);
     G4_STAGE(min(1, nt - 1), 1);
   }
-  const uint16_t* ct = (EPI == G4_HEAD && rp.ctab != nullptr) ? reinterpret_cast<const uint16_t*>(smem + 2 * STG)
-                                                               : nullptr;
+  const uint16_t* ct = reinterpret_cast<const uint16_t*>(smem + 2 * STG);   // G4_HEAD's softcap table
 #if G4_ASM_MFMA
   if constexpr (!LEPI) asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");   // last MFMA's D -> the accumulator reads
 #endif
@@ -471,42 +493,76 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
     // lane: columns nb + 16 i + r (i < 8, r < 4) of rows mb + 16 j; the 4 lanes lane&15 + 16 q share a row
     float4* part = reinterpret_cast<float4*>(EPI == G4_LENS ? rp.part : reinterpret_cast<float*>(C));
     const int npart = N / 128, pcol = (en0 >> 7) + wn;
+    // branch-free: every element takes the same instruction path (selects, one table read), the table reads run
+    // 2 fragments ahead of their use, the target logit is stored once per row
+    const uint32_t ctb = (uint32_t)(uintptr_t)((g4_lds_char*)smem) + 2 * STG;
+    constexpr float L2E = 1.4426950408889634f;
 #pragma unroll
     for (int j = 0; j < WM; ++j) {
       const int m = mb + j * 16;
-      const int t = (rp.tgt != nullptr && m < M) ? rp.tgt[m] : -1;
+      uint32_t bq[WN][4], tq[WN][4];
+#pragma unroll
+      for (int i = 0; i < WN; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bq[i][r] = f2bf(acc[i][j][r]);
+      if constexpr (EPI == G4_HEAD) {
+        auto rd = [&](auto ic) {
+          constexpr int i = decltype(ic)::value;
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            g4_ds_read_u16(tq[i][r], ctb + 2 * min(max((int)(bq[i][r] & 0x7fffu) - rp.clo, 0), rp.chi - rp.clo - 1));
+        };
+        rd(std::integral_constant<int, 0>{});
+        rd(std::integral_constant<int, 1>{});
+        g4_unroll<WN>([&](auto ic) {
+          constexpr int i = decltype(ic)::value;
+          if constexpr (i + 2 < WN) rd(std::integral_constant<int, i + 2>{});
+          g4_lgkm_hold4<4 * (WN - 1 - i < 2 ? WN - 1 - i : 2)>(tq[i]);
+        });
+      }
       float z[WN * 4];
-      float mx = -INFINITY;
-      int bi = 0x7fffffff;
+      float mx = -INFINITY, tl = 0.f;
+      int bi = nb;
 #pragma unroll
       for (int i = 0; i < WN; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const uint32_t b = f2bf(acc[i][j][r]);
+          const uint32_t b = bq[i][r];
           float v = __uint_as_float(b << 16);
-          if (ct != nullptr) {   // compact exact softcap (csrc/lens.hip capc1)
+          if constexpr (EPI == G4_HEAD) {   // compact exact softcap (csrc/lens.hip capc1); NaN passes through
             const uint32_t ab = b & 0x7fffu;
-            if (ab < (uint32_t)rp.clo) v = rbf(rbf(v * rp.crc) * rp.ccap);
-            else if (ab <= 0x7f80u) {
-              const float mag = ab < (uint32_t)rp.chi ? __uint_as_float((uint32_t)ct[ab - rp.clo] << 16) : rp.csat;
-              v = (b & 0x8000u) ? -mag : mag;
-            }
+            const float mag = ab < (uint32_t)rp.chi ? __uint_as_float(tq[i][r] << 16) : rp.csat;
+            const float cp = __uint_as_float(__float_as_uint(mag) | (b & 0x8000u) << 16);
+            const float ln = rbf(rbf(v * rp.crc) * rp.ccap);
+            v = ab < (uint32_t)rp.clo ? ln : (ab <= 0x7f80u ? cp : v);
           }
           const int n = nb + i * 16 + r;
           z[i * 4 + r] = v;
-          if (v > mx || (v == mx && n < bi)) { mx = v; bi = n; }
-          if (n == t) rp.tgt_logit[m] = v;
+          if constexpr (EPI == G4_HEAD) {
+            if (v > mx) { mx = v; bi = n; }   // the lane's columns ascend: the first maximum stays
+            tl = n == tj[j] ? v : tl;
+          } else {
+            mx = fmaxf(mx, v);                // G4_LENS: no argmax (the lens needs the row LSE only)
+          }
         }
+      if constexpr (EPI == G4_HEAD) {
+        const int d = tj[j] - nb;
+        if (d >= 0 && d < WN * 16 && (d & 15) < 4) rp.tgt_logit[m] = tl;
+      }
+      const float mxl = mx * L2E;
       float sum = 0.f;
 #pragma unroll
-      for (int e = 0; e < WN * 4; ++e) sum += __expf(z[e] - mx);
+      for (int e = 0; e < WN * 4; ++e) sum += __builtin_amdgcn_exp2f(fmaf(z[e], L2E, -mxl));
 #pragma unroll
-      for (int o = 16; o <= 32; o <<= 1) {
+      for (int o = 16; o <= 32; o <<= 1) {   // the 4 lanes of a row; ties keep the lower column
         const float m2 = __shfl_xor(mx, o, 64), s2 = __shfl_xor(sum, o, 64);
-        const int i2 = __shfl_xor(bi, o, 64);
-        if (m2 > mx) { sum = sum * __expf(mx - m2) + s2; mx = m2; bi = i2; }
-        else if (m2 == mx) { sum += s2; bi = min(bi, i2); }
-        else { sum += s2 * __expf(m2 - mx); }
+        const float nm = fmaxf(mx, m2);
+        sum = sum * __builtin_amdgcn_exp2f((mx - nm) * L2E) + s2 * __builtin_amdgcn_exp2f((m2 - nm) * L2E);
+        if constexpr (EPI == G4_HEAD) {
+          const int i2 = __shfl_xor(bi, o, 64);
+          bi = m2 > mx ? i2 : (m2 == mx ? min(bi, i2) : bi);
+        }
+        mx = nm;
       }
       if (lane < 16 && m < M) part[(size_t)m * npart + pcol] = make_float4(mx, sum, __int_as_float(bi), 0.f);
     }
@@ -679,6 +735,10 @@ void tb_head_fused4(const uint16_t* A, const uint16_t* W, float* part, float cap
     rp.csat = sat;
     rp.crc = 1.0f / cap;
     rp.ccap = cap;
+  } else {            // no softcap: every finite value takes the (identity) arithmetic branch
+    rp.clo = 0x7f81;
+    rp.chi = 0x7f82;
+    rp.crc = rp.ccap = 1.f;
   }
   rp.tgt = tgt;
   rp.tgt_logit = tgt_logit;
