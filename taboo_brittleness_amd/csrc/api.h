@@ -69,6 +69,9 @@ void tb_gemm4_qkv_rope(const uint16_t* A, const uint16_t* W, const int32_t* pos,
 bool tb_register_softcap_compact(float cap, const uint16_t* tab, int lo, int hi, float sat);
 bool tb_softcap_compact(const uint16_t* x, float* y, int n, float cap, hipStream_t st);
 bool tb_gemm4_ok(int M, int N, int K);
+int tb_gemm4_splitk_ks(int M, int N, int K, int tile_rows);
+void tb_gemm4_splitk(const uint16_t* A, const uint16_t* W, uint16_t* out, float* ws, int M, int N, int K, int ldo,
+                     int epi, int tile_rows, int ks, hipStream_t st);
 void tb_gemm4(const uint16_t* A, const uint16_t* W, void* C, const float* bias, const float* thr, int M, int N, int K,
               int ldc, int epi, int tile_rows, hipStream_t st);
 bool tb_gemm_pp_ok(int M, int N, int K);

@@ -452,6 +452,30 @@ void gemm4(torch::Tensor A, torch::Tensor W, torch::Tensor C, c10::optional<torc
 
 bool gemm4_ok(int64_t M, int64_t N, int64_t K) { return tb_gemm4_ok(M, N, K); }
 
+// Split-K gemm4 (thin grids): fp32 partials of ks K ranges into ws, then the ordered reduction into C (bf16 [M, N], or
+// the GeGLU [M, N/2] of the interleaved gate|up rows for epi 3).  ks <= 0: the launcher's heuristic.
+int64_t gemm4_splitk_ks(int64_t M, int64_t N, int64_t K, int64_t tile_rows) {
+  return tb_gemm4_splitk_ks(M, N, K, tile_rows);
+}
+void gemm4_splitk(torch::Tensor A, torch::Tensor W, torch::Tensor C, torch::Tensor ws, int64_t epi, int64_t tile_rows,
+                  int64_t ks) {
+  IN_BF16(A); IN_BF16(W); IN_BF16(C); IN_F32(ws);
+  TORCH_CHECK(W.dim() == 2, "gemm4_splitk: W must be [N, K]");
+  TORCH_CHECK(tile_rows == 256 || tile_rows == 128, "gemm4_splitk: tile_rows must be 256 or 128");
+  const int K = A.size(-1), M = A.numel() / K, N = W.size(0);
+  TORCH_CHECK(W.size(1) == K, "gemm4_splitk: K mismatch");
+  TORCH_CHECK(tb_gemm4_ok(M, N, K), "gemm4_splitk: need N % 256 == 0, K % 64 == 0, K >= 64");
+  TORCH_CHECK(epi == 0 || epi == 3, "gemm4_splitk: epi must be 0 (bf16) or 3 (GeGLU)");
+  const int64_t ncols = epi == 3 ? N / 2 : N;
+  TORCH_CHECK(C.numel() == (int64_t)M * ncols, "gemm4_splitk: C shape");
+  if (ks <= 0) ks = tb_gemm4_splitk_ks(M, N, K, tile_rows);
+  const int NT = K / 64, kc = (NT + (int)ks - 1) / (int)ks, kse = (NT + kc - 1) / kc;
+  TORCH_CHECK(ws.numel() >= (int64_t)kse * M * N, "gemm4_splitk: ws needs ks * M * N floats");
+  c10::DeviceGuard g(A.device());
+  tb_gemm4_splitk(cbf(A), cbf(W), reinterpret_cast<uint16_t*>(C.data_ptr()), ws.data_ptr<float>(), M, N, K, (int)ncols,
+                  (int)epi, (int)tile_rows, (int)ks, cur_stream());
+}
+
 // QKV projection with RoPE + KV-cache scatter in the epilogue (gemm4.hip G4_ROPE): x [M, K] @ wqkv [(Hq+2Hkv)*256, K]^T;
 // the same outputs as linear + rope_qkv_cache (head_dim 256 only), the qkv activation never reaches memory.
 void gemm4_qkv_rope(torch::Tensor x, torch::Tensor w, torch::Tensor pos, torch::Tensor slot_of_row, torch::Tensor cos_t,
@@ -768,6 +792,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_pp_ok", &gemm_pp_ok);
   m.def("gemm4", &gemm4);
   m.def("gemm4_ok", &gemm4_ok);
+  m.def("gemm4_splitk", &gemm4_splitk);
+  m.def("gemm4_splitk_ks", &gemm4_splitk_ks);
   m.def("gemm4_qkv_rope", &gemm4_qkv_rope);
   m.def("head_fused", &head_fused);
   m.def("lens_gemm", &lens_gemm);

@@ -154,6 +154,9 @@ struct G4Rope {
   // 128-column wave slice) is reduced to {max, sum exp(z - max), first argmax} into part (G4_HEAD's layout,
   // no softcap), so the row log-sum-exp needs no second pass over the logits (tb_head_merge folds the slices)
   float* part;
+  // split-K (G4_F32 only, tb_gemm4_splitk): the K tiles are cut into ksplit ranges of kchunk tiles; virtual tile v is
+  // (split v / nwg, output tile v % nwg) and split s writes its fp32 partial tile to C + s * M * ldc
+  int ksplit, kchunk;
 };
 constexpr int G4_CTAB_N = 32768;
 
@@ -177,19 +180,23 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
   __shared__ __attribute__((aligned(1024))) char smem[2 * STG + CTB];   // one array: glds trap (a)
 
   const int nbn = N / G4_BN, nbm = (M + BM - 1) / BM, nwg = nbn * nbm;
+  const int NT = K >> 6, KS = EPI == G4_F32 && rp.ksplit > 1 ? rp.ksplit : 1, KC = KS > 1 ? rp.kchunk : NT;
+  const int nwgv = nwg * KS;   // virtual tiles (x K splits)
   // Persistent: this workgroup runs the virtual tiles blockIdx.x, blockIdx.x + gridDim.x, ...  A virtual id v keeps
   // v % 8 = blockIdx.x % 8 (gridDim.x is a multiple of 8), i.e. the XCD the workgroup runs on; the bijective
   // remap (T1) gives each XCD a contiguous range of tiles, grouped GROUP_M tile rows deep (shared A / W panels).
 #define G4_TILE(v, m0_, n0_)                                                                              \
   do {                                                                                                    \
-    const int q_ = nwg / 8, r_ = nwg % 8, x_ = (v) % 8;                                                   \
-    const int b_ = (x_ < r_ ? x_ * (q_ + 1) : r_ * (q_ + 1) + (x_ - r_) * q_) + (v) / 8;                  \
+    const int q_ = nwgv / 8, r_ = nwgv % 8, x_ = (v) % 8;                                                 \
+    int b_ = (x_ < r_ ? x_ * (q_ + 1) : r_ * (q_ + 1) + (x_ - r_) * q_) + (v) / 8;                        \
+    sk = b_ / nwg;                                                                                        \
+    b_ -= sk * nwg;                                                                                       \
     const int pg_ = G4_GROUP_M * nbn, fb_ = (b_ / pg_) * G4_GROUP_M;                                      \
     const int gs_ = min(nbm - fb_, G4_GROUP_M), l_ = b_ % pg_;                                            \
     m0_ = (fb_ + l_ % gs_) * BM;                                                                          \
     n0_ = (l_ / gs_) * G4_BN;                                                                             \
   } while (0)
-  int tile = blockIdx.x, m0, n0;
+  int tile = blockIdx.x, m0, n0, sk;
   G4_TILE(tile, m0, n0);
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -203,13 +210,14 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
   uint32_t vp[PI], vq[QI];
 #pragma unroll
   for (int i = 0; i < PI; ++i) vp[i] = (uint32_t)((8 * (4 * i + wid) + (lane >> 3)) * K + lchunk * 8) * 2u;
-  int mrows, abytes;
+  int mrows, abytes, nt;
   void *wtile, *atile;
 #define G4_DESC()                                                                                 \
   do {                                                                                            \
     mrows = min(BM, M - m0);                                                                      \
-    wtile = (void*)(W + (size_t)n0 * K);                                                          \
-    atile = (void*)(A + (size_t)m0 * K);                                                          \
+    wtile = (void*)(W + (size_t)n0 * K + sk * KC * 64);                                           \
+    atile = (void*)(A + (size_t)m0 * K + sk * KC * 64);                                           \
+    nt = min(KC, NT - sk * KC);                                                                   \
     abytes = mrows * K * 2;                                                                       \
     int ln_ = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));   /* opaque copy: the offsets are recomputed per tile, not hoisted and spilled */ \
     asm volatile("" : "+v"(ln_));                                                                 \
@@ -281,7 +289,6 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
   constexpr int N2 = G4_AREG ? QI + (N2S < PI ? N2S : PI) : N2S;
   static_assert(GSP >= 1 && BAR1 < NMF && BAR1 < BAR2, "schedule");
 
-  const int nt = K >> 6;
   if constexpr (EPI == G4_HEAD) {
     if (rp.ctab != nullptr) {
       uint16_t* lt = reinterpret_cast<uint16_t*>(smem + 2 * STG);
@@ -376,7 +383,7 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
   // tile's first two K tiles load while this tile's epilogue stores run
   g4_vmcnt<0>();
   g4_bar();
-  const int em0 = m0, en0 = n0;
+  const int em0 = m0, en0 = n0, esk = sk;
   const int next = tile + (int)gridDim.x;
   // Row-coalesced bf16 epilogue (G4_BF16): a lane's accumulators are 4 consecutive columns of one row, so direct
   // stores put 16 rows x 32 B into every store instruction, one address translation per lane (the UTCL1 request
@@ -388,7 +395,7 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
   if constexpr (LEPI) {
     // K tile 0 of the next tile loads into stage 0 under the round trip, which uses stage 1 (ERR rows per wave
     // and round); the LDS accesses are asm, or hipcc would wait for that LDS-DMA (vmcnt(0)) in front of them
-    if (next < nwg) {
+    if (next < nwgv) {
       tile = next;
       G4_TILE(tile, m0, n0);
       G4_DESC();
@@ -457,7 +464,7 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
         __builtin_amdgcn_raw_buffer_store_b128(ev[k], ors, ((rnd * ERR + ERPI * k + ln / ECH) * ldc + oc0) * 2, 0, 0);
     });
     g4_bar();   // every wave's rows are out of stage 1
-    if (next < nwg) G4_STAGE(min(1, nt - 1), 1);
+    if (next < nwgv) G4_STAGE(min(1, nt - 1), 1);
   }
   // G4_HEAD: the rows' teacher targets, loaded before the next tile's LDS-DMA is issued (their wait then leaves
   // that DMA in flight)
@@ -473,7 +480,7 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
       }
     }
   }
-  if (!LEPI && next < nwg) {
+  if (!LEPI && next < nwgv) {
     tile = next;
     G4_TILE(tile, m0, n0);
     G4_DESC();
@@ -647,7 +654,8 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
         if (m >= M) continue;
         const f32x4 v = acc[i][j];
         if constexpr (EPI == G4_F32) {
-          *reinterpret_cast<float4*>(reinterpret_cast<float*>(C) + (size_t)m * ldc + n) = make_float4(v[0], v[1], v[2], v[3]);
+          *reinterpret_cast<float4*>(reinterpret_cast<float*>(C) + ((size_t)esk * M + m) * ldc + n) =
+              make_float4(v[0], v[1], v[2], v[3]);
         } else {
           const float a0 = v[0] + bn_.x, a1 = v[1] + bn_.y, a2 = v[2] + bn_.z, a3 = v[3] + bn_.w;
           *reinterpret_cast<float4*>(reinterpret_cast<float*>(C) + (size_t)m * ldc + n) =
@@ -657,7 +665,7 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
     }
   }
   }
-  if (next >= nwg) break;
+  if (next >= nwgv) break;
 #pragma unroll
   for (int i = 0; i < WN; ++i)
 #pragma unroll
@@ -669,6 +677,45 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
 #undef G4_TILE
 #undef G4_DESC
 #endif
+}
+
+// Split-K reduction: out = sum over the ks fp32 partials in split order (deterministic), then bf16 (epi 0) or the
+// GeGLU of the gate|up column pairs (epi 3, the interleaved layout of G4_GEGLU; same rounding chain).  8 outputs per
+// thread.
+template <int EPI>
+__global__ void __launch_bounds__(256) g4_splitk_reduce_kernel(const float* __restrict__ part, uint16_t* __restrict__ out,
+                                                               int M, int N, int ks, int ldo) {
+  const int nout = EPI == G4_GEGLU ? N / 2 : N;
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int per_row = nout / 8;
+  if (i >= (size_t)M * per_row) return;
+  const int m = (int)(i / per_row), c8 = (int)(i % per_row) * 8;
+  const size_t plane = (size_t)M * N;
+  float o[8];
+  if constexpr (EPI == G4_GEGLU) {
+    // output features f = c8 .. c8+7 live in 128-column block f/64: gate column 128*(f/64) + f%64, up +64
+    const int blk = c8 >> 6, fi = c8 & 63;
+    const float* g = part + (size_t)m * N + blk * 128 + fi;
+    float gs[8], us[8];
+    for (int e = 0; e < 8; ++e) gs[e] = us[e] = 0.f;
+    for (int s = 0; s < ks; ++s) {
+      const float4 g0 = *reinterpret_cast<const float4*>(g + s * plane), g1 = *reinterpret_cast<const float4*>(g + s * plane + 4);
+      const float4 u0 = *reinterpret_cast<const float4*>(g + s * plane + 64);
+      const float4 u1 = *reinterpret_cast<const float4*>(g + s * plane + 68);
+      gs[0] += g0.x; gs[1] += g0.y; gs[2] += g0.z; gs[3] += g0.w; gs[4] += g1.x; gs[5] += g1.y; gs[6] += g1.z; gs[7] += g1.w;
+      us[0] += u0.x; us[1] += u0.y; us[2] += u0.z; us[3] += u0.w; us[4] += u1.x; us[5] += u1.y; us[6] += u1.z; us[7] += u1.w;
+    }
+    for (int e = 0; e < 8; ++e) o[e] = rbf(gelu_tanh_fast(rbf(gs[e]))) * rbf(us[e]);
+  } else {
+    const float* p = part + (size_t)m * N + c8;
+    for (int e = 0; e < 8; ++e) o[e] = 0.f;
+    for (int s = 0; s < ks; ++s) {
+      const float4 a = *reinterpret_cast<const float4*>(p + s * plane), b = *reinterpret_cast<const float4*>(p + s * plane + 4);
+      o[0] += a.x; o[1] += a.y; o[2] += a.z; o[3] += a.w; o[4] += b.x; o[5] += b.y; o[6] += b.z; o[7] += b.w;
+    }
+  }
+  *reinterpret_cast<uint4*>(out + (size_t)m * ldo + c8) =
+      make_uint4(pack2(o[0], o[1]), pack2(o[2], o[3]), pack2(o[4], o[5]), pack2(o[6], o[7]));
 }
 
 }  // namespace
@@ -714,6 +761,45 @@ void tb_gemm4(const uint16_t* A, const uint16_t* W, void* C, const float* bias, 
     G4_EPI(256)
   }
 #undef G4_EPI
+}
+
+// Split-K for thin grids (few output tiles: o_proj / down at N = 3584, any projection at decode M): ks K ranges per
+// output tile, fp32 partials into ws [ks, M, N], then the ordered reduction (bf16, or GeGLU for epi 3).  Not batch
+// invariant against tb_gemm4 (the K sum is split), so the dispatch uses it only in "auto" mode.
+int tb_gemm4_splitk_ks(int M, int N, int K, int tile_rows) {
+  const int nwg = (N / G4_BN) * ((M + tile_rows - 1) / tile_rows), NT = K / 64;
+  int ks = std::max(1, std::min(g4_grid(1 << 30) / std::max(nwg, 1), NT / 4));
+  const int kc = (NT + ks - 1) / ks;
+  return (NT + kc - 1) / kc;
+}
+
+void tb_gemm4_splitk(const uint16_t* A, const uint16_t* W, uint16_t* out, float* ws, int M, int N, int K, int ldo,
+                     int epi, int tile_rows, int ks, hipStream_t st) {
+  if (M <= 0 || N <= 0) return;
+  const int NT = K / 64;
+  ks = std::max(1, std::min(ks, NT));
+  const int kc = (NT + ks - 1) / ks;
+  ks = (NT + kc - 1) / kc;
+  G4Rope rp{};
+  rp.ksplit = ks;
+  rp.kchunk = kc;
+  void* C = ws;
+  const float* bias = nullptr;
+  const float* thr = nullptr;
+  const int ldc = N;
+  const int nwg = (N / G4_BN) * ((M + tile_rows - 1) / tile_rows) * ks;
+  if (tile_rows == 128)
+    hipLaunchKernelGGL((gemm4_kernel<128, G4_F32>), dim3(g4_grid(nwg)), dim3(G4_THREADS), 0, st, A, W, C, bias, thr, M, N,
+                       K, ldc, rp);
+  else
+    hipLaunchKernelGGL((gemm4_kernel<256, G4_F32>), dim3(g4_grid(nwg)), dim3(G4_THREADS), 0, st, A, W, C, bias, thr, M, N,
+                       K, ldc, rp);
+  const size_t nthr = (size_t)M * ((epi == G4_GEGLU ? N / 2 : N) / 8);
+  const dim3 grid((unsigned)((nthr + 255) / 256));
+  if (epi == G4_GEGLU)
+    hipLaunchKernelGGL(g4_splitk_reduce_kernel<G4_GEGLU>, grid, dim3(256), 0, st, ws, out, M, N, ks, ldo);
+  else
+    hipLaunchKernelGGL(g4_splitk_reduce_kernel<G4_BF16>, grid, dim3(256), 0, st, ws, out, M, N, ks, ldo);
 }
 
 void tb_head_fused4(const uint16_t* A, const uint16_t* W, float* part, float cap, const int32_t* tgt,

@@ -100,8 +100,17 @@ SKINNY_MAX_M = int(os.environ.get("TB_SKINNY_MAX_M", "0"))   # v1 kernel loses t
 
 def tb_gemm(x, w, out, bias, thr, epi: int, choice) -> None:
     """One in-tree MFMA GEMM (``runtime.gemm_dispatch`` choice): ``"g256"`` / ``"g128"`` the four-wave kernel
-    (csrc/gemm4.hip), ``256`` / ``128`` the ping-pong kernel (csrc/gemm.hip); identical numerics."""
-    if isinstance(choice, str):
+    (csrc/gemm4.hip), ``256`` / ``128`` the ping-pong kernel (csrc/gemm.hip) -- identical numerics; ``"k256"`` /
+    ``"k128"`` the four-wave kernel split over K (thin grids; fp32 partials + ordered reduction, epi 0 / 3 only,
+    not bit-identical to the unsplit kernels)."""
+    if isinstance(choice, str) and choice[0] == "k":
+        K = x.shape[-1]
+        M, N = x.numel() // K, w.shape[0]
+        tr = int(choice[1:])
+        ks = int(_k().gemm4_splitk_ks(M, N, K, tr))
+        ws = torch.empty(ks * M * N, dtype=torch.float32, device=x.device)
+        _k().gemm4_splitk(x, w, out, ws, int(epi), tr, ks)
+    elif isinstance(choice, str):
         _k().gemm4(x, w, out, bias, thr, int(epi), int(choice[1:]))
     else:
         _k().gemm_pp(x, w, out, bias, thr, int(epi), int(choice))
@@ -199,7 +208,7 @@ def qkv_rope_fused_ok(x: torch.Tensor, wqkv: torch.Tensor, HD: int) -> bool:
         return True
     # the measured fused-vs-(hipBLASLt + rope_qkv_cache) table (key epilogue 4) when present, else the plain QKV
     c = _GD.choose(M, wqkv.shape[0], K, 4) if _GD.has_entry(wqkv.shape[0], K, 4) else _GD.choose(M, wqkv.shape[0], K, 0)
-    return c != "blas"
+    return c != "blas" and not str(c).startswith("k")      # (split-K has no fused RoPE epilogue)
 
 
 def qkv_rope_cache(x, wqkv, pos, slot_of_row, cos_t, sin_t, kc, vc, Hq, Hkv, HD, q_out=None, qkv_ws=None):
@@ -210,7 +219,9 @@ def qkv_rope_cache(x, wqkv, pos, slot_of_row, cos_t, sin_t, kc, vc, Hq, Hkv, HD,
         M = pos.numel()
         q_out = _out(q_out, (M, Hq, HD), x.dtype, x.device)
         c = _GD.choose(M, wqkv.shape[0], x.shape[-1], 4 if _GD.has_entry(wqkv.shape[0], x.shape[-1], 4) else 0)
-        rows = int(str(c).lstrip("g")) if c != "blas" else int(str(_GD.fill_choice(M, wqkv.shape[0])).lstrip("g"))
+        if c == "blas" or str(c).startswith("k"):
+            c = _GD.fill_choice(M, wqkv.shape[0])
+        rows = int(str(c).lstrip("g"))
         _k().gemm4_qkv_rope(x, wqkv, pos, slot_of_row, cos_t, sin_t, q_out, kc, vc, int(Hq), int(Hkv), rows)
         return q_out
     qkv = linear(x, wqkv, out=qkv_ws)

@@ -7,6 +7,9 @@ through :func:`taboo_brittleness_amd.ops.linear`, which asks :func:`choose` for 
   tile doubles the workgroup count for the N = 3584 projections at moderate M);
 * ``"g256"`` / ``"g128"`` — ``csrc/gemm4.hip``'s four-wave kernel (128x128 wave tiles), same tiles, same
   epilogues and bit-identical results;
+* ``"k256"`` / ``"k128"`` — the four-wave kernel split over K (``tb_gemm4_splitk``: as many K ranges as fill the
+  CUs, fp32 partials, ordered reduction) for thin grids (o_proj / down at N = 3584, every projection at decode M);
+  deterministic but not bit-identical to the unsplit kernels, so ``auto`` only;
 * ``"blas"`` — ``torch.matmul`` (hipBLASLt, with the TunableOp solution table the bench loads).
 
 Modes (``TB_GEMM``):
@@ -78,7 +81,7 @@ def set_kernel(kernel: str) -> None:
 
 
 def choose(M: int, N: int, K: int, epi: int = 0) -> Choice:
-    """``256`` | ``128`` | ``"g256"`` | ``"g128"`` | ``"blas"`` for ``C[M, N] = A[M, K] @ W[N, K]^T`` (epi 3: gate|up + GeGLU)."""
+    """``256`` | ``128`` | ``"g256"`` | ``"g128"`` | ``"k256"`` | ``"k128"`` | ``"blas"`` for ``C[M, N] = A[M, K] @ W[N, K]^T`` (epi 3: gate|up + GeGLU)."""
     m = _state["mode"]
     if m == "blas":
         return "blas"

@@ -542,6 +542,41 @@ def test_gemm4_bitequal_pingpong_and_batch_invariant(gpu, N, K, epi):
         _close(ref_pp[:64], r, atol=1e-2 * K ** 0.5, rtol=1e-2)
 
 
+@pytest.mark.parametrize("M,N,K,epi,ks", [(16, 3584, 14336, 0, 0), (100, 8192, 3584, 0, 3), (700, 3584, 4096, 0, 0),
+                                          (48, 28672, 3584, 3, 0), (300, 1024, 640, 3, 4), (1, 256, 64, 0, 1)])
+def test_gemm4_splitk(gpu, M, N, K, epi, ks):
+    """Split-K gemm4 (thin grids: fp32 partials of ks K ranges + ordered reduction, csrc/gemm4.hip
+    tb_gemm4_splitk) at Gemma-2-9B decode / o_proj / down / gate|up shapes vs a float32 reference of the same
+    bf16 operands, the heuristic split count and explicit uneven ones; deterministic across runs and within bf16
+    rounding of the unsplit kernel."""
+    torch.manual_seed(9)
+    A = ((torch.rand(M, K) * 2 - 1) * 0.5).to(BF)
+    W = ((torch.rand(N, K) * 2 - 1) * 0.5).to(BF)
+    Ag, Wg = A.to(gpu), W.to(gpu)
+    k = ops._k()
+    r = A.float() @ W.float().T
+    if epi == 3:
+        Wg = Wg[ops.geglu_interleave_index(N // 2, gpu)].contiguous()
+        want = ref.geglu(r.to(BF)).float()
+    else:
+        want = r
+    ncol = N // 2 if epi == 3 else N
+    for t in (128, 256):
+        kse = ks if ks > 0 else int(k.gemm4_splitk_ks(M, N, K, t))
+        ws = torch.full((kse * M * N,), float("nan"), device=gpu)
+        c = torch.full((M, ncol), float("nan"), device=gpu, dtype=BF)
+        k.gemm4_splitk(Ag, Wg, c, ws, epi, t, kse)
+        _close(c, want, atol=2e-2 * K ** 0.5, rtol=2e-2)
+        c2 = torch.empty_like(c)
+        k.gemm4_splitk(Ag, Wg, c2, ws, epi, t, kse)
+        assert torch.equal(c, c2), "split-K must be deterministic"
+        plain = torch.empty_like(c)
+        k.gemm4(Ag, Wg, plain, None, None, epi, t)
+        # a different K summation order: within one bf16 ulp of the unsplit result almost everywhere
+        d = (c.float() - plain.float()).abs()
+        assert (d <= plain.float().abs() * 2 ** -7 + 1e-3).float().mean() > 0.999
+
+
 @pytest.mark.parametrize("M,rows", [(300, 256), (77, 128)])
 def test_gemm4_qkv_rope_fused(gpu, M, rows):
     """QKV GEMM with RoPE + KV scatter in the epilogue (csrc/gemm4.hip G4_ROPE) at the Gemma-2-9B head layout

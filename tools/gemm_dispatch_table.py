@@ -1,7 +1,12 @@
-"""Rebuild ``configs/gemm_dispatch/<arch>.json`` from a ``tools/gemm_dispatch_tune.py`` raw JSONL with another
-tie rule (in-tree kernel kept when ``t_tb <= tie * t_blas``) and print the per-shape in-tree share.
+"""Build ``configs/gemm_dispatch/<arch>.json`` from one or more ``tools/gemm_dispatch_tune.py`` raw JSONL files.
 
-  python tools/gemm_dispatch_table.py profiles/r3/gemm_dispatch/raw_round1.jsonl --tie 1.02
+Each raw line times hipBLASLt (``blas``) and some in-tree variants at one ``(N, K, epilogue, M)``.  Files from
+different runs (e.g. a full sweep plus a later one with the split-K variants) are merged per point through the
+time RELATIVE to that run's own hipBLASLt time, so box-to-box clock differences cancel; the in-tree variant with
+the lowest ratio wins when ``ratio <= tie`` (``--tie-fused`` for the fused GeGLU epilogue, whose alternative is two
+kernels).  Prints the per-shape in-tree count.
+
+  python tools/gemm_dispatch_table.py gpurun_out/r4/raw.jsonl gpurun_out/r4/raw_splitk.jsonl --tie 1.01
 """
 import argparse
 import json
@@ -9,29 +14,45 @@ import os
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
-ap = argparse.ArgumentParser()
-ap.add_argument("raw")
-ap.add_argument("--tie", type=float, default=1.02)
-ap.add_argument("--tie-fused", type=float, default=1.04,
-                help="tie rule for the fused gate|up + GeGLU epilogue (epi 3), whose alternative is two kernels")
-ap.add_argument("--out", default=os.path.join(ROOT, "configs", "gemm_dispatch", "gemma2-9b.json"))
-ap.add_argument("--min-m", type=int, default=0, help="below this M always hipBLASLt")
-args = ap.parse_args()
-shapes, stats = {}, {}
-for line in open(args.raw):
-    r = json.loads(line)
-    us = {k: float(v) for k, v in r["us"].items()}
-    best = min(("256", "128"), key=lambda v: us[v])
-    tie = args.tie_fused if r["epi"] == 3 else args.tie
-    win = int(best) if (us[best] <= tie * us["blas"] and r["M"] >= args.min_m) else "blas"
-    key = f"{r['N']},{r['K']},{r['epi']}"
-    shapes.setdefault(key, []).append([r["M"], win])
-    s = stats.setdefault((r["shape"], r["epi"]), [0, 0])
-    s[0] += win != "blas"
-    s[1] += 1
-json.dump({"shapes": shapes, "meta": {"raw": os.path.relpath(args.raw, ROOT), "tie": args.tie,
-                                     "tie_fused": args.tie_fused}}, open(args.out, "w"),
-          indent=1)
-for (n, e), (a, b) in stats.items():
-    print(f"{n:5s} epi{e}: in-tree at {a}/{b} row counts")
-print("wrote", args.out)
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("raw", nargs="+")
+    ap.add_argument("--tie", type=float, default=1.01)
+    ap.add_argument("--tie-fused", type=float, default=1.01)
+    ap.add_argument("--out", default=os.path.join(ROOT, "configs", "gemm_dispatch", "gemma2-9b.json"))
+    ap.add_argument("--exclude", default="", help="comma-separated variants never chosen (e.g. 256,128)")
+    ap.add_argument("--tag", default="")
+    args = ap.parse_args()
+    excl = set(v for v in args.exclude.split(",") if v)
+    pts = {}                       # (shape, N, K, epi, M) -> {variant: ratio to blas}
+    for path in args.raw:
+        for line in open(path):
+            r = json.loads(line)
+            us = {k: float(v) for k, v in r["us"].items()}
+            key = (r["shape"], r["N"], r["K"], r["epi"], r["M"])
+            d = pts.setdefault(key, {})
+            for v, t in us.items():
+                if v != "blas" and v not in excl:
+                    d[v] = min(d.get(v, 1e9), t / us["blas"])
+    shapes, stats = {}, {}
+    for (shape, N, K, epi, M), d in sorted(pts.items()):
+        best = min(d, key=d.get)
+        tie = args.tie_fused if epi == 3 else args.tie
+        win = best if d[best] <= tie else "blas"
+        win = win if not win.isdigit() else int(win)
+        shapes.setdefault(f"{N},{K},{epi}", []).append([M, win])
+        s = stats.setdefault((shape, epi), [0, 0])
+        s[0] += win != "blas"
+        s[1] += 1
+    tab = {"shapes": shapes, "meta": {"tie": args.tie, "tie_fused": args.tie_fused, "sources": args.raw,
+                                      "tag": args.tag}}
+    os.makedirs(os.path.dirname(args.out), exist_ok=True)
+    json.dump(tab, open(args.out, "w"), indent=1)
+    for (shape, epi), (w, n) in sorted(stats.items()):
+        print(f"{shape:5s} epi {epi}: in-tree at {w}/{n} row counts")
+    print(f"wrote {args.out}")
+
+
+if __name__ == "__main__":
+    main()

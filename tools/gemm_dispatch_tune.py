@@ -67,7 +67,8 @@ def main():
     ap.add_argument("--max-m", type=int, default=33000)
     ap.add_argument("--only", default="", help="comma-separated shape names")
     ap.add_argument("--tie", type=float, default=1.01, help="in-tree wins when t_tb <= tie * t_blas")
-    ap.add_argument("--kernels", default="g256,g128,256,128", help="in-tree candidates (gNNN: gemm4.hip, NNN: gemm.hip)")
+    ap.add_argument("--kernels", default="g256,g128,k256,k128,256,128",
+                    help="in-tree candidates (gNNN: gemm4.hip, kNNN: gemm4.hip split over K, NNN: gemm.hip)")
     args = ap.parse_args()
     _ext.load()
     k = _ext.kernels()
@@ -133,7 +134,7 @@ def main():
                     var = {"blas": blas_geglu}
                 wsrc = Wi if epi == 3 else Ws
                 for ch in (args.kernels.split(",") if epi != 4 else []):
-                    ch = ch if ch.startswith("g") else int(ch)
+                    ch = ch if ch[0] in "gk" else int(ch)
                     var[ch] = (lambda ch_: lambda: ops.tb_gemm(A, nxt(wsrc), C, None, None, epi, ch_))(ch)
                 for f in var.values():      # warm-up (and TunableOp lookups)
                     f()
