@@ -70,6 +70,10 @@ bool tb_register_softcap_compact(float cap, const uint16_t* tab, int lo, int hi,
 bool tb_softcap_compact(const uint16_t* x, float* y, int n, float cap, hipStream_t st);
 bool tb_gemm4_ok(int M, int N, int K);
 int tb_gemm4_splitk_ks(int M, int N, int K, int tile_rows);
+int tb_gemm4_splitk_part(const uint16_t* A, const uint16_t* W, float* ws, int M, int N, int K, int tile_rows, int ks,
+                         hipStream_t st);
+void tb_add_rmsnorm2_part(uint16_t* h, const float* part, int ks, const uint16_t* w_post, const uint16_t* w_next,
+                          uint16_t* x, int M, int D, float eps, hipStream_t st);
 void tb_gemm4_splitk(const uint16_t* A, const uint16_t* W, uint16_t* out, float* ws, int M, int N, int K, int ldo,
                      int epi, int tile_rows, int ks, hipStream_t st);
 void tb_gemm4(const uint16_t* A, const uint16_t* W, void* C, const float* bias, const float* thr, int M, int N, int K,

@@ -66,6 +66,18 @@ void add_rmsnorm2(torch::Tensor h, torch::Tensor o, torch::Tensor w_post, torch:
   tb_add_rmsnorm2(bf(h), cbf(o), cbf(w_post), cbf(w_next), bf(x), M, D, (float)eps, cur_stream());
 }
 
+// add_rmsnorm2 with o given as ks fp32 split-K partials [ks, M, D] (gemm4_splitk_part)
+void add_rmsnorm2_part(torch::Tensor h, torch::Tensor part, int64_t ks, torch::Tensor w_post, torch::Tensor w_next,
+                       torch::Tensor x, double eps) {
+  IN_BF16(h); IN_F32(part); IN_BF16(w_post); IN_BF16(w_next); IN_BF16(x);
+  const int D = h.size(-1), M = h.numel() / D;
+  TORCH_CHECK(D % 8 == 0 && x.numel() == h.numel() && ks >= 1 && part.numel() >= ks * (int64_t)M * D,
+              "add_rmsnorm2_part shapes");
+  c10::DeviceGuard g(h.device());
+  tb_add_rmsnorm2_part(bf(h), part.data_ptr<float>(), (int)ks, cbf(w_post), cbf(w_next), bf(x), M, D, (float)eps,
+                       cur_stream());
+}
+
 void embed_rmsnorm(torch::Tensor ids, torch::Tensor E, torch::Tensor w, torch::Tensor h, torch::Tensor x,
                    double scale, double eps) {
   IN_I32(ids); IN_BF16(E); IN_BF16(w); IN_BF16(h); IN_BF16(x);
@@ -454,6 +466,19 @@ bool gemm4_ok(int64_t M, int64_t N, int64_t K) { return tb_gemm4_ok(M, N, K); }
 
 // Split-K gemm4 (thin grids): fp32 partials of ks K ranges into ws, then the ordered reduction into C (bf16 [M, N], or
 // the GeGLU [M, N/2] of the interleaved gate|up rows for epi 3).  ks <= 0: the launcher's heuristic.
+// split GEMM into fp32 partials only (no reduction); returns the split count used
+int64_t gemm4_splitk_part(torch::Tensor A, torch::Tensor W, torch::Tensor ws, int64_t tile_rows, int64_t ks) {
+  IN_BF16(A); IN_BF16(W); IN_F32(ws);
+  TORCH_CHECK(W.dim() == 2 && (tile_rows == 256 || tile_rows == 128), "gemm4_splitk_part: W [N, K], tile_rows 128|256");
+  const int K = A.size(-1), M = A.numel() / K, N = W.size(0);
+  TORCH_CHECK(W.size(1) == K && tb_gemm4_ok(M, N, K), "gemm4_splitk_part: need N % 256 == 0, K % 64 == 0");
+  if (ks <= 0) ks = tb_gemm4_splitk_ks(M, N, K, tile_rows);
+  const int NT = K / 64, kc = (NT + (int)ks - 1) / (int)ks, kse = (NT + kc - 1) / kc;
+  TORCH_CHECK(ws.numel() >= (int64_t)kse * M * N, "gemm4_splitk_part: ws needs ks * M * N floats");
+  c10::DeviceGuard g(A.device());
+  return tb_gemm4_splitk_part(cbf(A), cbf(W), ws.data_ptr<float>(), M, N, K, (int)tile_rows, (int)ks, cur_stream());
+}
+
 int64_t gemm4_splitk_ks(int64_t M, int64_t N, int64_t K, int64_t tile_rows) {
   return tb_gemm4_splitk_ks(M, N, K, tile_rows);
 }
@@ -794,6 +819,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm4_ok", &gemm4_ok);
   m.def("gemm4_splitk", &gemm4_splitk);
   m.def("gemm4_splitk_ks", &gemm4_splitk_ks);
+  m.def("gemm4_splitk_part", &gemm4_splitk_part);
+  m.def("add_rmsnorm2_part", &add_rmsnorm2_part);
   m.def("gemm4_qkv_rope", &gemm4_qkv_rope);
   m.def("head_fused", &head_fused);
   m.def("lens_gemm", &lens_gemm);

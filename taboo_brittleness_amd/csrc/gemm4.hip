@@ -79,6 +79,10 @@ constexpr int G4_THREADS = 256, G4_BN = 256;
 #define G4_LDS_GEGLU 0   // 1: the GeGLU output through the row-coalesced LDS epilogue too (measured no faster:
                          // its rows are half as wide and the direct stores overlap the next tile's loads)
 #endif
+#ifndef G4_EPI_SPARE
+#define G4_EPI_SPARE 1   // 1: the row-coalesced epilogue's LDS round trip in the 32 KB beside the two stages (both of the
+                         // next tile's first K tiles load under it); 0: in stage 1 (its DMA waits for the round trip)
+#endif
 #ifndef G4_ASM_MFMA
 #define G4_ASM_MFMA 1    // 1: MFMAs as asm statements with AGPR-tied accumulators (see G4_MFMA below)
 #endif
@@ -174,10 +178,13 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
   // GeGLU: its 64 features), ERPI rows per 16-B-per-lane store, ERR rows per LDS round trip, ENR stores per lane
   constexpr bool LEPI = EPI == G4_BF16 || EPI == G4_LENS || (EPI == G4_GEGLU && G4_LDS_GEGLU);
   constexpr int RB = EPI == G4_GEGLU ? 128 : 256, ECH = RB / 16, ERPI = 64 / ECH;
-  constexpr int ERR = EPI == G4_GEGLU ? BM / 2 : BM / 4;
+  constexpr bool SPARE = LEPI && G4_EPI_SPARE;
+  constexpr int EXB = SPARE ? 32768 : 0;                    // spare round-trip LDS (4 waves x ERR rows x RB)
+  constexpr int ERR = SPARE ? EXB / (4 * RB) : EPI == G4_GEGLU ? BM / 2 : BM / 4;
   constexpr int ENR = LEPI ? (BM / 2) / ERPI : 1;
   constexpr int CTB = EPI == G4_HEAD ? 4096 : 0;            // compact softcap table bytes (G4_HEAD)
-  __shared__ __attribute__((aligned(1024))) char smem[2 * STG + CTB];   // one array: glds trap (a)
+  static_assert(2 * STG + CTB + EXB <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STG + CTB + EXB];   // one array: glds trap (a)
 
   const int nbn = N / G4_BN, nbm = (M + BM - 1) / BM, nwg = nbn * nbm;
   const int NT = K >> 6, KS = EPI == G4_F32 && rp.ksplit > 1 ? rp.ksplit : 1, KC = KS > 1 ? rp.kchunk : NT;
@@ -400,9 +407,10 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
       G4_TILE(tile, m0, n0);
       G4_DESC();
       G4_STAGE(0, 0);
+      if constexpr (SPARE) G4_STAGE(min(1, nt - 1), 1);
     }
     asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");   // last MFMA's D -> the accumulator reads below
-    const uint32_t reg = (uint32_t)(uintptr_t)((g4_lds_char*)smem) + STG + wid * ERR * RB;
+    const uint32_t reg = (uint32_t)(uintptr_t)((g4_lds_char*)smem) + (SPARE ? 2 * STG + CTB : STG) + wid * ERR * RB;
     uint16_t* obase = reinterpret_cast<uint16_t*>(C) + (size_t)(em0 + wm * (BM / 2)) * ldc;
     const int nrow = min(BM / 2, M - em0 - wm * (BM / 2));
     const auto ors = __builtin_amdgcn_make_buffer_rsrc(obase, 0, nrow > 0 ? nrow * ldc * 2 : 0, 0x00020000);
@@ -463,8 +471,10 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
       for (int k = 0; k < ERR / ERPI; ++k)
         __builtin_amdgcn_raw_buffer_store_b128(ev[k], ors, ((rnd * ERR + ERPI * k + ln / ECH) * ldc + oc0) * 2, 0, 0);
     });
-    g4_bar();   // every wave's rows are out of stage 1
-    if (next < nwgv) G4_STAGE(min(1, nt - 1), 1);
+    if constexpr (!SPARE) {
+      g4_bar();   // every wave's rows are out of stage 1
+      if (next < nwgv) G4_STAGE(min(1, nt - 1), 1);
+    }
   }
   // G4_HEAD: the rows' teacher targets, loaded before the next tile's LDS-DMA is issued (their wait then leaves
   // that DMA in flight)
@@ -773,13 +783,15 @@ int tb_gemm4_splitk_ks(int M, int N, int K, int tile_rows) {
   return (NT + kc - 1) / kc;
 }
 
-void tb_gemm4_splitk(const uint16_t* A, const uint16_t* W, uint16_t* out, float* ws, int M, int N, int K, int ldo,
-                     int epi, int tile_rows, int ks, hipStream_t st) {
-  if (M <= 0 || N <= 0) return;
+// The split GEMM alone: fp32 partials [ks, M, N] into ws (a consumer that folds the ordered sum into its own pass,
+// e.g. tb_add_rmsnorm2_part).  Returns the split count actually used (ks rounded so every split is non-empty).
+int tb_gemm4_splitk_part(const uint16_t* A, const uint16_t* W, float* ws, int M, int N, int K, int tile_rows, int ks,
+                         hipStream_t st) {
   const int NT = K / 64;
   ks = std::max(1, std::min(ks, NT));
   const int kc = (NT + ks - 1) / ks;
   ks = (NT + kc - 1) / kc;
+  if (M <= 0 || N <= 0) return ks;
   G4Rope rp{};
   rp.ksplit = ks;
   rp.kchunk = kc;
@@ -794,6 +806,13 @@ void tb_gemm4_splitk(const uint16_t* A, const uint16_t* W, uint16_t* out, float*
   else
     hipLaunchKernelGGL((gemm4_kernel<256, G4_F32>), dim3(g4_grid(nwg)), dim3(G4_THREADS), 0, st, A, W, C, bias, thr, M, N,
                        K, ldc, rp);
+  return ks;
+}
+
+void tb_gemm4_splitk(const uint16_t* A, const uint16_t* W, uint16_t* out, float* ws, int M, int N, int K, int ldo,
+                     int epi, int tile_rows, int ks, hipStream_t st) {
+  if (M <= 0 || N <= 0) return;
+  ks = tb_gemm4_splitk_part(A, W, ws, M, N, K, tile_rows, ks, st);
   const size_t nthr = (size_t)M * ((epi == G4_GEGLU ? N / 2 : N) / 8);
   const dim3 grid((unsigned)((nthr + 255) / 256));
   if (epi == G4_GEGLU)

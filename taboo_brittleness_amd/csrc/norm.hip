@@ -98,6 +98,52 @@ __global__ void __launch_bounds__(1024) add_rmsnorm2_kernel(uint16_t* __restrict
   norm_store<VPT>(v, r2, w_next, x + (size_t)row * D, nvec);
 }
 
+// add_rmsnorm2 whose branch output o arrives as the ks fp32 split-K partials of the projection (gemm4.hip
+// tb_gemm4_splitk_part, [ks, M, D]): o = bf16(sum over the splits in order), exactly what the split-K reduction
+// kernel would have stored -- the reduction, its bf16 store and this kernel's re-read of o are one pass.
+template <int VPT>
+__global__ void __launch_bounds__(1024) add_rmsnorm2_part_kernel(uint16_t* __restrict__ h, const float* __restrict__ part,
+                                                                 int ks, int M, const uint16_t* __restrict__ w_post,
+                                                                 const uint16_t* __restrict__ w_next,
+                                                                 uint16_t* __restrict__ x, int D, float eps) {
+  __shared__ float red[16];
+  const int row = blockIdx.x, nvec = D >> 3;
+  float v[VPT][8];
+#pragma unroll
+  for (int s = 0; s < VPT; ++s) {
+    const int i = threadIdx.x + s * blockDim.x;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[s][j] = 0.f;
+    if (i < nvec) {
+      const float* pr = part + (size_t)row * D + i * 8;
+      for (int k = 0; k < ks; ++k) {
+        const float4 a = *reinterpret_cast<const float4*>(pr + (size_t)k * M * D);
+        const float4 b = *reinterpret_cast<const float4*>(pr + (size_t)k * M * D + 4);
+        v[s][0] += a.x; v[s][1] += a.y; v[s][2] += a.z; v[s][3] += a.w;
+        v[s][4] += b.x; v[s][5] += b.y; v[s][6] += b.z; v[s][7] += b.w;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[s][j] = rbf(v[s][j]);
+    }
+  }
+  const float r1 = rsqrtf(block_sum(sumsq<VPT>(v), red) / (float)D + eps);
+  uint16_t* hr = h + (size_t)row * D;
+#pragma unroll
+  for (int s = 0; s < VPT; ++s) {
+    const int i = threadIdx.x + s * blockDim.x;
+    if (i < nvec) {
+      float wf[8], hf[8];
+      unpack8(reinterpret_cast<const uint4*>(w_post)[i], wf);
+      unpack8(reinterpret_cast<const uint4*>(hr)[i], hf);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[s][j] = rbf(hf[j] + rbf(v[s][j] * r1 * (1.f + wf[j])));
+      reinterpret_cast<uint4*>(hr)[i] = pack8(v[s]);
+    }
+  }
+  const float r2 = rsqrtf(block_sum(sumsq<VPT>(v), red) / (float)D + eps);
+  norm_store<VPT>(v, r2, w_next, x + (size_t)row * D, nvec);
+}
+
 // h <- bf16(E[id] * bf16(scale));  x <- norm(h, w)
 template <int VPT>
 __global__ void __launch_bounds__(1024) embed_rmsnorm_kernel(const int32_t* __restrict__ ids,
@@ -156,6 +202,16 @@ void tb_add_rmsnorm2(uint16_t* h, const uint16_t* o, const uint16_t* w_post, con
   TB_DISPATCH_VPT(D, {
     const int thr = threads_for(nvec_, VPT);
     hipLaunchKernelGGL(add_rmsnorm2_kernel<VPT>, dim3(M), dim3(thr), 0, st, h, o, w_post, w_next, x, D, eps);
+  });
+}
+
+void tb_add_rmsnorm2_part(uint16_t* h, const float* part, int ks, const uint16_t* w_post, const uint16_t* w_next,
+                          uint16_t* x, int M, int D, float eps, hipStream_t st) {
+  if (M <= 0) return;
+  TB_DISPATCH_VPT(D, {
+    const int thr = threads_for(nvec_, VPT);
+    hipLaunchKernelGGL(add_rmsnorm2_part_kernel<VPT>, dim3(M), dim3(thr), 0, st, h, part, ks, M, w_post, w_next, x, D,
+                       eps);
   });
 }
 

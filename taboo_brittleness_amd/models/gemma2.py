@@ -10,12 +10,12 @@ Per decoder block (6 launches + 3 hipBLASLt GEMMs):
     qkv = x Wqkv^T ; q = rope(qkv), K/V -> cache   (one gemm4 launch with the G4_ROPE epilogue, or
                                                  hipBLASLt + rope_qkv_cache, per the GEMM dispatch)
     a   = attention(q, cache)             (HIP, softcap 50, GQA, sliding window)
-    o   = a Wo^T                           (hipBLASLt)
-    x   = add_rmsnorm2(h, o)  # h += post_attn_norm(o); x = pre_ffn_norm(h)   (HIP)
-    gu  = x Wgu^T                          (hipBLASLt)
-    act = geglu(gu)                        (HIP)
-    d   = act Wdown^T                      (hipBLASLt)
-    x   = add_rmsnorm2(h, d)  # h += post_ffn_norm(d); x = next input norm   (HIP)
+    o   = a Wo^T                           (gemm4 / split-K gemm4 / hipBLASLt, per the GEMM dispatch)
+    x   = add_rmsnorm2(h, o)  # h += post_attn_norm(o); x = pre_ffn_norm(h)   (HIP; with split-K o_proj the
+                              # fp32 partials are summed inside this pass, no reduction kernel)
+    act = geglu(x Wgu^T)                   (one gemm4 launch with the GeGLU epilogue, or hipBLASLt + geglu)
+    d   = act Wdown^T                      (as o)
+    x   = add_rmsnorm2(h, d)  # h += post_ffn_norm(d); x = next input norm   (HIP, as above)
     hooks[l](h, x, ctx)       # resid_post[l] == HF layer.output[0]
 
 Hooks are plain callables that may read or edit ``h`` in place (an editing
@@ -317,12 +317,16 @@ class Gemma2Model:
                 ops.rope_qkv_cache(ws.qkv, pos32, ws.slot_rows, self.cos_t, self.sin_t, cache.k[l], cache.v[l],
                                    ls.heads, ls.kv_heads, ls.head_dim, q_out=ws.q)
             attn(l, ws.q, cache.k[l], cache.v[l], pos32, s.sliding_window if s.is_sliding(l) else 0, ws.attn)
-            ops.linear(ws.attn, L.wo, out=ws.o)
-            if lora is not None:
-                lora.apply(l, "o", ws.attn, ws.o, lmask)
-            if self.tp is not None:
-                self.tp.all_reduce_(ws.o)
-            ops.add_rmsnorm2(h, ws.o, L.ln_post_attn, L.ln_pre_ffn, s.eps, out=x)
+            plain = lora is None and self.tp is None      # (split-K o_proj / down: partials fused into the norm)
+            if plain:
+                ops.linear_add_rmsnorm2(ws.attn, L.wo, h, L.ln_post_attn, L.ln_pre_ffn, s.eps, out=x, o_ws=ws.o)
+            else:
+                ops.linear(ws.attn, L.wo, out=ws.o)
+                if lora is not None:
+                    lora.apply(l, "o", ws.attn, ws.o, lmask)
+                if self.tp is not None:
+                    self.tp.all_reduce_(ws.o)
+                ops.add_rmsnorm2(h, ws.o, L.ln_post_attn, L.ln_pre_ffn, s.eps, out=x)
             if self._wgu_il is not None and ops.fused_geglu_wins(x, ls):
                 ops.gate_up_geglu(x, self._wgu_il[l], out=ws.act)
             else:
@@ -330,12 +334,15 @@ class Gemma2Model:
                 if lora is not None:
                     lora.apply(l, "gu", x, ws.gu, lmask)
                 ops.geglu(ws.gu, out=ws.act)
-            ops.linear(ws.act, L.wdown, out=ws.o)
-            if lora is not None:
-                lora.apply(l, "down", ws.act, ws.o, lmask)
-            if self.tp is not None:
-                self.tp.all_reduce_(ws.o)
-            ops.add_rmsnorm2(h, ws.o, L.ln_post_ffn, self.norm_next[l], s.eps, out=x)
+            if plain:
+                ops.linear_add_rmsnorm2(ws.act, L.wdown, h, L.ln_post_ffn, self.norm_next[l], s.eps, out=x, o_ws=ws.o)
+            else:
+                ops.linear(ws.act, L.wdown, out=ws.o)
+                if lora is not None:
+                    lora.apply(l, "down", ws.act, ws.o, lmask)
+                if self.tp is not None:
+                    self.tp.all_reduce_(ws.o)
+                ops.add_rmsnorm2(h, ws.o, L.ln_post_ffn, self.norm_next[l], s.eps, out=x)
             if hooks and l in hooks:
                 ctx = HookCtx(l, B, T, pos32, ctx_slot, self.norm_next[l], s.eps, self)
                 for hk in hooks[l]:

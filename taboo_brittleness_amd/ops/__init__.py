@@ -95,15 +95,17 @@ def softcap_values(v: torch.Tensor, cap: float) -> torch.Tensor:
     return ref.softcap_bf16(v, float(cap)).float()
 
 
-SKINNY_MAX_M = int(os.environ.get("TB_SKINNY_MAX_M", "0"))   # v1 kernel loses to hipBLASLt: opt-in
 
 
 def tb_gemm(x, w, out, bias, thr, epi: int, choice) -> None:
     """One in-tree MFMA GEMM (``runtime.gemm_dispatch`` choice): ``"g256"`` / ``"g128"`` the four-wave kernel
     (csrc/gemm4.hip), ``256`` / ``128`` the ping-pong kernel (csrc/gemm.hip) -- identical numerics; ``"k256"`` /
     ``"k128"`` the four-wave kernel split over K (thin grids; fp32 partials + ordered reduction, epi 0 / 3 only,
-    not bit-identical to the unsplit kernels)."""
-    if isinstance(choice, str) and choice[0] == "k":
+    not bit-identical to the unsplit kernels); ``"s"`` the weight-streaming decode kernel (csrc/skinny.hip, M <= 64,
+    epi 0)."""
+    if choice == "s":                 # weight-streaming kernel for decode M (csrc/skinny.hip; M <= 64, plain bf16)
+        _k().gemm_skinny(x, w, out)
+    elif isinstance(choice, str) and choice[0] == "k":
         K = x.shape[-1]
         M, N = x.numel() // K, w.shape[0]
         tr = int(choice[1:])
@@ -126,18 +128,38 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None)
         if M > 0 and x.is_contiguous() and w.is_contiguous() and (out is None or out.is_contiguous()) and \
                 _k().gemm_pp_ok(M, N, K):
             c = _GD.choose(M, N, K, 0)
+            if c == "s" and not _k().gemm_skinny_ok(M, N, K):
+                c = "blas"
             if c != "blas":
                 out = _out(out, x.shape[:-1] + (N,), BF16, x.device)
                 tb_gemm(x, w, out, None, None, 0, c)
                 return out
-        if M <= SKINNY_MAX_M and M * 16 <= N and x.is_contiguous() and w.is_contiguous() and \
-                _k().gemm_skinny_ok(M, N, K):
-            out = _out(out, x.shape[:-1] + (N,), BF16, x.device)
-            _k().gemm_skinny(x, w, out)
-            return out
     if out is not None:
         return torch.matmul(x, w.t(), out=out)
     return F.linear(x, w)
+
+
+def linear_add_rmsnorm2(a, w, h, w_post, w_next, eps, out=None, o_ws=None):
+    """``h += post_norm(a @ w^T)`` (in place); returns the next pre-norm of ``h`` -- a block's o_proj / down
+    projection and its residual norm.  When the dispatch runs the projection split over K (``"k256"`` /
+    ``"k128"``, thin grids), its fp32 partials go straight into ``add_rmsnorm2_part``, which sums them in split
+    order and rounds to bf16 exactly as the split-K reduction would: no reduction kernel and no bf16 ``o`` round
+    trip.  Otherwise ``linear`` into ``o_ws`` then ``add_rmsnorm2``."""
+    if a.is_cuda and a.dtype == BF16 and w.dtype == BF16 and a.is_contiguous() and w.is_contiguous():
+        K = a.shape[-1]
+        M, N = a.numel() // K, w.shape[0]
+        if M > 0 and _k().gemm4_ok(M, N, K):
+            c = _GD.choose(M, N, K, 0)
+            if isinstance(c, str) and c[0] == "k":
+                tr = int(c[1:])
+                ks = int(_k().gemm4_splitk_ks(M, N, K, tr))
+                ws = torch.empty(ks * M * N, dtype=torch.float32, device=a.device)
+                ks = int(_k().gemm4_splitk_part(a, w, ws, tr, ks))
+                out = _out(out, h.shape, h.dtype, h.device)
+                _k().add_rmsnorm2_part(h, ws, ks, w_post, w_next, out, float(eps))
+                return out
+    o = linear(a, w, out=o_ws)
+    return add_rmsnorm2(h, o, w_post, w_next, eps, out=out)
 
 
 def rmsnorm(x, w, eps, out=None):

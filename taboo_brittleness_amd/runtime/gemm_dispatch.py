@@ -10,6 +10,7 @@ through :func:`taboo_brittleness_amd.ops.linear`, which asks :func:`choose` for 
 * ``"k256"`` / ``"k128"`` — the four-wave kernel split over K (``tb_gemm4_splitk``: as many K ranges as fill the
   CUs, fp32 partials, ordered reduction) for thin grids (o_proj / down at N = 3584, every projection at decode M);
   deterministic but not bit-identical to the unsplit kernels, so ``auto`` only;
+* ``"s"`` — ``csrc/skinny.hip``'s weight-streaming kernel (M <= 64; wins only for o_proj at M <= 32);
 * ``"blas"`` — ``torch.matmul`` (hipBLASLt, with the TunableOp solution table the bench loads).
 
 Modes (``TB_GEMM``):
@@ -81,7 +82,7 @@ def set_kernel(kernel: str) -> None:
 
 
 def choose(M: int, N: int, K: int, epi: int = 0) -> Choice:
-    """``256`` | ``128`` | ``"g256"`` | ``"g128"`` | ``"k256"`` | ``"k128"`` | ``"blas"`` for ``C[M, N] = A[M, K] @ W[N, K]^T`` (epi 3: gate|up + GeGLU)."""
+    """``256`` | ``128`` | ``"g256"`` | ``"g128"`` | ``"k256"`` | ``"k128"`` | ``"s"`` | ``"blas"`` for ``C[M, N] = A[M, K] @ W[N, K]^T`` (epi 3: gate|up + GeGLU)."""
     m = _state["mode"]
     if m == "blas":
         return "blas"

@@ -577,6 +577,29 @@ def test_gemm4_splitk(gpu, M, N, K, epi, ks):
         assert (d <= plain.float().abs() * 2 ** -7 + 1e-3).float().mean() > 0.999
 
 
+@pytest.mark.parametrize("M,K,ks", [(64, 14336, 0), (700, 4096, 2), (5, 4096, 5)])
+def test_splitk_add_rmsnorm2_fused(gpu, M, K, ks):
+    """o_proj / down split over K with the fp32 partials summed inside add_rmsnorm2 (add_rmsnorm2_part): h and the
+    next pre-norm BIT-identical to the split-K reduction kernel's bf16 o followed by add_rmsnorm2."""
+    torch.manual_seed(4)
+    D = 3584
+    a = ((torch.rand(M, K) * 2 - 1) * 0.5).to(BF).to(gpu)
+    w = ((torch.rand(D, K) * 2 - 1) * 0.05).to(BF).to(gpu)
+    h0 = torch.randn(M, D).to(BF).to(gpu)
+    wp, wn = (torch.randn(D) * 0.1).to(BF).to(gpu), (torch.randn(D) * 0.1).to(BF).to(gpu)
+    k = ops._k()
+    kse = ks if ks > 0 else int(k.gemm4_splitk_ks(M, D, K, 128))
+    ws = torch.empty(kse * M * D, device=gpu)
+    o = torch.empty(M, D, device=gpu, dtype=BF)
+    k.gemm4_splitk(a, w, o, ws, 0, 128, kse)
+    h1, x1 = h0.clone(), torch.empty(M, D, device=gpu, dtype=BF)
+    k.add_rmsnorm2(h1, o, wp, wn, x1, 1e-6)
+    used = int(k.gemm4_splitk_part(a, w, ws, 128, kse))
+    h2, x2 = h0.clone(), torch.empty(M, D, device=gpu, dtype=BF)
+    k.add_rmsnorm2_part(h2, ws, used, wp, wn, x2, 1e-6)
+    assert torch.equal(h1, h2) and torch.equal(x1, x2)
+
+
 @pytest.mark.parametrize("M,rows", [(300, 256), (77, 128)])
 def test_gemm4_qkv_rope_fused(gpu, M, rows):
     """QKV GEMM with RoPE + KV scatter in the epilogue (csrc/gemm4.hip G4_ROPE) at the Gemma-2-9B head layout

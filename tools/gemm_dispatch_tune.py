@@ -134,6 +134,10 @@ def main():
                     var = {"blas": blas_geglu}
                 wsrc = Wi if epi == 3 else Ws
                 for ch in (args.kernels.split(",") if epi != 4 else []):
+                    if ch == "s":          # csrc/skinny.hip (M <= 64, plain bf16 only)
+                        if epi == 0 and k.gemm_skinny_ok(M, N, K):
+                            var["s"] = lambda: k.gemm_skinny(A, nxt(Ws), C)
+                        continue
                     ch = ch if ch[0] in "gk" else int(ch)
                     var[ch] = (lambda ch_: lambda: ops.tb_gemm(A, nxt(wsrc), C, None, None, epi, ch_))(ch)
                 for f in var.values():      # warm-up (and TunableOp lookups)

@@ -1,0 +1,85 @@
+"""Attribute every GEMM dispatch of a rocprofv3 kernel trace to its role in the Gemma-2 forward by the kernel that
+runs next on the stream (QKV -> rope / attention, o_proj -> add_rmsnorm2, gate|up -> geglu / down, down ->
+add_rmsnorm2 after a GeGLU, lm_head -> decode_head, lens -> lens readouts), then print time per (role, kernel).
+
+  python tools/gemm_roles.py gpurun_out/prof_x/run_kernel_trace.csv > summary.txt
+
+Runs on the GPU box right after the profile (the trace is hundreds of MB; only the summary is kept).
+"""
+import csv
+import sys
+from collections import defaultdict
+
+
+def is_gemm(n: str) -> bool:
+    return n.startswith(("Cijk_", "Custom_Cijk")) or "gemm4_kernel" in n or "gemm_pp_kernel" in n
+
+
+def short(n: str) -> str:
+    if n.startswith(("Cijk_", "Custom_Cijk")):
+        i = n.find("MT")
+        tag = n[i:n.find("_", i)] if i >= 0 else "?"
+        return ("hipblaslt SK " if "_SK" in n else "hipblaslt ") + tag
+    i = n.find("<")
+    return n[n.find("::") + 2 if "::" in n else 0:n.find("(", i) if i >= 0 else 60].strip()
+
+
+def role(prev: str, nxt: str) -> str:
+    if "rope_qkv" in nxt or "attn" in nxt or "attention" in nxt:
+        return "qkv"
+    if "decode_head" in nxt or "xent" in nxt:
+        return "lm_head"
+    if "lens" in nxt or "row_lse" in nxt or "gather_probs" in nxt or "topk" in nxt:
+        return "lens"
+    if "geglu_kernel" in nxt:
+        return "gate_up"
+    if "add_rmsnorm" in nxt or "splitk_reduce" in nxt:
+        if "geglu" in prev or "gemm4_kernel<256, 3>" in prev or "gemm4_kernel<128, 3>" in prev or \
+                "gemm_pp_kernel<3" in prev:
+            return "down"
+        return "o_proj"
+    if "gemm4_kernel<256, 3>" in nxt or "gemm4_kernel<128, 3>" in nxt or "gemm_pp_kernel<3" in nxt:
+        return "?"
+    if is_gemm(nxt):
+        return "gemm->gemm"
+    return "other(" + short(nxt)[:30] + ")"
+
+
+def main(path: str) -> None:
+    rows = list(csv.DictReader(open(path)))
+    key = lambda r: int(r["Start_Timestamp"])  # noqa: E731
+    rows.sort(key=key)
+    names = [r["Kernel_Name"] for r in rows]
+    dur = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows]
+    tot = sum(dur)
+    acc = defaultdict(lambda: [0, 0])
+    for i, n in enumerate(names):
+        if not is_gemm(n):
+            continue
+        nxt = names[i + 1] if i + 1 < len(names) else ""
+        if "splitk_reduce" in nxt and i + 2 < len(names):
+            nxt2 = names[i + 2]
+            rl = role(names[i - 1] if i else "", nxt2)
+        else:
+            rl = role(names[i - 1] if i else "", nxt)
+        # the fused gate|up + GeGLU GEMM is itself the gate_up role
+        if "gemm4_kernel<256, 3>" in n or "gemm4_kernel<128, 3>" in n or "gemm_pp_kernel<3" in n:
+            rl = "gate_up(fused)"
+        if "gemm4_kernel<256, 6>" in n:
+            rl = "lens(fused)"
+        a = acc[(rl, short(n))]
+        a[0] += dur[i]
+        a[1] += 1
+    print(f"kernel time {tot / 1e6:.1f} ms")
+    by_role = defaultdict(int)
+    for (rl, k), (t, c) in acc.items():
+        by_role[rl] += t
+    for rl, t in sorted(by_role.items(), key=lambda x: -x[1]):
+        print(f"{rl:16s} {t / 1e6:9.1f} ms  {100 * t / tot:5.1f} %")
+    print()
+    for (rl, k), (t, c) in sorted(acc.items(), key=lambda x: -x[1][0]):
+        print(f"{rl:16s} {k:40s} {t / 1e6:9.1f} ms {c:7d} calls  {t / max(c, 1) / 1e3:8.1f} us/call")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
