@@ -118,16 +118,17 @@ def tb_gemm(x, w, out, bias, thr, epi: int, choice) -> None:
         _k().gemm_pp(x, w, out, bias, thr, int(epi), int(choice))
 
 
-def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None, choice=None) -> torch.Tensor:
     """y = x @ w^T.  GPU: an in-tree MFMA GEMM (four-wave or ping-pong, 256- or 128-row tiles) or hipBLASLt, per shape
-    (``runtime.gemm_dispatch``: measured table, ``TB_GEMM=tb`` in-tree only / batch-invariant, ``blas``)."""
+    (``runtime.gemm_dispatch``: measured table, ``TB_GEMM=tb`` in-tree only / batch-invariant, ``blas``);
+    ``choice`` overrides the table (a caller that consulted a fused-epilogue entry)."""
     if x.is_cuda and x.dtype == BF16 and w.dtype == BF16:
         K = x.shape[-1]
         M = x.numel() // K
         N = w.shape[0]
         if M > 0 and x.is_contiguous() and w.is_contiguous() and (out is None or out.is_contiguous()) and \
                 _k().gemm_pp_ok(M, N, K):
-            c = _GD.choose(M, N, K, 0)
+            c = _GD.choose(M, N, K, 0) if choice is None else choice
             if c == "s" and not _k().gemm_skinny_ok(M, N, K):
                 c = "blas"
             if c != "blas":
@@ -149,7 +150,8 @@ def linear_add_rmsnorm2(a, w, h, w_post, w_next, eps, out=None, o_ws=None):
         K = a.shape[-1]
         M, N = a.numel() // K, w.shape[0]
         if M > 0 and _k().gemm4_ok(M, N, K):
-            c = _GD.choose(M, N, K, 0)
+            # the table's projection + norm entry (key epilogue 5) when measured, else the plain projection's
+            c = _GD.choose(M, N, K, 5) if _GD.has_entry(N, K, 5, M) else _GD.choose(M, N, K, 0)
             if isinstance(c, str) and c[0] == "k":
                 tr = int(c[1:])
                 ks = int(_k().gemm4_splitk_ks(M, N, K, tr))
@@ -158,6 +160,8 @@ def linear_add_rmsnorm2(a, w, h, w_post, w_next, eps, out=None, o_ws=None):
                 out = _out(out, h.shape, h.dtype, h.device)
                 _k().add_rmsnorm2_part(h, ws, ks, w_post, w_next, out, float(eps))
                 return out
+            o = linear(a, w, out=o_ws, choice=c)
+            return add_rmsnorm2(h, o, w_post, w_next, eps, out=out)
     o = linear(a, w, out=o_ws)
     return add_rmsnorm2(h, o, w_post, w_next, eps, out=out)
 

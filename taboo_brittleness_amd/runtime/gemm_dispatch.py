@@ -100,13 +100,16 @@ def choose(M: int, N: int, K: int, epi: int = 0) -> Choice:
     return "blas"
 
 
-def has_entry(N: int, K: int, epi: int) -> bool:
-    """Whether the loaded dispatch table measured ``(N, K, epi)`` (auto mode)."""
+def has_entry(N: int, K: int, epi: int, M: Optional[int] = None) -> bool:
+    """Whether the loaded dispatch table measured ``(N, K, epi)`` (auto mode), up to row count ``M`` if given."""
     if _state["mode"] != "auto":
         return False
     if not _state["loaded"]:
         load_table()
-    return _state["table"] is not None and (N, K, epi) in _state["table"]
+    tab = _state["table"]
+    if tab is None or (N, K, epi) not in tab:
+        return False
+    return M is None or M <= tab[(N, K, epi)][0][-1]
 
 
 def describe() -> dict:

@@ -93,7 +93,7 @@ def main():
         if name == "gu":
             idx = ops.geglu_interleave_index(N // 2, dev)
             Wi = [w.index_select(0, idx).contiguous() for w in Ws]
-        for epi in ([0, 3] if name == "gu" else [0, 4] if name == "qkv" else [0]):
+        for epi in ([0, 3] if name == "gu" else [0, 4] if name == "qkv" else [0, 5] if name in ("o", "down") else [0]):
             rows = []
             for M in Ms:
                 A = (torch.rand(M, K, device=dev, generator=g) * 2 - 1).to(torch.bfloat16)
@@ -125,6 +125,33 @@ def main():
                     for ch in [c_ for c_ in args.kernels.split(",") if c_.startswith("g")]:
                         var[ch] = (lambda r_: lambda: k.gemm4_qkv_rope(A, nxt(Ws), pos, slot, cos_t, sin_t, q, kc, vc,
                                                                        Hq, Hkv, r_))(int(ch[1:]))
+                elif epi == 5:
+                    # o_proj / down + the block's add_rmsnorm2 (ops.linear_add_rmsnorm2): split-K partials are summed
+                    # inside the norm pass, every other variant stores bf16 o first
+                    D = N
+                    h0 = (torch.rand(M, D, device=dev, generator=g) * 2 - 1).to(torch.bfloat16)
+                    wp = (torch.rand(D, device=dev, generator=g) * 0.2 - 0.1).to(torch.bfloat16)
+                    xo = torch.empty(M, D, device=dev, dtype=torch.bfloat16)
+                    wsp = {}
+
+                    def norm_var(ch_):
+                        if ch_ == "blas":
+                            return lambda: (torch.matmul(A, nxt(Ws).t(), out=C), k.add_rmsnorm2(h0, C, wp, wp, xo, 1e-6))
+                        if ch_[0] == "k":
+                            tr = int(ch_[1:])
+                            ks = int(k.gemm4_splitk_ks(M, N, K, tr))
+                            wsp[ch_] = torch.empty(ks * M * N, device=dev)
+                            return lambda: k.add_rmsnorm2_part(h0, wsp[ch_], int(k.gemm4_splitk_part(A, nxt(Ws), wsp[ch_], tr, ks)),
+                                                               wp, wp, xo, 1e-6)
+                        if ch_ == "s":
+                            return lambda: (k.gemm_skinny(A, nxt(Ws), C), k.add_rmsnorm2(h0, C, wp, wp, xo, 1e-6))
+                        c_ = ch_ if ch_[0] == "g" else int(ch_)
+                        return lambda: (ops.tb_gemm(A, nxt(Ws), C, None, None, 0, c_), k.add_rmsnorm2(h0, C, wp, wp, xo, 1e-6))
+                    var = {"blas": norm_var("blas")}
+                    for ch in args.kernels.split(","):
+                        if ch == "s" and not k.gemm_skinny_ok(M, N, K):
+                            continue
+                        var[ch] = norm_var(ch)
                 elif epi == 0:
                     var = {"blas": lambda: torch.matmul(A, nxt(Ws).t(), out=C)}
                 else:
@@ -133,7 +160,7 @@ def main():
                         ops.geglu(G, out=C)
                     var = {"blas": blas_geglu}
                 wsrc = Wi if epi == 3 else Ws
-                for ch in (args.kernels.split(",") if epi != 4 else []):
+                for ch in (args.kernels.split(",") if epi not in (4, 5) else []):
                     if ch == "s":          # csrc/skinny.hip (M <= 64, plain bf16 only)
                         if epi == 0 and k.gemm_skinny_ok(M, N, K):
                             var["s"] = lambda: k.gemm_skinny(A, nxt(Ws), C)
