@@ -24,15 +24,7 @@ int tb_attention_lds_bytes(int HD);
 void tb_attention(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, uint16_t* out, const int32_t* pos,
                   const int32_t* slot, int B, int T, int Hq, int Hkv, int HD, int S, float scale, float softcap,
                   int window, hipStream_t st, const uint16_t* pkc = nullptr, const uint16_t* pvc = nullptr,
-                  const int32_t* pslot = nullptr, const int32_t* plen = nullptr, const float* xm = nullptr,
-                  const float* xl = nullptr, const float* xo = nullptr);
-// Shared-prefix (cascade) pass of the decode attention (G = 2, S <= tb_attn_prefix_max_S()): per chunk of
-// rows sharing a prefix slot, (max, sum, unnormalised O) over keys [0, plen[row]) -> tb_attention's xm/xl/xo.
-int tb_attn_prefix_max_S();
-void tb_attn_prefix_partial(const uint16_t* q, const uint16_t* pkc, const uint16_t* pvc, const int32_t* chunks,
-                            const int32_t* nchunks, int max_chunks, const int32_t* plen, const int32_t* pos, int nb,
-                            int Hq, int Hkv, int HD, int S, float scale, float softcap, int window, float* out_m,
-                            float* out_l, float* out_o, hipStream_t st);
+                  const int32_t* pslot = nullptr, const int32_t* plen = nullptr);
 // blk [nblk, bw]: (first row, rows, slot) (bw = 3) or + (prefix slot, prefix length) (bw = 5, keys below the
 // prefix length read from that slot of pkc/pvc).
 void tb_attention_varlen(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, uint16_t* out, const int32_t* pos,
@@ -81,14 +73,6 @@ void tb_gemm4(const uint16_t* A, const uint16_t* W, void* C, const float* bias, 
 bool tb_gemm_pp_ok(int M, int N, int K);
 void tb_gemm_pp(const uint16_t* A, const uint16_t* W, void* C, const float* bias, const float* thr, int M, int N,
                 int K, int ldc, int epi, int tile_rows, hipStream_t st);
-// vocab head on the ping-pong GEMM: part [M, N/128] float4 workspace; tgt/tgt_logit[M]/nll_tgt all set or all null
-void tb_head_fused(const uint16_t* A, const uint16_t* W, float* part, const uint16_t* ctab, const int32_t* tgt,
-                   float* tgt_logit, int32_t* nxt, float* nll_self, float* nll_tgt, int M, int N, int K,
-                   hipStream_t st);
-const uint16_t* tb_find_softcap_table(float cap);
-// logit-lens unembedding on the ping-pong GEMM: bf16 logits [M, N] + per-row log-sum-exp (part: M*N/32 floats)
-void tb_lens_gemm(const uint16_t* A, const uint16_t* W, uint16_t* logits, float* part, float* lse, int M, int N, int K,
-                  hipStream_t st);
 void tb_gemm_nt(const uint16_t* A, const uint16_t* W, void* C, const float* bias, const float* thr, int M, int N,
                 int K, int ldc, int epi, hipStream_t st);
 void tb_lowrank_edit(uint16_t* h, uint16_t* x_next, const uint8_t* apply, const int32_t* idx, const int32_t* cnt,

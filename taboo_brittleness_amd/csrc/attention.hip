@@ -377,8 +377,7 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
     uint16_t* __restrict__ out, const int32_t* __restrict__ pos, const int32_t* __restrict__ slot, int Hq, int Hkv,
     int S, float scale, float softcap, int window, const uint16_t* __restrict__ pkc, const uint16_t* __restrict__ pvc,
-    const int32_t* __restrict__ pslot, const int32_t* __restrict__ plen, const float* __restrict__ xm,
-    const float* __restrict__ xl, const float* __restrict__ xo) {
+    const int32_t* __restrict__ pslot, const int32_t* __restrict__ plen) {
   constexpr int KS = HD / 32;
   constexpr int DPL = HD / 64;            // output dims per lane in the PV phase
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -389,7 +388,7 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(
   const int p = pos[b];
   const int SS = (S + 15) & ~15;                             // score row stride (whole 16-key tiles)
   float* opart = sc + G * SS;                                 // [4][G][HD]
-  float* stat = opart + 4 * G * HD;                           // [G] max, [G] 1/sum, [G] prefix-partial scale
+  float* stat = opart + 4 * G * HD;                           // [G] max, [G] 1/sum
   uint16_t* ob = out + ((size_t)b * Hq + kh * G) * HD;
   if (p < 0) {   // padding row
     for (int e = threadIdx.x; e < G * HD; e += blockDim.x) ob[e] = 0;
@@ -415,11 +414,7 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(
       vpre = pvc + po;
     }
   }
-  // External prefix partial (attn_prefix_partial_kernel, one pass per chunk of rows sharing the prefix):
-  // keys [0, np) are already reduced to (max, sum, unnormalised O) per head; this kernel only scores the
-  // row's own keys [np, kmax] and merges.
-  const bool ext = xo != nullptr && np > 0;
-  const int own_lo = ext ? min(max(kmin, np), kmax + 1) : kmin;
+  const int own_lo = kmin;
   // Q fragments: row = col (only rows < G real)
   bf16x8 qa[KS];
   {
@@ -466,22 +461,11 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(
     float m = -INFINITY;
     for (int j = lo + lane; j <= hi; j += 64) m = fmaxf(m, sh[j]);
     m = wave_max(m);
-    float xs = 0.f, xsum = 0.f;
-    if (ext) {
-      const size_t xi = (size_t)b * Hq + kh * G + wid;
-      const float mp = xm[xi];
-      const float mm = fmaxf(m, mp);
-      if (mm > -INFINITY) {
-        xs = mp > -INFINITY ? __expf(mp - mm) : 0.f;
-        xsum = xl[xi] * xs;
-        m = mm;
-      }
-    }
     float l = 0.f;
     if (m > -INFINITY)
       for (int j = lo + lane; j <= hi; j += 64) l += rbf(__expf(sh[j] - m));
-    l = wave_sum(l) + xsum;
-    if (lane == 0) { stat[wid] = m; stat[G + wid] = l > 0.f ? 1.f / l : 0.f; stat[2 * G + wid] = xs; }
+    l = wave_sum(l);
+    if (lane == 0) { stat[wid] = m; stat[G + wid] = l > 0.f ? 1.f / l : 0.f; }
   }
   __syncthreads();
   // PV: wave w takes keys [j0, j1): prefetched rows from registers, the rest streamed
@@ -527,7 +511,6 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(
   for (int e = threadIdx.x; e < G * HD; e += blockDim.x) {
     const int h = e / HD;
     float v = opart[e] + opart[G * HD + e] + opart[2 * G * HD + e] + opart[3 * G * HD + e];
-    if (ext) v += xo[((size_t)b * Hq + kh * G) * HD + e] * stat[2 * G + h];
     ob[e] = f2bf(v * stat[G + h]);
   }
 }
@@ -711,170 +694,7 @@ __global__ void __launch_bounds__(256) attn_decode_wave_kernel(
   }
 }
 
-// ---------------------------------------------------------------------------
-// Shared-prefix ("cascade") pass of the decode attention.  Prefix-shared sweep cells of one pair read the
-// same leading keys (the pair's baseline KV); instead of every row streaming them, one workgroup takes a
-// chunk of <= 8 decode rows of one pair x one kv head and reads the prefix K/V once for all of them: the
-// chunk's 8 x G = 16 query rows are ONE 16-row MFMA tile per 16 keys (v_mfma_f32_16x16x32_bf16), P V runs on
-// the VALU from an LDS copy of V (staged through registers while the scores are computed).  Output per
-// (row, q head): m = max score, l = sum rbf(exp(s - m)), O = sum rbf(exp(s - m)) v (fp32, unnormalised)
-// over keys [0, plen[row]); attn_decode_kernel merges them with the row's own keys.
-// Chunk records [slot, nrows, row0..row7] are sorted by their first (smallest) row, so the chunks a
-// row bucket needs (rows < nb) are a prefix of the table; workgroups grid-stride over them.
-constexpr int PC_ROWS = 8;
-constexpr int PC_W = 2 + PC_ROWS;
 
-template <int HD, int G, int NV>
-__global__ void __launch_bounds__(256) attn_prefix_partial_kernel(
-    const uint16_t* __restrict__ q, const uint16_t* __restrict__ pkc, const uint16_t* __restrict__ pvc,
-    const int32_t* __restrict__ chunks, const int32_t* __restrict__ nchunks, const int32_t* __restrict__ plen,
-    const int32_t* __restrict__ pos, int nb, int Hq, int Hkv, int S, float scale, float softcap, int window,
-    float* __restrict__ out_m, float* __restrict__ out_l, float* __restrict__ out_o) {
-  static_assert(PC_ROWS * G == 16, "one 16-row MFMA tile per chunk");
-  constexpr int KS = HD / 32;
-  constexpr int DPL = HD / 64;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int SS = (S + 15) & ~15;
-  float* sc = reinterpret_cast<float*>(smem);                          // [16][SS] scores -> probabilities
-  uint16_t* vl = reinterpret_cast<uint16_t*>(sc + 16 * SS);            // [SS][HD] prefix V
-  float* st = reinterpret_cast<float*>(vl + (size_t)SS * HD);          // [16] m, [16] l
-  int* ci = reinterpret_cast<int*>(st + 32);                           // [8] row, [8] len, [8] kmin, slot
-  const int kh = blockIdx.y;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, grp = lane >> 4, col = lane & 15;
-  const float inv_cap = softcap > 0.f ? 1.f / softcap : 0.f;
-  const int nch = *nchunks;
-  for (int c = blockIdx.x; c < nch; c += gridDim.x) {
-    const int32_t* cr = chunks + (size_t)c * PC_W;
-    if (cr[2] >= nb) break;                      // sorted by first row: the rest lie outside this bucket
-    __syncthreads();                             // LDS of the previous chunk is free
-    if (threadIdx.x < PC_ROWS) {
-      const int r = threadIdx.x;
-      int row = -1, n = 0, km = 0;
-      if (r < cr[1]) {
-        row = cr[2 + r];
-        const int p = row < nb ? pos[row] : -1;
-        if (p >= 0) {
-          const int kmax = p < S ? p : S - 1;
-          n = min(plen[row], kmax + 1);
-          if (window > 0) km = max(0, p - window + 1);
-          if (n <= km) n = 0;                    // window hides the prefix: empty partial (m = -inf)
-        } else {
-          row = -1;                              // outside the row bucket / padding: not computed at all
-        }
-      }
-      ci[r] = row; ci[PC_ROWS + r] = n; ci[2 * PC_ROWS + r] = km;
-    }
-    if (threadIdx.x == 0) ci[3 * PC_ROWS] = cr[0];
-    __syncthreads();
-    int L = 0;
-#pragma unroll
-    for (int r = 0; r < PC_ROWS; ++r) L = max(L, ci[PC_ROWS + r]);
-    const size_t base = ((size_t)ci[3 * PC_ROWS] * Hkv + kh) * (size_t)S * HD;
-    const uint16_t* kb = pkc + base;
-    const uint16_t* vb = pvc + base;
-    // V[0, L) -> registers now, LDS after the scores (the loads overlap the score phase)
-    const int nvc = L * (HD / 8);
-    uint4 vreg[NV];
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int e = threadIdx.x + i * 256;
-      vreg[i] = e < nvc ? reinterpret_cast<const uint4*>(vb)[e] : make_uint4(0, 0, 0, 0);
-    }
-    bf16x8 qa[KS];
-    {
-      const int row = ci[col / G];
-      const uint16_t* qrow = q + ((size_t)(row < 0 ? 0 : row) * Hq + kh * G + col % G) * HD;
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        uint4 u = {0, 0, 0, 0};
-        if (row >= 0) u = *reinterpret_cast<const uint4*>(qrow + ks * 32 + grp * 8);
-        qa[ks] = as_bf16x8(u);
-      }
-    }
-    const int nt = (L + 15) >> 4;
-    for (int t = wid; t < nt; t += 4) {
-      const int kk = t * 16 + col;
-      const int kr = kk < L ? kk : L - 1;
-      const uint16_t* krow = kb + (size_t)kr * HD + grp * 8;
-      uint4 kf[KS];
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) kf[ks] = *reinterpret_cast<const uint4*>(krow + ks * 32);
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[ks], as_bf16x8(kf[ks]), acc, 0, 0, 0);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {              // C row = query row 4*grp + i, C col = key
-        const int qr = 4 * grp + i, r = qr / G;
-        float s = acc[i] * scale;
-        if (softcap > 0.f) s = tanhf(s * inv_cap) * softcap;
-        const bool ok = kk < ci[PC_ROWS + r] && kk >= ci[2 * PC_ROWS + r];
-        sc[qr * SS + kk] = ok ? s : -INFINITY;
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int e = threadIdx.x + i * 256;
-      if (e < nvc) reinterpret_cast<uint4*>(vl)[e] = vreg[i];
-    }
-    __syncthreads();
-    // softmax statistics: wave w owns query rows 4w .. 4w+3 (and their P V below)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int qr = 4 * wid + i;
-      float* sh = sc + qr * SS;
-      float m = -INFINITY;
-      for (int j = lane; j < L; j += 64) m = fmaxf(m, sh[j]);
-      m = wave_max(m);
-      float l = 0.f;
-      for (int j = lane; j < L; j += 64) {
-        const float p = m > -INFINITY ? rbf(__expf(sh[j] - m)) : 0.f;
-        sh[j] = p;
-        l += p;
-      }
-      l = wave_sum(l);
-      if (lane == 0) { st[qr] = m; st[16 + qr] = l; }
-    }
-    float o[4][DPL];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int d = 0; d < DPL; ++d) o[i][d] = 0.f;
-    for (int j = 0; j < L; ++j) {
-      float vf[DPL];
-      if (DPL == 4) {
-        const uint2 w = *reinterpret_cast<const uint2*>(vl + (size_t)j * HD + lane * 4);
-        vf[0] = __uint_as_float(w.x << 16); vf[1] = __uint_as_float(w.x & 0xffff0000u);
-        vf[2] = __uint_as_float(w.y << 16); vf[3] = __uint_as_float(w.y & 0xffff0000u);
-      } else {
-#pragma unroll
-        for (int d = 0; d < DPL; ++d) vf[d] = bf2f(vl[(size_t)j * HD + lane * DPL + d]);
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float p = sc[(4 * wid + i) * SS + j];
-#pragma unroll
-        for (int d = 0; d < DPL; ++d) o[i][d] += p * vf[d];
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int qr = 4 * wid + i;
-      const int row = ci[qr / G];
-      if (row < 0) continue;
-      const size_t oi = (size_t)row * Hq + kh * G + qr % G;
-      float* dst = out_o + oi * HD + lane * DPL;
-#pragma unroll
-      for (int d = 0; d < DPL; ++d) dst[d] = o[i][d];
-      if (lane == 0) { out_m[oi] = st[qr]; out_l[oi] = st[16 + qr]; }
-    }
-  }
-}
-
-// TB_ATTN_DECODE_LEGACY=1 keeps the 4-waves-per-head decode kernel (A/B switch)
-inline bool decode_legacy() {
-  static const int v = [] { const char* e = getenv("TB_ATTN_DECODE_LEGACY"); return e && e[0] == '1' ? 1 : 0; }();
-  return v != 0;
-}
 // TB_ATTN_XCD=1: XCD-contiguous row blocks in the decode kernel (A/B switch)
 inline int decode_xcd_rows() {
   static const int v = [] { const char* e = getenv("TB_ATTN_XCD"); return e && e[0] == '1' ? 1 : 0; }();
@@ -885,8 +705,8 @@ template <int HD, int G>
 void launch_attn_decode(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, uint16_t* out, const int32_t* pos,
                         const int32_t* slot, int B, int Hq, int Hkv, int S, float scale, float softcap, int window,
                         const uint16_t* pkc, const uint16_t* pvc, const int32_t* pslot, const int32_t* plen,
-                        const float* xm, const float* xl, const float* xo, hipStream_t st) {
-  if (xo == nullptr && S <= 2048 && !decode_legacy()) {
+                        hipStream_t st) {
+  if (S <= 2048) {
     const int nwh = Hkv % 4 == 0 ? 4 : (Hkv % 2 == 0 ? 2 : 1);
     const size_t lds_w = (size_t)nwh * G * ((S + 15) & ~15) * sizeof(float);
     hipLaunchKernelGGL((attn_decode_wave_kernel<HD, G>), dim3(B, Hkv / nwh), dim3(64 * nwh), lds_w, st, q, kc, vc, out,
@@ -901,7 +721,7 @@ void launch_attn_decode(const uint16_t* q, const uint16_t* kc, const uint16_t* v
     attr_set = lds;
   }
   hipLaunchKernelGGL((attn_decode_kernel<HD, G>), dim3(B, Hkv), dim3(256), lds, st, q, kc, vc, out, pos, slot, Hq,
-                     Hkv, S, scale, softcap, window, pkc, pvc, pslot, plen, xm, xl, xo);
+                     Hkv, S, scale, softcap, window, pkc, pvc, pslot, plen);
 }
 
 }  // namespace
@@ -909,14 +729,14 @@ void launch_attn_decode(const uint16_t* q, const uint16_t* kc, const uint16_t* v
 void tb_attention(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, uint16_t* out, const int32_t* pos,
                   const int32_t* slot, int B, int T, int Hq, int Hkv, int HD, int S, float scale, float softcap,
                   int window, hipStream_t st, const uint16_t* pkc, const uint16_t* pvc, const int32_t* pslot,
-                  const int32_t* plen, const float* xm, const float* xl, const float* xo) {
+                  const int32_t* plen) {
   if (B <= 0 || T <= 0) return;
   const int G = Hq / Hkv;
   if (T == 1 && S <= 8192) {
 #define TB_DEC_CASE(hd, g)                                                                                   \
   if (HD == hd && G == g) {                                                                                  \
     launch_attn_decode<hd, g>(q, kc, vc, out, pos, slot, B, Hq, Hkv, S, scale, softcap, window, pkc, pvc,    \
-                              pslot, plen, xm, xl, xo, st);                                                  \
+                              pslot, plen, st);                                                              \
     return;                                                                                                  \
   }
     TB_DEC_CASE(256, 2)
@@ -961,23 +781,3 @@ void tb_attention_varlen(const uint16_t* q, const uint16_t* kc, const uint16_t* 
 #undef TB_VL_CASE
 }
 
-int tb_attn_prefix_max_S() { return 80; }
-
-void tb_attn_prefix_partial(const uint16_t* q, const uint16_t* pkc, const uint16_t* pvc, const int32_t* chunks,
-                            const int32_t* nchunks, int max_chunks, const int32_t* plen, const int32_t* pos, int nb,
-                            int Hq, int Hkv, int HD, int S, float scale, float softcap, int window, float* out_m,
-                            float* out_l, float* out_o, hipStream_t st) {
-  if (nb <= 0 || max_chunks <= 0) return;
-  const int SS = (S + 15) & ~15;
-  const size_t lds = (size_t)16 * SS * sizeof(float) + (size_t)SS * HD * sizeof(uint16_t) + 32 * sizeof(float) +
-                     (3 * PC_ROWS + 1) * sizeof(int);
-  const dim3 grid(max_chunks < 256 ? max_chunks : 256, Hkv);
-  // NV = 16-B V chunks per thread: L <= 80 keys x HD / 8 / 256 threads
-  if (HD == 256) {
-    hipLaunchKernelGGL((attn_prefix_partial_kernel<256, 2, 10>), grid, dim3(256), lds, st, q, pkc, pvc, chunks,
-                       nchunks, plen, pos, nb, Hq, Hkv, S, scale, softcap, window, out_m, out_l, out_o);
-  } else {
-    hipLaunchKernelGGL((attn_prefix_partial_kernel<128, 2, 5>), grid, dim3(256), lds, st, q, pkc, pvc, chunks,
-                       nchunks, plen, pos, nb, Hq, Hkv, S, scale, softcap, window, out_m, out_l, out_o);
-  }
-}

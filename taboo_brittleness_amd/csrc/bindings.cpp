@@ -141,12 +141,9 @@ void attention(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch::Tenso
 
 void attention_prefix(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch::Tensor out, torch::Tensor pos,
                       torch::Tensor slot, int64_t B, double scale, double softcap, int64_t window, torch::Tensor pk,
-                      torch::Tensor pv, torch::Tensor pslot, torch::Tensor plen,
-                      c10::optional<torch::Tensor> xm, c10::optional<torch::Tensor> xl,
-                      c10::optional<torch::Tensor> xo) {
+                      torch::Tensor pv, torch::Tensor pslot, torch::Tensor plen) {
   IN_BF16(q); IN_BF16(kc); IN_BF16(vc); IN_BF16(out); IN_I32(pos); IN_I32(slot);
   IN_BF16(pk); IN_BF16(pv); IN_I32(pslot); IN_I32(plen);
-  const bool ext = xo.has_value() && xo->defined();
   TORCH_CHECK(kc.dim() == 4, "cache must be [slots, Hkv, S, HD]");
   const int Hkv = kc.size(1), S = kc.size(2), HD = kc.size(3);
   TORCH_CHECK(S <= 8192, "shared-prefix attention is the decode kernel (S <= 8192)");
@@ -159,41 +156,10 @@ void attention_prefix(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch
   TORCH_CHECK(pk.dim() == 4 && pk.size(1) == Hkv && pk.size(2) == S && pk.size(3) == HD && pv.sizes() == pk.sizes(),
               "prefix cache must be [P, Hkv, S, HD] like the cache");
   TORCH_CHECK(pslot.numel() >= B && plen.numel() >= B, "prefix slot/len per row");
-  const float *pm = nullptr, *pl = nullptr, *po = nullptr;
-  if (ext) {
-    IN_F32((*xo)); IN_F32((*xm)); IN_F32((*xl));
-    TORCH_CHECK(xm->numel() >= (int64_t)B * Hq && xl->numel() >= (int64_t)B * Hq &&
-                xo->numel() >= (int64_t)B * Hq * HD, "prefix partial buffers [B, Hq(, HD)]");
-    pm = xm->data_ptr<float>(); pl = xl->data_ptr<float>(); po = xo->data_ptr<float>();
-  }
   c10::DeviceGuard g(q.device());
   tb_attention(cbf(q), cbf(kc), cbf(vc), bf(out), pos.data_ptr<int32_t>(), slot.data_ptr<int32_t>(), B, 1, Hq, Hkv,
                HD, S, (float)scale, (float)softcap, (int)window, cur_stream(), cbf(pk), cbf(pv),
-               pslot.data_ptr<int32_t>(), plen.data_ptr<int32_t>(), pm, pl, po);
-}
-
-int64_t attn_prefix_max_S() { return tb_attn_prefix_max_S(); }
-
-void attn_prefix_partial(torch::Tensor q, torch::Tensor pk, torch::Tensor pv, torch::Tensor chunks,
-                         torch::Tensor nchunks, torch::Tensor plen, torch::Tensor pos, int64_t B, double scale,
-                         double softcap, int64_t window, torch::Tensor xm, torch::Tensor xl, torch::Tensor xo) {
-  IN_BF16(q); IN_BF16(pk); IN_BF16(pv); IN_I32(chunks); IN_I32(nchunks); IN_I32(plen); IN_I32(pos);
-  IN_F32(xm); IN_F32(xl); IN_F32(xo);
-  TORCH_CHECK(pk.dim() == 4 && pv.sizes() == pk.sizes(), "prefix cache must be [P, Hkv, S, HD]");
-  const int Hkv = pk.size(1), S = pk.size(2), HD = pk.size(3);
-  TORCH_CHECK(HD == 256 || HD == 128, "head dim 128 or 256");
-  TORCH_CHECK(S <= tb_attn_prefix_max_S(), "cascade prefix pass needs S <= ", tb_attn_prefix_max_S());
-  TORCH_CHECK(q.numel() % (B * HD) == 0, "q shape");
-  const int Hq = q.numel() / (B * HD);
-  TORCH_CHECK(Hq == 2 * Hkv, "cascade prefix pass is instantiated for GQA ratio 2");
-  TORCH_CHECK(chunks.dim() == 2 && chunks.size(1) == 10, "chunk table [C, 10]: slot, nrows, 8 rows");
-  TORCH_CHECK(nchunks.numel() == 1 && plen.numel() >= B && pos.numel() >= B, "chunk count / per-row lengths");
-  TORCH_CHECK(xm.numel() >= B * Hq && xl.numel() >= B * Hq && xo.numel() >= B * Hq * HD, "partial buffers");
-  c10::DeviceGuard g(q.device());
-  tb_attn_prefix_partial(cbf(q), cbf(pk), cbf(pv), chunks.data_ptr<int32_t>(), nchunks.data_ptr<int32_t>(),
-                         (int)chunks.size(0), plen.data_ptr<int32_t>(), pos.data_ptr<int32_t>(), (int)B, Hq, Hkv, HD,
-                         S, (float)scale, (float)softcap, (int)window, xm.data_ptr<float>(), xl.data_ptr<float>(),
-                         xo.data_ptr<float>(), cur_stream());
+               pslot.data_ptr<int32_t>(), plen.data_ptr<int32_t>());
 }
 
 void attention_varlen(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch::Tensor out, torch::Tensor pos,
@@ -538,12 +504,13 @@ void lens_gemm(torch::Tensor x, torch::Tensor W, torch::Tensor logits, torch::Te
   tb_lens_gemm4(cbf(x), cbf(W), bf(logits), part.data_ptr<float>(), lse.data_ptr<float>(), M, N, K, cur_stream());
 }
 
-// Fused vocab head (gemm.hip EPI_HEAD + head_merge): x [M, K] final-normed rows, W = lm_head [V, K]; the
-// decode_head outputs (greedy token, its NLL, optional teacher-target NLL) with no logits in HBM.
+// Fused vocab head (gemm4.hip G4_HEAD, compact exact softcap, + head_merge): x [M, K] final-normed rows,
+// W = lm_head [V, K]; the decode_head outputs (greedy token, its NLL, optional teacher-target NLL) with no
+// logits in HBM.
 // part: f32 workspace >= M * (V / 128) * 4; tgt_logit: f32 [M] (with tgt).
 void head_fused(torch::Tensor x, torch::Tensor W, torch::Tensor part, double cap, c10::optional<torch::Tensor> tgt,
                 c10::optional<torch::Tensor> tgt_logit, torch::Tensor nxt, torch::Tensor nll_self,
-                c10::optional<torch::Tensor> nll_tgt, int64_t kernel) {
+                c10::optional<torch::Tensor> nll_tgt) {
   IN_BF16(x); IN_BF16(W); IN_F32(part); IN_I32(nxt); IN_F32(nll_self);
   TORCH_CHECK(W.dim() == 2, "head_fused: W must be [V, K]");
   const int K = x.size(-1), M = x.numel() / K, N = W.size(0);
@@ -563,27 +530,15 @@ void head_fused(torch::Tensor x, torch::Tensor W, torch::Tensor part, double cap
     np = nll_tgt->data_ptr<float>();
   }
   c10::DeviceGuard g(x.device());
-  const uint16_t* tab = nullptr;
   if (cap > 0) {
-    tab = tb_find_softcap_table((float)cap);
-    TORCH_CHECK(tab != nullptr, "head_fused: softcap table for this cap not registered on this device");
+    const uint16_t* ct = nullptr;
+    int lo = 0, hi = 0;
+    float sat = 0.f;
+    TORCH_CHECK(tb_softcap_compact_params((float)cap, &ct, &lo, &hi, &sat) && hi - lo <= 2048,
+                "head_fused: no compact softcap registered for this cap on this device");
   }
-  // kernel 4: the four-wave GEMM (gemm4.hip G4_HEAD, compact softcap), otherwise the ping-pong kernel (gemm.hip
-  // EPI_HEAD, 64 KB table)
-  if (kernel == 4) {
-    if (cap > 0) {
-      const uint16_t* ct = nullptr;
-      int lo = 0, hi = 0;
-      float sat = 0.f;
-      TORCH_CHECK(tb_softcap_compact_params((float)cap, &ct, &lo, &hi, &sat) && hi - lo <= 2048,
-                  "head_fused: no compact softcap registered for this cap on this device");
-    }
-    tb_head_fused4(cbf(x), cbf(W), part.data_ptr<float>(), (float)cap, tp, tl, nxt.data_ptr<int32_t>(),
-                   nll_self.data_ptr<float>(), np, M, N, K, cur_stream());
-  }
-  else
-    tb_head_fused(cbf(x), cbf(W), part.data_ptr<float>(), tab, tp, tl, nxt.data_ptr<int32_t>(),
-                  nll_self.data_ptr<float>(), np, M, N, K, cur_stream());
+  tb_head_fused4(cbf(x), cbf(W), part.data_ptr<float>(), (float)cap, tp, tl, nxt.data_ptr<int32_t>(),
+                 nll_self.data_ptr<float>(), np, M, N, K, cur_stream());
 }
 
 void lowrank_edit(torch::Tensor h, c10::optional<torch::Tensor> x_next, torch::Tensor apply, torch::Tensor idx,
@@ -796,8 +751,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("rope_qkv_cache", &rope_qkv_cache);
   m.def("kv_fanout", &kv_fanout);
   m.def("attention", &attention);
-  m.def("attn_prefix_partial", &attn_prefix_partial);
-  m.def("attn_prefix_max_S", &attn_prefix_max_S);
   m.def("attention_prefix", &attention_prefix);
   m.def("attention_varlen", &attention_varlen);
   m.def("attention_varlen_prefix", &attention_varlen_prefix);

@@ -75,9 +75,8 @@ __device__ __forceinline__ bf16x8 lds8(const char* p) {
 #endif
 }
 
-enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_JUMPRELU = 2, EPI_GEGLU = 3, EPI_HEAD = 4, EPI_LENS = 5 };
-constexpr int HEAD_COLS = 128;          // vocab columns per head partial (one wave group's half of a tile)
-constexpr int CTAB_N = 32768;           // entries of the exact bf16 softcap table (lens.hip)
+enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_JUMPRELU = 2, EPI_GEGLU = 3 };
+constexpr int HEAD_COLS = 128;          // vocab columns per head / lens partial (gemm4.hip G4_HEAD / G4_LENS)
 
 // QROWS = output rows (m) per tile: 256, or 128 for grids that would otherwise leave CUs idle (the N = 3584
 // projections at moderate M).  Every variant accumulates each output element over K in the same order with
@@ -86,9 +85,7 @@ constexpr int CTAB_N = 32768;           // entries of the exact bf16 softcap tab
 template <int EPI, int QROWS>
 __global__ void __launch_bounds__(PTHREADS, 1)
 gemm_pp_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, void* __restrict__ C,
-               const float* __restrict__ bias, const float* __restrict__ thr, int M, int N, int K, int ldc,
-               const uint16_t* __restrict__ ctab, const int32_t* __restrict__ tgt, float* __restrict__ tgt_logit,
-               float4* __restrict__ lpart) {
+               const float* __restrict__ bias, const float* __restrict__ thr, int M, int N, int K, int ldc) {
   static_assert(QROWS == 256 || QROWS == 128, "tile rows");
   static_assert(QROWS == 256 || !PP_MFMA32, "32x32 MFMA lab build: 256-row tiles only");
   constexpr int QW = QROWS / 4;          // output rows per wave (64 | 32)
@@ -348,76 +345,7 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, v
 #define E_N(qm, g) (n0 + grp * 128 + (qm) * 64 + (g) * 16 + 4 * (lane >> 4))
 #define E_V(qm, qn, rj, g, r) acc[qm][qn][g][rj][r]
 #endif
-  if constexpr (EPI == EPI_HEAD || EPI == EPI_LENS) {
-    // Vocab head: the bf16 logits (acc rounded like the bf16 GEMM output), then the exact
-    // bf16 final softcap by table (staged into the now idle staging LDS), reduced per (row, 128-column
-    // half-tile) to {max, sum exp(z - max), first argmax}; the row's teacher-target logit is written by the
-    // one lane that holds it.  head_merge_kernel folds the N/128 partials of a row.  No logit reaches HBM.
-    // Logit lens (EPI_LENS): no softcap; the bf16 logits ARE stored (the lens colsum / gathers
-    // read them) and the same per-slice {max, sum exp} partials go to lpart, so no row_lse pass is needed.
-    const uint16_t* ct = nullptr;
-    if constexpr (EPI == EPI_HEAD) {
-      __syncthreads();                     // every wave is past its last ds_read of the main loop
-      uint16_t* ctw = reinterpret_cast<uint16_t*>(smem);
-      if (ctab != nullptr) {
-        for (int i = tid; i < CTAB_N / 8; i += PTHREADS)
-          reinterpret_cast<uint4*>(ctw)[i] = reinterpret_cast<const uint4*>(ctab)[i];
-        ct = ctw;
-      }
-      __syncthreads();
-    }
-    float4* part = EPI == EPI_HEAD ? reinterpret_cast<float4*>(C) : lpart;
-    const int npart = N / HEAD_COLS, pcol = n0 / HEAD_COLS + grp;
-    constexpr int NZ = 2 * E_G * 4;
-#pragma unroll
-    for (int qn = 0; qn < 2; ++qn)
-#pragma unroll
-      for (int rj = 0; rj < E_RJ; ++rj) {
-        const int m = E_M(qn, rj);
-        const int t = (tgt != nullptr && m < M) ? tgt[m] : -1;
-        float z[NZ];
-        float mx = -INFINITY;
-        int bi = 0x7fffffff;
-#pragma unroll
-        for (int qm = 0; qm < 2; ++qm)
-#pragma unroll
-          for (int g = 0; g < E_G; ++g)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const uint32_t b = f2bf(E_V(qm, qn, rj, g, r));
-              const float v = ct != nullptr ? __uint_as_float(((uint32_t)ct[b & 0x7fffu] | (b & 0x8000u)) << 16)
-                                            : __uint_as_float(b << 16);
-              const int n = E_N(qm, g) + r;
-              z[(qm * E_G + g) * 4 + r] = v;
-              if (v > mx || (v == mx && n < bi)) { mx = v; bi = n; }
-              if (EPI == EPI_HEAD && n == t) tgt_logit[m] = v;
-            }
-        if constexpr (EPI == EPI_LENS) {
-          if (m < M) {
-#pragma unroll
-            for (int qm = 0; qm < 2; ++qm)
-#pragma unroll
-              for (int g = 0; g < E_G; ++g) {
-                const float* zz = z + (qm * E_G + g) * 4;
-                *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(C) + (size_t)m * ldc + E_N(qm, g)) =
-                    make_uint2(pack2(zz[0], zz[1]), pack2(zz[2], zz[3]));
-              }
-          }
-        }
-        float s = 0.f;
-#pragma unroll
-        for (int e = 0; e < NZ; ++e) s += __expf(z[e] - mx);
-#pragma unroll
-        for (int o = E_LO; o <= 32; o <<= 1) {
-          const float m2 = __shfl_xor(mx, o, 64), s2 = __shfl_xor(s, o, 64);
-          const int i2 = __shfl_xor(bi, o, 64);
-          if (m2 > mx) { s = s * __expf(mx - m2) + s2; mx = m2; bi = i2; }
-          else if (m2 == mx) { s += s2; bi = min(bi, i2); }
-          else { s += s2 * __expf(m2 - mx); }
-        }
-        if (lane < E_LO && m < M) part[(size_t)m * npart + pcol] = make_float4(mx, s, __int_as_float(bi), 0.f);
-      }
-  } else if constexpr (EPI == EPI_GEGLU) {
+  if constexpr (EPI == EPI_GEGLU) {
     // P rows are gate (qm = 0) / up (qm = 1) of feature E_N(0, g) - n0/2 - grp*64 + r; the gate|up values are
     // rounded to bf16 first so the result equals geglu(bf16 gate|up GEMM output)
     uint16_t* out = reinterpret_cast<uint16_t*>(C);
@@ -482,17 +410,13 @@ bool tb_gemm_pp_ok(int M, int N, int K) { return M > 0 && N > 0 && N % PBN == 0 
 
 #define PP_LAUNCH_T(E_, Q_)                                                                                        \
   hipLaunchKernelGGL((gemm_pp_kernel<E_, Q_>), dim3((N / PBN) * ((M + (Q_) - 1) / (Q_))), dim3(PTHREADS), 0, st, A, W, \
-                     C, bias, thr, M, N, K, ldc, ctab, tgt, tgt_logit, lpart)
+                     C, bias, thr, M, N, K, ldc)
 #define PP_LAUNCH(E_) PP_LAUNCH_T(E_, 256)
 
 // tile_rows: 256 or 128 (output rows per tile; identical numerics, see gemm_pp_kernel)
 void tb_gemm_pp(const uint16_t* A, const uint16_t* W, void* C, const float* bias, const float* thr, int M, int N,
                 int K, int ldc, int epi, int tile_rows, hipStream_t st) {
   if (M <= 0 || N <= 0) return;
-  const uint16_t* ctab = nullptr;
-  const int32_t* tgt = nullptr;
-  float* tgt_logit = nullptr;
-  float4* lpart = nullptr;
   if (tile_rows == 128) {
     switch (epi) {
       case EPI_BF16: PP_LAUNCH_T(EPI_BF16, 128); break;
@@ -566,32 +490,3 @@ void tb_head_merge(const float* part, int npart, const int32_t* tgt, const float
                      tgt_logit, nxt, nll_self, nll_tgt, lse, V);
 }
 
-void tb_head_fused(const uint16_t* A, const uint16_t* W, float* part, const uint16_t* ctab, const int32_t* tgt,
-                   float* tgt_logit, int32_t* nxt, float* nll_self, float* nll_tgt, int M, int N, int K,
-                   hipStream_t st) {
-  if (M <= 0) return;
-  const float* bias = nullptr;
-  const float* thr = nullptr;
-  void* C = part;
-  const int ldc = 0;
-  float4* lpart = nullptr;
-  PP_LAUNCH(EPI_HEAD);   // tgt / tgt_logit / nll_tgt are all set or all null (host-checked)
-  hipLaunchKernelGGL(head_merge_kernel, dim3(M), dim3(256), 0, st, reinterpret_cast<const float4*>(part),
-                     N / HEAD_COLS, tgt, tgt_logit, nxt, nll_self, nll_tgt, nullptr, N);
-}
-
-void tb_lens_gemm(const uint16_t* A, const uint16_t* W, uint16_t* logits, float* part, float* lse, int M, int N, int K,
-                  hipStream_t st) {
-  if (M <= 0) return;
-  const float* bias = nullptr;
-  const float* thr = nullptr;
-  void* C = logits;
-  const int ldc = N;
-  const uint16_t* ctab = nullptr;
-  const int32_t* tgt = nullptr;
-  float* tgt_logit = nullptr;
-  float4* lpart = reinterpret_cast<float4*>(part);
-  PP_LAUNCH(EPI_LENS);
-  hipLaunchKernelGGL(head_merge_kernel, dim3(M), dim3(256), 0, st, reinterpret_cast<const float4*>(part),
-                     N / HEAD_COLS, nullptr, nullptr, nullptr, nullptr, nullptr, lse, N);
-}

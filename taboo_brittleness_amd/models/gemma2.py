@@ -85,19 +85,9 @@ class KVPrefix:
     len_lo: torch.Tensor    # [B] int32
     len_hi: torch.Tensor    # [B] int32
     split: int
-    # cascade pass (GPU, optional): chunk table [C, 10] of rows sharing a prefix slot, its live count [1], and
-    # the per-(row, q head) prefix partials (max, sum, unnormalised O) the decode kernel merges
-    chunks: Optional[torch.Tensor] = None
-    nchunks: Optional[torch.Tensor] = None
-    xm: Optional[torch.Tensor] = None
-    xl: Optional[torch.Tensor] = None
-    xo: Optional[torch.Tensor] = None
 
     def layer(self, l: int, B: int):
         n = self.len_lo if l <= self.split else self.len_hi
-        if self.chunks is not None:
-            return (self.k[l], self.v[l], self.slot[:B], n[:B],
-                    (self.chunks, self.nchunks, self.xm, self.xl, self.xo))
         return (self.k[l], self.v[l], self.slot[:B], n[:B])
 
 

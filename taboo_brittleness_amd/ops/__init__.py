@@ -74,9 +74,6 @@ def softcap_compact_split(tab: torch.Tensor, cap: float):
     return lo, hi, sat
 
 
-COMPACT_SOFTCAP = os.environ.get("TB_COMPACT_SOFTCAP", "1") == "1"
-
-
 def softcap_values(v: torch.Tensor, cap: float) -> torch.Tensor:
     """fp32 values of the exact bf16 final softcap of bf16 logits ``v`` (any shape): the registered table on the
     GPU (bit-identical to the vocab kernels), the reference op on the CPU."""
@@ -85,7 +82,7 @@ def softcap_values(v: torch.Tensor, cap: float) -> torch.Tensor:
     if v.is_cuda:
         _softcap_table(cap, v.device)
         y = torch.empty(v.shape, dtype=torch.float32, device=v.device)
-        if COMPACT_SOFTCAP and _k().softcap_compact(v.contiguous(), y, float(cap)):
+        if _k().softcap_compact(v.contiguous(), y, float(cap)):     # compact exact form (csrc/lens.hip)
             return y
         tab = _CAP_TABLES[(float(cap), v.device.index if v.device.index is not None else torch.cuda.current_device())]
         b = v.contiguous().view(torch.int16).to(torch.int32)
@@ -273,16 +270,8 @@ def attention(q, kc, vc, pos, slot, B, T, scale, softcap, window, out=None, pref
         if prefix is not None:
             assert T == 1, "shared-prefix attention is decode-only"
             pk, pv, ps, pl = prefix[:4]
-            casc = prefix[4] if len(prefix) > 4 else None
-            if casc is not None:        # cascade: the pair prefix once per chunk of rows, then own keys + merge
-                chunks, nch, xm, xl, xo = casc
-                _k().attn_prefix_partial(q, pk, pv, chunks, nch, pl, pos, int(B), float(scale), float(softcap),
-                                         int(window), xm, xl, xo)
-                _k().attention_prefix(q, kc, vc, out, pos, slot, int(B), float(scale), float(softcap), int(window),
-                                      pk, pv, ps, pl, xm, xl, xo)
-                return out
             _k().attention_prefix(q, kc, vc, out, pos, slot, int(B), float(scale), float(softcap), int(window),
-                                  pk, pv, ps, pl, None, None, None)
+                                  pk, pv, ps, pl)
             return out
         _k().attention(q, kc, vc, out, pos, slot, int(B), int(T), float(scale), float(softcap), int(window))
         return out
@@ -292,46 +281,6 @@ def attention(q, kc, vc, pos, slot, B, T, scale, softcap, window, out=None, pref
         out.copy_(o.view_as(out))
         return out
     return o
-
-
-def attn_prefix_max_S() -> int:
-    """Longest cache (keys) the cascade prefix pass supports (its V tile lives in LDS); 0 without the
-    extension."""
-    try:
-        return int(_k().attn_prefix_max_S())
-    except Exception:
-        return 0
-
-
-def attn_prefix_chunks(pslot, plen_any, rows_per_chunk: int = 8):
-    """Host chunk table of the cascade decode-attention pass: rows with a shared prefix (``plen_any > 0``)
-    grouped by prefix slot, cut into chunks of ``rows_per_chunk`` rows (ascending), sorted by first row.
-    Returns int32 ``[C, 2 + rows_per_chunk]`` = (slot, nrows, rows..., -1 padded)."""
-    import numpy as np
-
-    ps = np.asarray(pslot, dtype=np.int64)
-    rows = np.nonzero(np.asarray(plen_any) > 0)[0]
-    if rows.size == 0:
-        return np.zeros((0, 2 + rows_per_chunk), np.int32)
-    order = np.lexsort((rows, ps[rows]))
-    rows = rows[order]
-    sl = ps[rows]
-    starts = np.concatenate([[0], np.nonzero(sl[1:] != sl[:-1])[0] + 1])
-    ends = np.concatenate([starts[1:], [rows.size]])
-    lens = ends - starts
-    nck = -(-lens // rows_per_chunk)
-    C = int(nck.sum())
-    out = np.full((C, 2 + rows_per_chunk), -1, np.int32)
-    g_of = np.repeat(np.arange(starts.size), nck)
-    k_in = np.arange(C) - np.repeat(np.cumsum(nck) - nck, nck)
-    first = starts[g_of] + k_in * rows_per_chunk
-    nr = np.minimum(rows_per_chunk, ends[g_of] - first)
-    out[:, 0] = sl[first]
-    out[:, 1] = nr
-    for j in range(rows_per_chunk):
-        ok = j < nr
-        out[ok, 2 + j] = rows[first[ok] + j]
-    return out[np.argsort(out[:, 2], kind="stable")]
 
 
 def attention_varlen(q, kc, vc, pos, slot_rows, blk, scale, softcap, window, out=None, prefix_kv=None):
@@ -493,9 +442,6 @@ def head_part_numel(rows: int, vocab: int) -> int:
     return rows * (vocab // 128) * 4
 
 
-HEAD_KERNEL = 4 if os.environ.get("TB_HEAD_KERNEL", "g4") == "g4" else 0   # fused head GEMM: gemm4.hip (default) | gemm.hip
-
-
 def vocab_head(x, w, cap, tgt=None, nxt=None, nll_self=None, nll_tgt=None, part=None, tgt_logit=None,
                fused: Optional[bool] = None):
     """``decode_head(x @ w^T, ...)`` from the final-normed rows ``x``: greedy token (bf16-softcap argmax), its
@@ -518,9 +464,9 @@ def vocab_head(x, w, cap, tgt=None, nxt=None, nll_self=None, nll_tgt=None, part=
         if tgt is not None:
             nll_tgt = _out(nll_tgt, (R,), torch.float32, dev)
             tgt_logit = _out(tgt_logit, (R,), torch.float32, dev)
-            _k().head_fused(x, w, part, float(cap), tgt, tgt_logit, nxt, nll_self, nll_tgt, HEAD_KERNEL)
+            _k().head_fused(x, w, part, float(cap), tgt, tgt_logit, nxt, nll_self, nll_tgt)
         else:
-            _k().head_fused(x, w, part, float(cap), None, None, nxt, nll_self, None, HEAD_KERNEL)
+            _k().head_fused(x, w, part, float(cap), None, None, nxt, nll_self, None)
         return nxt, nll_self, nll_tgt
     return decode_head(linear(x, w), cap, tgt, nxt, nll_self, nll_tgt)
 

@@ -1120,9 +1120,7 @@ class SweepRunner:
         divergent token of a new row, or the carry record of a carried one."""
         n = len(rows)
         kp = self.gen.kv_prefix
-        # the cascade attention (TB_ATTN_CASCADE=1, kv_prefix.chunks) reads each row's prefix in chunks the
-        # shared-prefix decode cannot fan out: plain decode then
-        if not self.trie_decode or n < 2 or kp is None or getattr(kp, "chunks", None) is not None:
+        if not self.trie_decode or n < 2 or kp is None:
             return None
         wk = max([1] + [len(cr.prefix) - cr.d for cr in rows if isinstance(cr, _Carry)])
         mat = np.full((n, 3 + wk), -2, np.int64)

@@ -109,16 +109,6 @@ class Generator:
         :class:`KVPrefix`; per-row slots/lengths are set by :meth:`decode`'s ``prefix_rows``)."""
         z = lambda: torch.zeros(self.B, dtype=torch.int32, device=self.dev)   # noqa: E731
         self.kv_prefix = KVPrefix(k, v, z(), z(), z(), split)
-        ls = self.m.lspec
-        if (self.dev.type == "cuda" and os.environ.get("TB_ATTN_CASCADE", "0") == "1" and
-                ls.heads == 2 * ls.kv_heads and self.S <= ops.attn_prefix_max_S()):
-            kp = self.kv_prefix
-            cmax = -(-self.B // 8) + k.shape[1] + 1          # chunks <= rows / 8 + one partial chunk per slot
-            kp.chunks = torch.full((cmax, 10), -1, dtype=torch.int32, device=self.dev)
-            kp.nchunks = torch.zeros(1, dtype=torch.int32, device=self.dev)
-            kp.xm = torch.zeros(self.B, ls.heads, dtype=torch.float32, device=self.dev)
-            kp.xl = torch.zeros(self.B, ls.heads, dtype=torch.float32, device=self.dev)
-            kp.xo = torch.zeros(self.B, ls.heads, ls.head_dim, dtype=torch.float32, device=self.dev)
         self._graphs.clear()
 
     # ------------------------------------------------------------------ steps
@@ -358,19 +348,9 @@ class Generator:
             if prefix_rows is None:
                 kp.len_lo.zero_()
                 kp.len_hi.zero_()
-                if kp.nchunks is not None:
-                    kp.nchunks.zero_()
             else:
                 for dst, src in zip((kp.slot, kp.len_lo, kp.len_hi), prefix_rows):
                     dst.copy_(_up(_padded(src, B, 0), self.dev), non_blocking=True)
-                if kp.chunks is not None:
-                    n_pr = min(B, len(prefix_rows[0]))
-                    anyp = (np.asarray(prefix_rows[1][:n_pr]) > 0) | (np.asarray(prefix_rows[2][:n_pr]) > 0)
-                    tab = ops.attn_prefix_chunks(np.asarray(prefix_rows[0][:n_pr]), anyp)
-                    assert tab.shape[0] <= kp.chunks.shape[0], "cascade chunk table overflow"
-                    if tab.shape[0]:
-                        kp.chunks[: tab.shape[0]].copy_(_up(tab, self.dev), non_blocking=True)
-                    kp.nchunks.fill_(int(tab.shape[0]))
         else:
             assert prefix_rows is None, "prefix_rows needs enable_kv_prefix()"
         if slots is None:
@@ -433,7 +413,6 @@ class Generator:
         share = share_keys is not None and share_split is not None
         if share:
             assert not hooks or min(hooks) >= share_split, "prefix-trie decode needs every hook at block >= split"
-            assert self.kv_prefix is None or self.kv_prefix.chunks is None, "prefix-trie decode: no cascade prefix"
             sh = self._share_bufs(int(share_split))
             keys = np.asarray(list(share_keys), np.int64)
             assert keys.size == n_rows, "share_keys: one key per row"
@@ -486,8 +465,6 @@ class Generator:
         if self.kv_prefix is not None:
             self.kv_prefix.len_lo.zero_()
             self.kv_prefix.len_hi.zero_()
-            if self.kv_prefix.nchunks is not None:
-                self.kv_prefix.nchunks.zero_()
         if self._share is not None:
             self._share["U"].zero_()          # every lo row parked
             self._share["src"].fill_(-1)

@@ -318,34 +318,6 @@ def test_sweep_gpu_cross_step_pipeline(gpu, tb_gemm):
         _assert_records_equal(out[(False, 0)], out[cfg_])
 
 
-def test_sweep_gpu_trie_with_cascade_attention(gpu, tb_gemm, monkeypatch):
-    """the prefix-trie decode (on by default) with the opt-in cascade attention (TB_ATTN_CASCADE=1,
-    kv_prefix.chunks) falls back to the plain decode instead of asserting, and gives the same records."""
-    from taboo_brittleness_amd.config import load_config
-    from taboo_brittleness_amd.interp.sae import JumpReLUSAE
-    from taboo_brittleness_amd.models.tokenizer import SyntheticTokenizer
-    from taboo_brittleness_amd.pipelines.sweep import SweepRunner
-
-    cfg = load_config(None, ["experiment.max_new_tokens=10", "intervention.budgets=[1, 4]",
-                             "intervention.random_trials=4"])
-    mg = Gemma2Model(random_gemma2(SPEC, dtype=torch.bfloat16, seed=5, norm_std=0.1, post_norm_gain=8.0,
-                                   device=gpu), gpu)
-    tok = SyntheticTokenizer(vocab_size=SPEC.vocab_size)
-    key = lambda r: (r["word"], r["prompt_idx"], r["method"], r["budget"], r["trial"])   # noqa: E731
-    out = {}
-    for casc in ("0", "1"):
-        monkeypatch.setenv("TB_ATTN_CASCADE", casc)
-        sae = JumpReLUSAE.random(SPEC.hidden, 1024, seed=2, device=gpu)
-        r = SweepRunner(cfg, mg, tok, sae, batch=64, device=gpu, layer=2, prefix_share=True, layer_resume=True,
-                        kv_pairs=8)
-        pairs = r.build_pairs(["ship"], cfg.prompts[:3])
-        r.run_baselines(pairs)
-        out[casc] = {key(x): x for x in r.run_cells(pairs, r.make_cells(pairs, ("sae_targeted", "sae_random")))}
-    assert set(out["0"]) == set(out["1"])
-    same = sum(out["0"][k]["response_ids"] == out["1"][k]["response_ids"] for k in out["0"])
-    assert same == len(out["0"]), f"{same} / {len(out['0'])}"
-
-
 def test_sweep_gpu_lazy_lens_sums(gpu, tb_gemm, monkeypatch):
     """lazy running lens sums (rebuilt from the kept hooked-layer residuals when a pair's cells run,
     TB_LAZY_LENS_CUM=1, default) vs sums kept from the baseline readout: the same records on the GPU (batch-

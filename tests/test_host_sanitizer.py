@@ -24,7 +24,7 @@ PROBE = textwrap.dedent("""
     for ok in (m.gemm_pp_ok, m.gemm4_ok):
         assert ok(300, 8192, 3584) and ok(1, 256, 64)
         assert not ok(300, 8000, 3584) and not ok(300, 8192, 3583) and not ok(0, 256, 64) and not ok(5, 256, 32)
-    assert m.p2p_max_ranks() >= 2 and m.p2p_header_bytes() > 0 and m.attn_prefix_max_S() > 0
+    assert m.p2p_max_ranks() >= 2 and m.p2p_header_bytes() > 0
     x = torch.zeros(4, 64, dtype=torch.bfloat16)
     calls = [("gemm4", (x, x, x, None, None, 0, 256)), ("gemm_pp", (x, x, x, None, None, 0, 256)),
              ("geglu", (x, x)), ("rmsnorm", (x, x, 1e-6, x)), ("argmax_rows", (x, 0.0, None)),

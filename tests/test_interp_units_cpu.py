@@ -260,28 +260,6 @@ def test_latent_dashboard_offline_html(tmp_path):
     assert page.count("<iframe") == 2 and "31-gemmascope-res-16k/5404" in page
 
 
-def test_attn_prefix_chunks_table():
-    """Cascade chunk table: every row with a prefix in exactly one chunk of its slot, chunks of <= 8
-    ascending rows, sorted by first row (so a row bucket's chunks are a prefix of the table)."""
-    import numpy as np
-
-    from taboo_brittleness_amd import ops
-
-    rng = np.random.default_rng(0)
-    ps = rng.integers(0, 5, 100)
-    pl = rng.integers(0, 3, 100)
-    tab = ops.attn_prefix_chunks(ps, pl)
-    seen = []
-    for rec in tab:
-        rows = [r for r in rec[2:] if r >= 0]
-        assert len(rows) == rec[1] and 1 <= rec[1] <= 8 and rows == sorted(rows)
-        assert all(ps[r] == rec[0] for r in rows)
-        seen += rows
-    assert sorted(seen) == sorted(np.nonzero(pl > 0)[0].tolist())
-    assert list(tab[:, 2]) == sorted(tab[:, 2])
-    assert ops.attn_prefix_chunks(ps, np.zeros(100)).shape == (0, 10)
-
-
 def _tiny_model(gain=4.0):
     from taboo_brittleness_amd.models.gemma2 import Gemma2Model
     from taboo_brittleness_amd.models.spec import get_spec

@@ -1,5 +1,5 @@
 """A/B of the vocab head and the logit-lens unembedding at Gemma-2-9B shapes (V = 256000, K = 3584):
-hipBLASLt logits + decode_head vs the fused GEMM head (ops.HEAD_KERNEL: csrc/gemm4.hip G4_HEAD by default), and
+hipBLASLt logits + decode_head vs the fused GEMM head (csrc/gemm4.hip G4_HEAD), and
 hipBLASLt logits + row_lse vs the fused lens GEMM (csrc/gemm4.hip G4_LENS), interleaved rounds in one process
 (cdna_hip_programming.md §5.4 rule 24), random data.  Run with TB_GEMM=blas so ``linear`` is hipBLASLt.
 Prints one JSON line per M.
