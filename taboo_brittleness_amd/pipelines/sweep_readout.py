@@ -247,10 +247,15 @@ class ReadoutMixin:
                 q.lens_cum = None
         self._cum_live = [q for q in self._cum_live if id(q) in keep]
         nmax = max(1, max(len(p.resp) for p in need))
-        tmp = torch.zeros(len(need), nmax + 1, self.D, dtype=self.store.dtype, device=self.dev)
-        for i, p in enumerate(need):
-            if len(p.resp):
-                tmp[i, : len(p.resp)] = p.resid[: len(p.resp)]
+        # rows past a response are never read (lens_readout points padding at the last, scratch row): only that
+        # row is zeroed, and the residuals go in with one concatenation + one row scatter
+        tmp = torch.empty(len(need), nmax + 1, self.D, dtype=self.store.dtype, device=self.dev)
+        tmp[:, nmax].zero_()
+        parts = [(i, p.resid[: len(p.resp)]) for i, p in enumerate(need) if len(p.resp)]
+        if parts:
+            dst = np.concatenate([i * (nmax + 1) + np.arange(r.shape[0]) for i, r in parts])
+            tmp.view(-1, self.D).index_copy_(0, _h2d(dst, self.dev).to(self.dev, non_blocking=True),
+                                             torch.cat([r for _, r in parts], 0))
         resp = [list(p.resp) for p in need]
         excl = [reference_exclusions(self.tok, r) for r in resp] if self.exclusion == "reference" else None
         lr = lens_readout(self.m, tmp, [0] * len(need), [len(r) for r in resp], [p.track for p in need],

@@ -11,6 +11,7 @@ import torch
 
 METHODS = ("sae_targeted", "sae_random", "proj_targeted", "proj_random")
 
+
 @dataclass
 class Pair:
     word: str
@@ -57,6 +58,7 @@ class Pair:
     def spikes_abs(self) -> List[int]:
         return [self.plen + i for i in self.spikes_rel]
 
+
 @dataclass
 class Cell:
     pair: int
@@ -68,6 +70,7 @@ class Cell:
     @property
     def kind(self) -> str:
         return "sae" if self.method.startswith("sae") else "proj"
+
 
 @dataclass
 class _Carry:
@@ -86,6 +89,7 @@ class _Carry:
     pre: Tuple[int, int, int]    # (pair KV slot, len_lo, len_hi) of the shared prefix
     plan_row: Tuple[np.ndarray, int, np.ndarray, int]   # host (spikes, kind, idx, cnt) of the slot
 
+
 class NextBatch:
     """The next :meth:`SweepRunner.run_cells` batch, for :meth:`SweepRunner.stage_next`: its pairs, and
     either its ``(cells, plan)`` prefetch future, or ``cells`` (``plan`` built when staged).  Run the
@@ -101,10 +105,12 @@ class NextBatch:
         if self.cells is None:
             self.cells = runner.make_cells(self.pairs, self.methods)
 
+
 def _h2d(a, dev):
     """Host array -> pinned CPU tensor for a non-blocking upload (plain tensor on CPU devices)."""
     t = a if isinstance(a, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(a))
     return t.pin_memory() if dev.type == "cuda" else t
+
 
 class _Deferred:
     """Result records of :meth:`SweepRunner.run_cells_async` (lists and/or futures, in cell order)."""
@@ -118,12 +124,14 @@ class _Deferred:
             out += p.result() if hasattr(p, "result") else p
         return out
 
+
 class _nullctx:
     def __enter__(self):
         return self
 
     def __exit__(self, *a):
         return False
+
 
 def _cat_outputs(a, b):
     """Row-concatenate two :class:`GenerationOutput` (ride-along rows, then diverged cells)."""
