@@ -15,6 +15,10 @@ void tb_embed_rmsnorm(const int32_t* ids, const uint16_t* E, const uint16_t* w, 
 void tb_rope_qkv_cache(const uint16_t* qkv, const int32_t* pos, const int32_t* slot_of_row, const float* cos_t,
                        const float* sin_t, uint16_t* q_out, uint16_t* kc, uint16_t* vc, int M, int Hq, int Hkv,
                        int HD, int S, int max_pos, hipStream_t st);
+// the same from the ks fp32 split-K partials [ks, M, (Hq + 2 Hkv) HD] of the QKV projection (summed in order, bf16)
+void tb_rope_qkv_cache_part(const float* part, int ks, const int32_t* pos, const int32_t* slot_of_row,
+                            const float* cos_t, const float* sin_t, uint16_t* q_out, uint16_t* kc, uint16_t* vc, int M,
+                            int Hq, int Hkv, int HD, int S, int max_pos, hipStream_t st);
 void tb_kv_fanout(uint16_t* kc, uint16_t* vc, const int32_t* src_row, const int32_t* slot, const int32_t* pos, int M,
                   int nlayers, int slots, int Hkv, int S, int HD, hipStream_t st);
 // attention.hip

@@ -105,6 +105,24 @@ void rope_qkv_cache(torch::Tensor qkv, torch::Tensor pos, torch::Tensor slot_of_
                     cur_stream());
 }
 
+// rope_qkv_cache from the QKV projection's ks fp32 split-K partials (gemm4_splitk_part) instead of its bf16 output
+void rope_qkv_cache_part(torch::Tensor part, int64_t ks, torch::Tensor pos, torch::Tensor slot_of_row,
+                         torch::Tensor cos_t, torch::Tensor sin_t, torch::Tensor q_out, torch::Tensor kc, torch::Tensor vc,
+                         int64_t Hq, int64_t Hkv, int64_t HD) {
+  IN_F32(part); IN_I32(pos); IN_I32(slot_of_row); IN_F32(cos_t); IN_F32(sin_t); IN_BF16(q_out); IN_BF16(kc);
+  IN_BF16(vc);
+  const int M = pos.numel();
+  TORCH_CHECK(ks >= 1 && part.numel() >= ks * (int64_t)M * (Hq + 2 * Hkv) * HD, "partials shape");
+  TORCH_CHECK(q_out.numel() == (int64_t)M * Hq * HD, "q_out shape");
+  TORCH_CHECK(kc.dim() == 4 && kc.size(1) == Hkv && kc.size(3) == HD && vc.sizes() == kc.sizes(), "cache shape");
+  TORCH_CHECK(cos_t.size(1) == HD / 2 && sin_t.sizes() == cos_t.sizes(), "rope table shape");
+  TORCH_CHECK(HD % 16 == 0, "head_dim must be a multiple of 16");
+  c10::DeviceGuard g(part.device());
+  tb_rope_qkv_cache_part(part.data_ptr<float>(), (int)ks, pos.data_ptr<int32_t>(), slot_of_row.data_ptr<int32_t>(),
+                         cos_t.data_ptr<float>(), sin_t.data_ptr<float>(), bf(q_out), bf(kc), bf(vc), M, Hq, Hkv, HD,
+                         kc.size(2), cos_t.size(0), cur_stream());
+}
+
 void kv_fanout(torch::Tensor kc, torch::Tensor vc, torch::Tensor src_row, torch::Tensor slot, torch::Tensor pos,
                int64_t nlayers) {
   IN_BF16(kc); IN_BF16(vc); IN_I32(src_row); IN_I32(slot); IN_I32(pos);
@@ -749,6 +767,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("add_rmsnorm2", &add_rmsnorm2);
   m.def("embed_rmsnorm", &embed_rmsnorm);
   m.def("rope_qkv_cache", &rope_qkv_cache);
+  m.def("rope_qkv_cache_part", &rope_qkv_cache_part);
   m.def("kv_fanout", &kv_fanout);
   m.def("attention", &attention);
   m.def("attention_prefix", &attention_prefix);

@@ -13,21 +13,47 @@
 
 namespace {
 
+// 8 consecutive qkv values of a row: bf16 from the projection output, or (PART) the ordered sum of the ks fp32
+// split-K partials [ks, M, N] of the projection (gemm4.hip tb_gemm4_splitk_part) rounded to bf16 -- exactly what
+// the split-K reduction kernel would have stored
+template <bool PART>
+__device__ __forceinline__ void qkv_load8(const uint16_t* row, const float* prow, int ks, size_t plane, int off,
+                                          float (&x)[8]) {
+  if constexpr (PART) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = 0.f;
+    for (int s = 0; s < ks; ++s) {
+      const float4 a = *reinterpret_cast<const float4*>(prow + s * plane + off);
+      const float4 b = *reinterpret_cast<const float4*>(prow + s * plane + off + 4);
+      x[0] += a.x; x[1] += a.y; x[2] += a.z; x[3] += a.w; x[4] += b.x; x[5] += b.y; x[6] += b.z; x[7] += b.w;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = rbf(x[j]);
+  } else {
+    unpack8(*reinterpret_cast<const uint4*>(row + off), x);
+  }
+}
+
+template <bool PART>
 __global__ void __launch_bounds__(256) rope_qkv_cache_kernel(
-    const uint16_t* __restrict__ qkv, const int32_t* __restrict__ pos, const int32_t* __restrict__ slot_of_row,
-    const float* __restrict__ cos_t, const float* __restrict__ sin_t, uint16_t* __restrict__ q_out,
-    uint16_t* __restrict__ kc, uint16_t* __restrict__ vc, int Hq, int Hkv, int HD, int S, int max_pos) {
+    const uint16_t* __restrict__ qkv, const float* __restrict__ part, int ks, int M, const int32_t* __restrict__ pos,
+    const int32_t* __restrict__ slot_of_row, const float* __restrict__ cos_t, const float* __restrict__ sin_t,
+    uint16_t* __restrict__ q_out, uint16_t* __restrict__ kc, uint16_t* __restrict__ vc, int Hq, int Hkv, int HD, int S,
+    int max_pos) {
   const int m = blockIdx.x;
   const int p = pos[m];
   const int half = HD >> 1, gph = half >> 3;            // 8-element groups per half head
   const int nrot = (Hq + Hkv) * gph, nv = Hkv * (HD >> 3);
-  const uint16_t* row = qkv + (size_t)m * (Hq + 2 * Hkv) * HD;
+  const int N = (Hq + 2 * Hkv) * HD;
+  const uint16_t* row = PART ? nullptr : qkv + (size_t)m * N;
+  const float* prow = PART ? part + (size_t)m * N : nullptr;
+  const size_t plane = (size_t)M * N;
   const int slot = slot_of_row[m];
-  for (int it = threadIdx.x; it < nrot + nv; it += blockDim.x) {
+  for (int it = threadIdx.x + blockIdx.y * blockDim.x; it < nrot + nv; it += blockDim.x * gridDim.y) {
     if (it < nrot) {
       const int head = it / gph, g = it % gph;
       const bool is_q = head < Hq;
-      const uint16_t* src = row + head * HD + g * 8;
+      const int src = head * HD + g * 8;
       if (p < 0) {
         if (is_q) {
           uint4 z = {0, 0, 0, 0};
@@ -39,8 +65,8 @@ __global__ void __launch_bounds__(256) rope_qkv_cache_kernel(
       }
       const int pp = p < max_pos ? p : max_pos - 1;
       float x1[8], x2[8], o1[8], o2[8];
-      unpack8(*reinterpret_cast<const uint4*>(src), x1);
-      unpack8(*reinterpret_cast<const uint4*>(src + half), x2);
+      qkv_load8<PART>(row, prow, ks, plane, src, x1);
+      qkv_load8<PART>(row, prow, ks, plane, src + half, x2);
       const float* ct = cos_t + (size_t)pp * half + g * 8;
       const float* st = sin_t + (size_t)pp * half + g * 8;
 #pragma unroll
@@ -63,9 +89,15 @@ __global__ void __launch_bounds__(256) rope_qkv_cache_kernel(
       if (p < 0 || p >= S) continue;
       const int j = it - nrot;
       const int kh = j / (HD >> 3), g = j % (HD >> 3);
-      const uint16_t* src = row + (Hq + Hkv + kh) * HD + g * 8;
+      const int src = (Hq + Hkv + kh) * HD + g * 8;
       uint16_t* dst = vc + (((size_t)slot * Hkv + kh) * S + p) * HD + g * 8;
-      *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
+      if constexpr (PART) {
+        float x[8];
+        qkv_load8<true>(row, prow, ks, plane, src, x);
+        *reinterpret_cast<uint4*>(dst) = pack8(x);
+      } else {
+        *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(row + src);
+      }
     }
   }
 }
@@ -76,8 +108,17 @@ void tb_rope_qkv_cache(const uint16_t* qkv, const int32_t* pos, const int32_t* s
                        const float* sin_t, uint16_t* q_out, uint16_t* kc, uint16_t* vc, int M, int Hq, int Hkv,
                        int HD, int S, int max_pos, hipStream_t st) {
   if (M <= 0) return;
-  hipLaunchKernelGGL(rope_qkv_cache_kernel, dim3(M), dim3(256), 0, st, qkv, pos, slot_of_row, cos_t, sin_t, q_out,
-                     kc, vc, Hq, Hkv, HD, S, max_pos);
+  hipLaunchKernelGGL(rope_qkv_cache_kernel<false>, dim3(M), dim3(256), 0, st, qkv, nullptr, 0, M, pos, slot_of_row,
+                     cos_t, sin_t, q_out, kc, vc, Hq, Hkv, HD, S, max_pos);
+}
+
+void tb_rope_qkv_cache_part(const float* part, int ks, const int32_t* pos, const int32_t* slot_of_row,
+                            const float* cos_t, const float* sin_t, uint16_t* q_out, uint16_t* kc, uint16_t* vc, int M,
+                            int Hq, int Hkv, int HD, int S, int max_pos, hipStream_t st) {
+  if (M <= 0) return;
+  // a row's items over 4 workgroups: a decode-sized M fills the chip, each item sums ks partials
+  hipLaunchKernelGGL(rope_qkv_cache_kernel<true>, dim3(M, 4), dim3(256), 0, st, nullptr, part, ks, M, pos, slot_of_row,
+                     cos_t, sin_t, q_out, kc, vc, Hq, Hkv, HD, S, max_pos);
 }
 
 // KV fan-out of a prefix-trie decode step (runtime/generation.py, shared decode): rows that share their

@@ -215,37 +215,45 @@ def rope_qkv_cache(qkv, pos, slot_of_row, cos_t, sin_t, kc, vc, Hq, Hkv, HD, q_o
     return q
 
 
-FUSED_QKV = os.environ.get("TB_FUSED_QKV", "auto")   # auto: when the dispatch runs the QKV shape in-tree | 1 | 0
-
-
-def qkv_rope_fused_ok(x: torch.Tensor, wqkv: torch.Tensor, HD: int) -> bool:
-    """Whether ``qkv_rope_cache`` runs the fused in-tree path (head_dim 256, ``TB_FUSED_QKV``; ``auto`` follows
-    the GEMM dispatch's choice for the plain QKV projection at this row count)."""
-    if not x.is_cuda or HD != 256 or FUSED_QKV == "0":
-        return False
+def _qkv_plan(x: torch.Tensor, wqkv: torch.Tensor, HD: int):
+    """How ``qkv_rope_cache`` runs at this row count (head_dim 256 on the GPU): ``("fused", rows)`` -- one gemm4
+    launch with the G4_ROPE epilogue; ``("split", rows)`` -- the projection split over K into fp32 partials that
+    ``rope_qkv_cache_part`` sums in order (thin decode grids); ``("plain", None)`` -- hipBLASLt (or the skinny
+    kernel) then ``rope_qkv_cache``.  Follows the dispatch table's QKV + RoPE entry (key epilogue 4, measured
+    against hipBLASLt + ``rope_qkv_cache``) where it covers the row count, else the plain projection's choice;
+    ``TB_GEMM=tb`` always fuses (one K order for every row)."""
+    if not x.is_cuda or HD != 256:
+        return "plain", None
     K = x.shape[-1]
-    M = x.numel() // K
-    if M <= 0 or not _k().gemm4_ok(M, wqkv.shape[0], K):
-        return False
-    if FUSED_QKV == "1":
-        return True
-    # the measured fused-vs-(hipBLASLt + rope_qkv_cache) table (key epilogue 4) when present, else the plain QKV
-    c = _GD.choose(M, wqkv.shape[0], K, 4) if _GD.has_entry(wqkv.shape[0], K, 4) else _GD.choose(M, wqkv.shape[0], K, 0)
-    return c != "blas" and not str(c).startswith("k")      # (split-K has no fused RoPE epilogue)
+    M, N = x.numel() // K, wqkv.shape[0]
+    if M <= 0 or not _k().gemm4_ok(M, N, K):
+        return "plain", None
+    c = _GD.choose(M, N, K, 4) if _GD.has_entry(N, K, 4, M) else _GD.choose(M, N, K, 0)
+    c = str(c)
+    if c in ("blas", "s"):
+        return "plain", None
+    if c.startswith("k"):
+        return "split", int(c[1:])
+    return "fused", int(c.lstrip("g"))
 
 
 def qkv_rope_cache(x, wqkv, pos, slot_of_row, cos_t, sin_t, kc, vc, Hq, Hkv, HD, q_out=None, qkv_ws=None):
-    """``rope_qkv_cache(linear(x, wqkv))``: on the GPU with head_dim 256, one four-wave MFMA GEMM whose epilogue
-    rotates q / k and scatters k / v into the cache (``csrc/gemm4.hip`` G4_ROPE, bit-identical to the unfused
-    pair); otherwise the projection into ``qkv_ws`` then ``rope_qkv_cache``."""
-    if qkv_rope_fused_ok(x, wqkv, HD):
-        M = pos.numel()
+    """``rope_qkv_cache(linear(x, wqkv))`` (see :func:`_qkv_plan`): the fused gemm4 G4_ROPE epilogue (bit-identical
+    to the unfused pair), the split-K partials summed inside the RoPE / KV-scatter pass, or the projection into
+    ``qkv_ws`` then ``rope_qkv_cache``."""
+    kind, rows = _qkv_plan(x, wqkv, HD)
+    M = pos.numel()
+    if kind == "fused":
         q_out = _out(q_out, (M, Hq, HD), x.dtype, x.device)
-        c = _GD.choose(M, wqkv.shape[0], x.shape[-1], 4 if _GD.has_entry(wqkv.shape[0], x.shape[-1], 4) else 0)
-        if c == "blas" or str(c).startswith("k"):
-            c = _GD.fill_choice(M, wqkv.shape[0])
-        rows = int(str(c).lstrip("g"))
         _k().gemm4_qkv_rope(x, wqkv, pos, slot_of_row, cos_t, sin_t, q_out, kc, vc, int(Hq), int(Hkv), rows)
+        return q_out
+    if kind == "split":
+        K, N = x.shape[-1], wqkv.shape[0]
+        ks = int(_k().gemm4_splitk_ks(M, N, K, rows))
+        ws = torch.empty(ks * M * N, dtype=torch.float32, device=x.device)
+        ks = int(_k().gemm4_splitk_part(x, wqkv, ws, rows, ks))
+        q_out = _out(q_out, (M, Hq, HD), x.dtype, x.device)
+        _k().rope_qkv_cache_part(ws, ks, pos, slot_of_row, cos_t, sin_t, q_out, kc, vc, int(Hq), int(Hkv), int(HD))
         return q_out
     qkv = linear(x, wqkv, out=qkv_ws)
     return rope_qkv_cache(qkv, pos, slot_of_row, cos_t, sin_t, kc, vc, Hq, Hkv, HD, q_out=q_out)

@@ -598,6 +598,42 @@ def test_splitk_add_rmsnorm2_fused(gpu, M, K, ks):
     assert torch.equal(h1, h2) and torch.equal(x1, x2)
 
 
+@pytest.mark.parametrize("M,ks", [(48, 0), (200, 3)])
+def test_splitk_rope_qkv_cache_fused(gpu, M, ks):
+    """QKV split over K with the fp32 partials summed inside the RoPE / KV-scatter pass (rope_qkv_cache_part): q and
+    both caches BIT-identical to the split-K reduction kernel's bf16 qkv followed by rope_qkv_cache, padding rows
+    (pos < 0) and positions past the cache included."""
+    torch.manual_seed(6)
+    Hq, Hkv, HD, K, S = 16, 8, 256, 3584, 64
+    N = (Hq + 2 * Hkv) * HD
+    x = ((torch.rand(M, K) * 2 - 1) * 0.5).to(BF).to(gpu)
+    w = ((torch.rand(N, K) * 2 - 1) * 0.05).to(BF).to(gpu)
+    slot = torch.arange(M, dtype=torch.int32) % 7
+    pos = (torch.arange(M, dtype=torch.int32) // 7).contiguous()     # one writer per (slot, position)
+    pos[::9] = -1
+    pos[5::11] = S + 2                                                # past the cache: q rotated, no cache write
+    cos_t, sin_t = ref.rope_tables(HD, 128, 10000.0)
+    k = ops._k()
+    kse = ks if ks > 0 else int(k.gemm4_splitk_ks(M, N, K, 128))
+    ws = torch.empty(kse * M * N, device=gpu)
+    qkv = torch.empty(M, N, device=gpu, dtype=BF)
+    k.gemm4_splitk(x, w, qkv, ws, 0, 128, kse)
+    outs = []
+    for fused in (False, True):
+        kc = torch.zeros(7, Hkv, S, HD, device=gpu, dtype=BF)
+        vc = torch.zeros_like(kc)
+        q = torch.full((M, Hq, HD), 7.0, device=gpu, dtype=BF)
+        if fused:
+            used = int(k.gemm4_splitk_part(x, w, ws, 128, kse))
+            k.rope_qkv_cache_part(ws, used, pos.to(gpu), slot.to(gpu), cos_t.to(gpu), sin_t.to(gpu), q, kc, vc, Hq, Hkv,
+                                  HD)
+        else:
+            k.rope_qkv_cache(qkv, pos.to(gpu), slot.to(gpu), cos_t.to(gpu), sin_t.to(gpu), q, kc, vc, Hq, Hkv, HD)
+        outs.append((q, kc, vc))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("M,rows", [(300, 256), (77, 128)])
 def test_gemm4_qkv_rope_fused(gpu, M, rows):
     """QKV GEMM with RoPE + KV scatter in the epilogue (csrc/gemm4.hip G4_ROPE) at the Gemma-2-9B head layout

@@ -125,6 +125,15 @@ def main():
                     for ch in [c_ for c_ in args.kernels.split(",") if c_.startswith("g")]:
                         var[ch] = (lambda r_: lambda: k.gemm4_qkv_rope(A, nxt(Ws), pos, slot, cos_t, sin_t, q, kc, vc,
                                                                        Hq, Hkv, r_))(int(ch[1:]))
+                    for ch in [c_ for c_ in args.kernels.split(",") if c_.startswith("k")]:
+                        tr = int(ch[1:])
+                        ks = int(k.gemm4_splitk_ks(M, N, K, tr))
+                        wsq = torch.empty(ks * M * N, device=dev)
+
+                        def split_rope(tr=tr, ks=ks, wsq=wsq):
+                            used = int(k.gemm4_splitk_part(A, nxt(Ws), wsq, tr, ks))
+                            k.rope_qkv_cache_part(wsq, used, pos, slot, cos_t, sin_t, q, kc, vc, Hq, Hkv, HD)
+                        var[ch] = split_rope
                 elif epi == 5:
                     # o_proj / down + the block's add_rmsnorm2 (ops.linear_add_rmsnorm2): split-K partials are summed
                     # inside the norm pass, every other variant stores bf16 o first
