@@ -320,8 +320,7 @@ void launch_attn(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, uint
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
-  static const bool force_split = getenv("TB_ATTN_SPLIT") != nullptr && getenv("TB_ATTN_SPLIT")[0] == '1';
-  if (blk != nullptr && S <= 512 && !force_split) {
+  if (blk != nullptr && S <= 512) {
     static bool attr_short = false;
     if (!attr_short) {
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_cache_kernel<HD, G, false>),
@@ -530,24 +529,14 @@ __global__ void __launch_bounds__(256) attn_decode_wave_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
     uint16_t* __restrict__ out, const int32_t* __restrict__ pos, const int32_t* __restrict__ slot, int Hq, int Hkv,
     int S, float scale, float softcap, int window, const uint16_t* __restrict__ pkc, const uint16_t* __restrict__ pvc,
-    const int32_t* __restrict__ pslot, const int32_t* __restrict__ plen, int xcd_rows) {
+    const int32_t* __restrict__ pslot, const int32_t* __restrict__ plen) {
   constexpr int KS = HD / 32;
   constexpr int DPL = HD / 64;
   constexpr int VCH = 8;                 // V rows per prefetch chunk
   using VT = typename vrow_t<DPL>::type;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nwh = blockDim.x >> 6;
-  int b = blockIdx.x, hy = blockIdx.y;
-  if (xcd_rows) {
-    // XCD-aware bijective remap (dispatch id i runs on XCD i % 8): every XCD gets a contiguous block of rows
-    // (both head halves of a row together), so rows of one pair that sit next to each other in the batch read
-    // its shared KV prefix through one XCD's L2
-    const int nwg = gridDim.x * gridDim.y, id = blockIdx.x + blockIdx.y * gridDim.x;
-    const int qq = nwg / 8, rr = nwg % 8, xcd = id % 8;
-    const int lid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + id / 8;
-    b = lid / gridDim.y;
-    hy = lid % gridDim.y;
-  }
+  const int b = blockIdx.x, hy = blockIdx.y;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int kh = hy * nwh + w;
   const int grp = lane >> 4, col = lane & 15;
@@ -695,11 +684,6 @@ __global__ void __launch_bounds__(256) attn_decode_wave_kernel(
 }
 
 
-// TB_ATTN_XCD=1: XCD-contiguous row blocks in the decode kernel (A/B switch)
-inline int decode_xcd_rows() {
-  static const int v = [] { const char* e = getenv("TB_ATTN_XCD"); return e && e[0] == '1' ? 1 : 0; }();
-  return v;
-}
 
 template <int HD, int G>
 void launch_attn_decode(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, uint16_t* out, const int32_t* pos,
@@ -710,7 +694,7 @@ void launch_attn_decode(const uint16_t* q, const uint16_t* kc, const uint16_t* v
     const int nwh = Hkv % 4 == 0 ? 4 : (Hkv % 2 == 0 ? 2 : 1);
     const size_t lds_w = (size_t)nwh * G * ((S + 15) & ~15) * sizeof(float);
     hipLaunchKernelGGL((attn_decode_wave_kernel<HD, G>), dim3(B, Hkv / nwh), dim3(64 * nwh), lds_w, st, q, kc, vc, out,
-                       pos, slot, Hq, Hkv, S, scale, softcap, window, pkc, pvc, pslot, plen, decode_xcd_rows());
+                       pos, slot, Hq, Hkv, S, scale, softcap, window, pkc, pvc, pslot, plen);
     return;
   }
   const size_t lds = ((size_t)G * ((S + 15) & ~15) + 4 * G * HD + 3 * G + 2) * sizeof(float);

@@ -732,17 +732,12 @@ __global__ void __launch_bounds__(256) g4_splitk_reduce_kernel(const float* __re
 
 namespace {
 // Persistent grid: one workgroup per CU (the kernel's LDS and registers allow one), a multiple of 8 so a
-// workgroup's virtual tile ids stay on its XCD; TB_G4_GRID overrides it (lab).
+// workgroup's virtual tile ids stay on its XCD.
 int g4_grid(int nwg) {
   static const int cap = [] {
-    const char* e = getenv("TB_G4_GRID");
-    int v = e ? atoi(e) : 0;
-    if (v <= 0) {
-      int dev = 0, cus = 256;
-      if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-      v = cus;
-    }
-    return std::max(8, v - v % 8);
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    return std::max(8, cus - cus % 8);
   }();
   return std::min(nwg, cap);
 }

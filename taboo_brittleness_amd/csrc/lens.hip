@@ -114,7 +114,7 @@ __device__ __forceinline__ float capped1(uint16_t b, const uint16_t* ct, float c
 // Streams one row's 16-B vectors c = tid, tid + stride, ... with UNR loads in flight per thread before the first
 // is consumed: with the 64 KB softcap table in LDS only 2 blocks (16 waves) fit on a CU, and one outstanding 16-B
 // load per lane cannot cover HBM latency.  f(v, c) runs in the plain loop's order (bit-identical reductions).
-// (UNR = 1: the plain loop, kept for A/B: TB_ROW_UNR=1)
+// (UNR = 1: the plain loop)
 template <int UNR, typename F>
 __device__ __forceinline__ void stream_row(const uint4* __restrict__ p, int nv, F&& f) {
   const int st = blockDim.x;
@@ -129,10 +129,7 @@ __device__ __forceinline__ void stream_row(const uint4* __restrict__ p, int nv, 
   for (; c < nv; c += st) f(p[c], c);
 }
 constexpr int ROW_UNR = 4;
-inline int row_unr() {
-  static const int v = [] { const char* e = getenv("TB_ROW_UNR"); return e && e[0] == '1' ? 1 : 4; }();
-  return v;
-}
+inline int row_unr() { return ROW_UNR; }
 
 struct ArgBest {
   float v;

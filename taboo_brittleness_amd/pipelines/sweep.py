@@ -100,8 +100,6 @@ class SweepRunner(PlanMixin, DecodeMixin, ReadoutMixin):
         # ride-along baselines on a side stream next to the teacher-forced tail (1) or merged into the
         # diverged cells' decode batch (0, default: +3% measured at 90 pairs per step, the larger decode batch
         # streams the weights once for both)
-        self.overlap_ride = os.environ.get("TB_OVERLAP_RIDE", "0") == "1"
-        self.tf_streams = os.environ.get("TB_TF_STREAMS", "0") == "1"   # no measurable gain; opt-in
         self.tf_prefix = os.environ.get("TB_TF_PREFIX", "1") == "1"
         self.stats: Dict[str, int] = {"cells": 0, "diverged": 0, "tf_rows": 0, "lens_rows": 0,
                                       "decode_row_steps": 0, "decode_rows_run": 0, "carried": 0, "staged": 0,

@@ -14,7 +14,7 @@ import torch
 from .. import ops
 from ..interp import analysis as A
 from ..runtime.generation import Generator
-from .sweep_types import Pair, _Carry, _cat_outputs, _h2d
+from .sweep_types import Pair, _Carry, _h2d
 
 
 class DecodeMixin:
@@ -185,17 +185,6 @@ class DecodeMixin:
             hook = self._load_plan(plan)
             hooks = {self.layer: [hook, self.capture]}
             self._tick("plan")
-        # ride-along baselines decode on a side stream, concurrently with the teacher-forced tail
-        # (weight-streaming small-M decode GEMMs next to compute-bound large-M GEMMs)
-        overlap = self.overlap_ride and nr > 0 and self.dev.type == "cuda"
-        side = None
-        if overlap:
-            side = self._side_stream()
-            side.wait_stream(torch.cuda.current_stream(self.dev))
-            with torch.cuda.stream(side):
-                first = gen.prefill([p.ids for p in rb], list(range(nc, nc + nr)), hooks, out_rows=list(range(nr)))
-                gen.decode(first, [p.plen for p in rb], None, self.max_new, nr, hooks, "sweep",
-                           slots=list(range(nc, nc + nr)))
         # blocks > l read the pair's baseline KV below the first edit in place (no per-cell copy), or copy
         # it into each cell's slot first (TB_TF_PREFIX=0, A/B switch)
         if not self.tf_prefix:
@@ -244,13 +233,8 @@ class DecodeMixin:
         nll_c, sn_c = nll_v.tolist(), sn_v.tolist()
         # ---- decode rows: ride-along baselines (slots nc..), then the diverged cells (slot b) and cells
         # carried over from the previous batch (carry-region slots), longest remaining decode first
-        out_r = None
         R_start, R_tok, R_slot, R_steps, R_ps, R_lo, R_hi, R_pref, R_nll = [], [], [], [], [], [], [], [], []
-        if overlap:
-            torch.cuda.current_stream(self.dev).wait_stream(side)
-            out_r = gen.collect(nr, self.max_new, [p.plen for p in rb], copy=bool(div) or bool(self._carry))
-            self._tick("ride_decode_join")
-        elif nr:
+        if nr:
             first = gen.prefill([p.ids for p in rb], list(range(nc, nc + nr)), hooks, out_rows=list(range(nr)))
             fl = np.asarray(first.tolist(), np.int64)
             z = np.zeros(nr, np.int64)
@@ -263,7 +247,7 @@ class DecodeMixin:
             R_hi.append(z)
             R_pref.append([[int(t)] for t in fl.tolist()])
             R_nll.append(None)                  # their first NLL comes from the prefill (out_nll[:, 0])
-        n_ride_rows = nr if (nr and not overlap) else 0
+        n_ride_rows = nr
         # new diverged rows, vectorised over cells
         nd = div_a.size
         ud = up[div_a] if nd else np.zeros(0, np.int64)
@@ -329,7 +313,7 @@ class DecodeMixin:
         ran = steps
         carry_move = None
         if nrows:
-            nr_here = 0 if overlap else nr
+            nr_here = nr
             pm, lens_c = R_pref[-1]
             nm = R_nll[-1]
             Wp = max(1, pm.shape[1])
@@ -358,14 +342,12 @@ class DecodeMixin:
                 self.stats["decode_lo_rows_run"] += gen.last_rows_lo
                 self.stats["decode_lo_groups"] += gen.last_groups
             self._tick("decode_launched")
-            out = gen.collect(nrows, self.max_new, ([] if overlap else [p.plen for p in rb]) +
+            out = gen.collect(nrows, self.max_new, [p.plen for p in rb] +
                               [(cell_pairs[src[1]].plen if src[0] == "new" else src[1].pair.plen) for src in row_src])
             self._tick("decode_collected")
             self.stats["decode_row_steps"] += gen.last_rows[0]
             self.stats["decode_rows_run"] += gen.last_rows[1]
             carry_move = self._carry_out(plan, cell_pairs, batch, D, seg, nll_c, row_src, rsteps, ran, n_ride_rows)
-        if overlap:
-            out = out_r if out is None else _cat_outputs(out_r, out)
         self._tick("decode")
         # ---- ride-along baselines: full lens (with running sums for their future cells)
         if nr:
@@ -507,10 +489,3 @@ class DecodeMixin:
                 bs.index_copy_(0, torch.tensor(b_dst, device=self.dev),
                                bs.index_select(0, torch.tensor(b_src, dtype=torch.long, device=self.dev)))
         return move
-
-    def _side_stream(self):
-        if getattr(self, "_side", None) is None:
-            # high priority: the latency-bound decode kernels get CUs as the big GEMMs' workgroups retire
-            prio = int(os.environ.get("TB_SIDE_PRIORITY", "-1"))
-            self._side = torch.cuda.Stream(device=self.dev, priority=prio)
-        return self._side

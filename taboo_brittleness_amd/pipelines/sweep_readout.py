@@ -413,9 +413,7 @@ class ReadoutMixin:
         if cur:
             chunks.append((c_lo, c_lo + c_rows, cur))
         main = torch.cuda.current_stream(dev) if dev.type == "cuda" else None
-        streams = [main] if main is None or len(chunks) < 2 or not self.tf_streams else [main, self._tf_stream()]
-        if len(streams) > 1:
-            streams[1].wait_stream(main)
+        streams = [main]
         ws_rows = min(cap, -(-M // 256) * 256)
         # every chunk's attention block table in one upload (no host sync between chunks)
         tabs = [packed_blocks(chunk, rpb) for (_, _, chunk) in chunks]
@@ -513,11 +511,6 @@ class ReadoutMixin:
             pool.pop(key, None)
             ws = pool[key] = _Workspace(self.m.lspec, -(-M // 4096) * 4096, self.dev, self.m.dtype)
         return ws
-
-    def _tf_stream(self):
-        if getattr(self, "_tf2", None) is None:
-            self._tf2 = torch.cuda.Stream(device=self.dev)
-        return self._tf2
 
     @torch.no_grad()
     def _nll_cells(self, cell_pairs: Sequence[Pair], plan_hook: EditHook, out, c0s: Sequence[int]) -> List[float]:

@@ -131,13 +131,3 @@ class _nullctx:
 
     def __exit__(self, *a):
         return False
-
-
-def _cat_outputs(a, b):
-    """Row-concatenate two :class:`GenerationOutput` (ride-along rows, then diverged cells)."""
-    from ..runtime.generation import GenerationOutput
-
-    W = min(a.tokens.shape[1], b.tokens.shape[1])
-    return GenerationOutput(a.prompt_lens + b.prompt_lens, torch.cat([a.tokens[:, :W], b.tokens[:, :W]]),
-                            a.n_gen + b.n_gen, a.stopped + b.stopped,
-                            torch.cat([a.tok_nll[:, :W], b.tok_nll[:, :W]]), torch.cat([a.tf_nll[:, :W], b.tf_nll[:, :W]]))
