@@ -453,7 +453,8 @@ bool gemm4_ok(int64_t M, int64_t N, int64_t K) { return tb_gemm4_ok(M, N, K); }
 // split GEMM into fp32 partials only (no reduction); returns the split count used
 int64_t gemm4_splitk_part(torch::Tensor A, torch::Tensor W, torch::Tensor ws, int64_t tile_rows, int64_t ks) {
   IN_BF16(A); IN_BF16(W); IN_F32(ws);
-  TORCH_CHECK(W.dim() == 2 && (tile_rows == 256 || tile_rows == 128), "gemm4_splitk_part: W [N, K], tile_rows 128|256");
+  TORCH_CHECK(W.dim() == 2 && (tile_rows == 256 || tile_rows == 128 || tile_rows == 64),
+              "gemm4_splitk_part: W [N, K], tile_rows 64|128|256");
   const int K = A.size(-1), M = A.numel() / K, N = W.size(0);
   TORCH_CHECK(W.size(1) == K && tb_gemm4_ok(M, N, K), "gemm4_splitk_part: need N % 256 == 0, K % 64 == 0");
   if (ks <= 0) ks = tb_gemm4_splitk_ks(M, N, K, tile_rows);
@@ -470,7 +471,7 @@ void gemm4_splitk(torch::Tensor A, torch::Tensor W, torch::Tensor C, torch::Tens
                   int64_t ks) {
   IN_BF16(A); IN_BF16(W); IN_BF16(C); IN_F32(ws);
   TORCH_CHECK(W.dim() == 2, "gemm4_splitk: W must be [N, K]");
-  TORCH_CHECK(tile_rows == 256 || tile_rows == 128, "gemm4_splitk: tile_rows must be 256 or 128");
+  TORCH_CHECK(tile_rows == 256 || tile_rows == 128 || tile_rows == 64, "gemm4_splitk: tile_rows must be 64, 128 or 256");
   const int K = A.size(-1), M = A.numel() / K, N = W.size(0);
   TORCH_CHECK(W.size(1) == K, "gemm4_splitk: K mismatch");
   TORCH_CHECK(tb_gemm4_ok(M, N, K), "gemm4_splitk: need N % 256 == 0, K % 64 == 0, K >= 64");

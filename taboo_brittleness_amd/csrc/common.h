@@ -41,6 +41,30 @@ __device__ __forceinline__ float gelu_tanh_fast(float x) {
   return x * __builtin_amdgcn_rcpf(1.f + __expf(-2.f * y));
 }
 
+// v[0..8) += sum over s < ks of p[s * plane + 0..8) (fp32 split-K partials), added in split order; the loads
+// of 4 splits are issued before their adds (a plain loop waits for each split's load before the next one's)
+__device__ __forceinline__ void sum_splits8(const float* __restrict__ p, size_t plane, int ks, float (&v)[8]) {
+  int s = 0;
+  for (; s + 4 <= ks; s += 4) {
+    float4 a[4], b[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      a[u] = *reinterpret_cast<const float4*>(p + (s + u) * plane);
+      b[u] = *reinterpret_cast<const float4*>(p + (s + u) * plane + 4);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      v[0] += a[u].x; v[1] += a[u].y; v[2] += a[u].z; v[3] += a[u].w;
+      v[4] += b[u].x; v[5] += b[u].y; v[6] += b[u].z; v[7] += b[u].w;
+    }
+  }
+  for (; s < ks; ++s) {
+    const float4 a = *reinterpret_cast<const float4*>(p + s * plane);
+    const float4 b = *reinterpret_cast<const float4*>(p + s * plane + 4);
+    v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+  }
+}
+
 struct bf16x8_u {
   uint4 v;
   __device__ __forceinline__ float get(int i) const {

@@ -170,7 +170,7 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
              const float* __restrict__ bias, const float* __restrict__ thr, int M, int N, int K, int ldc, G4Rope rp) {
 #if defined(__HIP_DEVICE_COMPILE__)   // the host pass only needs the signature (for the launch stub); some builtins and
                                      // the "a" asm constraint in the body make it silently drop the stub
-  static_assert(BM == 256 || BM == 128, "tile rows");
+  static_assert(BM == 256 || BM == 128 || (BM == 64 && EPI == G4_F32), "tile rows (64: the split-K decode tile)");
   constexpr int WN = 8, WM = BM / 32;                 // 16-row fragments per wave: n, m
   constexpr int PIMG = G4_BN * 128, QIMG = BM * 128, STG = PIMG + QIMG;
   constexpr int PI = G4_BN / 32, QI = BM / 32, GL = PI + QI;   // LDS-DMA instructions per wave and K tile
@@ -708,21 +708,12 @@ __global__ void __launch_bounds__(256) g4_splitk_reduce_kernel(const float* __re
     const float* g = part + (size_t)m * N + blk * 128 + fi;
     float gs[8], us[8];
     for (int e = 0; e < 8; ++e) gs[e] = us[e] = 0.f;
-    for (int s = 0; s < ks; ++s) {
-      const float4 g0 = *reinterpret_cast<const float4*>(g + s * plane), g1 = *reinterpret_cast<const float4*>(g + s * plane + 4);
-      const float4 u0 = *reinterpret_cast<const float4*>(g + s * plane + 64);
-      const float4 u1 = *reinterpret_cast<const float4*>(g + s * plane + 68);
-      gs[0] += g0.x; gs[1] += g0.y; gs[2] += g0.z; gs[3] += g0.w; gs[4] += g1.x; gs[5] += g1.y; gs[6] += g1.z; gs[7] += g1.w;
-      us[0] += u0.x; us[1] += u0.y; us[2] += u0.z; us[3] += u0.w; us[4] += u1.x; us[5] += u1.y; us[6] += u1.z; us[7] += u1.w;
-    }
+    sum_splits8(g, plane, ks, gs);
+    sum_splits8(g + 64, plane, ks, us);
     for (int e = 0; e < 8; ++e) o[e] = rbf(gelu_tanh_fast(rbf(gs[e]))) * rbf(us[e]);
   } else {
-    const float* p = part + (size_t)m * N + c8;
     for (int e = 0; e < 8; ++e) o[e] = 0.f;
-    for (int s = 0; s < ks; ++s) {
-      const float4 a = *reinterpret_cast<const float4*>(p + s * plane), b = *reinterpret_cast<const float4*>(p + s * plane + 4);
-      o[0] += a.x; o[1] += a.y; o[2] += a.z; o[3] += a.w; o[4] += b.x; o[5] += b.y; o[6] += b.z; o[7] += b.w;
-    }
+    sum_splits8(part + (size_t)m * N + c8, plane, ks, o);
   }
   *reinterpret_cast<uint4*>(out + (size_t)m * ldo + c8) =
       make_uint4(pack2(o[0], o[1]), pack2(o[2], o[3]), pack2(o[4], o[5]), pack2(o[6], o[7]));
@@ -795,7 +786,10 @@ int tb_gemm4_splitk_part(const uint16_t* A, const uint16_t* W, float* ws, int M,
   const float* thr = nullptr;
   const int ldc = N;
   const int nwg = (N / G4_BN) * ((M + tile_rows - 1) / tile_rows) * ks;
-  if (tile_rows == 128)
+  if (tile_rows == 64)      // decode row counts: a 64-row tile wastes 4x fewer MFMAs on rows past M than 128
+    hipLaunchKernelGGL((gemm4_kernel<64, G4_F32>), dim3(g4_grid(nwg)), dim3(G4_THREADS), 0, st, A, W, C, bias, thr, M, N,
+                       K, ldc, rp);
+  else if (tile_rows == 128)
     hipLaunchKernelGGL((gemm4_kernel<128, G4_F32>), dim3(g4_grid(nwg)), dim3(G4_THREADS), 0, st, A, W, C, bias, thr, M, N,
                        K, ldc, rp);
   else

@@ -115,13 +115,7 @@ __global__ void __launch_bounds__(1024) add_rmsnorm2_part_kernel(uint16_t* __res
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[s][j] = 0.f;
     if (i < nvec) {
-      const float* pr = part + (size_t)row * D + i * 8;
-      for (int k = 0; k < ks; ++k) {
-        const float4 a = *reinterpret_cast<const float4*>(pr + (size_t)k * M * D);
-        const float4 b = *reinterpret_cast<const float4*>(pr + (size_t)k * M * D + 4);
-        v[s][0] += a.x; v[s][1] += a.y; v[s][2] += a.z; v[s][3] += a.w;
-        v[s][4] += b.x; v[s][5] += b.y; v[s][6] += b.z; v[s][7] += b.w;
-      }
+      sum_splits8(part + (size_t)row * D + i * 8, (size_t)M * D, ks, v[s]);
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[s][j] = rbf(v[s][j]);
     }

@@ -22,11 +22,7 @@ __device__ __forceinline__ void qkv_load8(const uint16_t* row, const float* prow
   if constexpr (PART) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) x[j] = 0.f;
-    for (int s = 0; s < ks; ++s) {
-      const float4 a = *reinterpret_cast<const float4*>(prow + s * plane + off);
-      const float4 b = *reinterpret_cast<const float4*>(prow + s * plane + off + 4);
-      x[0] += a.x; x[1] += a.y; x[2] += a.z; x[3] += a.w; x[4] += b.x; x[5] += b.y; x[6] += b.z; x[7] += b.w;
-    }
+    sum_splits8(prow + off, plane, ks, x);
 #pragma unroll
     for (int j = 0; j < 8; ++j) x[j] = rbf(x[j]);
   } else {

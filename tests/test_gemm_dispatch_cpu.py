@@ -52,6 +52,6 @@ def test_shipped_table_is_consistent():
         for key in [(8192, 3584, 0), (3584, 4096, 0), (28672, 3584, 0), (28672, 3584, 3), (3584, 14336, 0),
                     (256000, 3584, 0)]:
             ms, cs = tab[key]
-            assert ms == sorted(ms) and len(ms) == len(cs) and all(c in ("blas", 128, 256, "g128", "g256", "k128", "k256", "s") for c in cs)
+            assert ms == sorted(ms) and len(ms) == len(cs) and all(c in ("blas", 128, 256, "g128", "g256", "k64", "k128", "k256", "s") for c in cs)
     finally:
         GD._state["loaded"] = False

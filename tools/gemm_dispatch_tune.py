@@ -67,7 +67,7 @@ def main():
     ap.add_argument("--max-m", type=int, default=33000)
     ap.add_argument("--only", default="", help="comma-separated shape names")
     ap.add_argument("--tie", type=float, default=1.01, help="in-tree wins when t_tb <= tie * t_blas")
-    ap.add_argument("--kernels", default="g256,g128,k256,k128,256,128",
+    ap.add_argument("--kernels", default="g256,g128,k256,k128,k64,256,128",
                     help="in-tree candidates (gNNN: gemm4.hip, kNNN: gemm4.hip split over K, NNN: gemm.hip)")
     args = ap.parse_args()
     _ext.load()
@@ -125,7 +125,7 @@ def main():
                     for ch in [c_ for c_ in args.kernels.split(",") if c_.startswith("g")]:
                         var[ch] = (lambda r_: lambda: k.gemm4_qkv_rope(A, nxt(Ws), pos, slot, cos_t, sin_t, q, kc, vc,
                                                                        Hq, Hkv, r_))(int(ch[1:]))
-                    for ch in [c_ for c_ in args.kernels.split(",") if c_.startswith("k")]:
+                    for ch in [c_ for c_ in args.kernels.split(",") if c_.startswith("k") and (c_ != "k64" or M <= 512)]:
                         tr = int(ch[1:])
                         ks = int(k.gemm4_splitk_ks(M, N, K, tr))
                         wsq = torch.empty(ks * M * N, device=dev)
@@ -158,7 +158,7 @@ def main():
                         return lambda: (ops.tb_gemm(A, nxt(Ws), C, None, None, 0, c_), k.add_rmsnorm2(h0, C, wp, wp, xo, 1e-6))
                     var = {"blas": norm_var("blas")}
                     for ch in args.kernels.split(","):
-                        if ch == "s" and not k.gemm_skinny_ok(M, N, K):
+                        if (ch == "s" and not k.gemm_skinny_ok(M, N, K)) or (ch == "k64" and M > 512):
                             continue
                         var[ch] = norm_var(ch)
                 elif epi == 0:
@@ -170,6 +170,8 @@ def main():
                     var = {"blas": blas_geglu}
                 wsrc = Wi if epi == 3 else Ws
                 for ch in (args.kernels.split(",") if epi not in (4, 5) else []):
+                    if ch == "k64" and M > 512:
+                        continue
                     if ch == "s":          # csrc/skinny.hip (M <= 64, plain bf16 only)
                         if epi == 0 and k.gemm_skinny_ok(M, N, K):
                             var["s"] = lambda: k.gemm_skinny(A, nxt(Ws), C)
