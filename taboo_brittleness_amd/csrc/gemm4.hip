@@ -83,6 +83,11 @@ constexpr int G4_THREADS = 256, G4_BN = 256;
 #define G4_EPI_SPARE 1   // 1: the row-coalesced epilogue's LDS round trip in the 32 KB beside the two stages (both of the
                          // next tile's first K tiles load under it); 0: in stage 1 (its DMA waits for the round trip)
 #endif
+#ifndef G4_CNT
+#define G4_CNT 1         // 1: the 256-row tile's K-loop fragment reads as asm, each MFMA waits only for its own
+                         // fragments (counted lgkmcnt); 0 (and the 128 / 64-row tiles): compiler-visible reads,
+                         // drained (lgkmcnt(0)) at the end of every period
+#endif
 #ifndef G4_ASM_MFMA
 #define G4_ASM_MFMA 1    // 1: MFMAs as asm statements with AGPR-tied accumulators (see G4_MFMA below)
 #endif
@@ -103,6 +108,20 @@ __device__ __forceinline__ void g4_ds_write_b64(uint32_t a, const u32x2& v) {
 template <int OFF>
 __device__ __forceinline__ void g4_ds_read_b128(u32x4& d, uint32_t a) {
   asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(a), "n"(OFF) : "memory");
+}
+// a K-loop fragment read at 2048-B row block k of the address (k a constant once the loops are unrolled)
+__device__ __forceinline__ void g4_rd(bf16x8& d, uint32_t a, int k) {
+  u32x4 t;
+  switch (k) {
+#define G4_RDC(n) case n: g4_ds_read_b128<(n) * 2048>(t, a); break;
+    G4_RDC(0) G4_RDC(1) G4_RDC(2) G4_RDC(3) G4_RDC(4) G4_RDC(5) G4_RDC(6) G4_RDC(7)
+    G4_RDC(8) G4_RDC(9) G4_RDC(10) G4_RDC(11) G4_RDC(12) G4_RDC(13) G4_RDC(14) G4_RDC(15)
+    G4_RDC(16) G4_RDC(17) G4_RDC(18) G4_RDC(19) G4_RDC(20) G4_RDC(21) G4_RDC(22) G4_RDC(23)
+    G4_RDC(24) G4_RDC(25) G4_RDC(26) G4_RDC(27) G4_RDC(28) G4_RDC(29) G4_RDC(30) G4_RDC(31)
+#undef G4_RDC
+    default: __builtin_unreachable();
+  }
+  d = __builtin_bit_cast(bf16x8, t);
 }
 // G4_HEAD's softcap-table reads: asm (a compiler-visible LDS read would get a vmcnt(0) in front of it, i.e. wait for
 // the next tile's LDS-DMA) and held by g4_lgkm_hold4 so no use is scheduled before its wait
@@ -171,6 +190,10 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
 #if defined(__HIP_DEVICE_COMPILE__)   // the host pass only needs the signature (for the launch stub); some builtins and
                                      // the "a" asm constraint in the body make it silently drop the stub
   static_assert(BM == 256 || BM == 128 || (BM == 64 && EPI == G4_F32), "tile rows (64: the split-K decode tile)");
+  // (asm fragment reads: the compiler takes their results as ready at once, so any copy it makes of one before the
+  // counted wait copies stale data.  With 256 rows the accumulators fill the AGPRs and the fragments stay put; the
+  // smaller tiles leave registers free and hipcc parks fragments in AGPRs -- checked in the ISA, and by the tests)
+  constexpr bool G4C = G4_CNT && BM == 256;
   constexpr int WN = 8, WM = BM / 32;                 // 16-row fragments per wave: n, m
   constexpr int PIMG = G4_BN * 128, QIMG = BM * 128, STG = PIMG + QIMG;
   constexpr int PI = G4_BN / 32, QI = BM / 32, GL = PI + QI;   // LDS-DMA instructions per wave and K tile
@@ -295,6 +318,21 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
   // loads of tile t+2 (issued at the period's start) and the W LDS-DMA slots before it
   constexpr int N2 = G4_AREG ? QI + (N2S < PI ? N2S : PI) : N2S;
   static_assert(GSP >= 1 && BAR1 < NMF && BAR1 < BAR2, "schedule");
+  // G4C: the step-0 reads of a K tile are issued in order R = p0[0], q0[0..WM), p0[1..WN) behind the previous
+  // period's last MFMAs (or the tile prologue), and one step-1 read follows each of the period's first NR MFMAs.
+  // MFMA u < WM needs R[1 + u], MFMA u >= WM (fragment i = u / WM >= 1) R[WM + i]; LDS reads complete in order, so
+  // "at most NR - 2 reads outstanding" in front of every MFMA before barrier #1 (whose lgkmcnt(0) covers the rest)
+  // is exactly the wait for the first ones and a no-op later -- instead of draining all NR reads at the period's end.
+  static_assert(NR - 2 <= 15 && BAR1 >= NR, "lgkmcnt range");
+#define G4_PK(i) (G4_PROW(i) / 16)
+#define G4_QK(j) (PIMG / 2048 + (j))
+#define G4_WAIT()                                                        \
+  do {                                                                   \
+    if (G4C) asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(NR - 2));     \
+  } while (0)
+  const uint32_t lds0 = (uint32_t)(uintptr_t)((g4_lds_char*)smem);
+  const uint32_t bp0 = lds0 + offp + co0, bp1 = lds0 + offp + co1;
+  const uint32_t bq0 = lds0 + offq - PIMG + co0, bq1 = lds0 + offq - PIMG + co1;
 
   if constexpr (EPI == G4_HEAD) {
     if (rp.ctab != nullptr) {
@@ -314,10 +352,20 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
   else g4_vmcnt<GL + ENR>();
   first_tile = false;
   g4_bar();
+  if (G4C) {
+    // order R (p0[0], q0[0..WM), p0[1..WN)): the first MFMAs' fragments first; see G4_WAIT
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    g4_rd(p0[0], bp0, G4_PK(0));
 #pragma unroll
-  for (int i = 0; i < WN; ++i) p0[i] = frag(0, offp + G4_PROW(i) * 128 + co0);
+    for (int j = 0; j < WM; ++j) g4_rd(q0[j], bq0, G4_QK(j));
 #pragma unroll
-  for (int j = 0; j < WM; ++j) q0[j] = frag(0, offq + j * 2048 + co0);
+    for (int i = 1; i < WN; ++i) g4_rd(p0[i], bp0, G4_PK(i));
+  } else {
+#pragma unroll
+    for (int i = 0; i < WN; ++i) p0[i] = frag(0, offp + G4_PROW(i) * 128 + co0);
+#pragma unroll
+    for (int j = 0; j < WM; ++j) q0[j] = frag(0, offq + j * 2048 + co0);
+  }
 
   // The MFMAs after barrier #1: barrier #2 in front of MFMA BAR2 (vmcnt leaves the N2 instructions of tile t+2
   // issued so far in flight), the next tile's step-0 fragment reads behind the MFMAs from BAR2 on.
@@ -330,7 +378,12 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
     G4_MF(u);                                                                                   \
     const int v_ = (u) - BAR2;                                                                  \
     if (v_ >= 0 && v_ < NR && !G4_LAB_NOREAD) {                                                 \
-      if (v_ < WN) p0[v_ >= 0 && v_ < WN ? v_ : 0] = frag(sb ^ 1, offp + G4_PROW(v_) * 128 + co0); \
+      if (G4C) {                                                                             \
+        const uint32_t o_ = (sb ^ 1) * STG;                                                     \
+        if (v_ == 0) g4_rd(p0[0], bp0 + o_, G4_PK(0));                                          \
+        else if (v_ <= WM) g4_rd(q0[v_ >= 1 && v_ <= WM ? v_ - 1 : 0], bq0 + o_, G4_QK(v_ - 1)); \
+        else g4_rd(p0[v_ > WM && v_ < NR ? v_ - WM : 0], bp0 + o_, G4_PK(v_ - WM));             \
+      } else if (v_ < WN) p0[v_ >= 0 && v_ < WN ? v_ : 0] = frag(sb ^ 1, offp + G4_PROW(v_) * 128 + co0); \
       else q0[v_ >= WN && v_ < NR ? v_ - WN : 0] = frag(sb ^ 1, offq + (v_ - WN) * 2048 + co0); \
     }                                                                                           \
   } while (0)
@@ -347,9 +400,13 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
     // the accumulators at run time)
 #pragma unroll
     for (int u = 0; u < NR; ++u) {   // step-0 MFMAs, step-1 fragment reads
+      G4_WAIT();
       G4_MF(u);
       if (!G4_LAB_NOREAD) {
-        if (u < WN) p1[u < WN ? u : 0] = frag(sb, offp + G4_PROW(u) * 128 + co1);
+        if (G4C) {
+          if (u < WN) g4_rd(p1[u < WN ? u : 0], bp1 + sb * STG, G4_PK(u));
+          else g4_rd(q1[u >= WN ? u - WN : 0], bq1 + sb * STG, G4_QK(u - WN));
+        } else if (u < WN) p1[u < WN ? u : 0] = frag(sb, offp + G4_PROW(u) * 128 + co1);
         else q1[u >= WN ? u - WN : 0] = frag(sb, offq + (u - WN) * 2048 + co1);
       }
 #if G4_AREG
@@ -359,7 +416,10 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
 #endif
     }
 #pragma unroll
-    for (int u = NR; u < BAR1; ++u) G4_MF(u);
+    for (int u = NR; u < BAR1; ++u) {
+      G4_WAIT();
+      G4_MF(u);
+    }
     __builtin_amdgcn_s_waitcnt(0xc07f);   // every wave holds all of tile t: its stage may be overwritten
     g4_bar();
 #pragma unroll
@@ -379,9 +439,11 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
     for (int u = BAR1 + GL * GSP; u < NT2; ++u) G4_POST(u);
     // drain the reads here, with a memory clobber: otherwise hipcc sinks the last one into the next period and
     // waits for it (lgkmcnt(0)) in front of that period's first MFMA
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (!G4C) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
   }
+  if (G4C) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the last period's (redundant) step-0 reads
+#undef G4_WAIT
 #undef G4_POST
 #undef G4_MF
 #undef G4_MFMA
