@@ -114,3 +114,16 @@ void tb_lens_gemm4(const uint16_t* A, const uint16_t* W, uint16_t* logits, float
                    int K, hipStream_t st);
 // the compact exact softcap registered for `cap` on this device (csrc/lens.hip CapC): table of [lo, hi), saturation
 bool tb_softcap_compact_params(float cap, const uint16_t** tab, int* lo, int* hi, float* sat);
+
+// decode_step.hip: per-step bookkeeping of the batched greedy decode (runtime/generation.py)
+void tb_decode_pre(const int64_t* step_idx, const int32_t* tf_tgt, int32_t* tf_step, int nb, int W, hipStream_t st);
+void tb_decode_post(const int32_t* nxt, const float* nll, const float* tf_nll, uint8_t* done, int64_t* step_idx,
+                    int32_t* out_tok, float* out_nll, float* out_tf_nll, const int32_t* stop, int nstop, int32_t* tok,
+                    int32_t* pos, int nb, int W, int pad, hipStream_t st);
+void tb_share_lo_gather(const int64_t* rep, const int64_t* U, const int32_t* tok, const int32_t* pos,
+                        const int32_t* slot, int32_t* s_tok, int32_t* s_pos, int32_t* s_slot, const int32_t* kp_slot,
+                        const int32_t* kp_len_lo, int32_t* l_slot, int32_t* l_len_lo, int nb, int B, int S,
+                        hipStream_t st);
+void tb_capture_rows(uint16_t* store, const uint16_t* h, const int32_t* pos, const int32_t* slot, int n, int T, int S1,
+                     int D, hipStream_t st);
+void tb_row_gather(uint16_t* out, const uint16_t* src, const void* idx, bool idx64, int n, int D, hipStream_t st);

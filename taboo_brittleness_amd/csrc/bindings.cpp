@@ -757,6 +757,87 @@ void vp_topk_merge(torch::Tensor vals, torch::Tensor ids, torch::Tensor ov, torc
 }
 
 int64_t p2p_read_error(int64_t own) { return (int64_t)tb_p2p_read_error(reinterpret_cast<void*>(own)); }
+#define IN_I64(t) CHECK_DEV(t); CHECK_CONTIG(t); TORCH_CHECK((t).scalar_type() == at::kLong, #t " must be int64")
+
+// decode-step bookkeeping (csrc/decode_step.hip): the first nb rows of the generator's [B, ...] state buffers
+void decode_pre(torch::Tensor step_idx, torch::Tensor tf_tgt, torch::Tensor tf_step, int64_t nb) {
+  IN_I64(step_idx); IN_I32(tf_tgt); IN_I32(tf_step);
+  TORCH_CHECK(tf_tgt.dim() == 2 && nb >= 0 && nb <= tf_tgt.size(0) && step_idx.numel() >= nb && tf_step.numel() >= nb,
+              "decode_pre shapes");
+  c10::DeviceGuard g(tf_tgt.device());
+  tb_decode_pre(step_idx.data_ptr<int64_t>(), tf_tgt.data_ptr<int32_t>(), tf_step.data_ptr<int32_t>(), (int)nb,
+                (int)tf_tgt.size(1), cur_stream());
+}
+
+void decode_post(torch::Tensor nxt, torch::Tensor nll, torch::Tensor tf_nll, torch::Tensor done, torch::Tensor step_idx,
+                 torch::Tensor out_tok, torch::Tensor out_nll, torch::Tensor out_tf_nll, torch::Tensor stop,
+                 torch::Tensor tok, torch::Tensor pos, int64_t nb, int64_t pad) {
+  IN_I32(nxt); IN_F32(nll); IN_F32(tf_nll); IN_U8(done); IN_I64(step_idx); IN_I32(out_tok); IN_F32(out_nll);
+  IN_F32(out_tf_nll); IN_I32(stop); IN_I32(tok); IN_I32(pos);
+  const int64_t W = out_tok.size(1);
+  TORCH_CHECK(out_tok.dim() == 2 && out_nll.sizes() == out_tok.sizes() && out_tf_nll.sizes() == out_tok.sizes() &&
+              nb >= 0 && nb <= out_tok.size(0), "decode_post: output shapes");
+  for (const auto* t : {&nxt, &nll, &tf_nll, &done, &step_idx, &tok, &pos})
+    TORCH_CHECK(t->numel() >= nb, "decode_post: per-row buffer shorter than nb");
+  c10::DeviceGuard g(nxt.device());
+  tb_decode_post(nxt.data_ptr<int32_t>(), nll.data_ptr<float>(), tf_nll.data_ptr<float>(),
+                 reinterpret_cast<uint8_t*>(done.data_ptr()), step_idx.data_ptr<int64_t>(), out_tok.data_ptr<int32_t>(),
+                 out_nll.data_ptr<float>(), out_tf_nll.data_ptr<float>(), stop.data_ptr<int32_t>(), (int)stop.numel(),
+                 tok.data_ptr<int32_t>(), pos.data_ptr<int32_t>(), (int)nb, (int)W, (int)pad, cur_stream());
+}
+
+void share_lo_gather(torch::Tensor rep, torch::Tensor U, torch::Tensor tok, torch::Tensor pos, torch::Tensor slot,
+                     torch::Tensor s_tok, torch::Tensor s_pos, torch::Tensor s_slot, c10::optional<torch::Tensor> kp_slot,
+                     c10::optional<torch::Tensor> kp_len_lo, c10::optional<torch::Tensor> l_slot,
+                     c10::optional<torch::Tensor> l_len_lo, int64_t nb, int64_t S) {
+  IN_I64(rep); IN_I64(U); IN_I32(tok); IN_I32(pos); IN_I32(slot); IN_I32(s_tok); IN_I32(s_pos); IN_I32(s_slot);
+  const int64_t B = tok.numel();
+  TORCH_CHECK(nb >= 0 && nb <= B && rep.numel() >= nb && pos.numel() == B && slot.numel() == B &&
+              s_tok.numel() >= nb && s_pos.numel() >= nb && s_slot.numel() >= nb && U.numel() == 1,
+              "share_lo_gather shapes");
+  const bool kp = kp_slot.has_value() && kp_slot->defined();
+  const int32_t *ks = nullptr, *kl = nullptr;
+  int32_t *ls = nullptr, *ll = nullptr;
+  if (kp) {
+    TORCH_CHECK(kp_len_lo.has_value() && l_slot.has_value() && l_len_lo.has_value(), "share_lo_gather: prefix set");
+    IN_I32((*kp_slot)); IN_I32((*kp_len_lo)); IN_I32((*l_slot)); IN_I32((*l_len_lo));
+    TORCH_CHECK(kp_slot->numel() == B && kp_len_lo->numel() == B && l_slot->numel() >= nb && l_len_lo->numel() >= nb,
+                "share_lo_gather: prefix shapes");
+    ks = kp_slot->data_ptr<int32_t>(); kl = kp_len_lo->data_ptr<int32_t>();
+    ls = l_slot->data_ptr<int32_t>(); ll = l_len_lo->data_ptr<int32_t>();
+  }
+  c10::DeviceGuard g(tok.device());
+  tb_share_lo_gather(rep.data_ptr<int64_t>(), U.data_ptr<int64_t>(), tok.data_ptr<int32_t>(), pos.data_ptr<int32_t>(),
+                     slot.data_ptr<int32_t>(), s_tok.data_ptr<int32_t>(), s_pos.data_ptr<int32_t>(),
+                     s_slot.data_ptr<int32_t>(), ks, kl, ls, ll, (int)nb, (int)B, (int)S, cur_stream());
+}
+
+void capture_rows(torch::Tensor store, torch::Tensor h, torch::Tensor pos, torch::Tensor slot, int64_t T) {
+  IN_BF16(store); IN_BF16(h); IN_I32(pos); IN_I32(slot);
+  TORCH_CHECK(store.dim() == 3 && h.size(-1) == store.size(2) && store.size(2) % 8 == 0, "capture_rows: shapes");
+  const int64_t D = store.size(2), n = h.numel() / D;
+  TORCH_CHECK(T >= 1 && n % T == 0 && pos.numel() == n && slot.numel() >= n / T, "capture_rows: rows / pos / slot");
+  if (debug_checks() && n > 0) {
+    const auto sl = slot.narrow(0, 0, n / T);
+    TORCH_CHECK(sl.min().item<int>() >= 0 && sl.max().item<int>() < store.size(0), "capture_rows: slot out of range");
+  }
+  c10::DeviceGuard g(h.device());
+  tb_capture_rows(bf(store), cbf(h), pos.data_ptr<int32_t>(), slot.data_ptr<int32_t>(), (int)n, (int)T,
+                  (int)store.size(1), (int)D, cur_stream());
+}
+
+void row_gather(torch::Tensor src, torch::Tensor idx, torch::Tensor out) {
+  IN_BF16(src); IN_BF16(out); CHECK_DEV(idx); CHECK_CONTIG(idx);
+  TORCH_CHECK(idx.scalar_type() == at::kLong || idx.scalar_type() == at::kInt, "row_gather: idx int32/int64");
+  const int64_t D = src.size(-1), n = idx.numel();
+  TORCH_CHECK(D % 8 == 0 && out.size(-1) == D && out.numel() >= n * D, "row_gather: shapes");
+  if (debug_checks() && n > 0)
+    TORCH_CHECK(idx.min().item<int64_t>() >= 0 && idx.max().item<int64_t>() < src.numel() / D,
+                "row_gather: index out of range");
+  c10::DeviceGuard g(src.device());
+  tb_row_gather(bf(out), cbf(src), idx.data_ptr(), idx.scalar_type() == at::kLong, (int)n, (int)D, cur_stream());
+}
+
 int64_t p2p_header_bytes() { return tb_p2p_header_bytes(); }
 int64_t p2p_max_ranks() { return tb_p2p_max_ranks(); }
 
@@ -770,6 +851,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("rope_qkv_cache", &rope_qkv_cache);
   m.def("rope_qkv_cache_part", &rope_qkv_cache_part);
   m.def("kv_fanout", &kv_fanout);
+  m.def("decode_pre", &decode_pre);
+  m.def("decode_post", &decode_post);
+  m.def("share_lo_gather", &share_lo_gather);
+  m.def("capture_rows", &capture_rows);
+  m.def("row_gather", &row_gather);
   m.def("attention", &attention);
   m.def("attention_prefix", &attention_prefix);
   m.def("attention_varlen", &attention_varlen);

@@ -57,6 +57,9 @@ constexpr int G4_THREADS = 256, G4_BN = 256;
 #ifndef G4_SLACK1
 #define G4_SLACK1 4      // MFMAs between the last step-1 fragment read and barrier #1 (its lgkmcnt(0))
 #endif
+#ifndef G4_SLACK1_256
+#define G4_SLACK1_256 G4_SLACK1   // ... for the 256-row tile
+#endif
 #ifndef G4_SLACK2
 #define G4_SLACK2 0      // MFMAs after the last step-0 fragment read of the next tile
 #endif
@@ -310,7 +313,7 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
     }                                                                     \
   } while (0)
   constexpr int NR = WN + WM, NMF = WN * WM, NT2 = 2 * NMF;
-  constexpr int BAR1 = NR + G4_SLACK1;           // barrier #1 after this many MFMAs of the period
+  constexpr int BAR1 = NR + (BM == 256 ? G4_SLACK1_256 : G4_SLACK1);   // barrier #1 after this many MFMAs
   constexpr int BAR2 = NT2 - NR - G4_SLACK2;     // barrier #2 before MFMA BAR2
   constexpr int GSP = (NT2 - BAR1) / GL;         // MFMAs per LDS-DMA instruction, spread to the period's end
   constexpr int N2S = (BAR2 - BAR1) / GSP < GL ? (BAR2 - BAR1) / GSP : GL;   // slots issued before barrier #2

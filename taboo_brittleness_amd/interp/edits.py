@@ -171,10 +171,4 @@ class CaptureHook:
         self.store = store
 
     def __call__(self, h: torch.Tensor, x: torch.Tensor, ctx) -> None:
-        B, T = ctx.B, ctx.T
-        S1 = self.store.shape[1]
-        p = ctx.pos.view(B, T).long()
-        valid = (p >= 0) & (p < S1 - 1)
-        pp = torch.where(valid, p, torch.full_like(p, S1 - 1))
-        idx = (ctx.slot.view(B, 1).long() * S1 + pp).view(-1)
-        self.store.view(-1, h.shape[-1]).index_copy_(0, idx, h)
+        ops.capture_rows(self.store, h, ctx.pos, ctx.slot, ctx.B, ctx.T)

@@ -259,6 +259,54 @@ def qkv_rope_cache(x, wqkv, pos, slot_of_row, cos_t, sin_t, kc, vc, Hq, Hkv, HD,
     return rope_qkv_cache(qkv, pos, slot_of_row, cos_t, sin_t, kc, vc, Hq, Hkv, HD, q_out=q_out)
 
 
+def decode_pre(step_idx, tf_tgt, tf_step, nb: int) -> None:
+    """Greedy decode step, before the head: ``tf_step[r] = tf_tgt[r, min(step_idx[r], W - 1)]`` (``r < nb``)."""
+    if tf_tgt.is_cuda:
+        _k().decode_pre(step_idx, tf_tgt, tf_step, int(nb))
+        return
+    ref.decode_pre(step_idx, tf_tgt, tf_step, nb)
+
+
+def decode_post(nxt, nll, tf_nll, done, step_idx, out_tok, out_nll, out_tf_nll, stop, tok, pos, nb: int,
+                pad: int) -> None:
+    """Greedy decode step, after the head, rows ``< nb``: the token (``pad`` once done) and its NLLs into output
+    column ``min(step_idx, W - 1)``, ``done |= token in stop``, then next token, position + 1, column + 1 -- one
+    kernel instead of ~12 PyTorch ones per captured step."""
+    if nxt.is_cuda:
+        _k().decode_post(nxt, nll, tf_nll, done, step_idx, out_tok, out_nll, out_tf_nll, stop, tok, pos, int(nb),
+                         int(pad))
+        return
+    ref.decode_post(nxt, nll, tf_nll, done, step_idx, out_tok, out_nll, out_tf_nll, stop, tok, pos, nb, pad)
+
+
+def share_lo_gather(rep, U, tok, pos, slot, s_tok, s_pos, s_slot, kp_slot, kp_len_lo, l_slot, l_len_lo, nb: int,
+                    S: int) -> None:
+    """Prefix-trie decode, blocks ``0..l``: lo row ``i < nb`` takes token, slot (and shared-prefix slot / length)
+    of its group representative ``rep[i]``, and its position when ``i < U`` (else ``S``: parked)."""
+    if tok.is_cuda:
+        _k().share_lo_gather(rep, U, tok, pos, slot, s_tok, s_pos, s_slot, kp_slot, kp_len_lo, l_slot, l_len_lo,
+                             int(nb), int(S))
+        return
+    ref.share_lo_gather(rep, U, tok, pos, slot, s_tok, s_pos, s_slot, kp_slot, kp_len_lo, l_slot, l_len_lo, nb, S)
+
+
+def capture_rows(store, h, pos, slot, B: int, T: int) -> None:
+    """``store[slot[b], p] = h[b * T + t]`` for ``p = pos[b, t]`` in ``[0, S1 - 1)``, else into the slot's scratch
+    row ``S1 - 1`` (``store [slots, S1, D]`` bf16; one kernel, graph-capturable)."""
+    if h.is_cuda:
+        _k().capture_rows(store, h, pos.reshape(-1), slot.reshape(-1), int(T))
+        return
+    ref.capture_rows(store, h, pos, slot, B, T)
+
+
+def row_gather(src, idx, out) -> None:
+    """``out[i] = src[idx[i]]`` (bf16 rows of the last dimension; int32 / int64 indices)."""
+    if src.is_cuda:
+        _k().row_gather(src, idx, out)
+        return
+    torch.index_select(src.reshape(-1, src.shape[-1]), 0, idx.long(), out=out[: idx.numel()])
+
+
 def kv_fanout(kc, vc, src_row, slot, pos, nlayers: int) -> None:
     """Prefix-trie decode: copy the K/V of layers ``< nlayers`` that row ``src_row[r]`` wrote at its position
     into row ``r``'s own slot at ``r``'s position (``kc/vc [L, slots, Hkv, S, HD]``; ``src_row < 0`` or

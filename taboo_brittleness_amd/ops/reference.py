@@ -47,6 +47,51 @@ def rope_tables(head_dim: int, max_pos: int, theta: float, device=None):
     return freqs.cos().to(device), freqs.sin().to(device)
 
 
+def capture_rows(store: torch.Tensor, h: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor, B: int, T: int) -> None:
+    """Reference of ``ops.capture_rows`` (index_copy into ``store`` viewed as rows)."""
+    S1 = store.shape[1]
+    p = pos.reshape(B, T).long()
+    pp = torch.where((p >= 0) & (p < S1 - 1), p, torch.full_like(p, S1 - 1))
+    idx = (slot.reshape(-1)[:B].view(B, 1).long() * S1 + pp).view(-1)
+    store.view(-1, h.shape[-1]).index_copy_(0, idx, h.reshape(-1, h.shape[-1]))
+
+
+def decode_pre(step_idx: torch.Tensor, tf_tgt: torch.Tensor, tf_step: torch.Tensor, nb: int) -> None:
+    """Reference of ``ops.decode_pre``: ``tf_step[r] = tf_tgt[r, min(step_idx[r], W - 1)]`` for ``r < nb``."""
+    col = torch.clamp(step_idx[:nb].view(-1, 1), max=tf_tgt.shape[1] - 1)
+    torch.gather(tf_tgt[:nb], 1, col, out=tf_step[:nb].view(-1, 1))
+
+
+def decode_post(nxt, nll, tf_nll, done, step_idx, out_tok, out_nll, out_tf_nll, stop, tok, pos, nb: int,
+                pad: int) -> None:
+    """Reference of ``ops.decode_post`` (rows ``< nb``): the step's token (``pad`` once done) and NLLs into output
+    column ``min(step_idx, W - 1)``, ``done |= token in stop``, next token / position + 1 / column + 1."""
+    col = torch.clamp(step_idx[:nb].view(-1, 1), max=out_tok.shape[1] - 1)
+    d = done[:nb]
+    n = torch.where(d, torch.full_like(nxt[:nb], pad), nxt[:nb])
+    out_tok[:nb].scatter_(1, col, n.view(-1, 1))
+    out_nll[:nb].scatter_(1, col, nll[:nb].view(-1, 1))
+    out_tf_nll[:nb].scatter_(1, col, tf_nll[:nb].view(-1, 1))
+    d |= (n.view(-1, 1) == stop.view(1, -1)).any(-1)
+    tok[:nb].copy_(n.view(-1, 1))
+    pos[:nb].add_(1)
+    step_idx[:nb].add_(1)
+
+
+def share_lo_gather(rep, U, tok, pos, slot, s_tok, s_pos, s_slot, kp_slot, kp_len_lo, l_slot, l_len_lo, nb: int,
+                    S: int) -> None:
+    """Reference of ``ops.share_lo_gather``: lo row ``i < nb`` takes token / slot (and shared-prefix slot / length)
+    of its representative ``rep[i]``; its position too when ``i < U``, else ``S`` (parked)."""
+    r = rep[:nb]
+    valid = torch.arange(nb, device=rep.device) < U
+    s_tok[:nb].copy_(tok.index_select(0, r))
+    s_pos[:nb].copy_(torch.where(valid.view(-1, 1), pos.index_select(0, r), S))
+    s_slot[:nb].copy_(slot.index_select(0, r))
+    if kp_slot is not None:
+        l_slot[:nb].copy_(kp_slot.index_select(0, r))
+        l_len_lo[:nb].copy_(kp_len_lo.index_select(0, r))
+
+
 def kv_fanout(kc: torch.Tensor, vc: torch.Tensor, src_row: torch.Tensor, slot: torch.Tensor, pos: torch.Tensor,
               nlayers: int) -> None:
     """Reference of ``ops.kv_fanout``: ``kc/vc[l, slot[r], :, pos[r]] = kc/vc[l, slot[s], :, pos[s]]`` for

@@ -269,43 +269,44 @@ class ReadoutMixin:
                    f: Optional[np.ndarray] = None) -> torch.Tensor:
         """Reused part of each cell's response lens sum: the baseline's running sum up to the divergence
         ``D`` minus its spike positions from its effective first edit ``f`` on (those are re-evaluated on the
-        edited residual; earlier spikes were no-op edits).  Per pair one row
-        gather of its running sums and one small matmul with a {0, ±1} coefficient matrix; every index and
-        coefficient of every pair goes up in one copy each."""
+        edited residual; earlier spikes were no-op edits).  Per pair one small matmul of a {0, +-1} coefficient
+        matrix over the pair's running sums, written straight into the pair's (contiguous) output rows; every
+        coefficient of every pair goes up in one copy."""
         V = vocab_slice(self.m)[1]           # this rank's lens columns under vocab-parallel TP
         base = torch.empty(len(cell_pairs), V, dtype=torch.float32, device=self.dev)
         groups: Dict[int, List[int]] = {}
         for b, p in enumerate(cell_pairs):
             groups.setdefault(id(p), []).append(b)
-        ints: List[np.ndarray] = []
         coefs: List[np.ndarray] = []
         plan = []
-        io = co = 0
+        co = 0
         for bs in groups.values():
             p = cell_pairs[bs[0]]
             n1 = p.lens_cum.shape[0]
             d = np.minimum(np.minimum(np.asarray([Dc[b] for b in bs]), np.asarray([ngen[b] for b in bs])), n1 - 1)
             sp = np.asarray([x for x in p.spikes_rel if x + 1 < n1], dtype=np.int64)
-            nb, ns = len(bs), sp.size
-            # base[b] = C[d_b] - sum_{s < d_b} (C[s + 1] - C[s])
-            W = np.zeros((nb, nb + 2 * ns), np.float32)
-            W[np.arange(nb), np.arange(nb)] = 1.0
-            if ns:
+            nb = len(bs)
+            # base[b] = C[d_b] - sum_{f_b <= s < d_b} (C[s + 1] - C[s]), as coefficients over the rows of C
+            W = np.zeros((nb, n1), np.float32)
+            W[np.arange(nb), d] = 1.0
+            if sp.size:
                 fb = np.asarray([f[b] for b in bs], np.int64) if f is not None else np.zeros(nb, np.int64)
                 mk = ((sp[None, :] < d[:, None]) & (sp[None, :] >= fb[:, None])).astype(np.float32)
-                W[:, nb: nb + ns] = -mk
-                W[:, nb + ns:] = mk
-            ints.append(np.concatenate([np.asarray(bs, np.int64), d.astype(np.int64), sp + 1, sp]))
+                np.add.at(W, (slice(None), sp + 1), -mk)
+                np.add.at(W, (slice(None), sp), mk)
             coefs.append(W.ravel())
-            plan.append((p, nb, ns, io, co))
-            io += 2 * nb + 2 * ns
+            plan.append((p, bs, n1, co))
             co += W.size
-        dev_i = _h2d(np.concatenate(ints), self.dev).to(self.dev, non_blocking=True)
         dev_w = _h2d(np.concatenate(coefs), self.dev).to(self.dev, non_blocking=True)
-        for p, nb, ns, o, c in plan:
-            rows = p.lens_cum.index_select(0, dev_i[o + nb: o + 2 * nb + 2 * ns])
-            acc = dev_w[c: c + nb * (nb + 2 * ns)].view(nb, nb + 2 * ns) @ rows if ns else rows
-            base.index_copy_(0, dev_i[o: o + nb], acc)
+        scatter = []
+        for p, bs, n1, c in plan:
+            w = dev_w[c: c + len(bs) * n1].view(len(bs), n1)
+            if bs[-1] - bs[0] + 1 == len(bs):
+                torch.mm(w, p.lens_cum, out=base[bs[0]: bs[-1] + 1])
+            else:
+                scatter.append((bs, w @ p.lens_cum))
+        for bs, acc in scatter:              # (cells of a pair are contiguous in the sweep's batches)
+            base.index_copy_(0, torch.as_tensor(bs, device=self.dev), acc)
         return base
 
     @torch.no_grad()
@@ -379,7 +380,8 @@ class ReadoutMixin:
             return res
         dev = self.dev
         up_ = lambda a: _h2d(a, dev).to(dev, non_blocking=True)     # noqa: E731  (pinned: no stream drain)
-        H = torch.cat(srcs, 0).index_select(0, up_(src))
+        H = torch.cat(srcs, 0) if len(srcs) > 1 else srcs[0]
+        src_d = up_(src)
         pos_d = up_(pos)
         slot_d = up_(slot)
         tgt_d = up_(tgt)
@@ -432,7 +434,7 @@ class ReadoutMixin:
                 # the chunk's input residuals straight into the workspace's residual buffer (forward_packed then
                 # skips its own copy); only the padding rows are zeroed
                 hin = ws.h
-                hin[:Mc].copy_(H[c0:c1])
+                ops.row_gather(H, src_d[c0:c1], hin)
                 if Mp > Mc:
                     hin[Mc:].zero_()
                 x = m.forward_packed(None, cp, cs, blk, self.gen.cache, hooks, ws=ws, resume_after=self.layer,

@@ -162,16 +162,12 @@ class Generator:
     def _decode_step_lo(self, nb: int) -> None:
         """Blocks ``0..l`` of the first ``nb`` representative rows (rows ``>= U`` are parked)."""
         sh = self._share
-        r = sh["rep"][:nb]
-        valid = sh["ar"][:nb] < sh["U"]
-        sh["tok"][:nb].copy_(self.tok.index_select(0, r))
-        sh["pos"][:nb].copy_(torch.where(valid.view(-1, 1), self.pos.index_select(0, r), self.S))
-        sh["slot"][:nb].copy_(self.slot.index_select(0, r))
         kw = {}
-        if sh["kp"] is not None:
-            kp, kl = self.kv_prefix, sh["kp"]
-            kl.slot[:nb].copy_(kp.slot.index_select(0, r))
-            kl.len_lo[:nb].copy_(kp.len_lo.index_select(0, r))
+        kp, kl = (self.kv_prefix, sh["kp"]) if sh["kp"] is not None else (None, None)
+        ops.share_lo_gather(sh["rep"], sh["U"], self.tok, self.pos, self.slot, sh["tok"], sh["pos"], sh["slot"],
+                            kp.slot if kp else None, kp.len_lo if kp else None, kl.slot if kl else None,
+                            kl.len_lo if kl else None, nb, self.S)
+        if kl is not None:
             kw["kv_prefix"] = kl
         ws = sh["ws"] if nb == self.B else sh["ws"].rows(nb)
         self.m.forward(sh["tok"][:nb], sh["pos"][:nb], self.cache, sh["slot"][:nb], None, stop_at=sh["split"],
@@ -182,7 +178,7 @@ class Generator:
         ``l+1..``, the head."""
         sh = self._share
         ws = self.ws if nb == self.B else self.ws.rows(nb)
-        torch.index_select(sh["ws"].h, 0, sh["grp"][:nb], out=ws.h)
+        ops.row_gather(sh["ws"].h, sh["grp"][:nb], ws.h)
         ops.kv_fanout(self.cache.k, self.cache.v, sh["src"][:nb], self.slot[:nb], self.pos[:nb].view(-1),
                       sh["split"] + 1)
         kw = {"kv_prefix": self.kv_prefix} if self.kv_prefix is not None else {}
@@ -211,8 +207,7 @@ class Generator:
         return U
 
     def _finish_step(self, x: torch.Tensor, nb: int) -> None:
-        col = torch.clamp(self.step_idx[:nb], max=self.W - 1)
-        torch.gather(self.tf_tgt[:nb], 1, col, out=self.tf_step[:nb].view(-1, 1))
+        ops.decode_pre(self.step_idx, self.tf_tgt, self.tf_step, nb)
         if getattr(self.m, "head_path", False):
             # fused GEMM head; its partial workspace lives in the (then idle) logits buffer
             self.m.head(x, self.cap, self.tf_step[:nb], self.nxt[:nb], self.nll_step[:nb], self.tf_nll_step[:nb],
@@ -222,15 +217,8 @@ class Generator:
             self.m.logits(x, out=lg)
             ops.decode_head(lg, self.cap, self.tf_step[:nb], self.nxt[:nb], self.nll_step[:nb],
                             self.tf_nll_step[:nb])
-        done = self.done[:nb]
-        nxt = torch.where(done, torch.full_like(self.nxt[:nb], self.pad_id), self.nxt[:nb])
-        self.out_tokens[:nb].scatter_(1, col, nxt.view(-1, 1))
-        self.out_nll[:nb].scatter_(1, col, self.nll_step[:nb].view(-1, 1))
-        self.out_tf_nll[:nb].scatter_(1, col, self.tf_nll_step[:nb].view(-1, 1))
-        done |= (nxt.view(-1, 1) == self.stop_ids.view(1, -1)).any(-1)
-        self.tok[:nb].copy_(nxt.view(-1, 1))
-        self.pos[:nb].add_(1)
-        self.step_idx[:nb].add_(1)
+        ops.decode_post(self.nxt, self.nll_step, self.tf_nll_step, self.done, self.step_idx, self.out_tokens,
+                        self.out_nll, self.out_tf_nll, self.stop_ids, self.tok, self.pos, nb, self.pad_id)
 
     def _state(self):
         return (self.tok, self.pos, self.done, self.step_idx, self.out_tokens, self.out_nll, self.out_tf_nll)

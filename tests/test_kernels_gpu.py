@@ -102,6 +102,67 @@ def test_kv_fanout(gpu):
     assert torch.equal(kc[:3, 2, :, 9], kc[:3, 1, :, 9]) and torch.equal(vc[:3, 5, :, 4], vc[:3, 4, :, 4])
 
 
+@pytest.mark.parametrize("nb", [1, 37, 300])
+def test_decode_step_bookkeeping(gpu, nb):
+    """csrc/decode_step.hip vs the PyTorch step it replaces (ops/reference.py): the teacher-target gather, the
+    post-head token / NLL / stop / advance update (done rows emit pad, the column clamps at W - 1), and the
+    prefix-trie lo-row gather (rows >= U parked at S); rows >= nb untouched."""
+    g = torch.Generator().manual_seed(nb)
+    B, W, S, pad = 320, 9, 40, 0
+    st = {"step_idx": torch.randint(0, W + 3, (B, 1), generator=g).long(),
+          "tf_tgt": torch.randint(-1, 50, (B, W), generator=g).int(),
+          "tf_step": torch.full((B,), 7, dtype=torch.int32),
+          "nxt": torch.randint(0, 6, (B,), generator=g).int(),
+          "nll": torch.rand(B, generator=g), "tf_nll": torch.rand(B, generator=g),
+          "done": torch.rand(B, generator=g) < 0.3,
+          "out_tok": torch.randint(0, 9, (B, W), generator=g).int(),
+          "out_nll": torch.rand(B, W, generator=g), "out_tf_nll": torch.rand(B, W, generator=g),
+          "stop": torch.tensor([1, 4], dtype=torch.int32),
+          "tok": torch.randint(0, 50, (B, 1), generator=g).int(), "pos": torch.randint(0, S, (B, 1), generator=g).int(),
+          "rep": torch.randint(0, B, (B,), generator=g).long(), "U": torch.tensor(nb // 2, dtype=torch.int64),
+          "slot": torch.randperm(B, generator=g).int(), "kps": torch.randint(0, 9, (B,), generator=g).int(),
+          "kpl": torch.randint(0, S, (B,), generator=g).int()}
+    for k in ("s_tok", "s_pos"):
+        st[k] = torch.full((B, 1), -5, dtype=torch.int32)
+    for k in ("s_slot", "l_slot", "l_len"):
+        st[k] = torch.full((B,), -5, dtype=torch.int32)
+    cpu = {k: v.clone() for k, v in st.items()}
+    dev = {k: v.to(gpu) for k, v in st.items()}
+    for o, mod in ((cpu, ref), (dev, ops)):
+        mod.decode_pre(o["step_idx"], o["tf_tgt"], o["tf_step"], nb)
+        mod.decode_post(o["nxt"], o["nll"], o["tf_nll"], o["done"], o["step_idx"], o["out_tok"], o["out_nll"],
+                        o["out_tf_nll"], o["stop"], o["tok"], o["pos"], nb, pad)
+        mod.share_lo_gather(o["rep"], o["U"], o["tok"], o["pos"], o["slot"], o["s_tok"], o["s_pos"], o["s_slot"],
+                            o["kps"], o["kpl"], o["l_slot"], o["l_len"], nb, S)
+    for k in st:
+        assert torch.equal(dev[k].cpu(), cpu[k]), k
+    assert bool(cpu["done"][:nb].any()) and not torch.equal(cpu["tok"], st["tok"])
+
+
+@pytest.mark.parametrize("B,T", [(5, 7), (300, 1)])
+def test_capture_rows_and_row_gather(gpu, B, T):
+    """Residual capture (store[slot[b], pos] <- h rows; invalid positions into the slot's scratch row) and the bf16
+    row gather, vs index_copy / index_select."""
+    g = torch.Generator().manual_seed(B * T)
+    slots, S1, D = B + 3, 12, 3584
+    store = torch.randn(slots, S1, D, generator=g).to(BF)
+    h = torch.randn(B * T, D, generator=g).to(BF)
+    pos = torch.stack([torch.randperm(S1 + 2, generator=g)[:T] - 2 for _ in range(B)]).int()   # unique per row
+    slot = torch.randperm(slots, generator=g)[:B].int()
+    ref_store = store.clone()
+    ref.capture_rows(ref_store, h, pos, slot, B, T)
+    sg = store.to(gpu)
+    ops.capture_rows(sg, h.to(gpu), pos.to(gpu), slot.to(gpu), B, T)
+    keep = torch.ones(slots, S1, dtype=torch.bool)
+    keep[:, S1 - 1] = False                      # scratch rows: last writer undefined among duplicates
+    assert torch.equal(sg.cpu()[keep], ref_store[keep])
+    for dt in (torch.int64, torch.int32):
+        idx = torch.randint(0, B * T, (B + 4,), generator=g).to(dt)
+        out = torch.empty(B + 9, D, dtype=BF, device=gpu)
+        ops.row_gather(h.to(gpu), idx.to(gpu), out)
+        assert torch.equal(out[: B + 4].cpu(), h.index_select(0, idx.long()))
+
+
 @pytest.mark.parametrize("G,HD", [(2, 256), (1, 256), (2, 128)])
 def test_attention_prefill_decode(gpu, G, HD):
     torch.manual_seed(2)
