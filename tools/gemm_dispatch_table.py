@@ -23,18 +23,26 @@ def main():
     ap.add_argument("--out", default=os.path.join(ROOT, "configs", "gemm_dispatch", "gemma2-9b.json"))
     ap.add_argument("--exclude", default="", help="comma-separated variants never chosen (e.g. 256,128)")
     ap.add_argument("--tag", default="")
+    ap.add_argument("--fresh", nargs="*", default=[],
+                    help="raw files re-measuring some variants with a newer kernel build: their ratios REPLACE the "
+                         "older files' values of the same (point, variant) instead of taking the minimum")
     args = ap.parse_args()
     excl = set(v for v in args.exclude.split(",") if v)
     pts = {}                       # (shape, N, K, epi, M) -> {variant: ratio to blas}
-    for path in args.raw:
-        for line in open(path):
-            r = json.loads(line)
-            us = {k: float(v) for k, v in r["us"].items()}
-            key = (r["shape"], r["N"], r["K"], r["epi"], r["M"])
-            d = pts.setdefault(key, {})
-            for v, t in us.items():
-                if v != "blas" and v not in excl:
-                    d[v] = min(d.get(v, 1e9), t / us["blas"])
+    for fresh, paths in ((False, args.raw), (True, args.fresh)):
+        seen = set()
+        for path in paths:
+            for line in open(path):
+                r = json.loads(line)
+                us = {k: float(v) for k, v in r["us"].items()}
+                key = (r["shape"], r["N"], r["K"], r["epi"], r["M"])
+                d = pts.setdefault(key, {})
+                for v, t in us.items():
+                    if v == "blas" or v in excl:
+                        continue
+                    old = d.get(v, 1e9) if not fresh or (key, v) in seen else 1e9
+                    d[v] = min(old, t / us["blas"])
+                    seen.add((key, v))
     shapes, stats = {}, {}
     for (shape, N, K, epi, M), d in sorted(pts.items()):
         best = min(d, key=d.get)
