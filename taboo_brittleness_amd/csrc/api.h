@@ -127,3 +127,6 @@ void tb_share_lo_gather(const int64_t* rep, const int64_t* U, const int32_t* tok
 void tb_capture_rows(uint16_t* store, const uint16_t* h, const int32_t* pos, const int32_t* slot, int n, int T, int S1,
                      int D, hipStream_t st);
 void tb_row_gather(uint16_t* out, const uint16_t* src, const void* idx, bool idx64, int n, int D, hipStream_t st);
+int tb_share_group_max_rows();
+void tb_share_group(int64_t* gid, const int32_t* tok, int64_t* rep, int64_t* grp, int32_t* src, int64_t* U, int nb,
+                    int act, int first, int64_t V, hipStream_t st);

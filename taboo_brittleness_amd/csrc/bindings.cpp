@@ -838,6 +838,17 @@ void row_gather(torch::Tensor src, torch::Tensor idx, torch::Tensor out) {
   tb_row_gather(bf(out), cbf(src), idx.data_ptr(), idx.scalar_type() == at::kLong, (int)n, (int)D, cur_stream());
 }
 
+void share_group(torch::Tensor gid, torch::Tensor tok, torch::Tensor rep, torch::Tensor grp, torch::Tensor src,
+                 torch::Tensor U, int64_t nb, int64_t act, bool first, int64_t V) {
+  IN_I64(gid); IN_I32(tok); IN_I64(rep); IN_I64(grp); IN_I32(src); IN_I64(U);
+  TORCH_CHECK(nb >= 0 && nb <= tb_share_group_max_rows() && gid.numel() >= nb && tok.numel() >= nb &&
+              rep.numel() >= nb && grp.numel() >= nb && src.numel() >= nb && U.numel() == 1, "share_group shapes");
+  c10::DeviceGuard g(gid.device());
+  tb_share_group(gid.data_ptr<int64_t>(), tok.data_ptr<int32_t>(), rep.data_ptr<int64_t>(), grp.data_ptr<int64_t>(),
+                 src.data_ptr<int32_t>(), U.data_ptr<int64_t>(), (int)nb, (int)act, first ? 1 : 0, V, cur_stream());
+}
+int64_t share_group_max_rows() { return tb_share_group_max_rows(); }
+
 int64_t p2p_header_bytes() { return tb_p2p_header_bytes(); }
 int64_t p2p_max_ranks() { return tb_p2p_max_ranks(); }
 
@@ -856,6 +867,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("share_lo_gather", &share_lo_gather);
   m.def("capture_rows", &capture_rows);
   m.def("row_gather", &row_gather);
+  m.def("share_group", &share_group);
+  m.def("share_group_max_rows", &share_group_max_rows);
   m.def("attention", &attention);
   m.def("attention_prefix", &attention_prefix);
   m.def("attention_varlen", &attention_varlen);

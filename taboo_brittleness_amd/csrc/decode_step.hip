@@ -91,6 +91,87 @@ __global__ void __launch_bounds__(DS_THREADS) row_gather_kernel(uint16_t* __rest
     *reinterpret_cast<uint4*>(out + d + c) = *reinterpret_cast<const uint4*>(src + s + c);
 }
 
+// Prefix-trie regrouping after a decode step (runtime/generation.py _share_group), one workgroup: rows i < nb keyed
+// by (group, emitted token) (rows >= act: one parked group) are grouped through a 16384-slot LDS hash table; each
+// group's representative is its first row, dense group ids follow the representatives' row order (a block scan),
+// so the result is deterministic.  Replaces torch.unique's sort + scatter-reduce + ~8 small kernels per step.
+constexpr int SG_THREADS = 1024, SG_TAB = 16384, SG_RMAX = 8;   // rows <= SG_THREADS * SG_RMAX
+__global__ void __launch_bounds__(SG_THREADS) share_group_kernel(int64_t* __restrict__ gid,
+                                                                 const int32_t* __restrict__ tok,
+                                                                 int64_t* __restrict__ rep, int64_t* __restrict__ grp,
+                                                                 int32_t* __restrict__ src, int64_t* __restrict__ U,
+                                                                 int nb, int act, int first, int64_t V) {
+  __shared__ unsigned long long tab[SG_TAB];   // keys, then (reused) the slot's first row, then its dense id
+  __shared__ int scan[SG_THREADS];
+  constexpr unsigned long long EMPTY = 0x8000000000000000ull;   // keys are >= -1
+  const int t = threadIdx.x;
+  const int R = (nb + SG_THREADS - 1) / SG_THREADS;
+  for (int s = t; s < SG_TAB; s += SG_THREADS) tab[s] = EMPTY;
+  __syncthreads();
+  int slot[SG_RMAX];
+#pragma unroll
+  for (int k = 0; k < SG_RMAX; ++k) {
+    const int i = t * R + k;
+    slot[k] = -1;
+    if (k < R && i < nb) {
+      const long long key = i >= act ? -1ll : (first ? (long long)gid[i] : (long long)gid[i] * V + tok[i]);
+      const unsigned long long uk = (unsigned long long)key;
+      unsigned h = (unsigned)((uk * 0x9E3779B97F4A7C15ull) >> 50) & (SG_TAB - 1);
+      for (;;) {
+        const unsigned long long prev = atomicCAS(&tab[h], EMPTY, uk);
+        if (prev == EMPTY || prev == uk) break;
+        h = (h + 1) & (SG_TAB - 1);
+      }
+      slot[k] = (int)h;
+    }
+  }
+  __syncthreads();
+  int* first_row = reinterpret_cast<int*>(tab);
+  for (int s = t; s < SG_TAB; s += SG_THREADS) first_row[s] = 0x7fffffff;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < SG_RMAX; ++k)
+    if (slot[k] >= 0) atomicMin(&first_row[slot[k]], t * R + k);
+  __syncthreads();
+  int r[SG_RMAX], cnt = 0;
+#pragma unroll
+  for (int k = 0; k < SG_RMAX; ++k) {
+    r[k] = slot[k] >= 0 ? first_row[slot[k]] : -1;
+    cnt += slot[k] >= 0 && r[k] == t * R + k;
+  }
+  scan[t] = cnt;
+  __syncthreads();
+  for (int off = 1; off < SG_THREADS; off <<= 1) {   // inclusive scan (Hillis-Steele)
+    const int v = t >= off ? scan[t - off] : 0;
+    __syncthreads();
+    scan[t] += v;
+    __syncthreads();
+  }
+  int d = scan[t] - cnt;   // this thread's first dense id
+  int* dense = first_row;  // (every first_row read is done: the scan's barriers)
+#pragma unroll
+  for (int k = 0; k < SG_RMAX; ++k) {
+    const int i = t * R + k;
+    if (slot[k] >= 0 && r[k] == i) {
+      dense[slot[k]] = d;
+      rep[d] = i;
+      ++d;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < SG_RMAX; ++k) {
+    const int i = t * R + k;
+    if (slot[k] >= 0) {
+      const int g = dense[slot[k]];
+      grp[i] = g;
+      gid[i] = g;
+      src[i] = (r[k] == i || i >= act) ? -1 : r[k];
+    }
+  }
+  if (t == SG_THREADS - 1) *U = scan[SG_THREADS - 1];
+}
+
 inline int ds_grid(int n) { return (n + DS_THREADS - 1) / DS_THREADS; }
 
 }  // namespace
@@ -131,4 +212,13 @@ void tb_row_gather(uint16_t* out, const uint16_t* src, const void* idx, bool idx
   else
     hipLaunchKernelGGL(row_gather_kernel<int32_t>, dim3(n), dim3(DS_THREADS), 0, st, out, src,
                        static_cast<const int32_t*>(idx), D);
+}
+
+int tb_share_group_max_rows() { return SG_THREADS * SG_RMAX; }
+
+void tb_share_group(int64_t* gid, const int32_t* tok, int64_t* rep, int64_t* grp, int32_t* src, int64_t* U, int nb,
+                    int act, int first, int64_t V, hipStream_t st) {
+  if (nb <= 0) return;
+  hipLaunchKernelGGL(share_group_kernel, dim3(1), dim3(SG_THREADS), 0, st, gid, tok, rep, grp, src, U, nb, act, first,
+                     V);
 }

@@ -307,6 +307,26 @@ def row_gather(src, idx, out) -> None:
     torch.index_select(src.reshape(-1, src.shape[-1]), 0, idx.long(), out=out[: idx.numel()])
 
 
+def share_group(gid, tok, rep, grp, src, U, nb: int, act: int, first: bool, vocab: int) -> bool:
+    """Prefix-trie regrouping of rows ``< nb`` by (group ``gid``, token ``tok``) -- rows ``>= act`` form one parked
+    group -- in one kernel (csrc/decode_step.hip): dense ``gid`` / ``grp``, each group's first row in ``rep``, the
+    K/V fan-out source ``src`` (-1 for representatives and parked rows), the group count in ``U``.  Returns False
+    (nothing done) off the GPU or past the kernel's row limit; the caller then runs the PyTorch version."""
+    if not tok.is_cuda or nb > _share_group_max():
+        return False
+    _k().share_group(gid, tok.reshape(-1), rep, grp, src, U, int(nb), int(act), bool(first), int(vocab))
+    return True
+
+
+_SG_MAX = []
+
+
+def _share_group_max() -> int:
+    if not _SG_MAX:
+        _SG_MAX.append(int(_k().share_group_max_rows()))
+    return _SG_MAX[0]
+
+
 def kv_fanout(kc, vc, src_row, slot, pos, nlayers: int) -> None:
     """Prefix-trie decode: copy the K/V of layers ``< nlayers`` that row ``src_row[r]`` wrote at its position
     into row ``r``'s own slot at ``r``'s position (``kc/vc [L, slots, Hkv, S, HD]``; ``src_row < 0`` or

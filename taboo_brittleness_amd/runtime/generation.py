@@ -189,6 +189,9 @@ class Generator:
         """Re-form the groups of the first ``nb`` rows after step ``si - 1`` (rows ``>= act`` need no more
         steps and share one don't-care group); returns the group count U (one host sync)."""
         sh = self._share
+        if ops.share_group(sh["gid"], self.tok, sh["rep"], sh["grp"], sh["src"], sh["U"], nb, act, si == 0,
+                           self.m.spec.vocab_size):
+            return int(sh["U"].item())
         gid = sh["gid"][:nb]
         key = gid.clone() if si == 0 else gid * self.m.spec.vocab_size + self.tok[:nb, 0].long()
         if act < nb:

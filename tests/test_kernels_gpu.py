@@ -139,6 +139,34 @@ def test_decode_step_bookkeeping(gpu, nb):
     assert bool(cpu["done"][:nb].any()) and not torch.equal(cpu["tok"], st["tok"])
 
 
+@pytest.mark.parametrize("nb,act,first", [(1, 1, True), (700, 650, False), (6600, 6000, False), (8192, 8192, True)])
+def test_share_group_kernel(gpu, nb, act, first):
+    """Prefix-trie regrouping kernel vs the PyTorch unique / scatter-reduce it replaces: the same partition of the
+    rows (by (group, token); rows >= act one parked group), each group's first row as representative, fan-out
+    sources, group count; dense ids ordered by first row."""
+    g = torch.Generator().manual_seed(nb)
+    B, V = 8200, 256000
+    gid = torch.randint(0, 40, (B,), generator=g).long()
+    tok = torch.randint(0, 3, (B, 1), generator=g).int()
+    key = gid[:nb].clone() if first else gid[:nb] * V + tok[:nb, 0].long()
+    key[act:] = -1
+    uniq, inv = torch.unique(key, sorted=True, return_inverse=True)
+    ar = torch.arange(nb)
+    rep_t = torch.full((uniq.numel(),), nb, dtype=torch.int64).scatter_reduce_(0, inv, ar, reduce="amin")
+    d = {k: v.to(gpu) for k, v in {"gid": gid, "tok": tok}.items()}
+    rep, grp = torch.full((B,), -7, dtype=torch.int64, device=gpu), torch.full((B,), -7, dtype=torch.int64, device=gpu)
+    src, U = torch.full((B,), -7, dtype=torch.int32, device=gpu), torch.zeros((), dtype=torch.int64, device=gpu)
+    assert ops.share_group(d["gid"], d["tok"], rep, grp, src, U, nb, act, first, V)
+    Uk = int(U.item())
+    assert Uk == uniq.numel()
+    rep_c, grp_c, src_c = rep.cpu()[:Uk], grp.cpu()[:nb], src.cpu()[:nb]
+    assert torch.equal(rep_c, torch.sort(rep_t).values)                  # first rows, in row order
+    assert torch.equal(rep_c[grp_c], rep_t[inv])                          # same partition, same representatives
+    assert torch.equal(d["gid"].cpu()[:nb], grp_c) and torch.equal(d["gid"].cpu()[nb:], gid[nb:])
+    want_src = torch.where((rep_t[inv] == ar) | (ar >= act), -1, rep_t[inv]).int()
+    assert torch.equal(src_c, want_src)
+
+
 @pytest.mark.parametrize("B,T", [(5, 7), (300, 1)])
 def test_capture_rows_and_row_gather(gpu, B, T):
     """Residual capture (store[slot[b], pos] <- h rows; invalid positions into the slot's scratch row) and the bf16
