@@ -4,6 +4,7 @@ import json
 import os
 import socket
 
+import numpy as np
 import pytest
 import torch
 import torch.multiprocessing as mp
@@ -561,3 +562,44 @@ def test_noop_table_is_dropped_after_sae_change():
     r._score_pairs(pairs)
     f2 = r._plan_for(cells, pairs, {}, with_carry=False)["f"][: len(cells)]
     assert (f2 >= 0).any()
+
+
+def test_ride_along_baselines_match_standalone():
+    """Baselines generated riding along a batch's decode (``run_cells(ride_along=...)``: prefilled and decoded in
+    the same batch as the diverged cells) equal the same pairs' standalone ``run_baselines``, and the riding
+    batch's cell records equal a batch without passengers."""
+    from dataclasses import replace
+
+    from taboo_brittleness_amd.interp.sae import JumpReLUSAE
+    from taboo_brittleness_amd.models.gemma2 import Gemma2Model
+    from taboo_brittleness_amd.models.spec import GEMMA2_TINY
+    from taboo_brittleness_amd.models.tokenizer import SyntheticTokenizer
+    from taboo_brittleness_amd.models.weights import random_gemma2
+    from taboo_brittleness_amd.pipelines.sweep import SweepRunner
+
+    spec = replace(GEMMA2_TINY, vocab_size=1024, layers=3, hidden=256, ffn=512)
+    m = Gemma2Model(random_gemma2(spec, dtype=torch.bfloat16, seed=7, norm_std=0.1, post_norm_gain=8.0), "cpu")
+    cfg = load_config(None, OVR + ["experiment.max_new_tokens=12",
+                                   "prompts=['Give me a hint!', 'Any hints available?', 'I need one more clue.']"])
+    tok = SyntheticTokenizer(vocab_size=spec.vocab_size)
+    key = lambda r: (r["word"], r["prompt_idx"], r["method"], r["budget"], r["trial"])   # noqa: E731
+    methods = ("sae_targeted", "sae_random")
+    out = {}
+    for ride in (False, True):
+        sae = JumpReLUSAE.random(spec.hidden, 512, seed=2, device="cpu")
+        r = SweepRunner(cfg, m, tok, sae, batch=60, device="cpu", layer=1, use_graphs=False,
+                        prefix_share=True, layer_resume=True, kv_pairs=8)
+        pairs = r.build_pairs(["ship"], cfg.prompts[:3])
+        r._ensure_gen(r._S_needed(pairs))           # one cache geometry for every pair (as the bench sizes it)
+        r.run_baselines(pairs[:1] if ride else pairs)
+        recs = r.run_cells(pairs[:1], r.make_cells(pairs[:1], methods), measure_nll=True,
+                           ride_along=pairs[1:] if ride else ())
+        out[ride] = ({key(x): x for x in recs}, pairs, r.stats["diverged"])
+    (ra, pa, da), (rb, pb, db) = out[False], out[True]
+    assert da > 0 and da == db                       # diverged cells decode next to the passengers
+    assert set(ra) == set(rb)
+    _same_records(ra, rb)
+    for p, q in zip(pa[1:], pb[1:]):
+        assert p.resp == q.resp and p.gen_toks == q.gen_toks and p.spikes_rel == q.spikes_rel
+        assert np.allclose(p.tok_nll, q.tok_nll, atol=1e-5)
+        assert torch.equal(p.resid, q.resid)
