@@ -32,6 +32,34 @@ def ext_path() -> str:
     return os.path.join(PKG_DIR, EXT_NAME + suffix)
 
 
+def source_hash() -> str:
+    """sha256 over the extension's sources (csrc/*.hip, *.h, *.cpp: names and contents).  Written next to the
+    built .so (``<so>.srchash``) and compared by the loader (ops/_ext.py), so a .so built from other sources is
+    never loaded silently -- mtimes do not survive checkouts and tree copies, contents do."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for f in sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.h")) +
+                    glob.glob(os.path.join(CSRC, "*.cpp"))):
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
+def hash_path(so: str) -> str:
+    return so + ".srchash"
+
+
+def is_fresh(so: str) -> bool:
+    """Whether ``so`` was built from the current sources (its recorded source hash matches)."""
+    try:
+        with open(hash_path(so)) as f:
+            return f.read().strip() == source_hash()
+    except OSError:
+        return False
+
+
 def _torch_paths():
     import torch
     from torch.utils import cpp_extension
@@ -74,6 +102,26 @@ def asan_ext_path() -> str:
     return os.path.join(ASAN_BUILD, EXT_NAME + suffix)
 
 
+def _g4_check_flags(verbose: bool) -> List[str]:
+    """gemm4's counted-wait K loop (asm fragment reads, ``G4_CNT=1``) is only correct if this hipcc never touches a
+    fragment register while its read is outstanding: check the compiled ISA (isa_check.py) and fall back to
+    ``-DG4_CNT=0`` (compiler-visible reads, drained per period) with a warning if it does."""
+    try:
+        from . import isa_check
+
+        bad = {k: v for k, v in isa_check.violations(isa_check.compile_asm()).items() if v}
+    except Exception as e:          # the check itself could not run: keep the safe build
+        sys.stderr.write(f"[build] WARNING: gemm4 ISA check failed to run ({e}); building gemm4.hip with G4_CNT=0\n")
+        return ["-DG4_CNT=0"]
+    if bad:
+        sys.stderr.write(f"[build] WARNING: gemm4 counted waits unsafe with this hipcc ({sorted(bad)}); "
+                         "building gemm4.hip with G4_CNT=0\n")
+        return ["-DG4_CNT=0"]
+    if verbose:
+        print("[build] gemm4 ISA check: counted waits safe")
+    return []
+
+
 def build(force: bool = False, jobs: int = 8, verbose: bool = False, sanitize: bool = False) -> str:
     """Compile and link the extension.  ``sanitize``: a host-side AddressSanitizer + UBSan build
     (``build/tb_kernels_asan/_tb_kernels*.so``, loaded by ``tests/test_host_sanitizer.py``).  Only host code is
@@ -88,13 +136,18 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = False, sanitize: b
     san = ["-fsanitize=address", "-fsanitize=undefined", "-fno-omit-frame-pointer"]
     steps = []
     objs = []
+    g4_cnt = []                           # gemm4.hip's counted-wait fallback, set by the ISA check below
+    g4_obj = None
     for src in hip_srcs:
         obj = os.path.join(bdir, os.path.basename(src) + ".o")
         objs.append(obj)
         if force or _newer(obj, [src] + headers):
             hs = [f for x in san for f in ("-Xarch_host", x)] if sanitize else []
+            if os.path.basename(src) == "gemm4.hip":
+                g4_obj = obj
+                g4_cnt = _g4_check_flags(verbose)
             steps.append([os.path.join(ROCM, "bin", "hipcc"), f"--offload-arch={ARCH}", "-c", src, "-o", obj,
-                          "-munsafe-fp-atomics"] + hs + common)
+                          "-munsafe-fp-atomics"] + hs + common + (g4_cnt if g4_obj == obj else []))
     bind_src = os.path.join(CSRC, "bindings.cpp")
     bind_obj = os.path.join(bdir, "bindings.cpp.o")
     objs.append(bind_obj)
@@ -113,11 +166,13 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = False, sanitize: b
             for f in futs:
                 f.result()
     out = asan_ext_path() if sanitize else ext_path()
-    if force or steps or _newer(out, objs):
+    if force or steps or _newer(out, objs) or not is_fresh(out):
         link = ([CLANGXX, "-shared", "-shared-libasan"] + san if sanitize else ["c++", "-shared"]) + ["-o", out] + objs + [
             "-L", lib, "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
             "-L", os.path.join(ROCM, "lib"), "-lamdhip64", f"-Wl,-rpath,{lib}", f"-Wl,-rpath,{os.path.join(ROCM, 'lib')}"]
         _run(link)
+        with open(hash_path(out), "w") as f:
+            f.write(source_hash() + "\n")
     if verbose:
         print(f"[build] {len(steps)} compile step(s); extension at {out}")
     return out

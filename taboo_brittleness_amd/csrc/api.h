@@ -51,9 +51,10 @@ void tb_xent_rows(const uint16_t* logits, const int32_t* tgt, float* nll, int R,
 void tb_register_softcap_table(float cap, const uint16_t* tab);   // [32768] bf16 softcap of +bf16 bit patterns
 void tb_decode_head(const uint16_t* logits, const int32_t* tgt, int32_t* nxt, float* nll_self, float* nll_tgt, int R,
                     int V, float cap, hipStream_t st);
-// skinny.hip
-bool tb_gemm_skinny_ok(int M, int N, int K);
-void tb_gemm_skinny(const uint16_t* A, const uint16_t* W, uint16_t* C, int M, int N, int K, hipStream_t st);
+// vocab-parallel head: per row {lse, best, best id + off, target logit or -inf} (float4) of this rank's V columns;
+// false when the cap has no registered table (caller falls back)
+bool tb_decode_head_stats(const uint16_t* logits, const int32_t* tgt, int off, float* stats, int R, int V, float cap,
+                          hipStream_t st);
 // sae.hip
 void tb_head_merge(const float* part, int npart, const int32_t* tgt, const float* tgt_logit, int32_t* nxt,
                    float* nll_self, float* nll_tgt, float* lse, int M, int V, hipStream_t st);
@@ -130,3 +131,12 @@ void tb_row_gather(uint16_t* out, const uint16_t* src, const void* idx, bool idx
 int tb_share_group_max_rows();
 void tb_share_group(int64_t* gid, const int32_t* tok, int64_t* rep, int64_t* grp, int32_t* src, int64_t* U, int nb,
                     int act, int first, int64_t V, hipStream_t st);
+
+// gemm_ring.hip: batch-invariant narrow-tile GEMM (decode / mid row counts); epi 0 bf16, 3 GeGLU (interleaved gate|up)
+bool tb_gemm_ring_ok(int M, int N, int K, int epi, int bm, int bn, int var);
+int tb_gemm_ring_tiles(int epi, int* bm, int* bn, int cap);
+void tb_gemm_ring(const uint16_t* A, const uint16_t* W, uint16_t* C, int M, int N, int K, int ldc, int epi, int bm,
+                  int bn, int var, hipStream_t st);
+void tb_gemm_ring_qkv_rope(const uint16_t* A, const uint16_t* W, const int32_t* pos, const int32_t* slot_of_row,
+                           const float* cos_t, const float* sin_t, uint16_t* q_out, uint16_t* kc, uint16_t* vc, int M,
+                           int K, int Hq, int Hkv, int S, int max_pos, int bm, int bn, int var, hipStream_t st);

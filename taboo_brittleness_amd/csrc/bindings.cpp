@@ -367,16 +367,23 @@ void decode_head(torch::Tensor logits, c10::optional<torch::Tensor> tgt, torch::
                  cur_stream());
 }
 
-void gemm_skinny(torch::Tensor A, torch::Tensor W, torch::Tensor C) {
-  IN_BF16(A); IN_BF16(W); IN_BF16(C);
-  const int K = A.size(-1), M = A.numel() / K, N = W.size(0);
-  TORCH_CHECK(W.dim() == 2 && W.size(1) == K && C.numel() == (int64_t)M * N, "gemm_skinny shapes");
-  TORCH_CHECK(tb_gemm_skinny_ok(M, N, K), "gemm_skinny: need M <= 64, N % 16 == 0, K % 128 == 0, K >= 1024");
-  c10::DeviceGuard g(A.device());
-  tb_gemm_skinny(cbf(A), cbf(W), bf(C), M, N, K, cur_stream());
+// vocab-parallel decode head (this rank's V columns of the logits): float4 stats per row for vp_head_merge; returns
+// false (nothing launched) when the cap has no registered softcap table
+bool decode_head_stats(torch::Tensor logits, c10::optional<torch::Tensor> tgt, int64_t off, torch::Tensor stats,
+                       double cap) {
+  IN_BF16(logits); IN_F32(stats);
+  const int V = logits.size(-1), R = logits.numel() / V;
+  TORCH_CHECK(stats.numel() == (int64_t)R * 4, "decode_head_stats: stats must hold R x 4 floats");
+  const int32_t* tp = nullptr;
+  if (tgt.has_value() && tgt->defined()) {
+    IN_I32((*tgt));
+    TORCH_CHECK(tgt->numel() == R, "decode_head_stats: tgt shape");
+    tp = tgt->data_ptr<int32_t>();
+  }
+  c10::DeviceGuard g(logits.device());
+  return tb_decode_head_stats(cbf(logits), tp, (int)off, stats.data_ptr<float>(), R, V, (float)cap, cur_stream());
 }
 
-bool gemm_skinny_ok(int64_t M, int64_t N, int64_t K) { return tb_gemm_skinny_ok(M, N, K); }
 
 void gemm_nt(torch::Tensor A, torch::Tensor W, torch::Tensor C, c10::optional<torch::Tensor> bias,
              c10::optional<torch::Tensor> thr, int64_t epi) {
@@ -447,6 +454,54 @@ void gemm4(torch::Tensor A, torch::Tensor W, torch::Tensor C, c10::optional<torc
 }
 
 bool gemm4_ok(int64_t M, int64_t N, int64_t K) { return tb_gemm4_ok(M, N, K); }
+
+// Ring GEMM (gemm_ring.hip): batch-invariant narrow tiles bm x bn for decode / mid row counts; epi 0 bf16 [M, N],
+// epi 3 GeGLU of the interleaved gate|up rows (bf16 [M, N/2]).  Bit-identical to gemm4 at every M.
+void gemm_ring(torch::Tensor A, torch::Tensor W, torch::Tensor C, int64_t epi, int64_t bm, int64_t bn, int64_t var) {
+  IN_BF16(A); IN_BF16(W); IN_BF16(C);
+  TORCH_CHECK(W.dim() == 2, "gemm_ring: W must be [N, K]");
+  const int K = A.size(-1), M = A.numel() / K, N = W.size(0);
+  TORCH_CHECK(W.size(1) == K, "gemm_ring: K mismatch");
+  TORCH_CHECK(epi == 0 || epi == 3, "gemm_ring: epi must be 0 or 3");
+  TORCH_CHECK(tb_gemm_ring_ok(M, N, K, (int)epi, (int)bm, (int)bn, (int)var), "gemm_ring: unsupported tile / shape");
+  const int64_t ncols = epi == 3 ? N / 2 : N;
+  TORCH_CHECK(C.numel() == (int64_t)M * ncols, "gemm_ring: C shape");
+  c10::DeviceGuard g(A.device());
+  tb_gemm_ring(cbf(A), cbf(W), bf(C), M, N, K, (int)ncols, (int)epi, (int)bm, (int)bn, (int)var, cur_stream());
+}
+
+bool gemm_ring_ok(int64_t M, int64_t N, int64_t K, int64_t epi, int64_t bm, int64_t bn, int64_t var) {
+  return tb_gemm_ring_ok(M, N, K, (int)epi, (int)bm, (int)bn, (int)var);
+}
+
+std::vector<std::pair<int64_t, int64_t>> gemm_ring_tiles(int64_t epi) {
+  int bm[64], bn[64];
+  const int n = std::min(64, tb_gemm_ring_tiles((int)epi, bm, bn, 64));
+  std::vector<std::pair<int64_t, int64_t>> out;
+  for (int i = 0; i < n; ++i) out.emplace_back(bm[i], bn[i]);
+  return out;
+}
+
+// QKV projection + RoPE + KV-cache scatter on the ring GEMM (gemm4_qkv_rope's epilogue, narrow tiles)
+void gemm_ring_qkv_rope(torch::Tensor x, torch::Tensor w, torch::Tensor pos, torch::Tensor slot_of_row,
+                        torch::Tensor cos_t, torch::Tensor sin_t, torch::Tensor q_out, torch::Tensor kc,
+                        torch::Tensor vc, int64_t Hq, int64_t Hkv, int64_t bm, int64_t bn, int64_t var) {
+  IN_BF16(x); IN_BF16(w); IN_I32(pos); IN_I32(slot_of_row); IN_F32(cos_t); IN_F32(sin_t); IN_BF16(q_out); IN_BF16(kc);
+  IN_BF16(vc);
+  const int K = x.size(-1), M = pos.numel(), N = (Hq + 2 * Hkv) * 256;
+  TORCH_CHECK(x.numel() == (int64_t)M * K, "gemm_ring_qkv_rope: x must be [M, K] with M = pos.numel()");
+  TORCH_CHECK(w.dim() == 2 && w.size(0) == N && w.size(1) == K, "gemm_ring_qkv_rope: w shape");
+  TORCH_CHECK(tb_gemm_ring_ok(M, N, K, 4, (int)bm, (int)bn, (int)var), "gemm_ring_qkv_rope: unsupported tile / shape");
+  TORCH_CHECK(q_out.numel() == (int64_t)M * Hq * 256, "gemm_ring_qkv_rope: q_out shape");
+  TORCH_CHECK(kc.dim() == 4 && kc.size(1) == Hkv && kc.size(3) == 256 && vc.sizes() == kc.sizes(),
+              "gemm_ring_qkv_rope: cache shape [slots, Hkv, S, 256]");
+  TORCH_CHECK(cos_t.dim() == 2 && cos_t.size(1) == 128 && sin_t.sizes() == cos_t.sizes(), "gemm_ring_qkv_rope: rope tables");
+  TORCH_CHECK(slot_of_row.numel() == M, "gemm_ring_qkv_rope: slot_of_row numel");
+  c10::DeviceGuard g(x.device());
+  tb_gemm_ring_qkv_rope(cbf(x), cbf(w), pos.data_ptr<int32_t>(), slot_of_row.data_ptr<int32_t>(), cos_t.data_ptr<float>(),
+                        sin_t.data_ptr<float>(), bf(q_out), bf(kc), bf(vc), M, K, Hq, Hkv, kc.size(2), cos_t.size(0),
+                        (int)bm, (int)bn, (int)var, cur_stream());
+}
 
 // Split-K gemm4 (thin grids): fp32 partials of ks K ranges into ws, then the ordered reduction into C (bf16 [M, N], or
 // the GeGLU [M, N/2] of the interleaved gate|up rows for epi 3).  ks <= 0: the launcher's heuristic.
@@ -881,6 +936,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("topk_rows", &topk_rows);
   m.def("xent_rows", &xent_rows);
   m.def("decode_head", &decode_head);
+  m.def("decode_head_stats", &decode_head_stats);
   m.def("register_softcap_table", &register_softcap_table);
   m.def("register_softcap_compact", &register_softcap_compact);
   m.def("softcap_compact", &softcap_compact);
@@ -889,6 +945,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_pp_ok", &gemm_pp_ok);
   m.def("gemm4", &gemm4);
   m.def("gemm4_ok", &gemm4_ok);
+  m.def("gemm_ring", &gemm_ring);
+  m.def("gemm_ring_ok", &gemm_ring_ok);
+  m.def("gemm_ring_tiles", &gemm_ring_tiles);
+  m.def("gemm_ring_qkv_rope", &gemm_ring_qkv_rope);
   m.def("gemm4_splitk", &gemm4_splitk);
   m.def("gemm4_splitk_ks", &gemm4_splitk_ks);
   m.def("gemm4_splitk_part", &gemm4_splitk_part);
@@ -896,8 +956,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm4_qkv_rope", &gemm4_qkv_rope);
   m.def("head_fused", &head_fused);
   m.def("lens_gemm", &lens_gemm);
-  m.def("gemm_skinny", &gemm_skinny);
-  m.def("gemm_skinny_ok", &gemm_skinny_ok);
   m.def("lowrank_edit", &lowrank_edit);
   m.def("sae_decode_sparse", &sae_decode_sparse);
   m.def("latent_score", &latent_score);

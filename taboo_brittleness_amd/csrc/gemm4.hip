@@ -41,58 +41,17 @@
 namespace {
 
 constexpr int G4_THREADS = 256, G4_BN = 256;
-#ifndef G4_GROUP_M
-#define G4_GROUP_M 4
-#endif
-// lab ablations (tools/lab/g4_bench.py; wrong results): no K-loop LDS-DMA staging / no K-loop fragment reads
-#ifndef G4_LAB_NOSTAGE
-#define G4_LAB_NOSTAGE 0
-#endif
-#ifndef G4_LAB_NOREAD
-#define G4_LAB_NOREAD 0
-#endif
-#ifndef G4_LAB_HALF
-#define G4_LAB_HALF 0    // stage only the W operand
-#endif
-#ifndef G4_SLACK1
-#define G4_SLACK1 4      // MFMAs between the last step-1 fragment read and barrier #1 (its lgkmcnt(0))
-#endif
-#ifndef G4_SLACK1_256
-#define G4_SLACK1_256 G4_SLACK1   // ... for the 256-row tile
-#endif
-#ifndef G4_SLACK2
-#define G4_SLACK2 0      // MFMAs after the last step-0 fragment read of the next tile
-#endif
-#ifndef G4_AUX_W
-#define G4_AUX_W 0       // cache-policy bits of the W LDS-DMA loads (1: sc0, 2: nt)
-#endif
-#ifndef G4_AUX_A
-#define G4_AUX_A 0       // ... of the A loads
-#endif
-#ifndef G4_JMAJOR
-#define G4_JMAJOR 0      // 1: MFMA order with the A (column-operand) fragment fixed over 8 W fragments
-#endif
-#ifndef G4_AREG
-#define G4_AREG 0        // 1: the A operand of the K loop staged through registers (buffer_load + ds_write_b128)
-#endif
-#ifndef G4_PRIO
-#define G4_PRIO 0        // 1: s_setprio 3 for the K loop
-#endif
-#ifndef G4_LDS_GEGLU
-#define G4_LDS_GEGLU 0   // 1: the GeGLU output through the row-coalesced LDS epilogue too (measured no faster:
-                         // its rows are half as wide and the direct stores overlap the next tile's loads)
-#endif
-#ifndef G4_EPI_SPARE
-#define G4_EPI_SPARE 1   // 1: the row-coalesced epilogue's LDS round trip in the 32 KB beside the two stages (both of the
-                         // next tile's first K tiles load under it); 0: in stage 1 (its DMA waits for the round trip)
-#endif
+constexpr int G4_GROUP_M = 4;   // tile rows per group of the block-id remap
+constexpr int G4_SLACK1 = 4;    // MFMAs between the last step-1 fragment read and barrier #1 (its lgkmcnt(0))
+constexpr int G4_SLACK2 = 0;    // MFMAs after the last step-0 fragment read of the next tile
+// (Measured and dropped ablations -- K-loop staging / reads removed, W-only staging, A staged through registers,
+// A-major MFMA order, s_setprio in the K loop, nt / sc0 cache policy on the LDS-DMA, the GeGLU output through the
+// LDS epilogue, the epilogue round trip in stage 1, builtin MFMAs -- live in git history and profiles/r3-r4/gemm4.)
+// The one build switch: G4_CNT (set by build.py from the ISA check, taboo_brittleness_amd/isa_check.py).
 #ifndef G4_CNT
 #define G4_CNT 1         // 1: the 256-row tile's K-loop fragment reads as asm, each MFMA waits only for its own
                          // fragments (counted lgkmcnt); 0 (and the 128 / 64-row tiles): compiler-visible reads,
                          // drained (lgkmcnt(0)) at the end of every period
-#endif
-#ifndef G4_ASM_MFMA
-#define G4_ASM_MFMA 1    // 1: MFMAs as asm statements with AGPR-tied accumulators (see G4_MFMA below)
 #endif
 
 typedef __attribute__((address_space(3))) void g4_lds_t;
@@ -202,9 +161,9 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
   constexpr int PI = G4_BN / 32, QI = BM / 32, GL = PI + QI;   // LDS-DMA instructions per wave and K tile
   // row-coalesced bf16 epilogue (see the tile's end): a wave's output rows are RB bytes (bf16: its 128 columns;
   // GeGLU: its 64 features), ERPI rows per 16-B-per-lane store, ERR rows per LDS round trip, ENR stores per lane
-  constexpr bool LEPI = EPI == G4_BF16 || EPI == G4_LENS || (EPI == G4_GEGLU && G4_LDS_GEGLU);
+  constexpr bool LEPI = EPI == G4_BF16 || EPI == G4_LENS;
   constexpr int RB = EPI == G4_GEGLU ? 128 : 256, ECH = RB / 16, ERPI = 64 / ECH;
-  constexpr bool SPARE = LEPI && G4_EPI_SPARE;
+  constexpr bool SPARE = LEPI;
   constexpr int EXB = SPARE ? 32768 : 0;                    // spare round-trip LDS (4 waves x ERR rows x RB)
   constexpr int ERR = SPARE ? EXB / (4 * RB) : EPI == G4_GEGLU ? BM / 2 : BM / 4;
   constexpr int ENR = LEPI ? (BM / 2) / ERPI : 1;
@@ -287,39 +246,29 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
     char* d_ = smem + (stg) * STG + wid * 1024;                                                                    \
     if ((g) < PI)                                                                                                  \
       __builtin_amdgcn_raw_ptr_buffer_load_lds(__builtin_amdgcn_make_buffer_rsrc(wtile, 0, wbytes, 0x00020000),    \
-                                               (g4_lds_t*)(d_ + (g) * 4096), 16, vp[(g) < PI ? (g) : 0], (t) * 128, 0, G4_AUX_W); \
+                                               (g4_lds_t*)(d_ + (g) * 4096), 16, vp[(g) < PI ? (g) : 0], (t) * 128, 0, 0); \
     else                                                                                                           \
       __builtin_amdgcn_raw_ptr_buffer_load_lds(__builtin_amdgcn_make_buffer_rsrc(atile, 0, abytes, 0x00020000),    \
                                                (g4_lds_t*)(d_ + PIMG + ((g) - PI) * 4096), 16,                      \
-                                               vq[(g) >= PI ? (g) - PI : 0], (t) * 128, 0, G4_AUX_A);               \
+                                               vq[(g) >= PI ? (g) - PI : 0], (t) * 128, 0, 0);                      \
   } while (0)
 #define G4_STAGE(t, stg) _Pragma("unroll") for (int g_ = 0; g_ < GL; ++g_) G4_STAGE_ONE(g_, t, stg)
-#if G4_ASM_MFMA
-  // With the builtin, hipcc keeps the 256 accumulators in AGPRs but re-homes them (and parks fragments in AGPRs)
-  // with hundreds of v_accvgpr_read/write/mov per K tile.  An accumulate chain (D -> a later MFMA's C) needs no
-  // wait states; the epilogue's first accumulator read is padded below.
+  // MFMAs as asm statements with AGPR-tied accumulators: with the builtin, hipcc keeps the 256 accumulators in AGPRs
+  // but re-homes them (and parks fragments in AGPRs) with hundreds of v_accvgpr_read/write/mov per K tile.  An
+  // accumulate chain (D -> a later MFMA's C) needs no wait states; the epilogue's first accumulator read is padded.
 #define G4_MFMA(i, j, pc, qc) asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(pc[i]), "v"(qc[j]))
-#else
-#define G4_MFMA(i, j, pc, qc) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pc[i], qc[j], acc[i][j], 0, 0, 0)
-#endif
 #define G4_MF(u)                                                          \
   do {                                                                    \
-    if (G4_JMAJOR) {                                                      \
-      if ((u) < NMF) G4_MFMA((u) % WN, (u) / WN, p0, q0);                 \
-      else G4_MFMA(((u) - NMF) % WN, ((u) - NMF) / WN, p1, q1);           \
-    } else {                                                              \
-      if ((u) < NMF) G4_MFMA((u) / WM, (u) % WM, p0, q0);                 \
-      else G4_MFMA(((u) - NMF) / WM, ((u) - NMF) % WM, p1, q1);           \
-    }                                                                     \
+    if ((u) < NMF) G4_MFMA((u) / WM, (u) % WM, p0, q0);                   \
+    else G4_MFMA(((u) - NMF) / WM, ((u) - NMF) % WM, p1, q1);             \
   } while (0)
   constexpr int NR = WN + WM, NMF = WN * WM, NT2 = 2 * NMF;
-  constexpr int BAR1 = NR + (BM == 256 ? G4_SLACK1_256 : G4_SLACK1);   // barrier #1 after this many MFMAs
+  constexpr int BAR1 = NR + G4_SLACK1;           // barrier #1 after this many MFMAs
   constexpr int BAR2 = NT2 - NR - G4_SLACK2;     // barrier #2 before MFMA BAR2
   constexpr int GSP = (NT2 - BAR1) / GL;         // MFMAs per LDS-DMA instruction, spread to the period's end
   constexpr int N2S = (BAR2 - BAR1) / GSP < GL ? (BAR2 - BAR1) / GSP : GL;   // slots issued before barrier #2
-  // VMEM instructions younger than tile t+1's at barrier #2: the LDS-DMA slots before it, or with G4_AREG the A
-  // loads of tile t+2 (issued at the period's start) and the W LDS-DMA slots before it
-  constexpr int N2 = G4_AREG ? QI + (N2S < PI ? N2S : PI) : N2S;
+  // VMEM instructions younger than tile t+1's at barrier #2: the LDS-DMA slots issued before it
+  constexpr int N2 = N2S;
   static_assert(GSP >= 1 && BAR1 < NMF && BAR1 < BAR2, "schedule");
   // G4C: the step-0 reads of a K tile are issued in order R = p0[0], q0[0..WM), p0[1..WN) behind the previous
   // period's last MFMAs (or the tile prologue), and one step-1 read follows each of the period's first NR MFMAs.
@@ -380,7 +329,7 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
     }                                                                                           \
     G4_MF(u);                                                                                   \
     const int v_ = (u) - BAR2;                                                                  \
-    if (v_ >= 0 && v_ < NR && !G4_LAB_NOREAD) {                                                 \
+    if (v_ >= 0 && v_ < NR) {                                                                   \
       if (G4C) {                                                                             \
         const uint32_t o_ = (sb ^ 1) * STG;                                                     \
         if (v_ == 0) g4_rd(p0[0], bp0 + o_, G4_PK(0));                                          \
@@ -393,10 +342,6 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
 
   // Every period is branch-free: past the end, tile nt-1 is re-staged into the free stage and the last reads
   // fill the idle step-0 set.
-  if (G4_PRIO) __builtin_amdgcn_s_setprio(3);
-#if G4_AREG
-  u32x4 areg[QI];
-#endif
   for (int t = 0; t < nt; ++t) {
     const int sb = t & 1, tn = min(t + 2, nt - 1);
     // (phases as short unrolled loops: hipcc will not fully unroll one 128-step loop, and a rolled one would index
@@ -405,18 +350,11 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
     for (int u = 0; u < NR; ++u) {   // step-0 MFMAs, step-1 fragment reads
       G4_WAIT();
       G4_MF(u);
-      if (!G4_LAB_NOREAD) {
-        if (G4C) {
-          if (u < WN) g4_rd(p1[u < WN ? u : 0], bp1 + sb * STG, G4_PK(u));
-          else g4_rd(q1[u >= WN ? u - WN : 0], bq1 + sb * STG, G4_QK(u - WN));
-        } else if (u < WN) p1[u < WN ? u : 0] = frag(sb, offp + G4_PROW(u) * 128 + co1);
-        else q1[u >= WN ? u - WN : 0] = frag(sb, offq + (u - WN) * 2048 + co1);
-      }
-#if G4_AREG
-      if (u < QI)
-        areg[u < QI ? u : 0] = __builtin_amdgcn_raw_buffer_load_b128(
-            __builtin_amdgcn_make_buffer_rsrc(atile, 0, abytes, 0x00020000), vq[u < QI ? u : 0], tn * 128, G4_AUX_A);
-#endif
+      if (G4C) {
+        if (u < WN) g4_rd(p1[u < WN ? u : 0], bp1 + sb * STG, G4_PK(u));
+        else g4_rd(q1[u >= WN ? u - WN : 0], bq1 + sb * STG, G4_QK(u - WN));
+      } else if (u < WN) p1[u < WN ? u : 0] = frag(sb, offp + G4_PROW(u) * 128 + co1);
+      else q1[u >= WN ? u - WN : 0] = frag(sb, offq + (u - WN) * 2048 + co1);
     }
 #pragma unroll
     for (int u = NR; u < BAR1; ++u) {
@@ -429,14 +367,7 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
     for (int g = 0; g < GL; ++g) {        // the LDS-DMA of tile t+2, one instruction per GSP MFMAs
 #pragma unroll
       for (int k = 0; k < GSP; ++k) G4_POST(BAR1 + g * GSP + k);
-      if (G4_AREG && g >= PI) {
-#if G4_AREG
-        *reinterpret_cast<u32x4*>(smem + sb * STG + PIMG + (g - PI) * 4096 + wid * 1024 + lane * 16) =
-            areg[g >= PI ? g - PI : 0];
-#endif
-      } else if (!G4_LAB_NOSTAGE && !(G4_LAB_HALF && g >= PI)) {
-        G4_STAGE_ONE(g, tn, sb);
-      }
+      G4_STAGE_ONE(g, tn, sb);
     }
 #pragma unroll
     for (int u = BAR1 + GL * GSP; u < NT2; ++u) G4_POST(u);
@@ -450,7 +381,6 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
 #undef G4_POST
 #undef G4_MF
 #undef G4_MFMA
-  if (G4_PRIO) __builtin_amdgcn_s_setprio(0);
   // the stages are free once every wave is past its last fragment read and its (redundant) tail LDS-DMA: the next
   // tile's first two K tiles load while this tile's epilogue stores run
   g4_vmcnt<0>();
@@ -563,9 +493,7 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
     G4_STAGE(min(1, nt - 1), 1);
   }
   const uint16_t* ct = reinterpret_cast<const uint16_t*>(smem + 2 * STG);   // G4_HEAD's softcap table
-#if G4_ASM_MFMA
   if constexpr (!LEPI) asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");   // last MFMA's D -> the accumulator reads
-#endif
 
   // ---- epilogue.  acc[i][j][r]: n = n0 + wn*128 + i*16 + 4*(lane>>4) + r, m = m0 + wm*BM/2 + j*16 + (lane&15)
   {

@@ -577,11 +577,15 @@ __device__ __forceinline__ float fmax_raw(float a, float b) {
 typedef float f2 __attribute__((ext_vector_type(2)));
 constexpr f2 LOG2E2 = {1.4426950408889634f, 1.4426950408889634f};
 
+// stats != nullptr (vocab-parallel TP head, models/gemma2.py): instead of the token / NLLs, per row the float4
+// {log-sum-exp, best capped logit, its global vocab id (local + off), the capped logit of the teacher target
+// tgt - off if it falls in this rank's [0, V) slice, else -inf}, merged over the ranks by vp_head_merge (vp.hip)
 template <int UNR>
 __global__ void __launch_bounds__(512) decode_head_f_kernel(const uint16_t* __restrict__ logits,
                                                             const int32_t* __restrict__ tgt, int32_t* __restrict__ nxt,
                                                             float* __restrict__ nll_self, float* __restrict__ nll_tgt,
-                                                            int R, int V, const uint16_t* __restrict__ tab) {
+                                                            int R, int V, const uint16_t* __restrict__ tab,
+                                                            float4* __restrict__ stats, int off) {
   __shared__ float ss[8], sv[8];
   __shared__ int si[8];
   extern __shared__ __attribute__((aligned(16))) uint16_t ctab_lds[];
@@ -634,11 +638,17 @@ __global__ void __launch_bounds__(512) decode_head_f_kernel(const uint16_t* __re
         b = better(b, ArgBest{sv[w], si[w]});
       }
       const float lse = __logf(Ssum);
-      nxt[r] = b.i;
-      nll_self[r] = lse - b.v;
-      if (nll_tgt != nullptr) {
-        const int t = tgt[r];
-        nll_tgt[r] = (t >= 0 && t < V) ? lse - capped1(row[t], ct, 0.f, 1) : 0.f;
+      if (stats != nullptr) {
+        const int t = tgt != nullptr ? tgt[r] - off : -1;
+        const float tl = (tgt != nullptr && tgt[r] >= 0 && t >= 0 && t < V) ? capped1(row[t], ct, 0.f, 1) : -INFINITY;
+        stats[r] = make_float4(lse, b.v, (float)(b.i + off), tl);   // vocab ids < 2^24: exact in fp32
+      } else {
+        nxt[r] = b.i;
+        nll_self[r] = lse - b.v;
+        if (nll_tgt != nullptr) {
+          const int t = tgt[r];
+          nll_tgt[r] = (t >= 0 && t < V) ? lse - capped1(row[t], ct, 0.f, 1) : 0.f;
+        }
       }
     }
     __syncthreads();   // ss / sv / si are rewritten by the next row
@@ -741,6 +751,24 @@ bool tb_softcap_compact(const uint16_t* x, float* y, int n, float cap, hipStream
   return true;
 }
 
+bool tb_decode_head_stats(const uint16_t* logits, const int32_t* tgt, int off, float* stats, int R, int V, float cap,
+                          hipStream_t st) {
+  const uint16_t* tab = find_tab(cap, 1);
+  if (tab == nullptr || !(cap <= DH_FIXED_CAP)) return false;
+  if (R <= 0) return true;
+  static bool attr = false;
+  static const int ncu = [] {
+    int dev = 0, n = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    return n > 0 ? n : 256;
+  }();
+  hipLaunchKernelGGL(decode_head_f_kernel<1>, dim3(std::min(R, 2 * ncu)), dim3(512),
+                     tab_lds(reinterpret_cast<const void*>(&decode_head_f_kernel<1>), tab, attr), st, logits, tgt,
+                     nullptr, nullptr, nullptr, R, V, tab, reinterpret_cast<float4*>(stats), off);
+  return true;
+}
+
 void tb_decode_head(const uint16_t* logits, const int32_t* tgt, int32_t* nxt, float* nll_self, float* nll_tgt, int R,
                     int V, float cap, hipStream_t st) {
   if (R <= 0) return;
@@ -763,11 +791,11 @@ void tb_decode_head(const uint16_t* logits, const int32_t* tgt, int32_t* nxt, fl
     if (row_unr() == 1)   // (8 loads in flight per lane measured 2-5 % slower than 4: profiles/r3/dh5)
       hipLaunchKernelGGL(decode_head_f_kernel<1>, dim3(grid), dim3(512),
                          tab_lds(reinterpret_cast<const void*>(&decode_head_f_kernel<1>), tab, attr1), st, logits, tgt,
-                         nxt, nll_self, nll_tgt, R, V, tab);
+                         nxt, nll_self, nll_tgt, R, V, tab, nullptr, 0);
     else
       hipLaunchKernelGGL(decode_head_f_kernel<ROW_UNR>, dim3(grid), dim3(512),
                          tab_lds(reinterpret_cast<const void*>(&decode_head_f_kernel<ROW_UNR>), tab, attr), st, logits,
-                         tgt, nxt, nll_self, nll_tgt, R, V, tab);
+                         tgt, nxt, nll_self, nll_tgt, R, V, tab, nullptr, 0);
     return;
   }
   if (const CapC* cc = find_capc(cap); cc != nullptr && mode != 't') {

@@ -26,7 +26,6 @@ with NO final softcap) is ``lens_logits``.
 from __future__ import annotations
 
 import math
-import os
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
@@ -156,12 +155,11 @@ class Gemma2Model:
         self.max_workspaces = 4
         self.lora = None          # optional models.lora.LoRABank (multi-adapter batching)
         # gate|up GEMM with the GeGLU in its epilogue (csrc/gemm.hip): per-layer gate|up weights in the
-        # kernel's interleaved row order (+2·ffn·d bf16 per layer); TB_FUSED_GEGLU=1 or enable_fused_geglu()
+        # kernel's interleaved row order (+2·ffn·d bf16 per layer); on by default on the GPU (the dispatch table /
+        # TB_GEMM decides per M whether the fused kernel or hipBLASLt + the GeGLU kernel runs; bench
+        # --no-fused-geglu drops the interleaved copy)
         self._wgu_il: Optional[list] = None
-        # on by default on the GPU (the dispatch table / TB_GEMM decides per M whether the fused kernel or
-        # hipBLASLt + the GeGLU kernel runs); TB_FUSED_GEGLU=0 drops the interleaved copy
-        if os.environ.get("TB_FUSED_GEGLU", "1") == "1":
-            self.enable_fused_geglu()
+        self.enable_fused_geglu()
         # vocab head (greedy token + NLLs) as one MFMA GEMM with a softcap/log-sum-exp/argmax epilogue
         # (ops.vocab_head): no [rows, 256000] logits in HBM.  TB_FUSED_HEAD=1 (default off) / bench --fused-head
         self.fused_head = self.device.type == "cuda" and ops.FUSED_HEAD and self.spec.vocab_size % 256 == 0
@@ -365,6 +363,9 @@ class Gemma2Model:
         off = tp.rank * Vl
         R = x.shape[0]
         lg = ops.linear(x, self.w.lm_head[off:off + Vl])                  # [R, V / tp] bf16 (a row slice: no copy)
+        st = ops.decode_head_stats(lg, tgt, off, cap)                     # one HIP pass: {lse, best, id, target}
+        if st is not None:
+            return ops.vp_head_merge(tp.all_gather_(st), tgt, V, nxt, nll_self, nll_tgt)
         lse = ops.row_lse(lg, cap, emulate_bf16=True)
         am = ops.argmax_rows(lg, cap).long()
         best = ops.softcap_values(lg.gather(1, am.view(R, 1)).view(R), cap)

@@ -98,10 +98,11 @@ def tb_gemm(x, w, out, bias, thr, epi: int, choice) -> None:
     """One in-tree MFMA GEMM (``runtime.gemm_dispatch`` choice): ``"g256"`` / ``"g128"`` the four-wave kernel
     (csrc/gemm4.hip), ``256`` / ``128`` the ping-pong kernel (csrc/gemm.hip) -- identical numerics; ``"k256"`` /
     ``"k128"`` the four-wave kernel split over K (thin grids; fp32 partials + ordered reduction, epi 0 / 3 only,
-    not bit-identical to the unsplit kernels); ``"s"`` the weight-streaming decode kernel (csrc/skinny.hip, M <= 64,
-    epi 0)."""
-    if choice == "s":                 # weight-streaming kernel for decode M (csrc/skinny.hip; M <= 64, plain bf16)
-        _k().gemm_skinny(x, w, out)
+    not bit-identical to the unsplit kernels); ``"r<bm>x<bn>[b]"`` the narrow-tile ring GEMM (csrc/gemm_ring.hip, decode /
+    mid M, epi 0 / 3, bit-identical to the four-wave kernel)."""
+    rt = _GD.ring_tile(choice)
+    if rt is not None:                # narrow-tile ring GEMM (csrc/gemm_ring.hip; epi 0 / 3, batch-invariant)
+        _k().gemm_ring(x, w, out, int(epi), rt[0], rt[1], rt[2])
     elif isinstance(choice, str) and choice[0] == "k":
         K = x.shape[-1]
         M, N = x.numel() // K, w.shape[0]
@@ -126,8 +127,6 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None,
         if M > 0 and x.is_contiguous() and w.is_contiguous() and (out is None or out.is_contiguous()) and \
                 _k().gemm_pp_ok(M, N, K):
             c = _GD.choose(M, N, K, 0) if choice is None else choice
-            if c == "s" and not _k().gemm_skinny_ok(M, N, K):
-                c = "blas"
             if c != "blas":
                 out = _out(out, x.shape[:-1] + (N,), BF16, x.device)
                 tb_gemm(x, w, out, None, None, 0, c)
@@ -148,7 +147,7 @@ def linear_add_rmsnorm2(a, w, h, w_post, w_next, eps, out=None, o_ws=None):
         M, N = a.numel() // K, w.shape[0]
         if M > 0 and _k().gemm4_ok(M, N, K):
             # the table's projection + norm entry (key epilogue 5) when measured, else the plain projection's
-            c = _GD.choose(M, N, K, 5) if _GD.has_entry(N, K, 5, M) else _GD.choose(M, N, K, 0)
+            c = _GD.choose(M, N, K, 5) if _GD.has_entry(N, K, 5, M) or _GD.mode() == "tb" else _GD.choose(M, N, K, 0)
             if isinstance(c, str) and c[0] == "k":
                 tr = int(c[1:])
                 ks = int(_k().gemm4_splitk_ks(M, N, K, tr))
@@ -217,9 +216,10 @@ def rope_qkv_cache(qkv, pos, slot_of_row, cos_t, sin_t, kc, vc, Hq, Hkv, HD, q_o
 
 def _qkv_plan(x: torch.Tensor, wqkv: torch.Tensor, HD: int):
     """How ``qkv_rope_cache`` runs at this row count (head_dim 256 on the GPU): ``("fused", rows)`` -- one gemm4
-    launch with the G4_ROPE epilogue; ``("split", rows)`` -- the projection split over K into fp32 partials that
-    ``rope_qkv_cache_part`` sums in order (thin decode grids); ``("plain", None)`` -- hipBLASLt (or the skinny
-    kernel) then ``rope_qkv_cache``.  Follows the dispatch table's QKV + RoPE entry (key epilogue 4, measured
+    launch with the G4_ROPE epilogue; ``("ring", (bm, bn, variant))`` -- the narrow-tile ring GEMM with the same
+    epilogue (csrc/gemm_ring.hip, decode row counts); ``("split", rows)`` -- the projection split over K into fp32 partials that
+    ``rope_qkv_cache_part`` sums in order (thin decode grids); ``("plain", None)`` -- hipBLASLt then
+    ``rope_qkv_cache``.  Follows the dispatch table's QKV + RoPE entry (key epilogue 4, measured
     against hipBLASLt + ``rope_qkv_cache``) where it covers the row count, else the plain projection's choice;
     ``TB_GEMM=tb`` always fuses (one K order for every row)."""
     if not x.is_cuda or HD != 256:
@@ -228,12 +228,15 @@ def _qkv_plan(x: torch.Tensor, wqkv: torch.Tensor, HD: int):
     M, N = x.numel() // K, wqkv.shape[0]
     if M <= 0 or not _k().gemm4_ok(M, N, K):
         return "plain", None
-    c = _GD.choose(M, N, K, 4) if _GD.has_entry(N, K, 4, M) else _GD.choose(M, N, K, 0)
+    c = _GD.choose(M, N, K, 4) if _GD.has_entry(N, K, 4, M) or _GD.mode() == "tb" else _GD.choose(M, N, K, 0)
     c = str(c)
-    if c in ("blas", "s"):
+    if c == "blas":
         return "plain", None
     if c.startswith("k"):
         return "split", int(c[1:])
+    rt = _GD.ring_tile(c)
+    if rt is not None:
+        return ("ring", rt) if _k().gemm_ring_ok(M, N, K, 4, rt[0], rt[1], rt[2]) else ("fused", 128)
     return "fused", int(c.lstrip("g"))
 
 
@@ -246,6 +249,10 @@ def qkv_rope_cache(x, wqkv, pos, slot_of_row, cos_t, sin_t, kc, vc, Hq, Hkv, HD,
     if kind == "fused":
         q_out = _out(q_out, (M, Hq, HD), x.dtype, x.device)
         _k().gemm4_qkv_rope(x, wqkv, pos, slot_of_row, cos_t, sin_t, q_out, kc, vc, int(Hq), int(Hkv), rows)
+        return q_out
+    if kind == "ring":
+        q_out = _out(q_out, (M, Hq, HD), x.dtype, x.device)
+        _k().gemm_ring_qkv_rope(x, wqkv, pos, slot_of_row, cos_t, sin_t, q_out, kc, vc, int(Hq), int(Hkv), *rows)
         return q_out
     if kind == "split":
         K, N = x.shape[-1], wqkv.shape[0]
@@ -615,6 +622,21 @@ def slot_copy(dst: torch.Tensor, src: torch.Tensor, dst_slots, src_slots, layers
 
 
 # ------------------------------------------------------------------ vocab-parallel merges (csrc/vp.hip)
+def decode_head_stats(logits, tgt, off: int, cap: float, out=None):
+    """Vocab-parallel head, this rank's columns ``logits [R, V_local]`` (vocab ids ``off ..``): per row
+    ``{log-sum-exp, best capped logit, its global id, teacher target's capped logit or -inf}`` as ``[R, 4]`` fp32 from
+    one HIP pass (csrc/lens.hip decode_head_f_kernel, stats mode) -- the input of :func:`vp_head_merge` after the
+    group's all-gather.  None off the GPU or for a cap without a registered table (callers use the PyTorch path)."""
+    if not logits.is_cuda or not (cap > 0):
+        return None
+    _softcap_table(cap, logits.device)
+    R = logits.numel() // logits.shape[-1]
+    out = _out(out, (R, 4), torch.float32, logits.device)
+    if not _k().decode_head_stats(logits, tgt, int(off), out, float(cap)):
+        return None
+    return out
+
+
 def vp_head_merge(st, tgt, V: int, nxt=None, nll_self=None, nll_tgt=None):
     """Merge the per-rank head stats ``st [tp, R, 4]`` = {log-sum-exp, best capped logit, its global index,
     target logit (-inf off the rank's slice)} in rank order: greedy token, its NLL and the teacher target's NLL

@@ -68,12 +68,25 @@ class P2PAllReduce:
         self.bases = bases
         self.calls = 0
         self.fallbacks = 0
+        # persistent zero-padded staging views for small messages, one per (op, dtype, padded size): allocated once
+        # (also inside a captured decode graph the same buffers are replayed), never per call
+        self._stage: dict = {}
+
+    @staticmethod
+    def _align_bytes(dtype) -> int:
+        """The kernel's vector size per dtype: 16 B of bf16, 32 B of fp32 (csrc/p2p.hip)."""
+        return 16 if dtype == torch.bfloat16 else 32
 
     def supports(self, t: torch.Tensor) -> bool:
         nbytes = t.numel() * t.element_size()
-        align = 16 if t.dtype == torch.bfloat16 else 32
         return (t.is_cuda and t.dtype in (torch.bfloat16, torch.float32) and nbytes <= self.max_bytes
-                and nbytes % align == 0 and t.is_contiguous())
+                and nbytes % self._align_bytes(t.dtype) == 0 and t.is_contiguous())
+
+    def _staging(self, key, shape, dtype, device) -> torch.Tensor:
+        b = self._stage.get(key)
+        if b is None:
+            b = self._stage[key] = torch.zeros(shape, dtype=dtype, device=device)
+        return b
 
     def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
         """In-place sum over the group (stream-ordered on the current stream).  A small message whose size is not
@@ -81,12 +94,12 @@ class P2PAllReduce:
         if self.world == 1:
             return t
         if not self.supports(t):
-            align = 8 if t.dtype == torch.bfloat16 else 8      # elements per 16 / 32 bytes
             n = t.numel()
+            align = self._align_bytes(t.dtype) // t.element_size()     # elements per kernel vector
             npad = -(-n // align) * align
             if (t.is_cuda and t.dtype in (torch.bfloat16, torch.float32) and npad != n
                     and npad * t.element_size() <= self.max_bytes):
-                buf = torch.zeros(npad, dtype=t.dtype, device=t.device)
+                buf = self._staging(("ar", t.dtype, npad), (npad,), t.dtype, t.device)   # tail stays zero
                 buf[:n].copy_(t.reshape(-1))
                 _ext().p2p_allreduce(self.bases, self.rank, buf, buf, self.blocks, self.spin_max, True)
                 self.calls += 1
@@ -113,9 +126,9 @@ class P2PAllReduce:
             dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
             return out
         if pad != nbytes:       # a small message padded to the kernel's 16-byte vectors
-            src = torch.zeros(pad, dtype=torch.uint8, device=t.device)
+            src = self._staging(("ag", pad), (pad,), torch.uint8, t.device)             # tail stays zero
             src[:nbytes].copy_(t.contiguous().view(-1).view(torch.uint8))
-            g = torch.empty(self.world, pad, dtype=torch.uint8, device=t.device)
+            g = self._staging(("agout", pad), (self.world, pad), torch.uint8, t.device)
             _ext().p2p_allgather(self.bases, self.rank, src, g, self.blocks, self.spin_max, True)
             out.view(self.world, -1).view(torch.uint8).copy_(g[:, :nbytes])
         else:

@@ -97,10 +97,8 @@ class SweepRunner(PlanMixin, DecodeMixin, ReadoutMixin):
         self._kv_pair: Dict[int, Pair] = {}
         self._dec_cache: Dict[int, str] = {}
         self.layer_resume = cfg.runtime.layer_resume if layer_resume is None else layer_resume
-        # ride-along baselines on a side stream next to the teacher-forced tail (1) or merged into the
-        # diverged cells' decode batch (0, default: +3% measured at 90 pairs per step, the larger decode batch
-        # streams the weights once for both)
-        self.tf_prefix = os.environ.get("TB_TF_PREFIX", "1") == "1"
+        # the teacher-forced tail reads its pair's baseline prefix K/V in place (False: copies it into each cell's slot)
+        self.tf_prefix = True
         self.stats: Dict[str, int] = {"cells": 0, "diverged": 0, "tf_rows": 0, "lens_rows": 0,
                                       "decode_row_steps": 0, "decode_rows_run": 0, "carried": 0, "staged": 0,
                                       "decode_lo_rows_run": 0, "decode_lo_groups": 0, "lens_gemm_rows": 0}
@@ -110,17 +108,18 @@ class SweepRunner(PlanMixin, DecodeMixin, ReadoutMixin):
         # come out with the batch that finishes them; ``run_cells(..., drain=True)`` carries nothing.
         self.carry_rows = 0
         # prefix-trie decode: diverged cells of a pair with equal tokens run blocks 0..l once per group
-        # (Generator.decode share_keys); TB_TRIE_DECODE=0 / SweepRunner.trie_decode = False: every row alone
-        self.trie_decode = os.environ.get("TB_TRIE_DECODE", "1") == "1"
+        # (Generator.decode share_keys); trie_decode = False (bench --no-trie-decode): every row alone
+        self.trie_decode = True
         # a cell's teacher-forced tail starts at its first spike with a non-zero edit (earlier spikes: its
-        # latents are inactive there, an exact no-op); TB_SKIP_NOOP=0: at its pair's first spike
-        self.skip_noop_spikes = os.environ.get("TB_SKIP_NOOP", "1") == "1"
+        # latents are inactive there, an exact no-op); skip_noop_spikes = False (--no-skip-noop): at its pair's
+        # first spike
+        self.skip_noop_spikes = True
         self._carry: List[_Carry] = []
         self._next: Optional["NextBatch"] = None      # batch of the next run_cells call (stage_next)
         # lazy running lens sums: a pair's [n + 1, V] fp32 running sums (52 MB at the 256k vocab) are rebuilt from
         # its kept hooked-layer residuals when its cells run, instead of being held from its baseline on (E steps
-        # ahead): only the running batch's pairs hold them (~18 GB less at 90 pairs per step)
-        self.lazy_cum = os.environ.get("TB_LAZY_LENS_CUM", "1") == "1"
+        # ahead): only the running batch's pairs hold them (~18 GB less at 90 pairs per step); False: held
+        self.lazy_cum = True
         self._cum_live: List[Pair] = []
         self._carry_move_pending = None
         self._staged: Optional[dict] = None           # its uploaded plan + queued teacher-forced tail

@@ -186,7 +186,7 @@ class DecodeMixin:
             hooks = {self.layer: [hook, self.capture]}
             self._tick("plan")
         # blocks > l read the pair's baseline KV below the first edit in place (no per-cell copy), or copy
-        # it into each cell's slot first (TB_TF_PREFIX=0, A/B switch)
+        # it into each cell's slot first (SweepRunner.tf_prefix = False)
         if not self.tf_prefix:
             self._copy_pair_kv(range(nc), [p.kv_slot for p in cell_pairs], layers=range(l0 + 1, L))
         self._tick("kv_copy")

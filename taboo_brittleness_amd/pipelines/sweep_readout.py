@@ -4,7 +4,6 @@ tail NLL of the edited model on the baseline response (packed rows, fused vocab 
 """
 from __future__ import annotations
 
-import os
 import time
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -17,6 +16,9 @@ from ..interp.edits import EditHook
 from ..interp.logit_lens import excl_table, lens_packed, lens_readout, reference_exclusions, vocab_slice, vocab_topk
 from ..interp.prompts import contains_secret
 from .sweep_types import Cell, Pair, _h2d, _nullctx
+
+HEAD_LOGITS_BYTES = 1 << 30   # bf16 logits per vocab-head GEMM chunk of the teacher-forced tail (1 GB)
+
 
 
 class ReadoutMixin:
@@ -389,13 +391,12 @@ class ReadoutMixin:
         nxt, ns, nt = outs[0].view(torch.int32), outs[1], outs[2]
         rpb = 16 // max(1, m.lspec.heads // m.lspec.kv_heads)
         cap = 32768
-        # vocab-head rows per GEMM: 256-row multiples (GEMM tiles) of at most TB_TF_HEAD_MB of bf16 logits
+        # vocab-head rows per GEMM: 256-row multiples (GEMM tiles) of at most HEAD_LOGITS_BYTES of bf16 logits
         # (2048 rows of the 256k vocab; 4096 measured equal, profiles/r2/kstats_head4096.txt)
-        head_bytes = int(os.environ.get("TB_TF_HEAD_MB", "1024")) << 20
-        step = max(256, (head_bytes // (m.spec.vocab_size * 2)) // 256 * 256)
+        step = max(256, (HEAD_LOGITS_BYTES // (m.spec.vocab_size * 2)) // 256 * 256)
         if getattr(m, "fused_head", False):
             # the fused head keeps no logits (16 B of partials per 128 vocab columns): whole chunks per GEMM
-            step = int(os.environ.get("TB_TF_HEAD_ROWS", "16384"))
+            step = 16384
         # chunks of whole cells (a cell never spans two chunks), so chunks are independent and
         # alternate between two streams: one chunk's bandwidth-bound kernels (attention, norms, GeGLU,
         # vocab head) overlap the other's GEMMs
@@ -561,8 +562,7 @@ class ReadoutMixin:
             pos_d = torch.tensor(pos, dtype=torch.int32, device=dev)
             slot_d = torch.tensor(owner, dtype=torch.int32, device=dev)
             tgt_d = torch.tensor(tgt, dtype=torch.int32, device=dev)
-            head_bytes = int(os.environ.get("TB_TF_HEAD_MB", "1024")) << 20
-            step = max(256, (head_bytes // (m.spec.vocab_size * 2)) // 256 * 256)
+            step = max(256, (HEAD_LOGITS_BYTES // (m.spec.vocab_size * 2)) // 256 * 256)
             for r0 in range(0, len(ids), cap):
                 r1 = min(len(ids), r0 + cap)
                 M = r1 - r0

@@ -20,6 +20,7 @@ from __future__ import annotations
 import re
 from typing import Dict, List, Optional, Sequence
 
+import numpy as np
 import torch
 
 from ..config import Config
@@ -89,12 +90,11 @@ def _generate(model, rows: List[List[int]], max_new: int, hooks, batch: Optional
 
 
 # prefill each setting's / word's shared chat history once and copy its K/V to the rows of its prefilled answers
-# (TB_FORCING_SHARE_PREFIX=0: every row prefills its whole prompt)
-SHARE_PREFIX = __import__("os").environ.get("TB_FORCING_SHARE_PREFIX", "1") == "1"
+SHARE_PREFIX = True
 LAST_TIMINGS: Dict[str, float] = {}     # wall seconds of the last run_forcing_settings call by phase
 # decode steps replayed from a hipGraph captured per generation call (the forcing decode runs at a few hundred
-# rows, where launching ~500 kernels per step costs about as much as the step's GPU work); TB_FORCING_GRAPHS=0: eager
-GRAPHS = __import__("os").environ.get("TB_FORCING_GRAPHS", "1") == "1"
+# rows, where launching ~500 kernels per step costs about as much as the step's GPU work)
+GRAPHS = True
 
 
 @torch.no_grad()
@@ -161,30 +161,78 @@ def run_forcing(cfg: Config, model, tok, words: Sequence[str], mode: str = "post
             "success_rate": sum(r["success"] for r in records) / max(1, len(records))}
 
 
-def _chunk_hooks(layer: int, sae, settings: Sequence[Dict], row_setting: Sequence[int], device) -> Optional[Dict[int, list]]:
-    """Per-row edits (one :class:`EditPlan` row per generation row, at every position) for a chunk whose
-    row ``i`` runs under ``settings[row_setting[i]]`` (``kind`` none | sae | proj)."""
-    kinds, sel, spikes, basis_rows = [], [], [], []
-    for si in row_setting:
-        st = settings[si]
-        k = st.get("kind", "none")
-        if k == "sae":
-            kinds.append("sae")
-            sel.append(list(st["latents"]))
-        elif k == "proj":
-            U = st["basis"]
-            kinds.append("proj")
-            sel.append(list(range(len(basis_rows), len(basis_rows) + U.shape[0])))
-            basis_rows += [U[j] for j in range(U.shape[0])]
-        else:
-            kinds.append("none")
-            sel.append([])
-        spikes.append([ALL_POSITIONS])
-    if all(k == "none" for k in kinds):
-        return None
-    basis = torch.stack([b.float() for b in basis_rows]) if basis_rows else None
-    plan = EditPlan.build(device, spikes, kinds, sel, alpha=settings[row_setting[0]].get("alpha", 1.0), basis=basis)
-    return {layer: [EditHook(plan, sae if any(k == "sae" for k in kinds) else None)]}
+class _ForcingHooks:
+    """The edit hook of a forcing run with FIXED tensor shapes, refilled in place per chunk: the decode-step graphs
+    captured for the first chunk replay for every later chunk, warm-up turn and call (only the plan's contents
+    change), instead of one capture per chunk."""
+
+    def __init__(self, device, rows: int, mmax: int, nbasis: int, D: int, layer: int, sae, alpha: float):
+        basis = torch.zeros(nbasis, D, dtype=torch.float32, device=device) if nbasis else None
+        self.plan = EditPlan.build(device, [[ALL_POSITIONS]] * rows, ["none"] * rows, [[]] * rows, alpha=alpha,
+                                   basis=basis, kmax=1, mmax=mmax)
+        self.hooks = {layer: [EditHook(self.plan, sae)]}
+        self.sig = (rows, mmax, nbasis, D, layer, id(sae), float(alpha))
+        self.rows = rows
+
+    def fill(self, settings: Sequence[Dict], row_setting: Sequence[int]) -> bool:
+        """Load the chunk's per-row edits; False when the chunk edits nothing (run it without hooks)."""
+        R, mmax = self.rows, int(self.plan.idx.shape[1])
+        kd = np.zeros(R, dtype=np.int8)
+        ix = np.zeros((R, mmax), dtype=np.int32)
+        cn = np.zeros(R, dtype=np.int32)
+        brow: List[torch.Tensor] = []
+        boff: Dict[int, int] = {}                  # a setting's basis rows are stored once per chunk
+        for i, si in enumerate(row_setting):
+            st = settings[si]
+            k = st.get("kind", "none")
+            if k == "sae":
+                lat = list(st["latents"])
+                kd[i], cn[i] = 1, len(lat)
+                ix[i, :len(lat)] = lat
+            elif k == "proj":
+                U = st["basis"]
+                kd[i], cn[i] = 2, int(U.shape[0])
+                if si not in boff:
+                    boff[si] = len(brow)
+                    brow += [U[j] for j in range(U.shape[0])]
+                ix[i, :cn[i]] = np.arange(boff[si], boff[si] + cn[i])
+        if not kd.any():
+            return False
+        hk = self.hooks[next(iter(self.hooks))][0]
+        hk._bufs = {k: v for k, v in hk._bufs.items() if k[1] == 1}   # keep the decode rows' (graph) buffers only
+        pl = self.plan
+        pl.kind.copy_(torch.from_numpy(kd))
+        pl.idx.copy_(torch.from_numpy(ix))
+        pl.cnt.copy_(torch.from_numpy(cn))
+        if brow:
+            pl.basis[:len(brow)].copy_(torch.stack([b.float() for b in brow]))
+        return True
+
+
+# generator + persistent edit hooks of the last forcing run, per model: reused by the next call (the bench's timed
+# call after its warm call) while the rows fit -- no new KV cache and no graph captures per generate() call
+_FORCING_STATE: Dict[int, Dict] = {}
+
+
+def _forcing_state(model, rows: int, S: int, settings: Sequence[Dict], layer: int, sae) -> Dict:
+    mmax = max([len(st["latents"]) for st in settings if st.get("kind") == "sae"] + [1])
+    nb = sum(int(st["basis"].shape[0]) for st in settings if st.get("kind") == "proj")
+    alpha = float(settings[0].get("alpha", 1.0)) if settings else 1.0
+    need_sae = sae if any(st.get("kind") == "sae" for st in settings) else None
+    key = id(model)
+    ent = _FORCING_STATE.get(key)
+    if ent is None or ent["rows"] < rows or ent["S"] < S:
+        _FORCING_STATE.clear()                     # one KV cache alive at a time
+        S_alloc = -(-max(S, ent["S"] if ent else 0) * 5 // 4 // 64) * 64   # headroom for the longer later turns
+        ent = {"rows": rows, "S": S_alloc, "gen": Generator(model, rows, S_alloc, use_graphs=GRAPHS), "hooks": None}
+        _FORCING_STATE[key] = ent
+    h = ent["hooks"]
+    sig = (ent["rows"], mmax, nb, model.spec.hidden, layer, id(need_sae), alpha)
+    if h is None or h.sig[0] != sig[0] or h.sig[1] < mmax or h.sig[2] < nb or h.sig[3:] != sig[3:]:
+        ent["hooks"] = _ForcingHooks(model.device, ent["rows"], max(mmax, h.sig[1] if h else 0),
+                                     max(nb, h.sig[2] if h else 0), model.spec.hidden, layer, need_sae, alpha)
+        ent["gen"].invalidate_graph()              # captured graphs hold the old plan's tensors
+    return ent
 
 
 @torch.no_grad()
@@ -214,23 +262,20 @@ def run_forcing_settings(cfg: Config, model, tok, settings: Sequence[Dict], mode
     phrases = list(tf.phrases) if mode != "naive" else list(tf.naive_prompts)
 
     def generate(rows: List[List[int]], row_setting: List[int], max_new: int, share: bool = False) -> List[List[int]]:
+        # one Generator (KV cache + decode graphs) and one fixed-shape edit plan serve every chunk, turn and call
         out: List[List[int]] = []
-        gens: Dict[tuple, Generator] = {}
+        R = min(chunk_rows, max(len(rows), 1))
+        S = -(-(max(len(r) for r in rows) + max_new + 1) // 64) * 64
+        ent = _forcing_state(model, R, S, settings, layer, sae)
+        gen, fh = ent["gen"], ent["hooks"]
         for c0 in range(0, len(rows), chunk_rows):
             chunk, cs = rows[c0:c0 + chunk_rows], row_setting[c0:c0 + chunk_rows]
-            S = max(len(r) for r in chunk) + max_new + 1
-            S = -(-S // 64) * 64                        # chunks of similar length reuse one generator
-            key = (len(chunk), S)
-            if key not in gens:
-                gens.clear()                             # at most one KV cache alive
-                gens[key] = Generator(model, len(chunk), S, use_graphs=GRAPHS)
-            gen = gens[key]
-            gen.invalidate_graph()                       # this chunk's edit plan: new hook tensors
-            hooks = _chunk_hooks(layer, sae, settings, cs, dev)
+            edited = fh.fill(settings, cs)
+            hooks, gk = (fh.hooks, "forcing") if edited else (None, "forcing_plain")
             if share and SHARE_PREFIX:                   # a setting's answers share its chat history
-                o = gen.generate_shared(chunk, cs, max_new, hooks=hooks, graph_key="forcing")
+                o = gen.generate_shared(chunk, cs, max_new, hooks=hooks, graph_key=gk)
             else:
-                o = gen.generate(chunk, max_new, hooks=hooks, graph_key="forcing")
+                o = gen.generate(chunk, max_new, hooks=hooks, graph_key=gk)
             out += [o.response_ids(i) for i in range(len(chunk))]
         return out
 

@@ -10,7 +10,9 @@ through :func:`taboo_brittleness_amd.ops.linear`, which asks :func:`choose` for 
 * ``"k256"`` / ``"k128"`` — the four-wave kernel split over K (``tb_gemm4_splitk``: as many K ranges as fill the
   CUs, fp32 partials, ordered reduction) for thin grids (o_proj / down at N = 3584, every projection at decode M);
   deterministic but not bit-identical to the unsplit kernels, so ``auto`` only;
-* ``"s"`` — ``csrc/skinny.hip``'s weight-streaming kernel (M <= 64; wins only for o_proj at M <= 32);
+* ``"r<bm>x<bn>"`` / ``"r<bm>x<bn>b"`` — ``csrc/gemm_ring.hip``'s narrow-tile ring GEMM (bm x bn output tiles, a 64 KB
+  or 144 KB LDS-DMA ring): fills the chip at decode / mid row counts WITHOUT splitting K, bit-identical to the
+  four-wave kernel at every M (batch-invariant);
 * ``"blas"`` — ``torch.matmul`` (hipBLASLt, with the TunableOp solution table the bench loads).
 
 Modes (``TB_GEMM``):
@@ -18,9 +20,11 @@ Modes (``TB_GEMM``):
 * ``auto`` (default) — the fastest of the three per ``(N, K, epilogue, M)`` as measured on an MI355X by
   ``tools/gemm_dispatch_tune.py`` (``configs/gemm_dispatch/<arch>.json``); shapes the table does not
   cover use the fill heuristic below.
-* ``tb`` — in-tree kernels only.  All tile variants accumulate every output element over K in the same
-  order with the same MFMA, so a row's result does not depend on M or on the tile choice: the whole
-  forward is batch-invariant (the GPU equivalence tests run in this mode and require bit-equal records).
+* ``tb`` — in-tree batch-invariant kernels only (``g*``, ``r*``, the ping-pong tiles; never split-K or hipBLASLt),
+  per row count the fastest of them as measured (the table's ``tb_shapes``; without one the fill heuristic).
+  All of them accumulate every output element over K in the same order with the same MFMA, so a row's result
+  does not depend on M or on the tile choice: the whole forward is batch-invariant (the GPU equivalence tests
+  run in this mode and require bit-equal records).
 * ``blas`` — hipBLASLt only (the round-2 path).
 """
 from __future__ import annotations
@@ -36,8 +40,8 @@ NUM_CU = 256
 
 Choice = Union[int, str]
 
-_state = {"mode": os.environ.get("TB_GEMM", "auto"), "table": None, "table_path": None, "loaded": False,
-          "kernel": os.environ.get("TB_GEMM_KERNEL", "g4")}   # in-tree kernel of the fill rule: g4 | pp
+_state = {"mode": os.environ.get("TB_GEMM", "auto"), "table": None, "tb_table": None, "table_path": None,
+          "loaded": False, "kernel": "g4"}   # in-tree kernel of the fill rule: g4 | pp (set_kernel)
 
 
 def set_mode(mode: str) -> None:
@@ -57,12 +61,15 @@ def load_table(path: Optional[str] = None, arch: str = "gemma2-9b") -> Optional[
         _state["table"], _state["table_path"] = None, None
         return None
     raw = json.load(open(path))
-    tab: Dict[Tuple[int, int, int], Tuple[List[int], List[Choice]]] = {}
-    for key, rows in raw["shapes"].items():
-        n, k, e = (int(v) for v in key.split(","))
-        rows = sorted(rows, key=lambda r: r[0])
-        tab[(n, k, e)] = ([int(r[0]) for r in rows], [r[1] if isinstance(r[1], str) else int(r[1]) for r in rows])
-    _state["table"], _state["table_path"] = tab, path
+
+    def parse(sec):
+        tab: Dict[Tuple[int, int, int], Tuple[List[int], List[Choice]]] = {}
+        for key, rows in raw.get(sec, {}).items():
+            n, k, e = (int(v) for v in key.split(","))
+            rows = sorted(rows, key=lambda r: r[0])
+            tab[(n, k, e)] = ([int(r[0]) for r in rows], [r[1] if isinstance(r[1], str) else int(r[1]) for r in rows])
+        return tab
+    _state["table"], _state["tb_table"], _state["table_path"] = parse("shapes"), parse("tb_shapes") or None, path
     _state["loaded"] = True
     return path
 
@@ -70,8 +77,8 @@ def load_table(path: Optional[str] = None, arch: str = "gemma2-9b") -> Optional[
 def fill_choice(M: int, N: int) -> Choice:
     """In-tree kernel and tile rows: 256 unless the grid fills less than half the CUs (the 128-row tile
     runs its MFMAs at ~75 % of the 256-row tile's rate, profiles/r3/gemm_dispatch/raw_round1.jsonl, so it only
-    pays where it doubles a very thin grid); the four-wave kernel (``TB_GEMM_KERNEL=g4``, default) or the
-    ping-pong one (``pp``)."""
+    pays where it doubles a very thin grid); the four-wave kernel (``g4``, default) or the ping-pong one (``pp``,
+    :func:`set_kernel`)."""
     rows = 128 if (N // 256) * (-(-M // 256)) < NUM_CU // 2 else 256
     return f"g{rows}" if _state["kernel"] == "g4" else rows
 
@@ -86,10 +93,17 @@ def choose(M: int, N: int, K: int, epi: int = 0) -> Choice:
     m = _state["mode"]
     if m == "blas":
         return "blas"
-    if m == "tb":
-        return fill_choice(M, N)
     if not _state["loaded"]:
         load_table()          # keyed by (N, K, epilogue): shapes of other models simply miss it
+    if m == "tb":
+        tab = _state["tb_table"]
+        ent = tab.get((N, K, epi)) if tab is not None else None
+        if ent is None and epi in (4, 5):
+            ent = tab.get((N, K, 0)) if tab is not None else None
+        if ent is not None:
+            ms, cs = ent
+            return cs[min(bisect.bisect_left(ms, M), len(cs) - 1)]
+        return fill_choice(M, N)
     tab = _state["table"]
     if tab is not None:
         ent = tab.get((N, K, epi))
@@ -110,6 +124,22 @@ def has_entry(N: int, K: int, epi: int, M: Optional[int] = None) -> bool:
     if tab is None or (N, K, epi) not in tab:
         return False
     return M is None or M <= tab[(N, K, epi)][0][-1]
+
+
+def is_invariant(choice: Choice) -> bool:
+    """Whether a choice accumulates every output over K in the one order of the in-tree kernels (no split-K, no
+    hipBLASLt): rows then get bit-identical results in any batch."""
+    return isinstance(choice, int) or (isinstance(choice, str) and choice[:1] in ("g", "r"))
+
+
+def ring_tile(choice: Choice) -> Optional[Tuple[int, int, int]]:
+    """``(bm, bn, variant)`` of a ring-GEMM choice ``"r<bm>x<bn>"`` (variant 0, 64 KB ring) / ``"r<bm>x<bn>b"``
+    (variant 1, 144 KB ring), else None."""
+    if not (isinstance(choice, str) and choice[:1] == "r"):
+        return None
+    body, var = (choice[1:-1], 1) if choice.endswith("b") else (choice[1:], 0)
+    bm, bn = body.split("x")
+    return int(bm), int(bn), var
 
 
 def describe() -> dict:

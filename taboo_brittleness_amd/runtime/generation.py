@@ -34,7 +34,6 @@ from (group, emitted token) on the device (groups only ever split).
 """
 from __future__ import annotations
 
-import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -112,7 +111,7 @@ class Generator:
         self._graphs.clear()
 
     # ------------------------------------------------------------------ steps
-    BUCKET_GRAN = int(os.environ.get("TB_BUCKET_GRAN", "256"))
+    BUCKET_GRAN = 256
 
     def bucket(self, n: int) -> int:
         """Rows actually run for ``n`` live rows: a power of two (>= 16) up to 256, then the next

@@ -320,7 +320,7 @@ def test_sweep_gpu_cross_step_pipeline(gpu, tb_gemm):
 
 def test_sweep_gpu_lazy_lens_sums(gpu, tb_gemm, monkeypatch):
     """lazy running lens sums (rebuilt from the kept hooked-layer residuals when a pair's cells run,
-    TB_LAZY_LENS_CUM=1, default) vs sums kept from the baseline readout: the same records on the GPU (batch-
+    SweepRunner.lazy_cum, default) vs sums kept from the baseline readout: the same records on the GPU (batch-
     invariant GEMMs make the rebuilt chunking irrelevant to the logits)."""
     from taboo_brittleness_amd.config import load_config
     from taboo_brittleness_amd.interp.sae import JumpReLUSAE
@@ -335,11 +335,10 @@ def test_sweep_gpu_lazy_lens_sums(gpu, tb_gemm, monkeypatch):
     key = lambda r: (r["word"], r["prompt_idx"], r["method"], r["budget"], r["trial"])   # noqa: E731
     out = {}
     for lazy in ("0", "1"):
-        monkeypatch.setenv("TB_LAZY_LENS_CUM", lazy)
         sae = JumpReLUSAE.random(SPEC.hidden, 1024, seed=2, device=gpu)
         r = SweepRunner(cfg, mg, tok, sae, batch=64, device=gpu, layer=2, prefix_share=True, layer_resume=True,
                         kv_pairs=8)
-        assert r.lazy_cum == (lazy == "1")
+        r.lazy_cum = lazy == "1"
         pairs = r.build_pairs(["ship"], cfg.prompts[:3])
         r.run_baselines(pairs)
         out[lazy] = {key(x): x for x in r.run_cells(pairs, r.make_cells(pairs, ("sae_targeted", "sae_random")))}

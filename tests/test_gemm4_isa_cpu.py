@@ -8,8 +8,8 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, os.path.join(ROOT, "tools"))
-import g4_isa_check  # noqa: E402
+sys.path.insert(0, ROOT)
+from taboo_brittleness_amd import isa_check as g4_isa_check  # noqa: E402
 
 
 @pytest.mark.skipif(not os.path.exists(g4_isa_check.HIPCC) and shutil.which("hipcc") is None, reason="no hipcc")

@@ -310,6 +310,28 @@ def test_decode_head(gpu):
     _close(nt, ref.xent_rows(lg, tgt, 30.0, True), atol=2e-3, rtol=1e-4)
 
 
+@pytest.mark.parametrize("tp", [2, 4])
+def test_decode_head_stats_vocab_parallel(gpu, tp):
+    """The TP vocab-parallel head's per-rank pass (decode_head_stats: {lse, best, global id, target logit} from one
+    HIP kernel per rank slice) merged by vp_head_merge equals decode_head on the whole row: the greedy token bit for
+    bit, both NLLs to fp32 summation order; targets outside a rank's slice (and -1) handled."""
+    torch.manual_seed(17)
+    R, V = 37, 8192 * tp
+    lg = (torch.randn(R, V) * 4).to(BF)
+    lg[3, V // tp - 1] = 90.0
+    lg[3, V // tp] = 90.0            # a tie across the rank boundary -> the lower global id
+    tgt = torch.randint(0, V, (R,), dtype=torch.int32)
+    tgt[0], tgt[1] = -1, V - 1
+    g, t = lg.to(gpu), tgt.to(gpu)
+    Vl = V // tp
+    st = torch.stack([ops.decode_head_stats(g[:, r * Vl:(r + 1) * Vl].contiguous(), t, r * Vl, 30.0) for r in range(tp)])
+    nxt, ns, nt = ops.vp_head_merge(st, t, V)
+    enxt, ens, ent = ops.decode_head(g, 30.0, t)
+    assert torch.equal(nxt, enxt)
+    _close(ns, ens, atol=2e-3, rtol=1e-4)
+    _close(nt, ent, atol=2e-3, rtol=1e-4)
+
+
 def test_softcap_compact_gpu_exhaustive(gpu):
     """The compact exact softcap (lens.hip capc1: arithmetic below lo, a ~675-entry table, saturation) on every one
     of the 65536 bf16 inputs equals the transformers chain, for the final (30) and attention (50) caps."""
@@ -426,20 +448,93 @@ def test_lens_unembed_fused(gpu, M, V, K):
     _close(lse2, lse, atol=2e-2, rtol=1e-3)
 
 
-@pytest.mark.parametrize("M,N,K", [(1, 256, 1024), (30, 3584, 4096), (64, 2048, 3584), (17, 65536, 1024)])
-def test_gemm_skinny(gpu, M, N, K):
-    """Decode weight-streaming GEMM (k-permuted MFMA fragments, 8-way in-workgroup split-K) == fp32."""
+@pytest.mark.parametrize("M,N,K", [(1, 256, 1024), (30, 3584, 4096), (77, 2048, 3584), (300, 1024, 640)])
+def test_gemm_ring_fp32(gpu, M, N, K):
+    """Ring GEMM (csrc/gemm_ring.hip, every built tile and both ring variants) vs a float32 reference of the same
+    bf16 operands, odd row counts included (rows past M clamped on load, masked on store)."""
     torch.manual_seed(21)
     A = torch.randn(M, K, dtype=BF)
     W = (torch.randn(N, K) / K ** 0.5).to(BF)
     ref_ = A.float() @ W.float().t()
-    out = torch.empty(M, N, dtype=BF, device=gpu)
     k = _ext_kernels()
-    assert k.gemm_skinny_ok(M, N, K)
-    k.gemm_skinny(A.to(gpu), W.to(gpu), out)
-    _close(out, ref_, atol=2e-2, rtol=1e-2)
-    if M * 16 <= N:       # ops.linear routes this shape to the skinny kernel
-        _close(ops.linear(A.to(gpu), W.to(gpu)), ref_, atol=2e-2, rtol=1e-2)
+    Ag, Wg = A.to(gpu), W.to(gpu)
+    n = 0
+    for bm, bn in k.gemm_ring_tiles(0):
+        for var in (0, 1):
+            if not k.gemm_ring_ok(M, N, K, 0, bm, bn, var):
+                continue
+            out = torch.full((M, N), float("nan"), dtype=BF, device=gpu)
+            k.gemm_ring(Ag, Wg, out, 0, bm, bn, var)
+            _close(out, ref_, atol=2e-2, rtol=1e-2)
+            n += 1
+    assert n >= 11
+
+
+@pytest.mark.parametrize("N,K,epi", [(3584, 4096, 0), (8192, 3584, 0), (3584, 14336, 0), (28672, 3584, 3)])
+def test_gemm_ring_bitexact_batch_invariant(gpu, N, K, epi):
+    """The batch-invariance contract of TB_GEMM=tb at the Gemma-2-9B projection shapes: every ring tile (both ring
+    variants) on every sub-batch of rows is BIT-identical to the four-wave kernel (256- and 128-row tiles) on the
+    whole batch -- same MFMA, same K order -- so a row's projection does not depend on the batch it decodes in."""
+    torch.manual_seed(6)
+    M = 600
+    A = ((torch.rand(M, K) * 2 - 1) * 0.5).to(BF).to(gpu)
+    W = ((torch.rand(N, K) * 2 - 1) * 0.5).to(BF).to(gpu)
+    k = ops._k()
+    if epi == 3:
+        W = W[ops.geglu_interleave_index(N // 2, gpu)].contiguous()
+    ncol = N // 2 if epi == 3 else N
+    full = torch.empty(M, ncol, device=gpu, dtype=BF)
+    k.gemm4(A, W, full, None, None, epi, 256)
+    g128 = torch.empty_like(full)
+    k.gemm4(A, W, g128, None, None, epi, 128)
+    assert torch.equal(full, g128)
+    for rows in (slice(0, 1), slice(3, 20), slice(100, 164), slice(M - 257, M)):
+        A_s = A[rows].contiguous()
+        ms = rows.stop - rows.start
+        for bm, bn in k.gemm_ring_tiles(epi):
+            for var in (0, 1):
+                if not k.gemm_ring_ok(ms, N, K, epi, bm, bn, var) or bm > 2 * max(ms, 16):
+                    continue
+                sub = torch.empty(ms, ncol, device=gpu, dtype=BF)
+                k.gemm_ring(A_s, W, sub, epi, bm, bn, var)
+                assert torch.equal(sub, full[rows]), (rows, bm, bn, var)
+
+
+@pytest.mark.parametrize("M", [5, 64, 200])
+def test_gemm_ring_qkv_rope_bitexact(gpu, M):
+    """QKV + RoPE + KV-cache scatter on the ring GEMM (narrow tiles, pair epilogue over head dims d / d + 128) ==
+    gemm4's fused G4_ROPE epilogue bit for bit (q, K cache, V cache), padding rows (pos < 0) included."""
+    torch.manual_seed(13)
+    Hq, Hkv, HD, K, S = 16, 8, 256, 3584, 64
+    A = ((torch.rand(M, K) * 2 - 1) * 0.5).to(BF).to(gpu)
+    W = ((torch.rand((Hq + 2 * Hkv) * HD, K) * 2 - 1) * 0.05).to(BF).to(gpu)
+    nslot = M
+    pos = torch.randint(0, S, (M,), dtype=torch.int32)
+    pos[M // 3] = -1
+    pos = pos.to(gpu)
+    slot = torch.arange(M, dtype=torch.int32, device=gpu)
+    cos_t, sin_t = ref.rope_tables(HD, 8192, 10000.0, gpu)
+    cos_t, sin_t = cos_t.contiguous(), sin_t.contiguous()
+    k = ops._k()
+
+    def run(fn):
+        q = torch.zeros(M, Hq, HD, device=gpu, dtype=BF)
+        kc = torch.zeros(nslot, Hkv, S, HD, device=gpu, dtype=BF)
+        vc = torch.zeros_like(kc)
+        fn(q, kc, vc)
+        return q, kc, vc
+
+    want = run(lambda q, kc, vc: k.gemm4_qkv_rope(A, W, pos, slot, cos_t, sin_t, q, kc, vc, Hq, Hkv, 128))
+    n = 0
+    for bm, bn in k.gemm_ring_tiles(4):
+        for var in (0, 1):
+            if not k.gemm_ring_ok(M, (Hq + 2 * Hkv) * HD, K, 4, bm, bn, var):
+                continue
+            got = run(lambda q, kc, vc: k.gemm_ring_qkv_rope(A, W, pos, slot, cos_t, sin_t, q, kc, vc, Hq, Hkv, bm, bn,
+                                                             var))
+            assert all(torch.equal(a, b) for a, b in zip(got, want)), (bm, bn, var)
+            n += 1
+    assert n >= 10
 
 
 def _ext_kernels():

@@ -387,7 +387,7 @@ def test_cli_sweep_pipelined_chunks_match_unchunked(tmp_path):
 
 def test_lazy_running_sums_match_kept_sums(monkeypatch):
     """Running lens sums rebuilt from the pairs' residuals when their cells run (default) give the records
-    of sums kept from each baseline on (TB_LAZY_LENS_CUM=0)."""
+    of sums kept from each baseline on (SweepRunner.lazy_cum = False)."""
     from dataclasses import replace
 
     from taboo_brittleness_amd.interp.sae import JumpReLUSAE
@@ -403,10 +403,10 @@ def test_lazy_running_sums_match_kept_sums(monkeypatch):
     tok = SyntheticTokenizer(vocab_size=spec.vocab_size)
     res = {}
     for lazy in ("0", "1"):
-        monkeypatch.setenv("TB_LAZY_LENS_CUM", lazy)
         sae = JumpReLUSAE.random(spec.hidden, 512, seed=2, device="cpu")
         r = SweepRunner(cfg, m, tok, sae, batch=24, device="cpu", layer=1, use_graphs=False, prefix_share=True,
                         layer_resume=True)
+        r.lazy_cum = lazy == "1"
         pairs = r.build_pairs(["ship"], cfg.prompts[:2])
         r.run_baselines(pairs)
         assert all((p.lens_cum is None) == (lazy == "1") for p in pairs)

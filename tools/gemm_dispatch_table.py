@@ -6,6 +6,9 @@ time RELATIVE to that run's own hipBLASLt time, so box-to-box clock differences 
 the lowest ratio wins when ``ratio <= tie`` (``--tie-fused`` for the fused GeGLU epilogue, whose alternative is two
 kernels).  Prints the per-shape in-tree count.
 
+The ``tb_shapes`` section (``TB_GEMM=tb``) is the fastest BATCH-INVARIANT variant per point (ring ``r*``, four-wave
+``g*``, ping-pong ``256`` / ``128``; never split-K or hipBLASLt), from the same merged ratios.
+
   python tools/gemm_dispatch_table.py gpurun_out/r4/raw.jsonl gpurun_out/r4/raw_splitk.jsonl --tie 1.01
 """
 import argparse
@@ -43,22 +46,29 @@ def main():
                     old = d.get(v, 1e9) if not fresh or (key, v) in seen else 1e9
                     d[v] = min(old, t / us["blas"])
                     seen.add((key, v))
-    shapes, stats = {}, {}
+    shapes, tb_shapes, stats = {}, {}, {}
     for (shape, N, K, epi, M), d in sorted(pts.items()):
         best = min(d, key=d.get)
         tie = args.tie_fused if epi == 3 else args.tie
         win = best if d[best] <= tie else "blas"
         win = win if not win.isdigit() else int(win)
         shapes.setdefault(f"{N},{K},{epi}", []).append([M, win])
-        s = stats.setdefault((shape, epi), [0, 0])
+        inv = [v for v in d if v[:1] in ("g", "r") or v.isdigit()]
+        if inv:
+            bi = min(inv, key=d.get)
+            tb_shapes.setdefault(f"{N},{K},{epi}", []).append([M, int(bi) if bi.isdigit() else bi])
+        s = stats.setdefault((shape, epi), [0, 0, 0.0, 0.0])
         s[0] += win != "blas"
         s[1] += 1
-    tab = {"shapes": shapes, "meta": {"tie": args.tie, "tie_fused": args.tie_fused, "sources": args.raw,
-                                      "tag": args.tag}}
+        s[2] += min(d[best], 1.0) if win != "blas" else 1.0
+        s[3] += d[bi] if inv else 1.0
+    tab = {"shapes": shapes, "tb_shapes": tb_shapes,
+           "meta": {"tie": args.tie, "tie_fused": args.tie_fused, "sources": args.raw + args.fresh, "tag": args.tag}}
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     json.dump(tab, open(args.out, "w"), indent=1)
-    for (shape, epi), (w, n) in sorted(stats.items()):
-        print(f"{shape:5s} epi {epi}: in-tree at {w}/{n} row counts")
+    for (shape, epi), (w, n, ra, rt) in sorted(stats.items()):
+        print(f"{shape:5s} epi {epi}: in-tree at {w}/{n} row counts; mean time vs hipBLASLt: auto {ra / n:.3f}, "
+              f"tb (batch-invariant) {rt / n:.3f}")
     print(f"wrote {args.out}")
 
 

@@ -5,7 +5,7 @@
 import csv
 import sys
 
-INTREE = ("gemm_pp_kernel", "gemm4_kernel", "gemm_nt_kernel", "gemm_skinny_kernel")
+INTREE = ("gemm_pp_kernel", "gemm4_kernel", "gemm_nt_kernel", "gemm_ring_kernel")
 rows = list(csv.DictReader(open(sys.argv[1])))
 tot = sum(float(r["TotalDurationNs"]) for r in rows)
 lib = sum(float(r["TotalDurationNs"]) for r in rows if r["Name"].startswith(("Cijk", "Custom_Cijk")))
