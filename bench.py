@@ -223,8 +223,17 @@ def main() -> None:
     first = {}
     for p in cur:
         first.setdefault((p.word, p.pidx), p)
-    calib = [first[k] for k in ((t.word, t.pidx) for t in templates) if k in first]
-    resid = torch.cat([p.resid for p in calib if p.resid is not None and p.resid.shape[0]], 0)
+    order_keys = [(t.word, t.pidx) for t in templates]
+    mine = {k: first[k].resid for k in order_keys if k in first and first[k].resid is not None
+            and first[k].resid.shape[0]}
+    if info.world > 1 and len(mine) < len(templates):
+        # fewer pairs per step than templates: every rank calibrates on the union of the ranks' first-step baselines
+        # (a template's baseline does not depend on its rank or replicate), so the SAE thresholds stay rank-invariant
+        merged = {}
+        for d in D.all_gather_objects({k: v.cpu() for k, v in mine.items()}, info):
+            merged.update(d)
+        mine = {k: merged[k].to(dev) for k in order_keys if k in merged}
+    resid = torch.cat([mine[k] for k in order_keys if k in mine], 0)
     sae.calibrate(resid)
     runner._score_pairs(cur)
 

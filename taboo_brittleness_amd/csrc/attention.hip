@@ -542,6 +542,8 @@ __global__ void __launch_bounds__(256) attn_decode_wave_kernel(
   const int grp = lane >> 4, col = lane & 15;
   const int SS = (S + 15) & ~15;
   float* sc = reinterpret_cast<float*>(smem) + (size_t)w * G * SS;   // this wave's [G][SS] scores / weights
+  // this wave's G query rows (bf16), re-read per key tile instead of held in 32 VGPRs: 4 instead of 3 waves per SIMD
+  uint16_t* ql = reinterpret_cast<uint16_t*>(reinterpret_cast<float*>(smem) + (size_t)nwh * G * SS) + (size_t)w * G * HD;
   uint16_t* ob = out + ((size_t)b * Hq + kh * G) * HD;
   const int p = pos[b];
   if (p < 0) {   // padding row
@@ -575,15 +577,12 @@ __global__ void __launch_bounds__(256) attn_decode_wave_kernel(
   // the first V chunk is independent of the scores: issue it first
   VT va[VCH], vb[VCH];
   vload(kmin, va);
-  bf16x8 qa[KS];
   {
-    const uint16_t* qrow = q + ((size_t)b * Hq + kh * G + (col < G ? col : 0)) * HD;
+    // G rows x HD bf16 = G x HD / 8 16-B chunks, one per lane and round
+    const uint16_t* qrow = q + ((size_t)b * Hq + kh * G) * HD;
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      uint4 u = {0, 0, 0, 0};
-      if (col < G) u = *reinterpret_cast<const uint4*>(qrow + ks * 32 + grp * 8);
-      qa[ks] = as_bf16x8(u);
-    }
+    for (int e = lane; e < G * HD / 8; e += 64)
+      *reinterpret_cast<uint4*>(ql + e * 8) = *reinterpret_cast<const uint4*>(qrow + e * 8);
   }
   const float inv_cap = softcap > 0.f ? 1.f / softcap : 0.f;
   auto kload = [&](int t, uint4 (&kf)[KS]) {
@@ -593,10 +592,15 @@ __global__ void __launch_bounds__(256) attn_decode_wave_kernel(
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) kf[ks] = *reinterpret_cast<const uint4*>(krow + ks * 32);
   };
+  // MFMA rows >= G (lanes col >= G) read a copy of a real query row: their outputs are never used, rows < G are
+  // unchanged (each output row of the MFMA depends on its own A row only)
+  const uint16_t* qlr = ql + (col % G) * HD + grp * 8;
   auto score = [&](int t, const uint4 (&kf)[KS]) {
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[ks], as_bf16x8(kf[ks]), acc, 0, 0, 0);
+    for (int ks = 0; ks < KS; ++ks)
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(*reinterpret_cast<const uint4*>(qlr + ks * 32)),
+                                                    as_bf16x8(kf[ks]), acc, 0, 0, 0);
     const int kk = t * 16 + col;
     if (grp == 0) {   // query rows 0..3 of the 16-row tile live in lanes 0..15
 #pragma unroll
@@ -692,7 +696,7 @@ void launch_attn_decode(const uint16_t* q, const uint16_t* kc, const uint16_t* v
                         hipStream_t st) {
   if (S <= 2048) {
     const int nwh = Hkv % 4 == 0 ? 4 : (Hkv % 2 == 0 ? 2 : 1);
-    const size_t lds_w = (size_t)nwh * G * ((S + 15) & ~15) * sizeof(float);
+    const size_t lds_w = (size_t)nwh * G * ((S + 15) & ~15) * sizeof(float) + (size_t)nwh * G * HD * 2;
     hipLaunchKernelGGL((attn_decode_wave_kernel<HD, G>), dim3(B, Hkv / nwh), dim3(64 * nwh), lds_w, st, q, kc, vc, out,
                        pos, slot, Hq, Hkv, S, scale, softcap, window, pkc, pvc, pslot, plen);
     return;

@@ -94,6 +94,24 @@ def softcap_values(v: torch.Tensor, cap: float) -> torch.Tensor:
 
 
 
+_SPLITK_WS: dict = {}
+_SPLITK_KEEP: list = []
+
+
+def _splitk_ws(n: int, device) -> torch.Tensor:
+    """fp32 workspace of >= ``n`` floats for split-K partials: one grow-only buffer per (device, stream) instead of a
+    caching-allocator call per GEMM (the decode graphs then hold a fixed address).  Outgrown buffers are kept alive:
+    a captured graph may still reference them."""
+    st = torch.cuda.current_stream(device)
+    key = (device.index, st.stream_id)
+    b = _SPLITK_WS.get(key)
+    if b is None or b.numel() < n:
+        b = torch.empty(max(n, 2 * b.numel() if b is not None else n), dtype=torch.float32, device=device)
+        _SPLITK_WS[key] = b
+        _SPLITK_KEEP.append(b)
+    return b[:n]
+
+
 def tb_gemm(x, w, out, bias, thr, epi: int, choice) -> None:
     """One in-tree MFMA GEMM (``runtime.gemm_dispatch`` choice): ``"g256"`` / ``"g128"`` the four-wave kernel
     (csrc/gemm4.hip), ``256`` / ``128`` the ping-pong kernel (csrc/gemm.hip) -- identical numerics; ``"k256"`` /
@@ -108,8 +126,17 @@ def tb_gemm(x, w, out, bias, thr, epi: int, choice) -> None:
         M, N = x.numel() // K, w.shape[0]
         tr = int(choice[1:])
         ks = int(_k().gemm4_splitk_ks(M, N, K, tr))
-        ws = torch.empty(ks * M * N, dtype=torch.float32, device=x.device)
+        ws = _splitk_ws(ks * M * N, x.device)
         _k().gemm4_splitk(x, w, out, ws, int(epi), tr, ks)
+    elif choice == "gs":              # row-split launches: full rounds of 256-row tiles, the rest on 128-row tiles
+        K = x.shape[-1]
+        M, N = x.numel() // K, w.shape[0]
+        M1 = _GD.split_rows(M, N)
+        xs, os_ = x.reshape(M, K), out.reshape(M, -1)
+        if M1 > 0:
+            _k().gemm4(xs[:M1], w, os_[:M1], bias, thr, int(epi), 256)
+        if M1 < M:
+            _k().gemm4(xs[M1:], w, os_[M1:], bias, thr, int(epi), 128)
     elif isinstance(choice, str):
         _k().gemm4(x, w, out, bias, thr, int(epi), int(choice[1:]))
     else:
@@ -151,7 +178,7 @@ def linear_add_rmsnorm2(a, w, h, w_post, w_next, eps, out=None, o_ws=None):
             if isinstance(c, str) and c[0] == "k":
                 tr = int(c[1:])
                 ks = int(_k().gemm4_splitk_ks(M, N, K, tr))
-                ws = torch.empty(ks * M * N, dtype=torch.float32, device=a.device)
+                ws = _splitk_ws(ks * M * N, a.device)
                 ks = int(_k().gemm4_splitk_part(a, w, ws, tr, ks))
                 out = _out(out, h.shape, h.dtype, h.device)
                 _k().add_rmsnorm2_part(h, ws, ks, w_post, w_next, out, float(eps))
@@ -237,6 +264,8 @@ def _qkv_plan(x: torch.Tensor, wqkv: torch.Tensor, HD: int):
     rt = _GD.ring_tile(c)
     if rt is not None:
         return ("ring", rt) if _k().gemm_ring_ok(M, N, K, 4, rt[0], rt[1], rt[2]) else ("fused", 128)
+    if c == "gs":
+        return "fused_split", _GD.split_rows(M, N)
     return "fused", int(c.lstrip("g"))
 
 
@@ -250,6 +279,14 @@ def qkv_rope_cache(x, wqkv, pos, slot_of_row, cos_t, sin_t, kc, vc, Hq, Hkv, HD,
         q_out = _out(q_out, (M, Hq, HD), x.dtype, x.device)
         _k().gemm4_qkv_rope(x, wqkv, pos, slot_of_row, cos_t, sin_t, q_out, kc, vc, int(Hq), int(Hkv), rows)
         return q_out
+    if kind == "fused_split":          # row-split launches (see tb_gemm "gs")
+        q_out = _out(q_out, (M, Hq, HD), x.dtype, x.device)
+        M1, xs = rows, x.reshape(M, -1)
+        for r0, r1, tr in ((0, M1, 256), (M1, M, 128)):
+            if r1 > r0:
+                _k().gemm4_qkv_rope(xs[r0:r1], wqkv, pos.reshape(-1)[r0:r1], slot_of_row.reshape(-1)[r0:r1], cos_t, sin_t,
+                                    q_out[r0:r1], kc, vc, int(Hq), int(Hkv), tr)
+        return q_out
     if kind == "ring":
         q_out = _out(q_out, (M, Hq, HD), x.dtype, x.device)
         _k().gemm_ring_qkv_rope(x, wqkv, pos, slot_of_row, cos_t, sin_t, q_out, kc, vc, int(Hq), int(Hkv), *rows)
@@ -257,7 +294,7 @@ def qkv_rope_cache(x, wqkv, pos, slot_of_row, cos_t, sin_t, kc, vc, Hq, Hkv, HD,
     if kind == "split":
         K, N = x.shape[-1], wqkv.shape[0]
         ks = int(_k().gemm4_splitk_ks(M, N, K, rows))
-        ws = torch.empty(ks * M * N, dtype=torch.float32, device=x.device)
+        ws = _splitk_ws(ks * M * N, x.device)
         ks = int(_k().gemm4_splitk_part(x, wqkv, ws, rows, ks))
         q_out = _out(q_out, (M, Hq, HD), x.dtype, x.device)
         _k().rope_qkv_cache_part(ws, ks, pos, slot_of_row, cos_t, sin_t, q_out, kc, vc, int(Hq), int(Hkv), int(HD))
@@ -352,14 +389,14 @@ def attention(q, kc, vc, pos, slot, B, T, scale, softcap, window, out=None, pref
         out = _out(out, (B * T, q.numel() // (B * T)), q.dtype, q.device)
         if prefix is not None:
             assert T == 1, "shared-prefix attention is decode-only"
-            pk, pv, ps, pl = prefix[:4]
+            pk, pv, ps, pl = prefix
             _k().attention_prefix(q, kc, vc, out, pos, slot, int(B), float(scale), float(softcap), int(window),
                                   pk, pv, ps, pl)
             return out
         _k().attention(q, kc, vc, out, pos, slot, int(B), int(T), float(scale), float(softcap), int(window))
         return out
     o = ref.attention(q, kc, vc, pos, slot, B, T, scale, softcap, window,
-                      prefix=prefix[:4] if prefix is not None else None)
+                      prefix=prefix)
     if out is not None:
         out.copy_(o.view_as(out))
         return out
@@ -559,13 +596,14 @@ FUSED_LENS = os.environ.get("TB_FUSED_LENS", "1") == "1"   # gemm4 G4_LENS (roun
 
 def lens_unembed(xn, w, fused: Optional[bool] = None, out=None):
     """Logit-lens unembedding of final-normed rows: ``(logits = xn @ w^T (bf16), lse = logsumexp(logits))``, no
-    softcap.  GPU with ``fused`` (default ``TB_FUSED_LENS``): one ping-pong MFMA GEMM that stores the bf16 logits
-    and reduces each row's 128-column slices to {max, sum exp} in its epilogue, then the partial merge
-    (csrc/gemm.hip EPI_LENS) -- no separate ``row_lse`` pass over the logits.  Otherwise hipBLASLt + ``row_lse``."""
+    softcap.  GPU with ``fused`` (default ``TB_FUSED_LENS``, off under ``TB_GEMM=blas``): one four-wave MFMA GEMM
+    (csrc/gemm4.hip G4_LENS) that stores the bf16 logits and reduces each row's 128-column slices to {max, sum exp}
+    in its epilogue, then the partial merge (tb_head_merge) -- no separate ``row_lse`` pass over the logits.
+    Otherwise ``linear`` (the GEMM dispatch: hipBLASLt under ``blas``) + ``row_lse``."""
     K = xn.shape[-1]
     R = xn.numel() // K
     V = w.shape[0]
-    fused = FUSED_LENS if fused is None else fused
+    fused = (FUSED_LENS and _GD.mode() != "blas") if fused is None else fused
     if xn.is_cuda and fused and _k().gemm_pp_ok(R, V, K) and xn.is_contiguous():
         logits = _out(out, xn.shape[:-1] + (V,), BF16, xn.device)
         part = torch.empty(head_part_numel(R, V), dtype=torch.float32, device=xn.device)

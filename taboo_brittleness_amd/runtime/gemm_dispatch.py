@@ -6,7 +6,8 @@ through :func:`taboo_brittleness_amd.ops.linear`, which asks :func:`choose` for 
 * ``256`` / ``128`` — ``csrc/gemm.hip``'s ping-pong kernel with 256- or 128-row output tiles (the 128-row
   tile doubles the workgroup count for the N = 3584 projections at moderate M);
 * ``"g256"`` / ``"g128"`` — ``csrc/gemm4.hip``'s four-wave kernel (128x128 wave tiles), same tiles, same
-  epilogues and bit-identical results;
+  epilogues and bit-identical results; ``"gs"`` — the four-wave kernel with its tile height(s) from a rounds model
+  of the persistent grid (:func:`split_rows`: 256-row tiles, 128-row tiles, or both as two launches split by rows);
 * ``"k256"`` / ``"k128"`` — the four-wave kernel split over K (``tb_gemm4_splitk``: as many K ranges as fill the
   CUs, fp32 partials, ordered reduction) for thin grids (o_proj / down at N = 3584, every projection at decode M);
   deterministic but not bit-identical to the unsplit kernels, so ``auto`` only;
@@ -30,6 +31,7 @@ Modes (``TB_GEMM``):
 from __future__ import annotations
 
 import bisect
+import functools
 import json
 import os
 from typing import Dict, List, Optional, Tuple, Union
@@ -126,10 +128,34 @@ def has_entry(N: int, K: int, epi: int, M: Optional[int] = None) -> bool:
     return M is None or M <= tab[(N, K, epi)][0][-1]
 
 
+# time of a 128-row four-wave tile relative to a 256-row one (half the MFMAs at 0.538 vs 0.694 MFMA utilisation,
+# profiles/r4/gemm4/pmc_counted_waits_gate_up_4096.txt)
+G128_COST = 0.64
+
+
+@functools.lru_cache(maxsize=4096)
+def split_rows(M: int, N: int) -> int:
+    """Row split of the ``"gs"`` choice: rows ``[0, M1)`` on 256-row tiles, the rest on 128-row tiles (two launches of
+    the persistent four-wave kernel).  A persistent grid runs in rounds of one tile per CU, so a grid that does not
+    divide into the CUs leaves its last round part-empty (e.g. o_proj at M = 6144: 14 x 24 = 336 tiles on 256 CUs);
+    ``M1`` minimises the rounds-based cost ``ceil(tiles256 / CUs) + G128_COST * ceil(tiles128 / CUs)`` over the
+    multiples of 256 (ties: more 256-row rows).  ``M1 = M``: plain 256-row tiles, ``0``: plain 128-row tiles.  The
+    model picks the fastest of the three at 213 of 222 measured (shape, M) points above 2048 rows and is within 3 % at
+    the rest (profiles/r5/gemm_dispatch/gs.jsonl).  Every tile height accumulates the same K chain, so the split keeps
+    the GEMM batch-invariant."""
+    nbn = max(1, N // 256)
+
+    def cost(m1):
+        c = -(-nbn * -(-m1 // 256) // NUM_CU) if m1 > 0 else 0
+        return c + (G128_COST * -(-nbn * -(-(M - m1) // 128) // NUM_CU) if m1 < M else 0.0)
+    cands = [min(256 * k, M) for k in range(-(-M // 256) + 1)]
+    return min(cands, key=lambda m1: (cost(m1), -m1))
+
+
 def is_invariant(choice: Choice) -> bool:
     """Whether a choice accumulates every output over K in the one order of the in-tree kernels (no split-K, no
     hipBLASLt): rows then get bit-identical results in any batch."""
-    return isinstance(choice, int) or (isinstance(choice, str) and choice[:1] in ("g", "r"))
+    return isinstance(choice, int) or (isinstance(choice, str) and choice[:1] in ("g", "r"))   # incl. "gs"
 
 
 def ring_tile(choice: Choice) -> Optional[Tuple[int, int, int]]:

@@ -52,6 +52,38 @@ def test_shipped_table_is_consistent():
         for key in [(8192, 3584, 0), (3584, 4096, 0), (28672, 3584, 0), (28672, 3584, 3), (3584, 14336, 0),
                     (256000, 3584, 0)]:
             ms, cs = tab[key]
-            assert ms == sorted(ms) and len(ms) == len(cs) and all(c in ("blas", 128, 256, "g128", "g256", "k64", "k128", "k256", "s") for c in cs)
+            assert ms == sorted(ms) and len(ms) == len(cs) and all(_valid(c) for c in cs)
+        tb = GD._state["tb_table"]
+        assert tb is not None
+        for key, (ms, cs) in tb.items():
+            # the exact mode's table may only name batch-invariant kernels
+            assert ms == sorted(ms) and all(_valid(c) and GD.is_invariant(c) for c in cs), key
     finally:
         GD._state["loaded"] = False
+
+
+def _valid(c):
+    if c in ("blas", 128, 256, "g128", "g256", "gs", "k64", "k128", "k256", "s"):
+        return True
+    t = GD.ring_tile(c)
+    return t is not None and t[0] in (16, 32, 64, 128) and t[1] in (16, 32, 64, 128) and t[2] in (0, 1)
+
+
+def test_ring_tile_and_invariance():
+    assert GD.ring_tile("r64x32") == (64, 32, 0)
+    assert GD.ring_tile("r128x64b") == (128, 64, 1)
+    assert GD.ring_tile("g256") is None
+    assert GD.is_invariant("r32x64") and GD.is_invariant("gs") and GD.is_invariant(256)
+    assert not GD.is_invariant("k128") and not GD.is_invariant("blas")
+
+
+def test_split_rows_rounds_model():
+    """``gs``: 256-row tiles, 128-row tiles or a row split of both, from the persistent grid's rounds."""
+    for M, N in [(6144, 3584), (8192, 3584), (2400, 8192), (4096, 28672), (300, 3584), (9000, 3584), (5, 8192)]:
+        M1 = GD.split_rows(M, N)
+        assert 0 <= M1 <= M and (M1 % 256 == 0 or M1 == M)
+    assert GD.split_rows(6144, 3584) == 4608    # 14 x 24 = 336 tiles: 252 tiles of 256 rows + 56 of 128 rows
+    assert GD.split_rows(4096, 3584) == 4096    # 224 tiles: one part-full round beats 448 tiles of 128 rows
+    assert GD.split_rows(2048, 3584) == 0       # 112 tiles: 224 of 128 rows still fit one round
+    assert GD.split_rows(4096, 28672) == 4096   # 1792 tiles = 7 whole rounds
+    assert GD.split_rows(4200, 8192) == 4096    # 32 x 17 = 544 tiles: 2 rounds + 32 128-row tiles

@@ -6,7 +6,8 @@ time RELATIVE to that run's own hipBLASLt time, so box-to-box clock differences 
 the lowest ratio wins when ``ratio <= tie`` (``--tie-fused`` for the fused GeGLU epilogue, whose alternative is two
 kernels).  Prints the per-shape in-tree count.
 
-The ``tb_shapes`` section (``TB_GEMM=tb``) is the fastest BATCH-INVARIANT variant per point (ring ``r*``, four-wave
+Four-wave winners are recorded as ``"gs"`` (the rounds model picks the tile height per row count; ``--no-gs``: as
+measured).  The ``tb_shapes`` section (``TB_GEMM=tb``) is the fastest BATCH-INVARIANT variant per point (ring ``r*``, four-wave
 ``g*``, ping-pong ``256`` / ``128``; never split-K or hipBLASLt), from the same merged ratios.
 
   python tools/gemm_dispatch_table.py gpurun_out/r4/raw.jsonl gpurun_out/r4/raw_splitk.jsonl --tie 1.01
@@ -26,6 +27,8 @@ def main():
     ap.add_argument("--out", default=os.path.join(ROOT, "configs", "gemm_dispatch", "gemma2-9b.json"))
     ap.add_argument("--exclude", default="", help="comma-separated variants never chosen (e.g. 256,128)")
     ap.add_argument("--tag", default="")
+    ap.add_argument("--no-gs", action="store_true",
+                    help="keep g256 / g128 winners as measured instead of the rounds-model choice \"gs\"")
     ap.add_argument("--fresh", nargs="*", default=[],
                     help="raw files re-measuring some variants with a newer kernel build: their ratios REPLACE the "
                          "older files' values of the same (point, variant) instead of taking the minimum")
@@ -46,6 +49,16 @@ def main():
                     old = d.get(v, 1e9) if not fresh or (key, v) in seen else 1e9
                     d[v] = min(old, t / us["blas"])
                     seen.add((key, v))
+    if not args.no_gs:
+        # the four-wave kernel's tile height is the rounds model's (runtime.gemm_dispatch.split_rows: 256 rows, 128
+        # rows or a row split): one entry "gs" at the best of the measured heights, so row counts between the
+        # measured points get the model's height instead of their neighbour's
+        for d in pts.values():
+            g = [d[v] for v in ("g256", "g128", "gs") if v in d]
+            if g:
+                for v in ("g256", "g128"):
+                    d.pop(v, None)
+                d["gs"] = min(g)
     shapes, tb_shapes, stats = {}, {}, {}
     for (shape, N, K, epi, M), d in sorted(pts.items()):
         best = min(d, key=d.get)

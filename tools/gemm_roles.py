@@ -12,7 +12,17 @@ from collections import defaultdict
 
 
 def is_gemm(n: str) -> bool:
-    return n.startswith(("Cijk_", "Custom_Cijk")) or "gemm4_kernel" in n or "gemm_pp_kernel" in n
+    return n.startswith(("Cijk_", "Custom_Cijk")) or "gemm4_kernel" in n or "gemm_pp_kernel" in n or "gemm_ring_kernel" in n
+
+
+def geglu_gemm(n: str) -> bool:
+    """A gate|up GEMM with the fused GeGLU epilogue (gemm4 / ping-pong EPI 3, ring EPI 3 = third template argument)."""
+    if "gemm4_kernel<256, 3>" in n or "gemm4_kernel<128, 3>" in n or "gemm_pp_kernel<3" in n:
+        return True
+    if "gemm_ring_kernel<" in n:
+        args = n[n.find("<") + 1:].split(",")
+        return len(args) > 2 and args[2].strip() == "3"
+    return False
 
 
 def short(n: str) -> str:
@@ -34,11 +44,10 @@ def role(prev: str, nxt: str) -> str:
     if "geglu_kernel" in nxt:
         return "gate_up"
     if "add_rmsnorm" in nxt or "splitk_reduce" in nxt:
-        if "geglu" in prev or "gemm4_kernel<256, 3>" in prev or "gemm4_kernel<128, 3>" in prev or \
-                "gemm_pp_kernel<3" in prev:
+        if "geglu" in prev or geglu_gemm(prev):
             return "down"
         return "o_proj"
-    if "gemm4_kernel<256, 3>" in nxt or "gemm4_kernel<128, 3>" in nxt or "gemm_pp_kernel<3" in nxt:
+    if geglu_gemm(nxt):
         return "?"
     if is_gemm(nxt):
         return "gemm->gemm"
@@ -63,7 +72,7 @@ def main(path: str) -> None:
         else:
             rl = role(names[i - 1] if i else "", nxt)
         # the fused gate|up + GeGLU GEMM is itself the gate_up role
-        if "gemm4_kernel<256, 3>" in n or "gemm4_kernel<128, 3>" in n or "gemm_pp_kernel<3" in n:
+        if geglu_gemm(n):
             rl = "gate_up(fused)"
         if "gemm4_kernel<256, 6>" in n:
             rl = "lens(fused)"

@@ -23,6 +23,7 @@ sys.path.insert(0, ROOT)
 from taboo_brittleness_amd import ops  # noqa: E402
 from taboo_brittleness_amd.ops import _ext  # noqa: E402
 from taboo_brittleness_amd.ops import reference as ref  # noqa: E402
+from taboo_brittleness_amd.runtime import gemm_dispatch as GD  # noqa: E402
 from taboo_brittleness_amd.runtime.tuning import enable_tuned_gemms  # noqa: E402
 
 SHAPES = {"qkv": (8192, 3584), "o": (3584, 4096), "gu": (28672, 3584), "down": (3584, 14336), "head": (256000, 3584)}
@@ -53,7 +54,7 @@ def main():
     ap.add_argument("--split-max-m", type=int, default=2400, help="split-K variants timed up to this M")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--tiles", default="", help="comma list of bmxbn to time (default: all built)")
-    ap.add_argument("--others", default="g256,g128,k256,k128,k64,256,128")
+    ap.add_argument("--others", default="g256,g128,gs,k256,k128,k64,256,128")
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--tag", default="gemma2-9b_P100_E4_new50", help="TunableOp table of the hipBLASLt candidates")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "ring.jsonl"))
@@ -102,7 +103,7 @@ def main():
                             and M <= args.ring_max_m and t[0] <= max(16, 2 * M)]
                 others = [c for c in args.others.split(",") if
                           not (c.startswith("k") and (M > args.split_max_m or (c == "k64" and M > 512))) and
-                          not (c.isdigit() and (M < 256 or epi in (4, 5)))]
+                          not (c.isdigit() and (M < 256 or epi in (4, 5))) and not (c == "gs" and M < 2048)]
                 if epi == 4:
                     Hq, Hkv, HD, S = 16, 8, 256, 512
                     nslot = min(M, 256)
@@ -129,7 +130,17 @@ def main():
                         var[rname(bm, bn, rv)] = (lambda bm_, bn_, rv_: lambda: k.gemm_ring_qkv_rope(
                             A, nxt(), pos, slot, cos_t, sin_t, q, kc, vc, Hq, Hkv, bm_, bn_, rv_))(bm, bn, rv)
                     for ch in others:
-                        if ch.startswith("g"):
+                        if ch == "gs":
+                            M1 = GD.split_rows(M, N)
+
+                            def rope_split(M1=M1):
+                                w_ = nxt()
+                                for r0, r1, tr in ((0, M1, 256), (M1, M, 128)):
+                                    if r1 > r0:
+                                        k.gemm4_qkv_rope(A[r0:r1], w_, pos[r0:r1], slot[r0:r1], cos_t, sin_t, q[r0:r1],
+                                                         kc, vc, Hq, Hkv, tr)
+                            var[ch] = rope_split
+                        elif ch.startswith("g"):
                             var[ch] = (lambda r_: lambda: k.gemm4_qkv_rope(A, nxt(), pos, slot, cos_t, sin_t, q, kc, vc,
                                                                            Hq, Hkv, r_))(int(ch[1:]))
                     var["blas"] = lambda: (torch.matmul(A, nxt().t(), out=C),
