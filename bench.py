@@ -20,8 +20,9 @@ words through the offline synthetic Gemma tokenizer.  The 30 (word, prompt) pair
 set of weights — the per-word taboo models merged (identical compute); ``--lora-rank`` batches
 unmerged per-word adapters instead.
 
-Exact reuse inside a step (every cell's results equal a from-scratch generation; tested on CPU and
-GPU): a cell resumes from its baseline's KV / hooked-layer residuals up to its first edit, replays
+Exact reuse inside a step (every cell's results equal a from-scratch generation; tested on CPU and on
+the GPU in the default ``--gemm tb`` mode, whose GEMMs are batch-invariant -- ``--gemm auto`` is faster
+per GEMM at some row counts but not exact, see runtime/gemm_dispatch.py): a cell resumes from its baseline's KV / hooked-layer residuals up to its first edit, replays
 only the blocks after the hooked layer while its tokens equal the baseline's (teacher-forced tail,
 which also yields the ΔNLL), and decodes the full model only from its divergence point; the JSON
 "work" block reports how much of each happened.
@@ -129,8 +130,9 @@ def main() -> None:
                          "dispatch table picks it or hipBLASLt + the GeGLU kernel per row count")
     ap.add_argument("--no-fused-geglu", action="store_true", help="never the fused gate|up + GeGLU kernel")
     ap.add_argument("--gemm", default=None, choices=["auto", "tb", "blas"],
-                    help="GEMM dispatch (runtime/gemm_dispatch.py): auto = measured per-shape table (default), "
-                         "tb = in-tree MFMA kernels only (batch-invariant), blas = hipBLASLt only")
+                    help="GEMM dispatch (runtime/gemm_dispatch.py): tb = in-tree batch-invariant MFMA kernels "
+                         "(default: the reuse levels are exact), auto = fastest measured per shape incl. split-K / "
+                         "hipBLASLt (not batch-invariant), blas = hipBLASLt only")
     ap.add_argument("--fused-head", action="store_true",
                     help="vocab head as the fused MFMA GEMM head (softcap / log-sum-exp / argmax in the GEMM epilogue, "
                          "no logits in HBM) instead of hipBLASLt logits + the decode_head kernel (default since it "

@@ -1,5 +1,5 @@
 // Ring GEMM for decode-to-mid row counts on gfx950: C = A[M,K] . W[N,K]^T with small output tiles (BM x BN from
-// 16 x 16 to 128 x 128) and a deep LDS-DMA ring, batch-invariant by construction (SURVEY K3/K6/K7/K8 at the row
+// 16 x 16 to 128 x 128, and 16..256 x 112 for the N = 3584 projections) and a deep LDS-DMA ring, batch-invariant by construction (SURVEY K3/K6/K7/K8 at the row
 // counts of the greedy decode and the ride-along baselines).
 //
 // Why: at M <= ~2k rows the N = 3584 / 8192 projections have too few 256-wide column tiles to fill 256 CUs, and the
@@ -32,6 +32,11 @@
 //    read its W panel through the same L2.
 // Requirements (host-checked, tb_gemm_ring_ok): K % 128 == 0, N % BN == 0 (pair epilogues: (N / 2) % (BN / 2) == 0),
 // any M.
+//
+// The 112-column tiles: at mid M (256 .. ~2k rows) a narrow-tile GEMM is bound by each CU's L2 -> LDS fill rate
+// (MI355X_MICROARCH.md: 66-73 GB/s per CU from an L2-resident panel), so its time is rounds x (BM + BN) K bytes: N =
+// 3584 = 32 x 112 columns with the row tile BM ~ M / 8 gives one round of ~256 tiles at the fewest bytes per tile (e.g.
+// M = 768: 96 x 112 tiles, 208 image rows per CU, vs 256 rows for 168 tiles of 128 x 128).
 #include "common.h"
 #include "api.h"
 #include <utility>
@@ -79,14 +84,15 @@ __device__ __forceinline__ void rg_bar() {
   asm volatile("" ::: "memory");
 }
 
-// wave grid of a tile: as many computing waves as the 16-row / 16-column (pair epilogues: 32-column) fragments
-// allow, then the squarest wave tile
+// wave grid of a tile: as many computing waves (<= 4, not necessarily a power of two: a 96-row tile runs 3) as the
+// 16-row / 16-column (pair epilogues: 32-column) fragments allow, then the squarest wave tile
 constexpr int rg_wgn(int BM, int BN, bool pair) {
   int best = 1, bestc = -1, bestd = 1 << 30;
-  for (int wn = 1; wn <= 4; wn *= 2) {
-    if (BN % wn || BN / wn < (pair ? 32 : 16)) continue;
-    for (int wm = 1; wm * wn <= 4; wm *= 2) {
-      if (BM % wm || BM / wm < 16) continue;
+  const int fn = pair ? 32 : 16;
+  for (int wn = 1; wn <= 4; ++wn) {
+    if (BN % (wn * fn)) continue;
+    for (int wm = 1; wm * wn <= 4; ++wm) {
+      if (BM % (wm * 16)) continue;
       const int c = wm * wn, tm = BM / wm, tn = BN / wn, d = tm > tn ? tm - tn : tn - tm;
       if (c > bestc || (c == bestc && (d < bestd || (d == bestd && tn > BN / best)))) {
         best = wn;
@@ -100,7 +106,8 @@ constexpr int rg_wgn(int BM, int BN, bool pair) {
 constexpr int rg_wgm(int BM, int BN, bool pair) {
   const int wn = rg_wgn(BM, BN, pair);
   int wm = 1;
-  while (wm * 2 * wn <= 4 && BM / (wm * 2) >= 16 && BM % (wm * 2) == 0) wm *= 2;
+  for (int w = 1; w * wn <= 4; ++w)
+    if (BM % (w * 16) == 0) wm = w;
   return wm;
 }
 // ring depth: the LDS budget (LKB KB) in stages of KU K-tile images, 3 .. 32, and the counted waits must fit
@@ -332,6 +339,10 @@ gemm_ring_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W,
 // (BM, BN) tiles built per epilogue; tb_gemm_ring_tiles() lists them for the tuner
 #define RG_PLAIN_TILES(X) X(16, 16) X(16, 32) X(16, 64) X(32, 32) X(32, 64) X(64, 32) X(64, 64) X(128, 32) X(64, 128) \
   X(128, 64) X(128, 128)
+// 112-column tiles for the N = 3584 projections (o_proj, down): 32 column tiles, and the row tile from the set
+// below chosen per M (measured, tools/ring_bench.py) so the grid is about one tile per CU; 144 KB ring only
+#define RG_N112_TILES(X) X(16, 112) X(32, 112) X(48, 112) X(64, 112) X(96, 112) X(128, 112) X(144, 112) X(192, 112) \
+  X(256, 112)
 #define RG_PAIR_TILES(X) X(16, 32) X(16, 64) X(32, 32) X(32, 64) X(64, 32) X(64, 64) X(128, 32) X(64, 128) X(128, 64) \
   X(128, 128)
 
@@ -348,6 +359,14 @@ void rg_launch(int var, const uint16_t* A, const uint16_t* W, uint16_t* C, int M
     hipLaunchKernelGGL((gemm_ring_kernel<BM, BN, EPI, 1, 64>), dim3(tiles), dim3(256), 0, st, A, W, C, M, N, K, ldc, ra);
 }
 
+template <int BM, int BN>
+void rg_launch_wide(const uint16_t* A, const uint16_t* W, uint16_t* C, int M, int N, int K, int ldc, hipStream_t st) {
+  const int tiles = ((M + BM - 1) / BM) * (N / BN);
+  const RingArgs ra{};
+  hipLaunchKernelGGL((gemm_ring_kernel<BM, BN, RG_BF16, 1, 144>), dim3(tiles), dim3(256), 0, st, A, W, C, M, N, K, ldc,
+                     ra);
+}
+
 template <int EPI>
 bool rg_dispatch(int bm, int bn, int var, const uint16_t* A, const uint16_t* W, uint16_t* C, int M, int N, int K, int ldc,
                  const RingArgs& ra, hipStream_t st) {
@@ -358,6 +377,14 @@ bool rg_dispatch(int bm, int bn, int var, const uint16_t* A, const uint16_t* W, 
   }
   if constexpr (EPI == RG_BF16) {
     RG_PLAIN_TILES(RG_CASE)
+#define RG_CASE_W(BM_, BN_)                                     \
+  if (bm == BM_ && bn == BN_) {                                 \
+    if (var != 1) return false;                                 \
+    rg_launch_wide<BM_, BN_>(A, W, C, M, N, K, ldc, st);        \
+    return true;                                                \
+  }
+    RG_N112_TILES(RG_CASE_W)
+#undef RG_CASE_W
   } else {
     RG_PAIR_TILES(RG_CASE)
   }
@@ -369,6 +396,7 @@ bool rg_has(int epi, int bm, int bn) {
 #define RG_HAS(BM_, BN_) if (bm == BM_ && bn == BN_) return true;
   if (epi == RG_BF16) {
     RG_PLAIN_TILES(RG_HAS)
+    RG_N112_TILES(RG_HAS)
   } else if (epi == RG_GEGLU || epi == RG_ROPE) {
     RG_PAIR_TILES(RG_HAS)
   }
@@ -381,6 +409,7 @@ bool rg_has(int epi, int bm, int bn) {
 bool tb_gemm_ring_ok(int M, int N, int K, int epi, int bm, int bn, int var) {
   if (M <= 0 || N <= 0 || K < 128 || K % 128 || var < 0 || var > 1 || !rg_has(epi, bm, bn) || N % bn) return false;
   if ((size_t)N * K * 2 >= ((size_t)1 << 40)) return false;
+  if (bn == 112 && var != 1) return false;   // the 112-column tiles are built with the 144 KB ring only
   if (epi == RG_ROPE) return N % 256 == 0;
   return true;
 }
@@ -390,6 +419,7 @@ int tb_gemm_ring_tiles(int epi, int* bm, int* bn, int cap) {
 #define RG_LIST(BM_, BN_) if (n < cap) { bm[n] = BM_; bn[n] = BN_; } ++n;
   if (epi == RG_BF16) {
     RG_PLAIN_TILES(RG_LIST)
+    RG_N112_TILES(RG_LIST)
   } else {
     RG_PAIR_TILES(RG_LIST)
   }

@@ -18,14 +18,17 @@ through :func:`taboo_brittleness_amd.ops.linear`, which asks :func:`choose` for 
 
 Modes (``TB_GEMM``):
 
-* ``auto`` (default) — the fastest of the three per ``(N, K, epilogue, M)`` as measured on an MI355X by
-  ``tools/gemm_dispatch_tune.py`` (``configs/gemm_dispatch/<arch>.json``); shapes the table does not
-  cover use the fill heuristic below.
-* ``tb`` — in-tree batch-invariant kernels only (``g*``, ``r*``, the ping-pong tiles; never split-K or hipBLASLt),
-  per row count the fastest of them as measured (the table's ``tb_shapes``; without one the fill heuristic).
-  All of them accumulate every output element over K in the same order with the same MFMA, so a row's result
-  does not depend on M or on the tile choice: the whole forward is batch-invariant (the GPU equivalence tests
-  run in this mode and require bit-equal records).
+* ``tb`` (default) — in-tree batch-invariant kernels only (``g*``, ``gs``, ``r*``, the ping-pong tiles; never split-K or
+  hipBLASLt), per row count the fastest of them as measured (the table's ``tb_shapes``; without one the fill
+  heuristic).  All of them accumulate every output element over K in the same order with the same MFMA, so a row's
+  result does not depend on M or on the tile choice: the whole forward is batch-invariant, which is what makes the
+  sweep's reuse levels (shared prefixes, layer resume, ride-along baselines, trie decode) exact -- every cell's
+  records equal a from-scratch generation of that cell (the GPU equivalence tests require bit-equal records).
+* ``auto`` — the fastest of in-tree / split-K / hipBLASLt per ``(N, K, epilogue, M)`` as measured on an MI355X by
+  ``tools/ring_bench.py`` / ``tools/gemm_dispatch_tune.py`` (``configs/gemm_dispatch/<arch>.json``); shapes the
+  table does not cover use hipBLASLt.  NOT batch-invariant: a row's bf16 projections depend on the batch's row
+  count, so reused and from-scratch results can differ in the last bits and then in greedy tokens
+  (``tests/test_drift_gpu.py`` measures how often).
 * ``blas`` — hipBLASLt only (the round-2 path).
 """
 from __future__ import annotations
@@ -42,7 +45,7 @@ NUM_CU = 256
 
 Choice = Union[int, str]
 
-_state = {"mode": os.environ.get("TB_GEMM", "auto"), "table": None, "tb_table": None, "table_path": None,
+_state = {"mode": os.environ.get("TB_GEMM", "tb"), "table": None, "tb_table": None, "table_path": None,
           "loaded": False, "kernel": "g4"}   # in-tree kernel of the fill rule: g4 | pp (set_kernel)
 
 

@@ -25,6 +25,20 @@ def geglu_gemm(n: str) -> bool:
     return False
 
 
+def g4_epi(n: str):
+    """EPI template argument of a gemm4_kernel<BM, EPI> name, else None."""
+    if "gemm4_kernel<" not in n:
+        return None
+    args = n[n.find("gemm4_kernel<") + 13:].split(">")[0].split(",")
+    return args[1].strip() if len(args) > 1 else None
+
+
+def same_split(a: str, b: str) -> bool:
+    """Two launches of one row-split GEMM ("gs": 256-row then 128-row tiles, same epilogue)."""
+    ea = g4_epi(a)
+    return ea is not None and ea == g4_epi(b) and ea != "3"
+
+
 def short(n: str) -> str:
     if n.startswith(("Cijk_", "Custom_Cijk")):
         i = n.find("MT")
@@ -65,12 +79,17 @@ def main(path: str) -> None:
     for i, n in enumerate(names):
         if not is_gemm(n):
             continue
-        nxt = names[i + 1] if i + 1 < len(names) else ""
-        if "splitk_reduce" in nxt and i + 2 < len(names):
-            nxt2 = names[i + 2]
-            rl = role(names[i - 1] if i else "", nxt2)
+        j, k = i + 1, i - 1
+        while j < len(names) and same_split(n, names[j]):
+            j += 1
+        while k >= 0 and same_split(n, names[k]):
+            k -= 1
+        nxt = names[j] if j < len(names) else ""
+        prev = names[k] if k >= 0 else ""
+        if "splitk_reduce" in nxt and j + 1 < len(names):
+            rl = role(prev, names[j + 1])
         else:
-            rl = role(names[i - 1] if i else "", nxt)
+            rl = role(prev, nxt)
         # the fused gate|up + GeGLU GEMM is itself the gate_up role
         if geglu_gemm(n):
             rl = "gate_up(fused)"
