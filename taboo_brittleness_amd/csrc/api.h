@@ -60,8 +60,10 @@ void tb_head_merge(const float* part, int npart, const int32_t* tgt, const float
                    float* nll_self, float* nll_tgt, float* lse, int M, int V, hipStream_t st);
 void tb_head_fused4(const uint16_t* A, const uint16_t* W, float* part, float cap, const int32_t* tgt,
                     float* tgt_logit, int32_t* nxt, float* nll_self, float* nll_tgt, int M, int N, int K, hipStream_t st);
+// cs: the RoPE table as bf16 (cos, sin) pairs [max_pos, 128, 2] (the fp32 tables rounded once: the epilogue rounds
+// them to bf16 anyway, rope.hip's chain)
 void tb_gemm4_qkv_rope(const uint16_t* A, const uint16_t* W, const int32_t* pos, const int32_t* slot_of_row,
-                       const float* cos_t, const float* sin_t, uint16_t* q_out, uint16_t* kc, uint16_t* vc, int M, int K,
+                       const uint16_t* cs, uint16_t* q_out, uint16_t* kc, uint16_t* vc, int M, int K,
                        int Hq, int Hkv, int S, int max_pos, int tile_rows, hipStream_t st);
 bool tb_register_softcap_compact(float cap, const uint16_t* tab, int lo, int hi, float sat);
 bool tb_softcap_compact(const uint16_t* x, float* y, int n, float cap, hipStream_t st);
@@ -138,5 +140,5 @@ int tb_gemm_ring_tiles(int epi, int* bm, int* bn, int cap);
 void tb_gemm_ring(const uint16_t* A, const uint16_t* W, uint16_t* C, int M, int N, int K, int ldc, int epi, int bm,
                   int bn, int var, hipStream_t st);
 void tb_gemm_ring_qkv_rope(const uint16_t* A, const uint16_t* W, const int32_t* pos, const int32_t* slot_of_row,
-                           const float* cos_t, const float* sin_t, uint16_t* q_out, uint16_t* kc, uint16_t* vc, int M,
+                           const uint16_t* cs, uint16_t* q_out, uint16_t* kc, uint16_t* vc, int M,
                            int K, int Hq, int Hkv, int S, int max_pos, int bm, int bn, int var, hipStream_t st);

@@ -484,9 +484,9 @@ std::vector<std::pair<int64_t, int64_t>> gemm_ring_tiles(int64_t epi) {
 
 // QKV projection + RoPE + KV-cache scatter on the ring GEMM (gemm4_qkv_rope's epilogue, narrow tiles)
 void gemm_ring_qkv_rope(torch::Tensor x, torch::Tensor w, torch::Tensor pos, torch::Tensor slot_of_row,
-                        torch::Tensor cos_t, torch::Tensor sin_t, torch::Tensor q_out, torch::Tensor kc,
+                        torch::Tensor cs, torch::Tensor q_out, torch::Tensor kc,
                         torch::Tensor vc, int64_t Hq, int64_t Hkv, int64_t bm, int64_t bn, int64_t var) {
-  IN_BF16(x); IN_BF16(w); IN_I32(pos); IN_I32(slot_of_row); IN_F32(cos_t); IN_F32(sin_t); IN_BF16(q_out); IN_BF16(kc);
+  IN_BF16(x); IN_BF16(w); IN_I32(pos); IN_I32(slot_of_row); IN_BF16(cs); IN_BF16(q_out); IN_BF16(kc);
   IN_BF16(vc);
   const int K = x.size(-1), M = pos.numel(), N = (Hq + 2 * Hkv) * 256;
   TORCH_CHECK(x.numel() == (int64_t)M * K, "gemm_ring_qkv_rope: x must be [M, K] with M = pos.numel()");
@@ -495,11 +495,11 @@ void gemm_ring_qkv_rope(torch::Tensor x, torch::Tensor w, torch::Tensor pos, tor
   TORCH_CHECK(q_out.numel() == (int64_t)M * Hq * 256, "gemm_ring_qkv_rope: q_out shape");
   TORCH_CHECK(kc.dim() == 4 && kc.size(1) == Hkv && kc.size(3) == 256 && vc.sizes() == kc.sizes(),
               "gemm_ring_qkv_rope: cache shape [slots, Hkv, S, 256]");
-  TORCH_CHECK(cos_t.dim() == 2 && cos_t.size(1) == 128 && sin_t.sizes() == cos_t.sizes(), "gemm_ring_qkv_rope: rope tables");
+  TORCH_CHECK(cs.dim() == 3 && cs.size(1) == 128 && cs.size(2) == 2, "gemm_ring_qkv_rope: rope table [max_pos, 128, 2]");
   TORCH_CHECK(slot_of_row.numel() == M, "gemm_ring_qkv_rope: slot_of_row numel");
   c10::DeviceGuard g(x.device());
-  tb_gemm_ring_qkv_rope(cbf(x), cbf(w), pos.data_ptr<int32_t>(), slot_of_row.data_ptr<int32_t>(), cos_t.data_ptr<float>(),
-                        sin_t.data_ptr<float>(), bf(q_out), bf(kc), bf(vc), M, K, Hq, Hkv, kc.size(2), cos_t.size(0),
+  tb_gemm_ring_qkv_rope(cbf(x), cbf(w), pos.data_ptr<int32_t>(), slot_of_row.data_ptr<int32_t>(), cbf(cs),
+                        bf(q_out), bf(kc), bf(vc), M, K, Hq, Hkv, kc.size(2), cs.size(0),
                         (int)bm, (int)bn, (int)var, cur_stream());
 }
 
@@ -543,10 +543,10 @@ void gemm4_splitk(torch::Tensor A, torch::Tensor W, torch::Tensor C, torch::Tens
 
 // QKV projection with RoPE + KV-cache scatter in the epilogue (gemm4.hip G4_ROPE): x [M, K] @ wqkv [(Hq+2Hkv)*256, K]^T;
 // the same outputs as linear + rope_qkv_cache (head_dim 256 only), the qkv activation never reaches memory.
-void gemm4_qkv_rope(torch::Tensor x, torch::Tensor w, torch::Tensor pos, torch::Tensor slot_of_row, torch::Tensor cos_t,
-                    torch::Tensor sin_t, torch::Tensor q_out, torch::Tensor kc, torch::Tensor vc, int64_t Hq, int64_t Hkv,
+void gemm4_qkv_rope(torch::Tensor x, torch::Tensor w, torch::Tensor pos, torch::Tensor slot_of_row, torch::Tensor cs,
+                    torch::Tensor q_out, torch::Tensor kc, torch::Tensor vc, int64_t Hq, int64_t Hkv,
                     int64_t tile_rows) {
-  IN_BF16(x); IN_BF16(w); IN_I32(pos); IN_I32(slot_of_row); IN_F32(cos_t); IN_F32(sin_t); IN_BF16(q_out); IN_BF16(kc);
+  IN_BF16(x); IN_BF16(w); IN_I32(pos); IN_I32(slot_of_row); IN_BF16(cs); IN_BF16(q_out); IN_BF16(kc);
   IN_BF16(vc);
   const int K = x.size(-1), M = pos.numel();
   TORCH_CHECK(x.numel() == (int64_t)M * K, "gemm4_qkv_rope: x must be [M, K] with M = pos.numel()");
@@ -555,12 +555,12 @@ void gemm4_qkv_rope(torch::Tensor x, torch::Tensor w, torch::Tensor pos, torch::
   TORCH_CHECK(q_out.numel() == (int64_t)M * Hq * 256, "gemm4_qkv_rope: q_out shape");
   TORCH_CHECK(kc.dim() == 4 && kc.size(1) == Hkv && kc.size(3) == 256 && vc.sizes() == kc.sizes(),
               "gemm4_qkv_rope: cache shape [slots, Hkv, S, 256]");
-  TORCH_CHECK(cos_t.dim() == 2 && cos_t.size(1) == 128 && sin_t.sizes() == cos_t.sizes(), "gemm4_qkv_rope: rope tables");
+  TORCH_CHECK(cs.dim() == 3 && cs.size(1) == 128 && cs.size(2) == 2, "gemm4_qkv_rope: rope table [max_pos, 128, 2]");
   TORCH_CHECK(slot_of_row.numel() == M, "gemm4_qkv_rope: slot_of_row numel");
   TORCH_CHECK(tile_rows == 256 || tile_rows == 128, "gemm4_qkv_rope: tile_rows must be 256 or 128");
   c10::DeviceGuard g(x.device());
-  tb_gemm4_qkv_rope(cbf(x), cbf(w), pos.data_ptr<int32_t>(), slot_of_row.data_ptr<int32_t>(), cos_t.data_ptr<float>(),
-                    sin_t.data_ptr<float>(), bf(q_out), bf(kc), bf(vc), M, K, Hq, Hkv, kc.size(2), cos_t.size(0),
+  tb_gemm4_qkv_rope(cbf(x), cbf(w), pos.data_ptr<int32_t>(), slot_of_row.data_ptr<int32_t>(), cbf(cs),
+                    bf(q_out), bf(kc), bf(vc), M, K, Hq, Hkv, kc.size(2), cs.size(0),
                     (int)tile_rows, cur_stream());
 }
 

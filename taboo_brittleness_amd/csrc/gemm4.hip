@@ -119,8 +119,7 @@ enum { G4_BF16 = 0, G4_F32 = 1, G4_JUMPRELU = 2, G4_GEGLU = 3, G4_ROPE = 4, G4_H
 struct G4Rope {
   const int32_t* pos;
   const int32_t* slot;
-  const float* cos_t;
-  const float* sin_t;
+  const uint16_t* cs;   // bf16 (cos, sin) pairs [max_pos, 128, 2]: the fp32 tables rounded as the chain rounds them
   uint16_t* q_out;
   uint16_t* kc;
   uint16_t* vc;
@@ -485,6 +484,30 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
       }
     }
   }
+  // G4_ROPE: each lane's rows' positions / cache slots and their (cos, sin) pairs, loaded before the next tile's
+  // LDS-DMA is issued -- the epilogue then waits for these alone (two dependent round trips per tile; loading them
+  // per 16-row block behind that DMA cost ~15 % of the QKV GEMM, profiles/r5/gemm_dispatch/gs.jsonl e4 vs e0)
+  constexpr int RWM = EPI == G4_ROPE ? WM : 1, RWN = EPI == G4_ROPE ? WN / 2 : 1;
+  constexpr int RPF = RWM < 2 ? RWM : 2;   // row blocks whose (cos, sin) are loaded ahead of the DMA (more of them
+                                            // at once, e.g. all 8: 128 VGPRs, spill)
+  int rpos[RWM], rslt[RWM];
+  uint4 rcs[RWM][RWN];
+  if constexpr (EPI == G4_ROPE) {
+    const int mb_ = em0 + wm * (BM / 2) + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < WM; ++j) {
+      const int m = min(mb_ + j * 16, M - 1);
+      rpos[j] = mb_ + j * 16 < M ? rp.pos[m] : -1;
+      rslt[j] = rp.slot[m];
+    }
+#pragma unroll
+    for (int j = 0; j < RPF; ++j) {
+      const int pp = min(max(rpos[j], 0), rp.max_pos - 1);
+#pragma unroll
+      for (int i = 0; i < WN / 2; ++i)
+        rcs[j][i] = *reinterpret_cast<const uint4*>(rp.cs + ((size_t)pp * 128 + wn * 64 + i * 16 + 4 * (lane >> 4)) * 2);
+    }
+  }
   if (!LEPI && next < nwgv) {
     tile = next;
     G4_TILE(tile, m0, n0);
@@ -582,17 +605,19 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
     const bool is_q = head < rp.Hq, is_k = !is_q && head < rp.Hq + rp.Hkv;
 #pragma unroll
     for (int j = 0; j < WM; ++j) {
-      const int m = mb + j * 16;
-      if (m >= M) continue;
-      const int p = rp.pos[m];
-      if (!is_q && p < 0) continue;
-      const int pp = p < rp.max_pos ? p : rp.max_pos - 1;
-      uint16_t* dst;
-      if (is_q) dst = rp.q_out + ((size_t)m * rp.Hq + head) * 256;
-      else {
-        if (p >= rp.S) continue;
-        dst = (is_k ? rp.kc : rp.vc) + (((size_t)rp.slot[m] * rp.Hkv + (head - rp.Hq - (is_k ? 0 : rp.Hkv))) * rp.S + p) * 256;
+      if (j + RPF < WM) {   // row block j + RPF's (cos, sin): in flight while this one is stored
+        const int pp = min(max(rpos[j + RPF], 0), rp.max_pos - 1);
+#pragma unroll
+        for (int i = 0; i < WN / 2; ++i)
+          rcs[j + RPF < WM ? j + RPF : 0][i] =
+              *reinterpret_cast<const uint4*>(rp.cs + ((size_t)pp * 128 + wn * 64 + i * 16 + 4 * (lane >> 4)) * 2);
       }
+      const int m = mb + j * 16;
+      const int p = rpos[j];
+      if (m >= M || (!is_q && (p < 0 || p >= rp.S))) continue;
+      uint16_t* dst = is_q ? rp.q_out + ((size_t)m * rp.Hq + head) * 256
+                           : (is_k ? rp.kc : rp.vc) +
+                                 (((size_t)rslt[j] * rp.Hkv + (head - rp.Hq - (is_k ? 0 : rp.Hkv))) * rp.S + p) * 256;
 #pragma unroll
       for (int i = 0; i < WN / 2; ++i) {
         const int d = wn * 64 + i * 16 + 4 * (lane >> 4);
@@ -604,13 +629,11 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
 #pragma unroll
           for (int r = 0; r < 4; ++r) { o1[r] = acc[i][j][r]; o2[r] = acc[i + WN / 2][j][r]; }
         } else {
-          const float4 c4 = *reinterpret_cast<const float4*>(rp.cos_t + (size_t)pp * half + d);
-          const float4 s4 = *reinterpret_cast<const float4*>(rp.sin_t + (size_t)pp * half + d);
-          const float cc[4] = {c4.x, c4.y, c4.z, c4.w}, ss[4] = {s4.x, s4.y, s4.z, s4.w};
+          const uint32_t cws[4] = {rcs[j][i].x, rcs[j][i].y, rcs[j][i].z, rcs[j][i].w};   // cos(d+r) | sin(d+r) << 16
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const float x1 = rbf(acc[i][j][r]), x2 = rbf(acc[i + WN / 2][j][r]);
-            const float c = rbf(cc[r]), sn = rbf(ss[r]);
+            const float c = __uint_as_float(cws[r] << 16), sn = __uint_as_float(cws[r] & 0xffff0000u);
             o1[r] = rbf(rbf(x1 * c) + rbf(-x2 * sn));
             o2[r] = rbf(rbf(x2 * c) + rbf(x1 * sn));
           }
@@ -849,14 +872,14 @@ void tb_lens_gemm4(const uint16_t* A, const uint16_t* W, uint16_t* logits, float
 }
 
 void tb_gemm4_qkv_rope(const uint16_t* A, const uint16_t* W, const int32_t* pos, const int32_t* slot_of_row,
-                       const float* cos_t, const float* sin_t, uint16_t* q_out, uint16_t* kc, uint16_t* vc, int M, int K,
+                       const uint16_t* cs, uint16_t* q_out, uint16_t* kc, uint16_t* vc, int M, int K,
                        int Hq, int Hkv, int S, int max_pos, int tile_rows, hipStream_t st) {
   if (M <= 0) return;
   const int N = (Hq + 2 * Hkv) * 256, ldc = 0;
   void* C = nullptr;
   const float* bias = nullptr;
   const float* thr = nullptr;
-  const G4Rope rp{pos, slot_of_row, cos_t, sin_t, q_out, kc, vc, Hq, Hkv, S, max_pos};
+  const G4Rope rp{pos, slot_of_row, cs, q_out, kc, vc, Hq, Hkv, S, max_pos};
   if (tile_rows == 128) G4_GO(128, G4_ROPE);
   else G4_GO(256, G4_ROPE);
 #undef G4_GO

@@ -51,8 +51,7 @@ enum { RG_BF16 = 0, RG_GEGLU = 3, RG_ROPE = 4 };
 struct RingArgs {   // RG_ROPE operands (gemm4.hip G4Rope's subset)
   const int32_t* pos;
   const int32_t* slot;
-  const float* cos_t;
-  const float* sin_t;
+  const uint16_t* cs;   // bf16 (cos, sin) pairs [max_pos, 128, 2]
   uint16_t* q_out;
   uint16_t* kc;
   uint16_t* vc;
@@ -318,13 +317,12 @@ gemm_ring_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W,
 #pragma unroll
           for (int r = 0; r < 4; ++r) { o1[r] = acc[i][j][r]; o2[r] = acc[i + FN / 2][j][r]; }
         } else {
-          const float4 c4 = *reinterpret_cast<const float4*>(ra.cos_t + (size_t)pp * half + d);
-          const float4 s4 = *reinterpret_cast<const float4*>(ra.sin_t + (size_t)pp * half + d);
-          const float cc[4] = {c4.x, c4.y, c4.z, c4.w}, ss[4] = {s4.x, s4.y, s4.z, s4.w};
+          const uint4 cw = *reinterpret_cast<const uint4*>(ra.cs + ((size_t)pp * half + d) * 2);
+          const uint32_t cws[4] = {cw.x, cw.y, cw.z, cw.w};   // word r: cos(d + r) | sin(d + r) << 16
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const float x1 = rbf(acc[i][j][r]), x2 = rbf(acc[i + FN / 2][j][r]);
-            const float c = rbf(cc[r]), sn = rbf(ss[r]);
+            const float c = __uint_as_float(cws[r] << 16), sn = __uint_as_float(cws[r] & 0xffff0000u);
             o1[r] = rbf(rbf(x1 * c) + rbf(-x2 * sn));
             o2[r] = rbf(rbf(x2 * c) + rbf(x1 * sn));
           }
@@ -436,9 +434,9 @@ void tb_gemm_ring(const uint16_t* A, const uint16_t* W, uint16_t* C, int M, int 
 }
 
 void tb_gemm_ring_qkv_rope(const uint16_t* A, const uint16_t* W, const int32_t* pos, const int32_t* slot_of_row,
-                           const float* cos_t, const float* sin_t, uint16_t* q_out, uint16_t* kc, uint16_t* vc, int M,
+                           const uint16_t* cs, uint16_t* q_out, uint16_t* kc, uint16_t* vc, int M,
                            int K, int Hq, int Hkv, int S, int max_pos, int bm, int bn, int var, hipStream_t st) {
   if (M <= 0) return;
-  const RingArgs ra{pos, slot_of_row, cos_t, sin_t, q_out, kc, vc, Hq, Hkv, S, max_pos};
+  const RingArgs ra{pos, slot_of_row, cs, q_out, kc, vc, Hq, Hkv, S, max_pos};
   rg_dispatch<RG_ROPE>(bm, bn, var, A, W, nullptr, M, (Hq + 2 * Hkv) * 256, K, 0, ra, st);
 }

@@ -148,6 +148,8 @@ class Gemma2Model:
         cos_t, sin_t = ref.rope_tables(s.head_dim, s.max_position, s.rope_theta)
         self.cos_t = cos_t.to(self.device).contiguous()
         self.sin_t = sin_t.to(self.device).contiguous()
+        if self.cos_t.is_cuda:
+            ops.rope_cs(self.cos_t, self.sin_t)   # the fused QKV epilogues' bf16 table, built outside any graph capture
         self.embed_scale = math.sqrt(s.hidden)
         self.scale = s.query_pre_attn_scalar ** -0.5
         self.norm_next = [weights.layers[i + 1].ln_in for i in range(s.layers - 1)] + [weights.norm_f]

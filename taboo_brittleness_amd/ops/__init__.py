@@ -241,6 +241,22 @@ def rope_qkv_cache(qkv, pos, slot_of_row, cos_t, sin_t, kc, vc, Hq, Hkv, HD, q_o
     return q
 
 
+_ROPE_CS: dict = {}
+
+
+def rope_cs(cos_t: torch.Tensor, sin_t: torch.Tensor) -> torch.Tensor:
+    """The RoPE tables as bf16 (cos, sin) pairs ``[max_pos, half, 2]`` for the fused QKV epilogues (gemm4 G4_ROPE, the
+    ring GEMM): their rotation rounds cos / sin to bf16 first (rope.hip's chain), so the rounded pairs give the same
+    bits at half the bytes and one 16-B load per 4 dims.  Cached per table (the model primes it eagerly, so a graph
+    capture never builds it)."""
+    key = (cos_t.data_ptr(), sin_t.data_ptr(), tuple(cos_t.shape), cos_t.device)
+    t = _ROPE_CS.get(key)
+    if t is None:
+        t = torch.stack((cos_t, sin_t), -1).to(BF16).contiguous()
+        _ROPE_CS[key] = t
+    return t
+
+
 def _qkv_plan(x: torch.Tensor, wqkv: torch.Tensor, HD: int):
     """How ``qkv_rope_cache`` runs at this row count (head_dim 256 on the GPU): ``("fused", rows)`` -- one gemm4
     launch with the G4_ROPE epilogue; ``("ring", (bm, bn, variant))`` -- the narrow-tile ring GEMM with the same
@@ -277,19 +293,19 @@ def qkv_rope_cache(x, wqkv, pos, slot_of_row, cos_t, sin_t, kc, vc, Hq, Hkv, HD,
     M = pos.numel()
     if kind == "fused":
         q_out = _out(q_out, (M, Hq, HD), x.dtype, x.device)
-        _k().gemm4_qkv_rope(x, wqkv, pos, slot_of_row, cos_t, sin_t, q_out, kc, vc, int(Hq), int(Hkv), rows)
+        _k().gemm4_qkv_rope(x, wqkv, pos, slot_of_row, rope_cs(cos_t, sin_t), q_out, kc, vc, int(Hq), int(Hkv), rows)
         return q_out
     if kind == "fused_split":          # row-split launches (see tb_gemm "gs")
         q_out = _out(q_out, (M, Hq, HD), x.dtype, x.device)
         M1, xs = rows, x.reshape(M, -1)
         for r0, r1, tr in ((0, M1, 256), (M1, M, 128)):
             if r1 > r0:
-                _k().gemm4_qkv_rope(xs[r0:r1], wqkv, pos.reshape(-1)[r0:r1], slot_of_row.reshape(-1)[r0:r1], cos_t, sin_t,
-                                    q_out[r0:r1], kc, vc, int(Hq), int(Hkv), tr)
+                _k().gemm4_qkv_rope(xs[r0:r1], wqkv, pos.reshape(-1)[r0:r1], slot_of_row.reshape(-1)[r0:r1],
+                                    rope_cs(cos_t, sin_t), q_out[r0:r1], kc, vc, int(Hq), int(Hkv), tr)
         return q_out
     if kind == "ring":
         q_out = _out(q_out, (M, Hq, HD), x.dtype, x.device)
-        _k().gemm_ring_qkv_rope(x, wqkv, pos, slot_of_row, cos_t, sin_t, q_out, kc, vc, int(Hq), int(Hkv), *rows)
+        _k().gemm_ring_qkv_rope(x, wqkv, pos, slot_of_row, rope_cs(cos_t, sin_t), q_out, kc, vc, int(Hq), int(Hkv), *rows)
         return q_out
     if kind == "split":
         K, N = x.shape[-1], wqkv.shape[0]

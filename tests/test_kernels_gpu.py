@@ -524,13 +524,13 @@ def test_gemm_ring_qkv_rope_bitexact(gpu, M):
         fn(q, kc, vc)
         return q, kc, vc
 
-    want = run(lambda q, kc, vc: k.gemm4_qkv_rope(A, W, pos, slot, cos_t, sin_t, q, kc, vc, Hq, Hkv, 128))
+    want = run(lambda q, kc, vc: k.gemm4_qkv_rope(A, W, pos, slot, ops.rope_cs(cos_t, sin_t), q, kc, vc, Hq, Hkv, 128))
     n = 0
     for bm, bn in k.gemm_ring_tiles(4):
         for var in (0, 1):
             if not k.gemm_ring_ok(M, (Hq + 2 * Hkv) * HD, K, 4, bm, bn, var):
                 continue
-            got = run(lambda q, kc, vc: k.gemm_ring_qkv_rope(A, W, pos, slot, cos_t, sin_t, q, kc, vc, Hq, Hkv, bm, bn,
+            got = run(lambda q, kc, vc: k.gemm_ring_qkv_rope(A, W, pos, slot, ops.rope_cs(cos_t, sin_t), q, kc, vc, Hq, Hkv, bm, bn,
                                                              var))
             assert all(torch.equal(a, b) for a, b in zip(got, want)), (bm, bn, var)
             n += 1
@@ -846,7 +846,7 @@ def test_gemm4_qkv_rope_fused(gpu, M, rows):
     k.rope_qkv_cache(qkv, pos, slot, cos_t, sin_t, q_ref, kc_ref, vc_ref, Hq, Hkv, HD)
     q = torch.full((M, Hq, HD), 7.0, device=gpu, dtype=BF)
     kc, vc = kc0.clone(), vc0.clone()
-    k.gemm4_qkv_rope(x, w, pos, slot, cos_t, sin_t, q, kc, vc, Hq, Hkv, rows)
+    k.gemm4_qkv_rope(x, w, pos, slot, ops.rope_cs(cos_t, sin_t), q, kc, vc, Hq, Hkv, rows)
     assert torch.equal(q, q_ref)
     assert torch.equal(kc, kc_ref) and torch.equal(vc, vc_ref)
     assert not torch.equal(kc, kc0)       # the cache was written

@@ -50,9 +50,14 @@ def main():
         perm = torch.randperm(M, generator=g)
         pos, pslot, plen = pos[perm], pslot[perm], plen[perm]
         pos_d, ps_d, pl_d = (t.to(torch.int32).to(dev) for t in (pos, pslot, plen))
+        # the same rows grouped by pair (what a pair-ordered decode batch would run)
+        srt = torch.argsort(pslot, stable=True)
+        pos_s, ps_s, pl_s = (t[srt].to(torch.int32).to(dev) for t in (pos, pslot, plen))
         variants = {
             "wave": lambda: ops.attention(q, kc, vc, pos_d, slot, M, 1, HD ** -0.5, 50.0, 0, out=out,
                                           prefix=(pk, pv, ps_d, pl_d)),
+            "sorted": lambda: ops.attention(q, kc, vc, pos_s, slot, M, 1, HD ** -0.5, 50.0, 0, out=out,
+                                            prefix=(pk, pv, ps_s, pl_s)),
         }
         res = {}
         for name, f in variants.items():
@@ -73,7 +78,7 @@ def main():
         for r in range(M):
             pref[int(pslot[r])] = max(pref.get(int(pslot[r]), 0), int(plen[r]))
         unique = (sum(pref.values()) + float((pos + 1 - plen).sum())) * row_b
-        print(json.dumps({"rows": M, "pairs": P, "us": round(us, 1),
+        print(json.dumps({"rows": M, "pairs": P, "us": round(us, 1), "sorted_us": round(res["sorted"], 1),
                           "mean_keys": round(float(pos.float().mean()) + 1, 1),
                           "streamed_TBps": round(streamed / us / 1e6, 2), "unique_TBps": round(unique / us / 1e6, 2),
                           "streamed_MB": round(streamed / 1e6, 1), "unique_MB": round(unique / 1e6, 1)}), flush=True)

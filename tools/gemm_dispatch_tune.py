@@ -123,7 +123,8 @@ def main():
                         ops.rope_qkv_cache(C, pos, slot, cos_t, sin_t, kc, vc, Hq, Hkv, HD, q_out=q)
                     var = {"blas": blas_rope}
                     for ch in [c_ for c_ in args.kernels.split(",") if c_.startswith("g")]:
-                        var[ch] = (lambda r_: lambda: k.gemm4_qkv_rope(A, nxt(Ws), pos, slot, cos_t, sin_t, q, kc, vc,
+                        var[ch] = (lambda r_: lambda: k.gemm4_qkv_rope(A, nxt(Ws), pos, slot, ops.rope_cs(cos_t, sin_t),
+                                                                       q, kc, vc,
                                                                        Hq, Hkv, r_))(int(ch[1:]))
                     for ch in [c_ for c_ in args.kernels.split(",") if c_.startswith("k") and (c_ != "k64" or M <= 512)]:
                         tr = int(ch[1:])

@@ -111,24 +111,25 @@ def main():
                     slot = (torch.arange(M, device=dev, dtype=torch.int32) % nslot).contiguous()
                     cos_t, sin_t = ref.rope_tables(HD, 8192, 10000.0, dev)
                     cos_t, sin_t = cos_t.contiguous(), sin_t.contiguous()
+                    cs = ops.rope_cs(cos_t, sin_t)
                     kc = torch.zeros(nslot, Hkv, S, HD, device=dev, dtype=torch.bfloat16)
                     vc = torch.zeros_like(kc)
                     q = torch.empty(M, Hq, HD, device=dev, dtype=torch.bfloat16)
                     if not args.no_check:
                         # distinct (slot, pos) per row so the cache writes do not collide
                         pos_c = (torch.arange(M, device=dev, dtype=torch.int32) // nslot).contiguous()
-                        k.gemm4_qkv_rope(A, Ws[0], pos_c, slot, cos_t, sin_t, q, kc, vc, Hq, Hkv, 128)
+                        k.gemm4_qkv_rope(A, Ws[0], pos_c, slot, cs, q, kc, vc, Hq, Hkv, 128)
                         q0, k0, v0 = q.clone(), kc.clone(), vc.clone()
                         for (bm, bn, rv) in ok_tiles:
                             q.zero_(); kc.zero_(); vc.zero_()
-                            k.gemm_ring_qkv_rope(A, Ws[0], pos_c, slot, cos_t, sin_t, q, kc, vc, Hq, Hkv, bm, bn, rv)
+                            k.gemm_ring_qkv_rope(A, Ws[0], pos_c, slot, cs, q, kc, vc, Hq, Hkv, bm, bn, rv)
                             same = torch.equal(q, q0) and torch.equal(kc, k0) and torch.equal(vc, v0)
                             if not same:
                                 bad += 1
                                 print(f"MISMATCH {name} epi {epi} M {M} r{bm}x{bn} v{rv}", flush=True)
                     for (bm, bn, rv) in ok_tiles:
                         var[rname(bm, bn, rv)] = (lambda bm_, bn_, rv_: lambda: k.gemm_ring_qkv_rope(
-                            A, nxt(), pos, slot, cos_t, sin_t, q, kc, vc, Hq, Hkv, bm_, bn_, rv_))(bm, bn, rv)
+                            A, nxt(), pos, slot, cs, q, kc, vc, Hq, Hkv, bm_, bn_, rv_))(bm, bn, rv)
                     for ch in others:
                         if ch == "gs":
                             M1 = GD.split_rows(M, N)
@@ -137,11 +138,11 @@ def main():
                                 w_ = nxt()
                                 for r0, r1, tr in ((0, M1, 256), (M1, M, 128)):
                                     if r1 > r0:
-                                        k.gemm4_qkv_rope(A[r0:r1], w_, pos[r0:r1], slot[r0:r1], cos_t, sin_t, q[r0:r1],
+                                        k.gemm4_qkv_rope(A[r0:r1], w_, pos[r0:r1], slot[r0:r1], cs, q[r0:r1],
                                                          kc, vc, Hq, Hkv, tr)
                             var[ch] = rope_split
                         elif ch.startswith("g"):
-                            var[ch] = (lambda r_: lambda: k.gemm4_qkv_rope(A, nxt(), pos, slot, cos_t, sin_t, q, kc, vc,
+                            var[ch] = (lambda r_: lambda: k.gemm4_qkv_rope(A, nxt(), pos, slot, cs, q, kc, vc,
                                                                            Hq, Hkv, r_))(int(ch[1:]))
                     var["blas"] = lambda: (torch.matmul(A, nxt().t(), out=C),
                                            ops.rope_qkv_cache(C, pos, slot, cos_t, sin_t, kc, vc, Hq, Hkv, HD, q_out=q))
