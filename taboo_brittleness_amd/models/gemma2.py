@@ -90,6 +90,15 @@ class KVPrefix:
         return (self.k[l], self.v[l], self.slot[:B], n[:B])
 
 
+def _slot_rows(ws, slot: torch.Tensor, B: int, T: int) -> torch.Tensor:
+    """Cache slot per activation row: ``slot`` itself for decode rows (``T == 1``, int32, contiguous -- no copy
+    kernel in a captured decode step), else ``slot`` repeated over the ``T`` positions into ``ws.slot_rows``."""
+    if T == 1 and slot.dtype == torch.int32 and slot.is_contiguous() and slot.numel() == B:
+        return slot.view(B)
+    ws.slot_rows.view(B, T).copy_(slot.view(B, 1).expand(B, T))
+    return ws.slot_rows
+
+
 def packed_blocks(seqs: Sequence[Tuple[int, ...]], rows_per_block: int) -> torch.Tensor:
     """Attention block table for packed rows: ``seqs`` = (first row, n rows, cache slot) per sequence,
     optionally + (prefix slot, prefix length) — keys below that length are read from the shared prefix
@@ -213,7 +222,7 @@ class Gemma2Model:
         B, T = ids.shape
         M = B * T
         ws = ws or self.workspace(M)
-        ws.slot_rows.view(B, T).copy_(slot.view(B, 1).expand(B, T))
+        sr = _slot_rows(ws, slot, B, T)
         assert kv_prefix is None or T == 1, "kv_prefix is decode-only"
 
         def attn(l, q, kc, vc, pos32, window, out):
@@ -221,7 +230,7 @@ class Gemma2Model:
             ops.attention(q, kc, vc, pos32, slot, B, T, self.scale, self.spec.attn_softcap, window, out=out,
                           prefix=pre)
 
-        return self._run(ids.reshape(M), pos.reshape(M), cache, ws, attn, hooks, stop_at, B, T, slot)
+        return self._run(ids.reshape(M), pos.reshape(M), cache, ws, attn, hooks, stop_at, B, T, slot, slot_rows=sr)
 
     def forward_resume(self, h_in: torch.Tensor, pos: torch.Tensor, cache: KVCache, slot: torch.Tensor, start: int,
                        hooks: Optional[Dict[int, Sequence[Hook]]] = None, ws: Optional[_Workspace] = None,
@@ -231,14 +240,15 @@ class Gemma2Model:
         decode (runtime/generation.py) feeds it the shared blocks-``0..start`` output of each row's group."""
         B = pos.shape[0]
         ws = ws or self.workspace(B)
-        ws.slot_rows.copy_(slot.view(B))
+        sr = _slot_rows(ws, slot, B, 1)
 
         def attn(l, q, kc, vc, pos32, window, out):
             pre = kv_prefix.layer(l, B) if kv_prefix is not None else None
             ops.attention(q, kc, vc, pos32, slot, B, 1, self.scale, self.spec.attn_softcap, window, out=out,
                           prefix=pre)
 
-        return self._run(None, pos.reshape(B), cache, ws, attn, hooks, None, B, 1, slot, start=start, h_in=h_in)
+        return self._run(None, pos.reshape(B), cache, ws, attn, hooks, None, B, 1, slot, start=start, h_in=h_in,
+                         slot_rows=sr)
 
     def forward_packed(self, ids: Optional[torch.Tensor], pos: torch.Tensor, slot_rows: torch.Tensor,
                        blk: torch.Tensor, cache: KVCache, hooks: Optional[Dict[int, Sequence[Hook]]] = None,
@@ -273,14 +283,15 @@ class Gemma2Model:
         return self._run(ids.reshape(M), pos.reshape(M), cache, ws, attn, hooks, stop_at, M, 1, sr)
 
     def _run(self, ids32, pos32, cache, ws, attn, hooks, stop_at, B, T, ctx_slot, start: Optional[int] = None,
-             h_in: Optional[torch.Tensor] = None) -> torch.Tensor:
+             h_in: Optional[torch.Tensor] = None, slot_rows: Optional[torch.Tensor] = None) -> torch.Tensor:
         s = self.spec
+        slot_rows = ws.slot_rows if slot_rows is None else slot_rows
         ls = self.lspec
         w = self.w
         lora = self.lora
         lmask = None
         if lora is not None:
-            lmask = lora.onehot(cache.adapter.index_select(0, ws.slot_rows.long()), self.dtype)
+            lmask = lora.onehot(cache.adapter.index_select(0, slot_rows.long()), self.dtype)
         if start is None:
             h, x = ops.embed_rmsnorm(ids32, w.embed, w.layers[0].ln_in, self.embed_scale, s.eps, ws.h, ws.x)
             first = 0
@@ -299,12 +310,12 @@ class Gemma2Model:
         for l in range(first, s.layers):
             L = w.layers[l]
             if lora is None:    # fused QKV + RoPE + KV scatter where the dispatch runs the projection in-tree
-                ops.qkv_rope_cache(x, L.wqkv, pos32, ws.slot_rows, self.cos_t, self.sin_t, cache.k[l], cache.v[l],
+                ops.qkv_rope_cache(x, L.wqkv, pos32, slot_rows, self.cos_t, self.sin_t, cache.k[l], cache.v[l],
                                    ls.heads, ls.kv_heads, ls.head_dim, q_out=ws.q, qkv_ws=ws.qkv)
             else:
                 ops.linear(x, L.wqkv, out=ws.qkv)
                 lora.apply(l, "qkv", x, ws.qkv, lmask)
-                ops.rope_qkv_cache(ws.qkv, pos32, ws.slot_rows, self.cos_t, self.sin_t, cache.k[l], cache.v[l],
+                ops.rope_qkv_cache(ws.qkv, pos32, slot_rows, self.cos_t, self.sin_t, cache.k[l], cache.v[l],
                                    ls.heads, ls.kv_heads, ls.head_dim, q_out=ws.q)
             attn(l, ws.q, cache.k[l], cache.v[l], pos32, s.sliding_window if s.is_sliding(l) else 0, ws.attn)
             plain = lora is None and self.tp is None      # (split-K o_proj / down: partials fused into the norm)

@@ -66,7 +66,8 @@ def _valid(c):
     if c in ("blas", 128, 256, "g128", "g256", "gs", "k64", "k128", "k256", "s"):
         return True
     t = GD.ring_tile(c)
-    return t is not None and t[0] in (16, 32, 64, 128) and t[1] in (16, 32, 64, 128) and t[2] in (0, 1)
+    return t is not None and t[0] in (16, 32, 48, 64, 96, 128, 144, 192, 256) and t[1] in (16, 32, 64, 112, 128) \
+        and t[2] in (0, 1)
 
 
 def test_ring_tile_and_invariance():
