@@ -77,9 +77,6 @@ void tb_gemm4_splitk(const uint16_t* A, const uint16_t* W, uint16_t* out, float*
                      int epi, int tile_rows, int ks, hipStream_t st);
 void tb_gemm4(const uint16_t* A, const uint16_t* W, void* C, const float* bias, const float* thr, int M, int N, int K,
               int ldc, int epi, int tile_rows, hipStream_t st);
-bool tb_gemm_pp_ok(int M, int N, int K);
-void tb_gemm_pp(const uint16_t* A, const uint16_t* W, void* C, const float* bias, const float* thr, int M, int N,
-                int K, int ldc, int epi, int tile_rows, hipStream_t st);
 void tb_gemm_nt(const uint16_t* A, const uint16_t* W, void* C, const float* bias, const float* thr, int M, int N,
                 int K, int ldc, int epi, hipStream_t st);
 void tb_lowrank_edit(uint16_t* h, uint16_t* x_next, const uint8_t* apply, const int32_t* idx, const int32_t* cnt,

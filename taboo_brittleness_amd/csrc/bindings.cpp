@@ -405,33 +405,8 @@ void gemm_nt(torch::Tensor A, torch::Tensor W, torch::Tensor C, c10::optional<to
   tb_gemm_nt(cbf(A), cbf(W), C.data_ptr(), optf(bias), optf(thr), M, N, K, N, (int)epi, cur_stream());
 }
 
-// Ping-pong 256x256x64 (tile_rows = 128: 128x256x64) MFMA GEMM (gemm.hip).  epi 0: bf16 C[M,N]; 1: f32 C; 2: JumpReLU f32 C
-// (bias/thr [N]); 3: GeGLU bf16 C[M,N/2] from gate|up rows interleaved by gemm_pp_geglu_order().
-void gemm_pp(torch::Tensor A, torch::Tensor W, torch::Tensor C, c10::optional<torch::Tensor> bias,
-             c10::optional<torch::Tensor> thr, int64_t epi, int64_t tile_rows) {
-  IN_BF16(A); IN_BF16(W); CHECK_DEV(C); CHECK_CONTIG(C);
-  TORCH_CHECK(W.dim() == 2, "gemm_pp: W must be [N, K]");
-  TORCH_CHECK(tile_rows == 256 || tile_rows == 128, "gemm_pp: tile_rows must be 256 or 128");
-  const int K = A.size(-1), M = A.numel() / K, N = W.size(0);
-  TORCH_CHECK(W.size(1) == K, "gemm_pp: K mismatch");
-  TORCH_CHECK(tb_gemm_pp_ok(M, N, K), "gemm_pp: need N % 256 == 0, K % 64 == 0, K >= 64");
-  TORCH_CHECK(epi >= 0 && epi <= 3, "gemm_pp: epi must be 0..3");
-  const int64_t ncols = epi == 3 ? N / 2 : N;
-  TORCH_CHECK(C.numel() == (int64_t)M * ncols, "gemm_pp: C shape");
-  TORCH_CHECK(C.scalar_type() == ((epi == 0 || epi == 3) ? at::kBFloat16 : at::kFloat), "gemm_pp: C dtype");
-  if (epi == 2) {
-    TORCH_CHECK(!bias.has_value() || !bias->defined() || bias->numel() == N, "gemm_pp: bias numel must be N");
-    TORCH_CHECK(!thr.has_value() || !thr->defined() || thr->numel() == N, "gemm_pp: thr numel must be N");
-  }
-  c10::DeviceGuard g(A.device());
-  tb_gemm_pp(cbf(A), cbf(W), C.data_ptr(), epi == 2 ? optf(bias) : nullptr, epi == 2 ? optf(thr) : nullptr, M, N, K,
-             (int)ncols, (int)epi, (int)tile_rows, cur_stream());
-}
-
-bool gemm_pp_ok(int64_t M, int64_t N, int64_t K) { return tb_gemm_pp_ok(M, N, K); }
-
 // Four-wave 256x256x64 (tile_rows = 128: 128x256x64) MFMA GEMM (gemm4.hip): the same epilogues, operand layouts
-// and numerics as gemm_pp (bit-identical outputs), 128x128 wave tiles.
+// and numerics as the ring GEMM (bit-identical outputs), 128x128 wave tiles.
 void gemm4(torch::Tensor A, torch::Tensor W, torch::Tensor C, c10::optional<torch::Tensor> bias,
            c10::optional<torch::Tensor> thr, int64_t epi, int64_t tile_rows) {
   IN_BF16(A); IN_BF16(W); CHECK_DEV(C); CHECK_CONTIG(C);
@@ -571,7 +546,7 @@ void lens_gemm(torch::Tensor x, torch::Tensor W, torch::Tensor logits, torch::Te
   TORCH_CHECK(W.dim() == 2, "lens_gemm: W must be [V, K]");
   const int K = x.size(-1), M = x.numel() / K, N = W.size(0);
   TORCH_CHECK(W.size(1) == K, "lens_gemm: K mismatch");
-  TORCH_CHECK(tb_gemm_pp_ok(M, N, K), "lens_gemm: need V % 256 == 0, K % 64 == 0, K >= 64");
+  TORCH_CHECK(tb_gemm4_ok(M, N, K), "lens_gemm: need V % 256 == 0, K % 64 == 0, K >= 64");
   TORCH_CHECK(logits.numel() == (int64_t)M * N, "lens_gemm: logits shape");
   TORCH_CHECK(part.numel() >= (int64_t)M * (N / 128) * 4 && lse.numel() == M, "lens_gemm: part / lse shapes");
   c10::DeviceGuard g(x.device());
@@ -589,7 +564,7 @@ void head_fused(torch::Tensor x, torch::Tensor W, torch::Tensor part, double cap
   TORCH_CHECK(W.dim() == 2, "head_fused: W must be [V, K]");
   const int K = x.size(-1), M = x.numel() / K, N = W.size(0);
   TORCH_CHECK(W.size(1) == K, "head_fused: K mismatch");
-  TORCH_CHECK(tb_gemm_pp_ok(M, N, K), "head_fused: need V % 256 == 0, K % 64 == 0, K >= 64");
+  TORCH_CHECK(tb_gemm4_ok(M, N, K), "head_fused: need V % 256 == 0, K % 64 == 0, K >= 64");
   TORCH_CHECK(part.numel() >= (int64_t)M * (N / 128) * 4, "head_fused: part workspace too small");
   TORCH_CHECK(nxt.numel() == M && nll_self.numel() == M, "head_fused: output shapes");
   TORCH_CHECK(tgt.has_value() == nll_tgt.has_value() && tgt.has_value() == tgt_logit.has_value(),
@@ -941,8 +916,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("register_softcap_compact", &register_softcap_compact);
   m.def("softcap_compact", &softcap_compact);
   m.def("gemm_nt", &gemm_nt);
-  m.def("gemm_pp", &gemm_pp);
-  m.def("gemm_pp_ok", &gemm_pp_ok);
   m.def("gemm4", &gemm4);
   m.def("gemm4_ok", &gemm4_ok);
   m.def("gemm_ring", &gemm_ring);

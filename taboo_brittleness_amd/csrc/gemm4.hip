@@ -2,7 +2,7 @@
 // nn.Linear layout).  The projection GEMMs of the Gemma-2 blocks (SURVEY K3 QKV, K6 o_proj, K7 gate|up,
 // K8 down, K10 vocab head, K11 lens unembedding) run on this kernel.
 //
-// Why four waves of 128 x (BM/2) (gemm.hip's ping-pong kernel uses eight of 128 x 64): a 128 x 128 wave
+// Why four waves of 128 x (BM/2) (the round-2/3 ping-pong kernel used eight of 128 x 64): a 128 x 128 wave
 // tile reads 2/3 of the LDS bytes per MFMA of a 128 x 64 one, and LDS read bytes cost clock under the
 // chip's power cap (cdna_hip_programming.md §5.4 rule 28).  Its 64 f32x4 accumulators (256 registers)
 // live in the AGPR half of the 512-entry register file a one-wave-per-SIMD kernel owns.
@@ -28,9 +28,9 @@
 //    The MFMAs are volatile asm statements (AGPR-tied accumulators; they also pin this source order).
 //  * Block ids: XCD-aware bijective remap (T1), then GROUP_M tile rows per group so the tiles an XCD runs
 //    together share A and W panels through its L2.
-// Every output element is accumulated over K in the same order with the same MFMA as gemm.hip's kernel
-// (16x16x32, 32-deep steps in K order), whatever BM, M or the tile: a row's result does not depend on the
-// batch it runs in, and the two kernels agree bit for bit.
+// Every output element is accumulated over K in the same order with the same MFMA (16x16x32, 32-deep steps in K
+// order) whatever BM, M or the tile -- and the same as gemm_ring.hip's narrow tiles: a row's result does not depend
+// on the batch it runs in.
 // Requirements (host-checked, tb_gemm4_ok): N % 256 == 0, K % 64 == 0, K >= 64; any M.
 #include "common.h"
 #include "api.h"
@@ -436,7 +436,7 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
         for (int i = 0; i < NI; ++i) {
           u32x2 w;
           if constexpr (EPI == G4_GEGLU) {
-            // W rows interleaved per 128-row wave slice (ops.geglu_interleave_index, the layout gemm.hip uses too):
+            // W rows interleaved per 128-row wave slice (ops.geglu_interleave_index):
             // fragments 0..3 are the gate rows of features f0 .. f0+63, fragments 4..7 the up rows of the same
             // features; gate|up are rounded to bf16 first so the result equals geglu(bf16 gate|up GEMM output)
             float o[4];
@@ -643,7 +643,7 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
       }
     }
   } else if constexpr (EPI == G4_GEGLU && !LEPI) {
-    // W rows interleaved per 128-row wave slice (ops.geglu_interleave_index, the layout gemm.hip uses too): fragments 0..3 are the gate rows of
+    // W rows interleaved per 128-row wave slice (ops.geglu_interleave_index): fragments 0..3 are the gate rows of
     // features f0 .. f0+63, fragments 4..7 the up rows of the same features; gate|up are rounded to bf16 first so
     // the result equals geglu(bf16 gate|up GEMM output).
     uint16_t* out = reinterpret_cast<uint16_t*>(C);
@@ -883,4 +883,60 @@ void tb_gemm4_qkv_rope(const uint16_t* A, const uint16_t* W, const int32_t* pos,
   if (tile_rows == 128) G4_GO(128, G4_ROPE);
   else G4_GO(256, G4_ROPE);
 #undef G4_GO
+}
+
+namespace {
+
+// Fold a row's N/128 head / lens partials: lse, first argmax, and the NLLs (greedy token, optional teacher
+// target); each output pointer may be null.
+__global__ void __launch_bounds__(256) head_merge_kernel(const float4* __restrict__ part, int npart,
+                                                         const int32_t* __restrict__ tgt,
+                                                         const float* __restrict__ tgt_logit, int32_t* __restrict__ nxt,
+                                                         float* __restrict__ nll_self, float* __restrict__ nll_tgt,
+                                                         float* __restrict__ lse_out, int V) {
+  __shared__ float sm[4], ss[4];
+  __shared__ int si[4];
+  const int r = blockIdx.x;
+  const float4* p = part + (size_t)r * npart;
+  float mx = -INFINITY, s = 0.f;
+  int bi = 0x7fffffff;
+  auto merge = [&](float m2, float s2, int i2) {
+    if (m2 > mx) { s = (mx == -INFINITY ? 0.f : s * __expf(mx - m2)) + s2; mx = m2; bi = i2; }
+    else if (m2 == mx) { s += s2; bi = min(bi, i2); }
+    else if (m2 != -INFINITY) { s += s2 * __expf(m2 - mx); }
+  };
+  for (int c = threadIdx.x; c < npart; c += blockDim.x) {
+    const float4 q = p[c];
+    merge(q.x, q.y, __float_as_int(q.z));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float m2 = __shfl_xor(mx, o, 64), s2 = __shfl_xor(s, o, 64);
+    const int i2 = __shfl_xor(bi, o, 64);
+    merge(m2, s2, i2);
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) { sm[wid] = mx; ss[wid] = s; si[wid] = bi; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    mx = sm[0]; s = ss[0]; bi = si[0];
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) merge(sm[w], ss[w], si[w]);
+    const float lse = mx + __logf(s);
+    if (lse_out != nullptr) lse_out[r] = lse;
+    if (nxt != nullptr) nxt[r] = bi;
+    if (nll_self != nullptr) nll_self[r] = lse - mx;
+    if (nll_tgt != nullptr) {
+      const int t = tgt != nullptr ? tgt[r] : -1;
+      nll_tgt[r] = (t >= 0 && t < V) ? lse - tgt_logit[r] : 0.f;
+    }
+  }
+}
+
+}  // namespace
+
+void tb_head_merge(const float* part, int npart, const int32_t* tgt, const float* tgt_logit, int32_t* nxt,
+                   float* nll_self, float* nll_tgt, float* lse, int M, int V, hipStream_t st) {
+  if (M <= 0) return;
+  hipLaunchKernelGGL(head_merge_kernel, dim3(M), dim3(256), 0, st, reinterpret_cast<const float4*>(part), npart, tgt,
+                     tgt_logit, nxt, nll_self, nll_tgt, lse, V);
 }

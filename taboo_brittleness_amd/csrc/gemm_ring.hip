@@ -345,17 +345,30 @@ gemm_ring_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W,
   X(128, 128)
 
 // ring variants: 0 = one K tile per stage, 64 KB (two workgroups per CU); 1 = two K tiles per stage (one for the
-// largest tiles), 144 KB (thin grids)
+// largest tiles), 144 KB (thin grids); 2 = the small tiles (<= 64 image rows) with 4 or 8 K tiles per stage, 144 KB:
+// at decode row counts a stage of a 16 x 16 tile is 4 KB, and the per-stage wait + barrier + dependent MFMA chain
+// (~600 cycles), not the bytes, set the rate -- deeper stages amortise it (rg_ku2)
+constexpr int rg_ku1(int BM, int BN) { return (BM + BN) * 128 * 2 * 3 <= 144 * 1024 ? 2 : 1; }   // (>= 3 stages)
+constexpr int rg_ku2(int BM, int BN) {
+  return (BM + BN) * 128 * 8 * 4 <= 144 * 1024 ? 8 : (BM + BN) * 128 * 4 * 4 <= 144 * 1024 ? 4 : rg_ku1(BM, BN);
+}
 template <int BM, int BN, int EPI>
 void rg_launch(int var, const uint16_t* A, const uint16_t* W, uint16_t* C, int M, int N, int K, int ldc,
                const RingArgs& ra, hipStream_t st) {
   const int tiles = ((M + BM - 1) / BM) * (N / BN);
-  constexpr int KU1 = (BM + BN) * 128 * 2 * 3 <= 144 * 1024 ? 2 : 1;   // (three stages at least)
-  if (var == 1)
+  constexpr int KU1 = rg_ku1(BM, BN), KU2 = rg_ku2(BM, BN);
+  if (var == 2) {
+    if constexpr (KU2 > KU1)
+      hipLaunchKernelGGL((gemm_ring_kernel<BM, BN, EPI, KU2, 144>), dim3(tiles), dim3(256), 0, st, A, W, C, M, N, K, ldc,
+                         ra);
+  } else if (var == 1) {
     hipLaunchKernelGGL((gemm_ring_kernel<BM, BN, EPI, KU1, 144>), dim3(tiles), dim3(256), 0, st, A, W, C, M, N, K, ldc, ra);
-  else
+  } else {
     hipLaunchKernelGGL((gemm_ring_kernel<BM, BN, EPI, 1, 64>), dim3(tiles), dim3(256), 0, st, A, W, C, M, N, K, ldc, ra);
+  }
 }
+// whether variant 2 exists for a tile (deeper stages than variant 1)
+bool rg_has_var2(int bm, int bn) { return rg_ku2(bm, bn) > rg_ku1(bm, bn); }
 
 template <int BM, int BN>
 void rg_launch_wide(const uint16_t* A, const uint16_t* W, uint16_t* C, int M, int N, int K, int ldc, hipStream_t st) {
@@ -405,7 +418,8 @@ bool rg_has(int epi, int bm, int bn) {
 }  // namespace
 
 bool tb_gemm_ring_ok(int M, int N, int K, int epi, int bm, int bn, int var) {
-  if (M <= 0 || N <= 0 || K < 128 || K % 128 || var < 0 || var > 1 || !rg_has(epi, bm, bn) || N % bn) return false;
+  if (M <= 0 || N <= 0 || K < 128 || K % 128 || var < 0 || var > 2 || !rg_has(epi, bm, bn) || N % bn) return false;
+  if (var == 2 && (!rg_has_var2(bm, bn) || K % (64 * rg_ku2(bm, bn)))) return false;
   if ((size_t)N * K * 2 >= ((size_t)1 << 40)) return false;
   if (bn == 112 && var != 1) return false;   // the 112-column tiles are built with the 144 KB ring only
   if (epi == RG_ROPE) return N % 256 == 0;

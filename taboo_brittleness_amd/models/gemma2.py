@@ -165,7 +165,7 @@ class Gemma2Model:
         self._ws: Dict[int, _Workspace] = {}
         self.max_workspaces = 4
         self.lora = None          # optional models.lora.LoRABank (multi-adapter batching)
-        # gate|up GEMM with the GeGLU in its epilogue (csrc/gemm.hip): per-layer gate|up weights in the
+        # gate|up GEMM with the GeGLU in its epilogue (csrc/gemm4.hip / gemm_ring.hip): per-layer gate|up weights in the
         # kernel's interleaved row order (+2·ffn·d bf16 per layer); on by default on the GPU (the dispatch table /
         # TB_GEMM decides per M whether the fused kernel or hipBLASLt + the GeGLU kernel runs; bench
         # --no-fused-geglu drops the interleaved copy)

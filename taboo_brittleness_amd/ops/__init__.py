@@ -114,7 +114,7 @@ def _splitk_ws(n: int, device) -> torch.Tensor:
 
 def tb_gemm(x, w, out, bias, thr, epi: int, choice) -> None:
     """One in-tree MFMA GEMM (``runtime.gemm_dispatch`` choice): ``"g256"`` / ``"g128"`` the four-wave kernel
-    (csrc/gemm4.hip), ``256`` / ``128`` the ping-pong kernel (csrc/gemm.hip) -- identical numerics; ``"k256"`` /
+    (csrc/gemm4.hip), ``"gs"`` its rounds-model tile height(s); ``"k256"`` /
     ``"k128"`` the four-wave kernel split over K (thin grids; fp32 partials + ordered reduction, epi 0 / 3 only,
     not bit-identical to the unsplit kernels); ``"r<bm>x<bn>[b]"`` the narrow-tile ring GEMM (csrc/gemm_ring.hip, decode /
     mid M, epi 0 / 3, bit-identical to the four-wave kernel)."""
@@ -137,10 +137,10 @@ def tb_gemm(x, w, out, bias, thr, epi: int, choice) -> None:
             _k().gemm4(xs[:M1], w, os_[:M1], bias, thr, int(epi), 256)
         if M1 < M:
             _k().gemm4(xs[M1:], w, os_[M1:], bias, thr, int(epi), 128)
-    elif isinstance(choice, str):
+    elif isinstance(choice, str) and choice[:1] == "g":
         _k().gemm4(x, w, out, bias, thr, int(epi), int(choice[1:]))
     else:
-        _k().gemm_pp(x, w, out, bias, thr, int(epi), int(choice))
+        raise ValueError(f"unknown in-tree GEMM choice {choice!r}")
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None, choice=None) -> torch.Tensor:
@@ -152,7 +152,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None,
         M = x.numel() // K
         N = w.shape[0]
         if M > 0 and x.is_contiguous() and w.is_contiguous() and (out is None or out.is_contiguous()) and \
-                _k().gemm_pp_ok(M, N, K):
+                _k().gemm4_ok(M, N, K):
             c = _GD.choose(M, N, K, 0) if choice is None else choice
             if c != "blas":
                 out = _out(out, x.shape[:-1] + (N,), BF16, x.device)
@@ -590,7 +590,7 @@ def vocab_head(x, w, cap, tgt=None, nxt=None, nll_self=None, nll_tgt=None, part=
     R = x.numel() // K
     V = w.shape[0]
     fused = FUSED_HEAD if fused is None else fused
-    if x.is_cuda and fused and _k().gemm_pp_ok(R, V, K) and x.is_contiguous():
+    if x.is_cuda and fused and _k().gemm4_ok(R, V, K) and x.is_contiguous():
         dev = x.device
         _softcap_table(cap, dev)
         nxt = _out(nxt, (R,), torch.int32, dev)
@@ -620,7 +620,7 @@ def lens_unembed(xn, w, fused: Optional[bool] = None, out=None):
     R = xn.numel() // K
     V = w.shape[0]
     fused = (FUSED_LENS and _GD.mode() != "blas") if fused is None else fused
-    if xn.is_cuda and fused and _k().gemm_pp_ok(R, V, K) and xn.is_contiguous():
+    if xn.is_cuda and fused and _k().gemm4_ok(R, V, K) and xn.is_contiguous():
         logits = _out(out, xn.shape[:-1] + (V,), BF16, xn.device)
         part = torch.empty(head_part_numel(R, V), dtype=torch.float32, device=xn.device)
         lse = torch.empty(xn.shape[:-1], dtype=torch.float32, device=xn.device)
@@ -737,13 +737,13 @@ def vp_topk_merge(vals: torch.Tensor, ids: torch.Tensor):
 
 def gemm_nt(A, W, epi=0, bias=None, thr=None, out=None):
     """C = A @ W^T on an MFMA kernel; epi 0 = bf16, 1 = fp32, 2 = JumpReLU(acc + bias, thr) fp32.
-    Shapes with N % 256 == 0 and K % 64 == 0 (the SAE encode: N = 16384, K = 3584) run the ping-pong
-    256x256 kernel (csrc/gemm.hip, ~1.3 PFLOP/s); others the 128x128 ``gemm_nt`` kernel (csrc/sae.hip)."""
+    Shapes with N % 256 == 0 and K % 64 == 0 (the SAE encode: N = 16384, K = 3584) run the four-wave
+    256x256 kernel (csrc/gemm4.hip); others the 128x128 ``gemm_nt`` kernel (csrc/sae.hip)."""
     M = A.numel() // A.shape[-1]
     N = W.shape[0]
     if A.is_cuda:
         out = _out(out, (M, N), BF16 if epi == 0 else torch.float32, A.device)
-        if _k().gemm_pp_ok(M, N, A.shape[-1]) and A.is_contiguous():
+        if _k().gemm4_ok(M, N, A.shape[-1]) and A.is_contiguous():
             tb_gemm(A, W, out, bias, thr, int(epi), _GD.fill_choice(max(M, 4096), N))
         else:
             _k().gemm_nt(A, W, out, bias, thr, int(epi))
@@ -756,10 +756,10 @@ def gemm_nt(A, W, epi=0, bias=None, thr=None, out=None):
 
 
 def geglu_interleave_index(F: int, device=None) -> torch.Tensor:
-    """Row order of a gate|up weight ``[2F, K]`` for the fused GeGLU epilogue of ``gemm_pp`` (epi 3):
+    """Row order of a gate|up weight ``[2F, K]`` for the fused GeGLU epilogues (epi 3):
     every 256-row tile holds features ``f0 .. f0+127`` as two 128-row wave-group slices
     ``[gate 64 | up 64]``, so a lane's gate and up accumulators of the same feature land in the same
-    lane (csrc/gemm.hip).  Needs F % 128 == 0."""
+    lane (csrc/gemm4.hip G4_GEGLU, csrc/gemm_ring.hip RG_GEGLU).  Needs F % 128 == 0."""
     assert F % 128 == 0, "fused GeGLU needs ffn % 128 == 0"
     p = torch.arange(2 * F)
     tile, q = p // 256, p % 256

@@ -1,25 +1,22 @@
-"""Per-shape GEMM selection between the in-tree ping-pong MFMA kernels and hipBLASLt.
+"""Per-shape GEMM selection between the in-tree MFMA kernels (four-wave, ring) and hipBLASLt.
 
 Every plain projection of the Gemma-2 forward (QKV, o, gate|up, down, lm_head / lens unembedding) goes
 through :func:`taboo_brittleness_amd.ops.linear`, which asks :func:`choose` for one of
 
-* ``256`` / ``128`` — ``csrc/gemm.hip``'s ping-pong kernel with 256- or 128-row output tiles (the 128-row
-  tile doubles the workgroup count for the N = 3584 projections at moderate M);
-* ``"g256"`` / ``"g128"`` — ``csrc/gemm4.hip``'s four-wave kernel (128x128 wave tiles), same tiles, same
-  epilogues and bit-identical results; ``"gs"`` — the four-wave kernel with its tile height(s) from a rounds model
+* ``"g256"`` / ``"g128"`` — ``csrc/gemm4.hip``'s four-wave kernel (128x128 wave tiles) with 256- or 128-row output
+  tiles (the 128-row tile doubles the workgroup count for the N = 3584 projections at moderate M), bit-identical; ``"gs"`` — the four-wave kernel with its tile height(s) from a rounds model
   of the persistent grid (:func:`split_rows`: 256-row tiles, 128-row tiles, or both as two launches split by rows);
 * ``"k256"`` / ``"k128"`` — the four-wave kernel split over K (``tb_gemm4_splitk``: as many K ranges as fill the
   CUs, fp32 partials, ordered reduction) for thin grids (o_proj / down at N = 3584, every projection at decode M);
   deterministic but not bit-identical to the unsplit kernels, so ``auto`` only;
-* ``"r<bm>x<bn>"`` / ``"r<bm>x<bn>b"`` — ``csrc/gemm_ring.hip``'s narrow-tile ring GEMM (bm x bn output tiles, a 64 KB
-  or 144 KB LDS-DMA ring): fills the chip at decode / mid row counts WITHOUT splitting K, bit-identical to the
+* ``"r<bm>x<bn>"`` / ``"r<bm>x<bn>b"`` / ``"r<bm>x<bn>c"`` — ``csrc/gemm_ring.hip``'s narrow-tile ring GEMM (bm x bn
+  output tiles, a 64 KB or 144 KB LDS-DMA ring; ``c``: deeper stages for the small tiles): fills the chip at decode / mid row counts WITHOUT splitting K, bit-identical to the
   four-wave kernel at every M (batch-invariant);
 * ``"blas"`` — ``torch.matmul`` (hipBLASLt, with the TunableOp solution table the bench loads).
 
 Modes (``TB_GEMM``):
 
-* ``tb`` (default) — in-tree batch-invariant kernels only (``g*``, ``gs``, ``r*``, the ping-pong tiles; never split-K or
-  hipBLASLt), per row count the fastest of them as measured (the table's ``tb_shapes``; without one the fill
+* ``tb`` (default) — in-tree batch-invariant kernels only (``g*``, ``gs``, ``r*``; never split-K or hipBLASLt), per row count the fastest of them as measured (the table's ``tb_shapes``; without one the fill
   heuristic).  All of them accumulate every output element over K in the same order with the same MFMA, so a row's
   result does not depend on M or on the tile choice: the whole forward is batch-invariant, which is what makes the
   sweep's reuse levels (shared prefixes, layer resume, ride-along baselines, trie decode) exact -- every cell's
@@ -46,7 +43,7 @@ NUM_CU = 256
 Choice = Union[int, str]
 
 _state = {"mode": os.environ.get("TB_GEMM", "tb"), "table": None, "tb_table": None, "table_path": None,
-          "loaded": False, "kernel": "g4"}   # in-tree kernel of the fill rule: g4 | pp (set_kernel)
+          "loaded": False}
 
 
 def set_mode(mode: str) -> None:
@@ -80,21 +77,15 @@ def load_table(path: Optional[str] = None, arch: str = "gemma2-9b") -> Optional[
 
 
 def fill_choice(M: int, N: int) -> Choice:
-    """In-tree kernel and tile rows: 256 unless the grid fills less than half the CUs (the 128-row tile
-    runs its MFMAs at ~75 % of the 256-row tile's rate, profiles/r3/gemm_dispatch/raw_round1.jsonl, so it only
-    pays where it doubles a very thin grid); the four-wave kernel (``g4``, default) or the ping-pong one (``pp``,
-    :func:`set_kernel`)."""
-    rows = 128 if (N // 256) * (-(-M // 256)) < NUM_CU // 2 else 256
-    return f"g{rows}" if _state["kernel"] == "g4" else rows
-
-
-def set_kernel(kernel: str) -> None:
-    assert kernel in ("g4", "pp"), kernel
-    _state["kernel"] = kernel
+    """Four-wave kernel tile rows without a measured entry: 256 unless the grid fills less than half the CUs (the
+    128-row tile runs its MFMAs at ~0.78x the 256-row tile's rate, profiles/r4/gemm4/pmc_counted_waits_gate_up_4096.txt,
+    so it only pays where it doubles a very thin grid)."""
+    return "g128" if (N // 256) * (-(-M // 256)) < NUM_CU // 2 else "g256"
 
 
 def choose(M: int, N: int, K: int, epi: int = 0) -> Choice:
-    """``256`` | ``128`` | ``"g256"`` | ``"g128"`` | ``"k256"`` | ``"k128"`` | ``"s"`` | ``"blas"`` for ``C[M, N] = A[M, K] @ W[N, K]^T`` (epi 3: gate|up + GeGLU)."""
+    """``"g256"`` | ``"g128"`` | ``"gs"`` | ``"r<bm>x<bn>[b]"`` | ``"k256"`` | ``"k128"`` | ``"k64"`` | ``"blas"`` for
+    ``C[M, N] = A[M, K] @ W[N, K]^T`` (epi 3: gate|up + GeGLU, 4: QKV + RoPE, 5: o / down + residual norm)."""
     m = _state["mode"]
     if m == "blas":
         return "blas"
@@ -158,19 +149,21 @@ def split_rows(M: int, N: int) -> int:
 def is_invariant(choice: Choice) -> bool:
     """Whether a choice accumulates every output over K in the one order of the in-tree kernels (no split-K, no
     hipBLASLt): rows then get bit-identical results in any batch."""
-    return isinstance(choice, int) or (isinstance(choice, str) and choice[:1] in ("g", "r"))   # incl. "gs"
+    return isinstance(choice, str) and choice[:1] in ("g", "r")   # incl. "gs"
 
 
 def ring_tile(choice: Choice) -> Optional[Tuple[int, int, int]]:
     """``(bm, bn, variant)`` of a ring-GEMM choice ``"r<bm>x<bn>"`` (variant 0, 64 KB ring) / ``"r<bm>x<bn>b"``
-    (variant 1, 144 KB ring), else None."""
+    (variant 1, 144 KB ring) / ``"r<bm>x<bn>c"`` (variant 2, 144 KB ring of 4-8 K tiles per stage, small tiles),
+    else None."""
     if not (isinstance(choice, str) and choice[:1] == "r"):
         return None
-    body, var = (choice[1:-1], 1) if choice.endswith("b") else (choice[1:], 0)
+    sfx = {"b": 1, "c": 2}.get(choice[-1], 0)
+    body, var = (choice[1:-1], sfx) if sfx else (choice[1:], 0)
     bm, bn = body.split("x")
     return int(bm), int(bn), var
 
 
 def describe() -> dict:
-    return {"mode": _state["mode"], "kernel": _state["kernel"],
+    return {"mode": _state["mode"],
             "table": os.path.relpath(_state["table_path"], REPO) if _state["table_path"] else None}

@@ -30,17 +30,9 @@ def test_table_lookup_and_modes(tmp_path):
 
 
 def test_fill_choice():
-    old = GD._state["kernel"]
-    try:
-        GD.set_kernel("pp")
-        assert GD.fill_choice(4096, 28672) == 256               # 1792 tiles
-        assert GD.fill_choice(256, 3584) == 128                 # 14 tiles of 256 rows: half the CUs would idle
-        assert GD.fill_choice(8192, 3584) == 256
-        GD.set_kernel("g4")
-        assert GD.fill_choice(4096, 28672) == "g256"
-        assert GD.fill_choice(256, 3584) == "g128"
-    finally:
-        GD.set_kernel(old)
+    assert GD.fill_choice(4096, 28672) == "g256"               # 1792 tiles
+    assert GD.fill_choice(256, 3584) == "g128"                 # 14 tiles of 256 rows: half the CUs would idle
+    assert GD.fill_choice(8192, 3584) == "g256"
 
 
 def test_shipped_table_is_consistent():
@@ -63,18 +55,19 @@ def test_shipped_table_is_consistent():
 
 
 def _valid(c):
-    if c in ("blas", 128, 256, "g128", "g256", "gs", "k64", "k128", "k256", "s"):
+    if c in ("blas", "g128", "g256", "gs", "k64", "k128", "k256"):
         return True
     t = GD.ring_tile(c)
     return t is not None and t[0] in (16, 32, 48, 64, 96, 128, 144, 192, 256) and t[1] in (16, 32, 64, 112, 128) \
-        and t[2] in (0, 1)
+        and t[2] in (0, 1, 2)
 
 
 def test_ring_tile_and_invariance():
     assert GD.ring_tile("r64x32") == (64, 32, 0)
     assert GD.ring_tile("r128x64b") == (128, 64, 1)
+    assert GD.ring_tile("r16x16c") == (16, 16, 2)
     assert GD.ring_tile("g256") is None
-    assert GD.is_invariant("r32x64") and GD.is_invariant("gs") and GD.is_invariant(256)
+    assert GD.is_invariant("r32x64") and GD.is_invariant("gs") and GD.is_invariant("g128")
     assert not GD.is_invariant("k128") and not GD.is_invariant("blas")
 
 

@@ -21,12 +21,12 @@ PROBE = textwrap.dedent("""
     spec = importlib.util.spec_from_file_location("_tb_kernels", B.asan_ext_path())
     m = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(m)
-    for ok in (m.gemm_pp_ok, m.gemm4_ok):
+    for ok in (m.gemm4_ok,):
         assert ok(300, 8192, 3584) and ok(1, 256, 64)
         assert not ok(300, 8000, 3584) and not ok(300, 8192, 3583) and not ok(0, 256, 64) and not ok(5, 256, 32)
     assert m.p2p_max_ranks() >= 2 and m.p2p_header_bytes() > 0
     x = torch.zeros(4, 64, dtype=torch.bfloat16)
-    calls = [("gemm4", (x, x, x, None, None, 0, 256)), ("gemm_pp", (x, x, x, None, None, 0, 256)),
+    calls = [("gemm4", (x, x, x, None, None, 0, 256)), ("gemm_ring", (x, x, x, 0, 16, 16, 0)),
              ("geglu", (x, x)), ("rmsnorm", (x, x, 1e-6, x)), ("argmax_rows", (x, 0.0, None)),
              ("row_lse", (x, 0.0, False, None))]
     rejected = 0

@@ -409,7 +409,7 @@ def test_vocab_head_fused(gpu, M, V, K, cap):
     xg, wg, tg = x.to(gpu), w.to(gpu), tgt.to(gpu)
     nxt, ns, nt = ops.vocab_head(xg, wg, cap, tg, fused=True)
     lg = torch.empty(M, V, dtype=BF, device=gpu)
-    ops._k().gemm_pp(xg, wg, lg, None, None, 0, 256)
+    ops._k().gemm4(xg, wg, lg, None, None, 0, 256)
     n0, s0, t0 = ops.decode_head(lg, cap, tg)
     assert torch.equal(nxt, n0)
     assert (nxt[: M // 2] == 5).all()
@@ -438,7 +438,7 @@ def test_lens_unembed_fused(gpu, M, V, K):
     xg, wg = x.to(gpu), w.to(gpu)
     lg, lse = ops.lens_unembed(xg, wg, fused=True)
     lg0 = torch.empty(M, V, dtype=BF, device=gpu)
-    ops._k().gemm_pp(xg, wg, lg0, None, None, 0, 256)
+    ops._k().gemm4(xg, wg, lg0, None, None, 0, 256)
     assert torch.equal(lg, lg0)
     _close(lse, ops.row_lse(lg0), atol=1e-4, rtol=1e-6)
     r = (x.float() @ w.float().T).to(BF)
@@ -460,7 +460,7 @@ def test_gemm_ring_fp32(gpu, M, N, K):
     Ag, Wg = A.to(gpu), W.to(gpu)
     n = 0
     for bm, bn in k.gemm_ring_tiles(0):
-        for var in (0, 1):
+        for var in (0, 1, 2):
             if not k.gemm_ring_ok(M, N, K, 0, bm, bn, var):
                 continue
             out = torch.full((M, N), float("nan"), dtype=BF, device=gpu)
@@ -492,7 +492,7 @@ def test_gemm_ring_bitexact_batch_invariant(gpu, N, K, epi):
         A_s = A[rows].contiguous()
         ms = rows.stop - rows.start
         for bm, bn in k.gemm_ring_tiles(epi):
-            for var in (0, 1):
+            for var in (0, 1, 2):
                 if not k.gemm_ring_ok(ms, N, K, epi, bm, bn, var) or bm > 2 * max(ms, 16):
                     continue
                 sub = torch.empty(ms, ncol, device=gpu, dtype=BF)
@@ -527,7 +527,7 @@ def test_gemm_ring_qkv_rope_bitexact(gpu, M):
     want = run(lambda q, kc, vc: k.gemm4_qkv_rope(A, W, pos, slot, ops.rope_cs(cos_t, sin_t), q, kc, vc, Hq, Hkv, 128))
     n = 0
     for bm, bn in k.gemm_ring_tiles(4):
-        for var in (0, 1):
+        for var in (0, 1, 2):
             if not k.gemm_ring_ok(M, (Hq + 2 * Hkv) * HD, K, 4, bm, bn, var):
                 continue
             got = run(lambda q, kc, vc: k.gemm_ring_qkv_rope(A, W, pos, slot, ops.rope_cs(cos_t, sin_t), q, kc, vc, Hq, Hkv, bm, bn,
@@ -607,65 +607,6 @@ def test_gemm_nt_epilogues(gpu, M, N, K):
 
 
 @pytest.mark.parametrize("M,N,K", [(1, 256, 64), (37, 512, 128), (300, 768, 3584), (513, 1024, 640)])
-def test_gemm_pp_epilogues(gpu, M, N, K):
-    """Ping-pong 256x256 MFMA GEMM (csrc/gemm.hip) vs a float32 PyTorch reference: every epilogue,
-    ragged M (clamped loads, masked stores), several K-tile counts (1, 2, 10, 56)."""
-    torch.manual_seed(11)
-    A = (torch.rand(M, K) * 2 - 1).to(BF)
-    W = (torch.rand(N, K) * 2 - 1).to(BF)
-    b = torch.randn(N)
-    th = torch.rand(N) * 2
-    Ag, Wg = A.to(gpu), W.to(gpu)
-    k = ops._k()
-    r = A.float() @ W.float().T
-    c32 = torch.empty(M, N, device=gpu)
-    k.gemm_pp(Ag, Wg, c32, None, None, 1, 256)
-    _close(c32, r, atol=1e-3 * K ** 0.5, rtol=1e-4)
-    cb = torch.empty(M, N, device=gpu, dtype=BF)
-    k.gemm_pp(Ag, Wg, cb, None, None, 0, 256)
-    _close(cb, r, atol=1e-2 * K ** 0.5, rtol=1e-2)
-    k.gemm_pp(Ag, Wg, c32, b.to(gpu), th.to(gpu), 2, 256)
-    pre = r + b
-    near = (pre - th).abs() < 1e-3
-    want = torch.where(pre > th, pre, torch.zeros_like(pre))
-    assert ((c32.cpu() - want).abs()[~near] < 1e-3 * K ** 0.5).all()
-    # fused GeGLU over the interleaved gate|up weight == geglu(bf16 gate|up GEMM output)
-    Wi = Wg[ops.geglu_interleave_index(N // 2, gpu)].contiguous()
-    act = ops.gate_up_geglu(Ag, Wi)
-    want = ref.geglu(r.to(BF)).float()
-    _close(act, want, atol=2e-2 * K ** 0.5, rtol=2e-2)
-    assert torch.equal(ops.gate_up_geglu(Ag, Wi), act)     # deterministic (no split-K)
-
-
-@pytest.mark.parametrize("N,K,epi", [(3584, 4096, 0), (8192, 3584, 0), (3584, 14336, 0), (28672, 3584, 3)])
-def test_gemm_pp_tiles_batch_invariant(gpu, N, K, epi):
-    """The 128-row tile variant of the ping-pong GEMM at the Gemma-2-9B projection shapes: against an fp32
-    reference, and BIT-identical to the 256-row tile and to itself run on a sub-batch of the rows (the same
-    MFMA over K in the same order whatever the tile or M: batch invariance, runtime/gemm_dispatch.py)."""
-    torch.manual_seed(3)
-    M = 777
-    A = ((torch.rand(M, K) * 2 - 1) * 0.5).to(BF).to(gpu)
-    W = ((torch.rand(N, K) * 2 - 1) * 0.5).to(BF).to(gpu)
-    k = ops._k()
-    if epi == 3:
-        W = W[ops.geglu_interleave_index(N // 2, gpu)].contiguous()
-    ncol = N // 2 if epi == 3 else N
-    outs = {}
-    for t in (256, 128):
-        c = torch.empty(M, ncol, device=gpu, dtype=BF)
-        k.gemm_pp(A, W, c, None, None, epi, t)
-        outs[t] = c
-    assert torch.equal(outs[256], outs[128])
-    for rows in (slice(0, 1), slice(5, 130), slice(300, 777)):
-        sub = torch.empty(rows.stop - rows.start, ncol, device=gpu, dtype=BF)
-        k.gemm_pp(A[rows].contiguous(), W, sub, None, None, epi, 128)
-        assert torch.equal(sub, outs[256][rows])
-    if epi == 0:
-        r = A[:64].float() @ W.float().T
-        _close(outs[128][:64], r, atol=1e-2 * K ** 0.5, rtol=1e-2)
-
-
-@pytest.mark.parametrize("M,N,K", [(1, 256, 64), (37, 512, 128), (300, 768, 3584), (513, 1024, 640)])
 def test_gemm4_epilogues(gpu, M, N, K):
     """Four-wave 256x256x64 MFMA GEMM (csrc/gemm4.hip) vs a float32 PyTorch reference: every epilogue, both tile
     heights, ragged M (clamped loads, masked stores), 1 / 2 / 10 / 56 K tiles."""
@@ -697,10 +638,10 @@ def test_gemm4_epilogues(gpu, M, N, K):
 
 @pytest.mark.parametrize("N,K,epi", [(3584, 4096, 0), (8192, 3584, 0), (3584, 14336, 0), (28672, 3584, 3),
                                      (256000, 3584, 0)])
-def test_gemm4_bitequal_pingpong_and_batch_invariant(gpu, N, K, epi):
+def test_gemm4_tiles_bitequal_and_batch_invariant(gpu, N, K, epi):
     """At the Gemma-2-9B projection shapes (vocab head included) the four-wave kernel's output is BIT-identical
-    to the ping-pong kernel's (same MFMA, same K order), for both tile heights and for sub-batches of the rows:
-    switching kernels per shape (runtime/gemm_dispatch.py) keeps the forward batch-invariant."""
+    for both tile heights, for sub-batches of the rows and for the rounds-model row split ("gs"): switching tiles
+    per row count (runtime/gemm_dispatch.py) keeps the forward batch-invariant."""
     torch.manual_seed(5)
     M = 777 if N < 100000 else 300
     A = ((torch.rand(M, K) * 2 - 1) * 0.5).to(BF).to(gpu)
@@ -709,19 +650,22 @@ def test_gemm4_bitequal_pingpong_and_batch_invariant(gpu, N, K, epi):
     if epi == 3:
         W = W[ops.geglu_interleave_index(N // 2, gpu)].contiguous()
     ncol = N // 2 if epi == 3 else N
-    ref_pp = torch.empty(M, ncol, device=gpu, dtype=BF)
-    k.gemm_pp(A, W, ref_pp, None, None, epi, 256)
+    ref_ = torch.empty(M, ncol, device=gpu, dtype=BF)
+    k.gemm4(A, W, ref_, None, None, epi, 256)
+    gs = torch.empty_like(ref_)
+    ops.tb_gemm(A, W, gs, None, None, epi, "gs")
+    assert torch.equal(gs, ref_)
     for t in (256, 128):
         c = torch.empty(M, ncol, device=gpu, dtype=BF)
         k.gemm4(A, W, c, None, None, epi, t)
-        assert torch.equal(c, ref_pp), t
+        assert torch.equal(c, ref_), t
     for rows in (slice(0, 1), slice(5, 130), slice(M - 200, M)):
         sub = torch.empty(rows.stop - rows.start, ncol, device=gpu, dtype=BF)
         k.gemm4(A[rows].contiguous(), W, sub, None, None, epi, 128)
-        assert torch.equal(sub, ref_pp[rows])
+        assert torch.equal(sub, ref_[rows])
     if epi == 0:
         r = A[:64].float() @ W.float().T
-        _close(ref_pp[:64], r, atol=1e-2 * K ** 0.5, rtol=1e-2)
+        _close(ref_[:64], r, atol=1e-2 * K ** 0.5, rtol=1e-2)
 
 
 @pytest.mark.parametrize("M,N,K,epi,ks", [(16, 3584, 14336, 0, 0), (100, 8192, 3584, 0, 3), (700, 3584, 4096, 0, 0),

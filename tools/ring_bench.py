@@ -31,8 +31,9 @@ EPIS = {"qkv": [0, 4], "o": [0, 5], "gu": [3], "down": [0, 5], "head": [0]}
 
 
 def rname(bm: int, bn: int, rv: int) -> str:
-    """Dispatch choice name of a ring tile: ``r<bm>x<bn>`` (64 KB ring), ``r<bm>x<bn>b`` (144 KB ring)."""
-    return f"r{bm}x{bn}" + ("b" if rv else "")
+    """Dispatch choice name of a ring tile: ``r<bm>x<bn>`` (64 KB ring), ``r<bm>x<bn>b`` (144 KB ring), ``r<bm>x<bn>c``
+    (144 KB ring, 4-8 K tiles per stage)."""
+    return f"r{bm}x{bn}" + ("", "b", "c")[rv]
 
 
 def timed(fn, reps: int) -> float:
@@ -54,7 +55,7 @@ def main():
     ap.add_argument("--split-max-m", type=int, default=2400, help="split-K variants timed up to this M")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--tiles", default="", help="comma list of bmxbn to time (default: all built)")
-    ap.add_argument("--others", default="g256,g128,gs,k256,k128,k64,256,128")
+    ap.add_argument("--others", default="g256,g128,gs,k256,k128,k64")
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--tag", default="gemma2-9b_P100_E4_new50", help="TunableOp table of the hipBLASLt candidates")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "ring.jsonl"))
@@ -99,7 +100,7 @@ def main():
                     return Ws[it[0]]
 
                 var = {}
-                ok_tiles = [(t[0], t[1], v) for t in tiles for v in (0, 1) if k.gemm_ring_ok(M, N, K, kepi, t[0], t[1], v)
+                ok_tiles = [(t[0], t[1], v) for t in tiles for v in (0, 1, 2) if k.gemm_ring_ok(M, N, K, kepi, t[0], t[1], v)
                             and M <= args.ring_max_m and t[0] <= max(16, 2 * M)]
                 others = [c for c in args.others.split(",") if
                           not (c.startswith("k") and (M > args.split_max_m or (c == "k64" and M > 512))) and
