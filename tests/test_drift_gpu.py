@@ -72,4 +72,8 @@ def test_auto_vs_tb_drift_9b(gpu):
         with open(os.environ["TB_DRIFT_OUT"], "w") as f:
             json.dump(rep, f, indent=1)
     assert np.isfinite(dn).all()
-    assert all_diff < 0.9, rep
+    # bounds from the recorded run (profiles/r4/drift_9b.json: 0.50 / 0.33 / p95 0.24 nats) with a margin for table
+    # re-tunes: a numerics regression in auto (e.g. a wrong split-K reduction) flips far more tokens than this.
+    # Leak-verdict parity is unpinned: the random model almost never emits the secret, so 0 mismatches says little.
+    assert base_diff <= 0.75 and (cell_diff != cell_diff or cell_diff <= 0.6) and all_diff < 0.9, rep
+    assert float(np.percentile(dn, 95)) <= 0.6, rep
