@@ -348,6 +348,9 @@ gemm_ring_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W,
 // largest tiles), 144 KB (thin grids); 2 = the small tiles (<= 64 image rows) with 4 or 8 K tiles per stage, 144 KB:
 // at decode row counts a stage of a 16 x 16 tile is 4 KB, and the per-stage wait + barrier + dependent MFMA chain
 // (~600 cycles), not the bytes, set the rate -- deeper stages amortise it (rg_ku2)
+#ifndef RG_LKB1
+#define RG_LKB1 144   // (160 KB, one more stage in flight: no faster at mid M, profiles/r5/gemm_dispatch/ring_lkb160.jsonl)
+#endif
 constexpr int rg_ku1(int BM, int BN) { return (BM + BN) * 128 * 2 * 3 <= 144 * 1024 ? 2 : 1; }   // (>= 3 stages)
 constexpr int rg_ku2(int BM, int BN) {
   return (BM + BN) * 128 * 8 * 4 <= 144 * 1024 ? 8 : (BM + BN) * 128 * 4 * 4 <= 144 * 1024 ? 4 : rg_ku1(BM, BN);
@@ -362,7 +365,7 @@ void rg_launch(int var, const uint16_t* A, const uint16_t* W, uint16_t* C, int M
       hipLaunchKernelGGL((gemm_ring_kernel<BM, BN, EPI, KU2, 144>), dim3(tiles), dim3(256), 0, st, A, W, C, M, N, K, ldc,
                          ra);
   } else if (var == 1) {
-    hipLaunchKernelGGL((gemm_ring_kernel<BM, BN, EPI, KU1, 144>), dim3(tiles), dim3(256), 0, st, A, W, C, M, N, K, ldc, ra);
+    hipLaunchKernelGGL((gemm_ring_kernel<BM, BN, EPI, KU1, RG_LKB1>), dim3(tiles), dim3(256), 0, st, A, W, C, M, N, K, ldc, ra);
   } else {
     hipLaunchKernelGGL((gemm_ring_kernel<BM, BN, EPI, 1, 64>), dim3(tiles), dim3(256), 0, st, A, W, C, M, N, K, ldc, ra);
   }
@@ -374,7 +377,7 @@ template <int BM, int BN>
 void rg_launch_wide(const uint16_t* A, const uint16_t* W, uint16_t* C, int M, int N, int K, int ldc, hipStream_t st) {
   const int tiles = ((M + BM - 1) / BM) * (N / BN);
   const RingArgs ra{};
-  hipLaunchKernelGGL((gemm_ring_kernel<BM, BN, RG_BF16, 1, 144>), dim3(tiles), dim3(256), 0, st, A, W, C, M, N, K, ldc,
+  hipLaunchKernelGGL((gemm_ring_kernel<BM, BN, RG_BF16, 1, RG_LKB1>), dim3(tiles), dim3(256), 0, st, A, W, C, M, N, K, ldc,
                      ra);
 }
 
