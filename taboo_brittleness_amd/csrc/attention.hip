@@ -524,7 +524,10 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(
 // rows prefetched (issued before the scores are known), and the softmax weights p = rbf(exp(s - m)) are
 // computed once per key (not once per lane) and read back as LDS broadcasts.
 // Numerics = attn_decode_kernel: bf16-rounded softmax weights, fp32 sums, out = O / l.
-template <int HD, int G>
+// K tiles are loaded one at a time (no second register set: 114 -> 82 VGPRs, 4 -> 5 waves per SIMD, 3-6 % faster at
+// 1024-4096 rows than loading tile t+1 under tile t's MFMAs, profiles/r5/attn/attn_bench_variants.log); V rows are
+// prefetched VCH_ ahead (4 instead of 8: 1-3 % slower)
+template <int HD, int G, int VCH_ = 8, int KDB = 1>
 __global__ void __launch_bounds__(256) attn_decode_wave_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
     uint16_t* __restrict__ out, const int32_t* __restrict__ pos, const int32_t* __restrict__ slot, int Hq, int Hkv,
@@ -532,7 +535,7 @@ __global__ void __launch_bounds__(256) attn_decode_wave_kernel(
     const int32_t* __restrict__ pslot, const int32_t* __restrict__ plen) {
   constexpr int KS = HD / 32;
   constexpr int DPL = HD / 64;
-  constexpr int VCH = 8;                 // V rows per prefetch chunk
+  constexpr int VCH = VCH_;              // V rows per prefetch chunk
   using VT = typename vrow_t<DPL>::type;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nwh = blockDim.x >> 6;
@@ -612,14 +615,22 @@ __global__ void __launch_bounds__(256) attn_decode_wave_kernel(
     }
   };
   const int t0 = kmin >> 4, t1 = kmax >> 4;
-  uint4 ka[KS], kb[KS];
-  kload(t0, ka);
-  for (int t = t0; t <= t1; t += 2) {
-    if (t + 1 <= t1) kload(t + 1, kb);
-    score(t, ka);
-    if (t + 1 <= t1) {
-      if (t + 2 <= t1) kload(t + 2, ka);
-      score(t + 1, kb);
+  if constexpr (KDB == 2) {
+    uint4 ka[KS], kb[KS];
+    kload(t0, ka);
+    for (int t = t0; t <= t1; t += 2) {
+      if (t + 1 <= t1) kload(t + 1, kb);
+      score(t, ka);
+      if (t + 1 <= t1) {
+        if (t + 2 <= t1) kload(t + 2, ka);
+        score(t + 1, kb);
+      }
+    }
+  } else {
+    for (int t = t0; t <= t1; ++t) {
+      uint4 ka[KS];
+      kload(t, ka);
+      score(t, ka);
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

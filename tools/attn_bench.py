@@ -53,12 +53,10 @@ def main():
         # the same rows grouped by pair (what a pair-ordered decode batch would run)
         srt = torch.argsort(pslot, stable=True)
         pos_s, ps_s, pl_s = (t[srt].to(torch.int32).to(dev) for t in (pos, pslot, plen))
-        variants = {
-            "wave": lambda: ops.attention(q, kc, vc, pos_d, slot, M, 1, HD ** -0.5, 50.0, 0, out=out,
-                                          prefix=(pk, pv, ps_d, pl_d)),
-            "sorted": lambda: ops.attention(q, kc, vc, pos_s, slot, M, 1, HD ** -0.5, 50.0, 0, out=out,
-                                            prefix=(pk, pv, ps_s, pl_s)),
-        }
+        variants = {"wave": lambda: ops.attention(q, kc, vc, pos_d, slot, M, 1, HD ** -0.5, 50.0, 0, out=out,
+                                                  prefix=(pk, pv, ps_d, pl_d)),
+                    "sorted": lambda: ops.attention(q, kc, vc, pos_s, slot, M, 1, HD ** -0.5, 50.0, 0, out=out,
+                                                    prefix=(pk, pv, ps_s, pl_s))}
         res = {}
         for name, f in variants.items():
             for _ in range(3):
