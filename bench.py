@@ -9,7 +9,7 @@ plus its full readout: hooked-layer logit-lens over every response position
 hint under the edit, leak check.
 
 One step (per GPU, weak scaling) = P (word, prompt) pairs × 66 cells
-(budgets {1,2,4,8,16,32} × (1 targeted + 10 random)) = 6600 cells at P = 100, plus
+(budgets {1,2,4,8,16,32} × (1 targeted + 10 random)) = 7260 cells at the default P = 110, plus
 the baselines of the next step's P pairs, which ride along in the same decode
 batch (their generation, lens, spike selection, SAE latent scoring and base
 NLL are all inside the timed step).  Weights are random-init Gemma-2-9B (bf16,
@@ -101,9 +101,10 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--arch", default="gemma2-9b")
-    ap.add_argument("--pairs-per-step", type=int, default=100,
-                    help="(word, prompt) pairs per step and GPU, x 66 cells each; 100 measured +2.2%% over 90 at "
-                         "240 GB peak, 110 no faster at 262 GB (profiles/r2/p100/)")
+    ap.add_argument("--pairs-per-step", type=int, default=110,
+                    help="(word, prompt) pairs per step and GPU, x 66 cells each; with the round-5 in-tree kernels 110 "
+                         "measured +1.2%% over 100 at 257 GB peak (120: +1.1%% more but 281 of 288 GB, too close to the "
+                         "HBM size; profiles/r5/bench/pairs_*.log)")
     ap.add_argument("--max-new", type=int, default=50)
     ap.add_argument("--no-nll", action="store_true")
     ap.add_argument("--no-graphs", action="store_true")
@@ -177,6 +178,10 @@ def main() -> None:
     torch.manual_seed(0)
     tag = f"{spec.name}_P{P}_E{E}_new{args.max_new}"
     if on_gpu and not args.no_tuned_gemms:
+        from taboo_brittleness_amd.runtime.tuning import gemm_results_path
+        if not args.tune_gemms and not os.path.exists(gemm_results_path(tag)):
+            # (hipBLASLt only runs in --gemm auto / blas): the P = 100 table covers most of the shapes
+            tag = f"{spec.name}_P100_E{E}_new{args.max_new}"
         enable_tuned_gemms(tag, tune=args.tune_gemms)
     weights = random_gemma2(spec, device=dev, dtype=torch.bfloat16, seed=1234, post_norm_gain=args.init_gain)
     model = Gemma2Model(weights, dev)
