@@ -2,7 +2,7 @@
 
   python tools/lab/g4_bench.py check            exactness vs an fp32 torch reference (bf16 / f32 / GeGLU epilogues)
   python tools/lab/g4_bench.py time [shapes]    interleaved rounds in one process: hipBLASLt (torch.matmul, with the
-                                                bench's TunableOp table), gemm_pp (csrc/gemm.hip), gemm4 256 / 128
+                                                bench's TunableOp table), the extension's gemm4 (ext256), the lab build 256 / 128
 Operands are uniform [-1, 1) bf16 (cdna_hip_programming.md §5.4 rule 25); the weight rotates over copies larger than
 the Infinity Cache.
 """
@@ -75,8 +75,8 @@ def check() -> int:
                 ok = ok and eg < 2e-2
             if rows == 256:
                 Cp = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-                _ext.kernels().gemm_pp(A, W, Cp, None, None, 0, 256)
-                rec["bitequal_pp"] = bool(torch.equal(Cp, Cb))
+                _ext.kernels().gemm4(A, W, Cp, None, None, 0, 256)
+                rec["bitequal_ext"] = bool(torch.equal(Cp, Cb))
             rec["ok"] = ok
             bad += not ok
             print(json.dumps(rec), flush=True)
@@ -120,7 +120,7 @@ def time_shapes(shapes, rounds=int(os.environ.get("G4_ROUNDS", "7"))):
         epi = int(os.environ.get("G4_EPI", "0"))      # 3: the fused GeGLU epilogue ([M, N/2] output)
         Cg = torch.empty(M, N // 2, device="cuda", dtype=torch.bfloat16) if epi == 3 else C
         var = {"blas": lambda: torch.matmul(A, nxt().t(), out=C),
-               "pp256": lambda: k.gemm_pp(A, nxt(), Cg, None, None, epi, 256),
+               "ext256": lambda: k.gemm4(A, nxt(), Cg, None, None, epi, 256),
                "g4_256": lambda: g4(A, nxt(), Cg, epi, 256),
                "g4_128": lambda: g4(A, nxt(), Cg, epi, 128)}
         for name, lib in EXTRA.items():      # G4_LIBS: more builds of the kernel, interleaved in this process

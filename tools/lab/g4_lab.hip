@@ -1,6 +1,5 @@
-// ctypes shim over csrc/gemm4.hip for tools/lab/g4_bench.py (in-process A/B against hipBLASLt and gemm_pp)
+// ctypes shim over csrc/gemm4.hip for tools/lab/g4_bench.py (in-process A/B against hipBLASLt and the extension)
 #include "../../taboo_brittleness_amd/csrc/gemm4.hip"
-#include "../../taboo_brittleness_amd/csrc/gemm.hip"   // tb_head_merge
 // the lab never runs the fused head: its softcap-table lookup (csrc/lens.hip) is stubbed
 bool tb_softcap_compact_params(float, const uint16_t**, int*, int*, float*) { return false; }
 extern "C" int g4_gemm(const void* A, const void* W, void* C, int M, int N, int K, int ldc, int epi, int rows,
