@@ -24,11 +24,13 @@ void tb_kv_fanout(uint16_t* kc, uint16_t* vc, const int32_t* src_row, const int3
 // attention.hip
 int tb_attention_lds_bytes(int HD);
 // pkc/pvc/pslot/plen (decode only, T == 1; nullptr = none): row b reads keys [0, plen[b]) from slot
-// pslot[b] of the shared prefix cache (pkc, pvc) [P, Hkv, S, HD] instead of its own slot.
+// pslot[b] of the shared prefix cache (pkc, pvc) [P, Hkv, S, HD] instead of its own slot.  rowmap (decode, S <= 2048,
+// nullptr = identity): a permutation of [0, B) -- workgroup x computes row rowmap[x] (the order only moves work
+// between XCDs: every row's output is the same bits).
 void tb_attention(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, uint16_t* out, const int32_t* pos,
                   const int32_t* slot, int B, int T, int Hq, int Hkv, int HD, int S, float scale, float softcap,
                   int window, hipStream_t st, const uint16_t* pkc = nullptr, const uint16_t* pvc = nullptr,
-                  const int32_t* pslot = nullptr, const int32_t* plen = nullptr);
+                  const int32_t* pslot = nullptr, const int32_t* plen = nullptr, const int32_t* rowmap = nullptr);
 // blk [nblk, bw]: (first row, rows, slot) (bw = 3) or + (prefix slot, prefix length) (bw = 5, keys below the
 // prefix length read from that slot of pkc/pvc).
 void tb_attention_varlen(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, uint16_t* out, const int32_t* pos,
@@ -128,6 +130,10 @@ void tb_capture_rows(uint16_t* store, const uint16_t* h, const int32_t* pos, con
                      int D, hipStream_t st);
 void tb_row_gather(uint16_t* out, const uint16_t* src, const void* idx, bool idx64, int n, int D, hipStream_t st);
 int tb_share_group_max_rows();
+// rowmap[0..nb) = rows 0..nb counting-sorted by prefix slot pslot (rows with len_a == 0 (and len_b == 0 / nullptr)
+// last): the shared-prefix decode attention's launch order (tb_attention rowmap)
+void tb_attn_rowmap(const int32_t* pslot, const int32_t* len_a, const int32_t* len_b, int32_t* rowmap, int nb,
+                    hipStream_t st);
 void tb_share_group(int64_t* gid, const int32_t* tok, int64_t* rep, int64_t* grp, int32_t* src, int64_t* U, int nb,
                     int act, int first, int64_t V, hipStream_t st);
 

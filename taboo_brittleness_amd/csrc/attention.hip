@@ -532,14 +532,16 @@ __global__ void __launch_bounds__(256) attn_decode_wave_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
     uint16_t* __restrict__ out, const int32_t* __restrict__ pos, const int32_t* __restrict__ slot, int Hq, int Hkv,
     int S, float scale, float softcap, int window, const uint16_t* __restrict__ pkc, const uint16_t* __restrict__ pvc,
-    const int32_t* __restrict__ pslot, const int32_t* __restrict__ plen) {
+    const int32_t* __restrict__ pslot, const int32_t* __restrict__ plen, const int32_t* __restrict__ rowmap) {
   constexpr int KS = HD / 32;
   constexpr int DPL = HD / 64;
   constexpr int VCH = VCH_;              // V rows per prefetch chunk
   using VT = typename vrow_t<DPL>::type;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nwh = blockDim.x >> 6;
-  const int b = blockIdx.x, hy = blockIdx.y;
+  // rowmap (optional): workgroup x runs row rowmap[x] -- rows sharing a prefix slot placed on one XCD (attn_row_order)
+  const int b = rowmap != nullptr ? rowmap[blockIdx.x] : (int)blockIdx.x, hy = blockIdx.y;
+  if ((unsigned)b >= gridDim.x) return;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int kh = hy * nwh + w;
   const int grp = lane >> 4, col = lane & 15;
@@ -704,12 +706,12 @@ template <int HD, int G>
 void launch_attn_decode(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, uint16_t* out, const int32_t* pos,
                         const int32_t* slot, int B, int Hq, int Hkv, int S, float scale, float softcap, int window,
                         const uint16_t* pkc, const uint16_t* pvc, const int32_t* pslot, const int32_t* plen,
-                        hipStream_t st) {
+                        hipStream_t st, const int32_t* rowmap) {
   if (S <= 2048) {
     const int nwh = Hkv % 4 == 0 ? 4 : (Hkv % 2 == 0 ? 2 : 1);
     const size_t lds_w = (size_t)nwh * G * ((S + 15) & ~15) * sizeof(float) + (size_t)nwh * G * HD * 2;
     hipLaunchKernelGGL((attn_decode_wave_kernel<HD, G>), dim3(B, Hkv / nwh), dim3(64 * nwh), lds_w, st, q, kc, vc, out,
-                       pos, slot, Hq, Hkv, S, scale, softcap, window, pkc, pvc, pslot, plen);
+                       pos, slot, Hq, Hkv, S, scale, softcap, window, pkc, pvc, pslot, plen, rowmap);
     return;
   }
   const size_t lds = ((size_t)G * ((S + 15) & ~15) + 4 * G * HD + 3 * G + 2) * sizeof(float);
@@ -728,14 +730,14 @@ void launch_attn_decode(const uint16_t* q, const uint16_t* kc, const uint16_t* v
 void tb_attention(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, uint16_t* out, const int32_t* pos,
                   const int32_t* slot, int B, int T, int Hq, int Hkv, int HD, int S, float scale, float softcap,
                   int window, hipStream_t st, const uint16_t* pkc, const uint16_t* pvc, const int32_t* pslot,
-                  const int32_t* plen) {
+                  const int32_t* plen, const int32_t* rowmap) {
   if (B <= 0 || T <= 0) return;
   const int G = Hq / Hkv;
   if (T == 1 && S <= 8192) {
 #define TB_DEC_CASE(hd, g)                                                                                   \
   if (HD == hd && G == g) {                                                                                  \
     launch_attn_decode<hd, g>(q, kc, vc, out, pos, slot, B, Hq, Hkv, S, scale, softcap, window, pkc, pvc,    \
-                              pslot, plen, st);                                                              \
+                              pslot, plen, st, rowmap);                                                      \
     return;                                                                                                  \
   }
     TB_DEC_CASE(256, 2)

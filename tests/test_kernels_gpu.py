@@ -925,6 +925,40 @@ def test_attention_decode_shared_prefix_buckets(gpu, HD):
         _close(og, orf, atol=2e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("nb", [61, 5000])
+def test_attention_decode_rowmap(gpu, nb):
+    """ops.attn_rowmap: a permutation of the rows grouped by prefix slot (rows without a prefix last); decode
+    attention launched in that order is BIT-identical per row to the identity order (incl. a padding row and a
+    sliding window)."""
+    torch.manual_seed(17)
+    Hkv, G, HD, S, P = 8, 2, 256, 72, 40
+    d = lambda t: t.to(gpu)                               # noqa: E731
+    slot = torch.randperm(nb).to(torch.int32)
+    pos = torch.randint(10, S, (nb,), dtype=torch.int32)
+    ps = torch.randint(0, P, (nb,), dtype=torch.int32)
+    pl = torch.minimum(torch.randint(0, 50, (nb,), dtype=torch.int32), pos)
+    pos[7] = -1
+    rm = ops.attn_rowmap(d(ps), d(pl), None, nb).cpu()
+    assert torch.equal(torch.sort(rm.long())[0], torch.arange(nb))
+    key = torch.where(pl > 0, ps, torch.full_like(ps, 10 ** 6))[rm.long()]
+    assert bool((key[1:] >= key[:-1]).all())              # grouped by slot, no-prefix rows last
+    assert torch.equal(ops.attn_rowmap(ps, pl, None, nb), torch.argsort(
+        torch.where(pl > 0, ps, torch.full_like(ps, 2047)).long(), stable=True).to(torch.int32))   # CPU version
+    if nb > 100:
+        return
+    kc = d(torch.randn(nb, Hkv, S, HD, dtype=BF))
+    vc = d(torch.randn(nb, Hkv, S, HD, dtype=BF))
+    pk = d(torch.randn(P, Hkv, S, HD, dtype=BF))
+    pv = d(torch.randn(P, Hkv, S, HD, dtype=BF))
+    q = d(torch.randn(nb, Hkv * G, HD, dtype=BF) * 2)
+    for window in (0, 24):
+        base = ops.attention(q, kc, vc, d(pos), d(slot), nb, 1, HD ** -0.5, 50.0, window,
+                             prefix=(pk, pv, d(ps), d(pl)))
+        og = ops.attention(q, kc, vc, d(pos), d(slot), nb, 1, HD ** -0.5, 50.0, window,
+                           prefix=(pk, pv, d(ps), d(pl), d(rm)))
+        assert torch.equal(og, base)
+
+
 @pytest.mark.parametrize("bf16_rows", [True, False])
 def test_sae_fp32_encode_firing_set(gpu, bf16_rows):
     """fp32 SAE parity (reference encodes the fp32 residual with fp32 Gemma Scope weights,
