@@ -276,6 +276,8 @@ def run_forcing_settings(cfg: Config, model, tok, settings: Sequence[Dict], mode
                 o = gen.generate_shared(chunk, cs, max_new, hooks=hooks, graph_key=gk)
             else:
                 o = gen.generate(chunk, max_new, hooks=hooks, graph_key=gk)
+                for k_, v_ in getattr(gen, "last_phases", {}).items():
+                    clk["gen_" + k_] = clk.get("gen_" + k_, 0.0) + v_
             out += [o.response_ids(i) for i in range(len(chunk))]
         return out
 

@@ -37,6 +37,8 @@ from __future__ import annotations
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
 
+import time
+
 import numpy as np
 import torch
 
@@ -562,10 +564,14 @@ class Generator:
         assert 0 < n <= self.B, f"{n} prompts for batch {self.B}"
         plen = [len(p) for p in prompts]
         assert max(plen) + max_new_tokens <= self.S, f"need S >= {max(plen) + max_new_tokens}, have {self.S}"
+        t0 = time.perf_counter()
         first = self.prefill(prompts, list(range(n)), hooks, teacher)
-        self.decode(first, plen, [[int(t)] for t in first.tolist()], max_new_tokens, n, hooks, graph_key,
-                    teacher=teacher)
-        return self.collect(n, max_new_tokens, plen)
+        f0 = [[int(t)] for t in first.tolist()]
+        t1 = time.perf_counter()
+        self.decode(first, plen, f0, max_new_tokens, n, hooks, graph_key, teacher=teacher)
+        out = self.collect(n, max_new_tokens, plen)
+        self.last_phases = {"prefill": t1 - t0, "decode": time.perf_counter() - t1}
+        return out
 
     def invalidate_graph(self) -> None:
         self._graphs.clear()
