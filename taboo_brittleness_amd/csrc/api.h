@@ -23,6 +23,9 @@ void tb_kv_fanout(uint16_t* kc, uint16_t* vc, const int32_t* src_row, const int3
                   int nlayers, int slots, int Hkv, int S, int HD, hipStream_t st);
 // attention.hip
 int tb_attention_lds_bytes(int HD);
+// decode row count at or below which the 4-wave-per-(row, kv head) decode kernel runs (bit-identical to the one-wave
+// kernel), for rows without / with a shared prefix; n < 0: query only; returns the previous value
+int tb_attention_split_rows(int n, bool prefix);
 // pkc/pvc/pslot/plen (decode only, T == 1; nullptr = none): row b reads keys [0, plen[b]) from slot
 // pslot[b] of the shared prefix cache (pkc, pvc) [P, Hkv, S, HD] instead of its own slot.  rowmap (decode, S <= 2048,
 // nullptr = identity): a permutation of [0, B) -- workgroup x computes row rowmap[x] (the order only moves work

@@ -701,12 +701,178 @@ __global__ void __launch_bounds__(256) attn_decode_wave_kernel(
 }
 
 
+// Decode, one 4-wave workgroup per (row, kv head): attn_decode_wave_kernel's arithmetic spread over 4 waves, for the
+// small decode buckets (<= 64 rows: 2 or fewer waves per SIMD in the wave kernel, each walking its keys alone).
+// Bit-identical to the wave kernel per row (so switching kernels by row count keeps the decode batch-invariant):
+// the 16-key score tiles are strided over the waves (one MFMA per tile, the same operands);
+// the max is exact in any order; each wave forms the weights p = rbf(exp(s - m)) of a quarter of the keys, and every
+// wave then sums them in the wave kernel's lane-strided order + butterfly; the P V chain of each output dim runs over
+// the keys in ascending order in one lane, the waves taking (head, dim range) slices instead of the wave kernel's
+// whole rows (tests/test_kernels_gpu.py::test_attention_decode_split_bitequal).
+template <int HD, int G>
+__global__ void __launch_bounds__(256) attn_decode_split_kernel(
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
+    uint16_t* __restrict__ out, const int32_t* __restrict__ pos, const int32_t* __restrict__ slot, int Hq, int Hkv,
+    int S, float scale, float softcap, int window, const uint16_t* __restrict__ pkc, const uint16_t* __restrict__ pvc,
+    const int32_t* __restrict__ pslot, const int32_t* __restrict__ plen, const int32_t* __restrict__ rowmap) {
+  constexpr int KS = HD / 32;
+  constexpr int PARTS = 4 / G;                 // waves per head in the P V phase
+  constexpr int DPW = HD / PARTS / 64;         // output dims per lane
+  constexpr int VCH = 8;
+  static_assert(PARTS * G == 4 && (DPW == 2 || DPW == 4), "geometry");
+  using VT = typename vrow_t<DPW>::type;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int b = rowmap != nullptr ? rowmap[blockIdx.x] : (int)blockIdx.x, kh = blockIdx.y;
+  if ((unsigned)b >= gridDim.x) return;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int grp = lane >> 4, col = lane & 15;
+  const int SS = (S + 15) & ~15;
+  float* sc = reinterpret_cast<float*>(smem);                                   // [G][SS] scores, then weights
+  uint16_t* ql = reinterpret_cast<uint16_t*>(sc + (size_t)G * SS);               // [G][HD] query rows
+  uint16_t* ob = out + ((size_t)b * Hq + kh * G) * HD;
+  const int p = pos[b];
+  if (p < 0) {   // padding row
+    for (int e = threadIdx.x; e < G * HD; e += 256) ob[e] = 0;
+    return;
+  }
+  const int kmax = p < S ? p : S - 1;
+  int kmin = 0;
+  if (window > 0) { kmin = p - window + 1; if (kmin < 0) kmin = 0; }
+  const int cs = slot[b];
+  const uint16_t* kbase = kc + ((size_t)cs * Hkv + kh) * (size_t)S * HD;
+  const uint16_t* vbase = vc + ((size_t)cs * Hkv + kh) * (size_t)S * HD;
+  int np = 0;
+  const uint16_t* kpre = kbase;
+  const uint16_t* vpre = vbase;
+  if (plen != nullptr) {
+    np = plen[b];
+    if (np > 0) {
+      const size_t po = ((size_t)pslot[b] * Hkv + kh) * (size_t)S * HD;
+      kpre = pkc + po;
+      vpre = pvc + po;
+    }
+  }
+  // this wave's P V slice: head h, dims d0 .. d0 + DPW of each V row; its first V chunk goes out first
+  const int h = w / PARTS, d0 = (w % PARTS) * (HD / PARTS) + lane * DPW;
+  auto vload = [&](int j, VT (&v)[VCH]) {
+#pragma unroll
+    for (int u = 0; u < VCH; ++u) {
+      const int jj = j + u <= kmax ? j + u : kmax;
+      v[u] = *reinterpret_cast<const VT*>((jj < np ? vpre : vbase) + (size_t)jj * HD + d0);
+    }
+  };
+  VT va[VCH], vb[VCH];
+  vload(kmin, va);
+  {
+    const uint16_t* qrow = q + ((size_t)b * Hq + kh * G) * HD;
+    for (int e = threadIdx.x; e < G * HD / 8; e += 256)
+      *reinterpret_cast<uint4*>(ql + e * 8) = *reinterpret_cast<const uint4*>(qrow + e * 8);
+  }
+  __syncthreads();
+  const float inv_cap = softcap > 0.f ? 1.f / softcap : 0.f;
+  const uint16_t* qlr = ql + (col % G) * HD + grp * 8;
+  const int t0 = kmin >> 4, t1 = kmax >> 4;
+  for (int t = t0 + w; t <= t1; t += 4) {
+    uint4 kf[KS];
+    const int kk = t * 16 + col;
+    const int kr = kk < kmin ? kmin : (kk > kmax ? kmax : kk);
+    const uint16_t* krow = (kr < np ? kpre : kbase) + (size_t)kr * HD + grp * 8;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) kf[ks] = *reinterpret_cast<const uint4*>(krow + ks * 32);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(*reinterpret_cast<const uint4*>(qlr + ks * 32)),
+                                                    as_bf16x8(kf[ks]), acc, 0, 0, 0);
+    if (grp == 0) {
+#pragma unroll
+      for (int hh = 0; hh < G; ++hh) {
+        float s = acc[hh] * scale;
+        if (softcap > 0.f) s = tanhf(s * inv_cap) * softcap;
+        sc[hh * SS + kk] = (kk >= kmin && kk <= kmax) ? s : -INFINITY;
+      }
+    }
+  }
+  __syncthreads();
+  // row max (exact in any order; every wave for itself), then this wave's quarter of the weights
+  float m[G];
+#pragma unroll
+  for (int hh = 0; hh < G; ++hh) {
+    const float* sh = sc + hh * SS;
+    float mm = -INFINITY;
+    for (int j = kmin + lane; j <= kmax; j += 64) mm = fmaxf(mm, sh[j]);
+    m[hh] = wave_max(mm);
+  }
+  __syncthreads();   // every wave has read the scores it needs for its max
+#pragma unroll
+  for (int hh = 0; hh < G; ++hh) {
+    float* sh = sc + hh * SS;
+    for (int j = kmin + lane + 64 * w; j <= kmax; j += 256)
+      sh[j] = m[hh] > -INFINITY ? rbf(__expf(sh[j] - m[hh])) : 0.f;
+  }
+  __syncthreads();
+  // l in the wave kernel's order: lane-strided ascending partial sums, then the butterfly
+  float inv_l;
+  {
+    const float* sh = sc + h * SS;
+    float l = 0.f;
+    for (int j = kmin + lane; j <= kmax; j += 64) l += sh[j];
+    l = wave_sum(l);
+    inv_l = l > 0.f ? 1.f / l : 0.f;
+  }
+  float o[DPW];
+#pragma unroll
+  for (int d = 0; d < DPW; ++d) o[d] = 0.f;
+  const float* ph = sc + h * SS;
+  auto accum = [&](int j, const VT (&v)[VCH]) {
+#pragma unroll
+    for (int u = 0; u < VCH; ++u) {
+      if (j + u > kmax) break;
+      float vf[DPW];
+      vrow_t<DPW>::unpack(v[u], vf);
+      const float pw = ph[j + u];
+#pragma unroll
+      for (int d = 0; d < DPW; ++d) o[d] += pw * vf[d];
+    }
+  };
+  for (int j = kmin; j <= kmax; j += 2 * VCH) {
+    if (j + VCH <= kmax) vload(j + VCH, vb);
+    accum(j, va);
+    if (j + VCH <= kmax) {
+      if (j + 2 * VCH <= kmax) vload(j + 2 * VCH, va);
+      accum(j + VCH, vb);
+    }
+  }
+  float r[DPW];
+#pragma unroll
+  for (int d = 0; d < DPW; ++d) r[d] = o[d] * inv_l;
+  uint16_t* dst = ob + h * HD + d0;
+  if constexpr (DPW == 4) {
+    *reinterpret_cast<uint2*>(dst) = make_uint2(pack2(r[0], r[1]), pack2(r[2], r[3]));
+  } else {
+    *reinterpret_cast<uint32_t*>(dst) = pack2(r[0], r[1]);
+  }
+}
+
+// rows at or below which the decode (S <= 2048, HD 256, G 2 / 4) runs attn_decode_split_kernel (same bits), for rows
+// with their own keys only / rows reading a shared prefix: at 64 rows 15-18 % faster than the one-wave kernel (too
+// few waves to cover its latency), from 128 rows on 3-20 % slower (profiles/r5/attn/attn_bench_split_own.log,
+// attn_bench_split_sweep.log)
+int g_attn_split_rows[2] = {64, 64};
 
 template <int HD, int G>
 void launch_attn_decode(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, uint16_t* out, const int32_t* pos,
                         const int32_t* slot, int B, int Hq, int Hkv, int S, float scale, float softcap, int window,
                         const uint16_t* pkc, const uint16_t* pvc, const int32_t* pslot, const int32_t* plen,
                         hipStream_t st, const int32_t* rowmap) {
+  if constexpr (HD == 256 && (G == 2 || G == 4)) {
+    if (S <= 2048 && B <= g_attn_split_rows[pkc != nullptr ? 1 : 0]) {
+      const size_t lds_s = (size_t)G * ((S + 15) & ~15) * sizeof(float) + (size_t)G * HD * 2;
+      hipLaunchKernelGGL((attn_decode_split_kernel<HD, G>), dim3(B, Hkv), dim3(256), lds_s, st, q, kc, vc, out, pos,
+                         slot, Hq, Hkv, S, scale, softcap, window, pkc, pvc, pslot, plen, rowmap);
+      return;
+    }
+  }
   if (S <= 2048) {
     const int nwh = Hkv % 4 == 0 ? 4 : (Hkv % 2 == 0 ? 2 : 1);
     const size_t lds_w = (size_t)nwh * G * ((S + 15) & ~15) * sizeof(float) + (size_t)nwh * G * HD * 2;
@@ -726,6 +892,12 @@ void launch_attn_decode(const uint16_t* q, const uint16_t* kc, const uint16_t* v
 }
 
 }  // namespace
+
+int tb_attention_split_rows(int n, bool prefix) {
+  const int old = g_attn_split_rows[prefix ? 1 : 0];
+  if (n >= 0) g_attn_split_rows[prefix ? 1 : 0] = n;
+  return old;
+}
 
 void tb_attention(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, uint16_t* out, const int32_t* pos,
                   const int32_t* slot, int B, int T, int Hq, int Hkv, int HD, int S, float scale, float softcap,

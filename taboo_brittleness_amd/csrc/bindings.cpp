@@ -921,6 +921,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("share_group", &share_group);
   m.def("share_group_max_rows", &share_group_max_rows);
   m.def("attn_rowmap", &attn_rowmap);
+  m.def("attention_split_rows", [](int64_t n, bool prefix) { return (int64_t)tb_attention_split_rows((int)n, prefix); });
   m.def("attention", &attention);
   m.def("attention_prefix", &attention_prefix);
   m.def("attention_varlen", &attention_varlen);

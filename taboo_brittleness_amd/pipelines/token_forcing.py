@@ -95,6 +95,9 @@ LAST_TIMINGS: Dict[str, float] = {}     # wall seconds of the last run_forcing_s
 # decode steps replayed from a hipGraph captured per generation call (the forcing decode runs at a few hundred
 # rows, where launching ~500 kernels per step costs about as much as the step's GPU work)
 GRAPHS = True
+# a warm-up turn re-prefills only what follows its longest common token prefix with the previous turn's prompt, whose
+# K/V (prefilled under the same edit) is still in the row's cache slot
+RESUME_TURNS = True
 
 
 @torch.no_grad()
@@ -209,6 +212,14 @@ class _ForcingHooks:
         return True
 
 
+def _lcp(a: Sequence[int], b: Sequence[int]) -> int:
+    n = min(len(a), len(b))
+    i = 0
+    while i < n and a[i] == b[i]:
+        i += 1
+    return i
+
+
 # generator + persistent edit hooks of the last forcing run, per model: reused by the next call (the bench's timed
 # call after its warm call) while the rows fit -- no new KV cache and no graph captures per generate() call
 _FORCING_STATE: Dict[int, Dict] = {}
@@ -268,6 +279,11 @@ def run_forcing_settings(cfg: Config, model, tok, settings: Sequence[Dict], mode
         S = -(-(max(len(r) for r in rows) + max_new + 1) // 64) * 64
         ent = _forcing_state(model, R, S, settings, layer, sae)
         gen, fh = ent["gen"], ent["hooks"]
+        # the previous single-chunk call's prompts, still in the cache slots under the same edits (the warm-up turn
+        # before this one): each row's new prompt re-prefills only what follows its longest common token prefix
+        # with the old one (the chat history grows by the reply and the next user turn)
+        prev = ent.pop("prev", None)
+        single = len(rows) <= chunk_rows
         for c0 in range(0, len(rows), chunk_rows):
             chunk, cs = rows[c0:c0 + chunk_rows], row_setting[c0:c0 + chunk_rows]
             edited = fh.fill(settings, cs)
@@ -275,7 +291,14 @@ def run_forcing_settings(cfg: Config, model, tok, settings: Sequence[Dict], mode
             if share and SHARE_PREFIX:                   # a setting's answers share its chat history
                 o = gen.generate_shared(chunk, cs, max_new, hooks=hooks, graph_key=gk)
             else:
-                o = gen.generate(chunk, max_new, hooks=hooks, graph_key=gk)
+                keep = None
+                if (RESUME_TURNS and single and prev is not None and prev["fh"] is fh and prev["gen"] is gen
+                        and prev["cs"] == list(cs) and prev["edited"] == edited):
+                    keep = [_lcp(a_, b_) for a_, b_ in zip(chunk, prev["rows"])]
+                o = gen.generate(chunk, max_new, hooks=hooks, graph_key=gk, keep=keep)
+                if single:
+                    ent["prev"] = {"rows": [list(r) for r in chunk], "cs": list(cs), "fh": fh, "gen": gen,
+                                   "edited": edited}
                 for k_, v_ in getattr(gen, "last_phases", {}).items():
                     clk["gen_" + k_] = clk.get("gen_" + k_, 0.0) + v_
             out += [o.response_ids(i) for i in range(len(chunk))]

@@ -550,22 +550,41 @@ class Generator:
                           torch.tensor(e_pos, dtype=torch.int32, device=self.dev), int(c.k.shape[0]))
         first = self.prefill([list(p[share[i]:]) for i, p in enumerate(prompts)], list(range(n)), hooks,
                              starts=share)
-        self.decode(first, plen, [[int(t)] for t in first.tolist()], max_new_tokens, n, hooks, graph_key)
+        prefix_rows = None
+        if reps and self.dev.type == "cuda" and (self.kv_prefix is None or self.kv_prefix.k is self.cache.k):
+            # the decode reads each group's prefix keys from its first row's slot (the same bits as the member's
+            # copy): the rows of a group then share those K/V reads through L2 instead of streaming one copy each
+            if self.kv_prefix is None:
+                self.enable_kv_prefix(self.cache.k, self.cache.v, int(self.cache.k.shape[0]))
+            src = [0] * n
+            for rows, lcp in fan:
+                for r in rows:
+                    src[r] = rows[0]
+            prefix_rows = (src, share, share)
+        self.decode(first, plen, [[int(t)] for t in first.tolist()], max_new_tokens, n, hooks, graph_key,
+                    prefix_rows=prefix_rows)
         return self.collect(n, max_new_tokens, plen)
 
     @torch.no_grad()
     def generate(self, prompts: Sequence[Sequence[int]], max_new_tokens: int,
                  hooks: Optional[Dict[int, list]] = None, graph_key=None,
-                 teacher: Optional[Sequence[Sequence[int]]] = None) -> GenerationOutput:
+                 teacher: Optional[Sequence[Sequence[int]]] = None,
+                 keep: Optional[Sequence[int]] = None) -> GenerationOutput:
         """Greedy-decode ``prompts`` from scratch (len <= batch).  ``graph_key`` identifies a hook set
         whose captured graph may be replayed (hooks must keep the same tensors across calls);
-        ``teacher``: see :meth:`decode`."""
+        ``teacher``: see :meth:`decode`.  ``keep[b]``: the first ``keep[b]`` tokens of ``prompts[b]`` are already
+        in slot ``b``'s cache (prefilled there earlier under the same hooks, e.g. the previous chat turn's prompt):
+        only the rest is prefilled, at its positions (the suffix prefill of :meth:`generate_shared`)."""
         n = len(prompts)
         assert 0 < n <= self.B, f"{n} prompts for batch {self.B}"
         plen = [len(p) for p in prompts]
         assert max(plen) + max_new_tokens <= self.S, f"need S >= {max(plen) + max_new_tokens}, have {self.S}"
         t0 = time.perf_counter()
-        first = self.prefill(prompts, list(range(n)), hooks, teacher)
+        if keep is not None and any(keep):
+            kp = [min(max(int(k), 0), len(p) - 1) for k, p in zip(keep, prompts)]
+            first = self.prefill([list(p[k:]) for p, k in zip(prompts, kp)], list(range(n)), hooks, teacher, starts=kp)
+        else:
+            first = self.prefill(prompts, list(range(n)), hooks, teacher)
         f0 = [[int(t)] for t in first.tolist()]
         t1 = time.perf_counter()
         self.decode(first, plen, f0, max_new_tokens, n, hooks, graph_key, teacher=teacher)

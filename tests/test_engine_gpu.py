@@ -104,6 +104,58 @@ def test_sweep_gpu_prefix_share_equivalence(gpu, tb_gemm):
     _assert_records_equal(out[False], out[True], float_rtol=1e-6)
 
 
+def test_generate_resume_bitwise(gpu, tb_gemm):
+    """A chat turn prefilled as a suffix behind the previous turn's cached prompt K/V (Generator.generate
+    ``keep``, the token-forcing warm-up turns) gives BIT-identical tokens and NLLs to prefilling the whole new prompt
+    (tb GEMMs: row results independent of the batch; prefill attention: a query row's output independent of the
+    rows after it)."""
+    _, mg = _models(gpu)
+    g = torch.Generator().manual_seed(5)
+    p1 = [[2] + torch.randint(3, SPEC.vocab_size, (n,), generator=g).tolist() for n in (21, 34, 9, 27, 40)]
+    S = 128
+    a = Generator(mg, len(p1), S, use_graphs=True, stop_ids=(100_000,))
+    o1 = a.generate(p1, 8, graph_key="t")
+    p2 = [p + o1.response_ids(i)[:-1] + torch.randint(3, SPEC.vocab_size, (5 + i,), generator=g).tolist()
+          for i, p in enumerate(p1)]
+    p2[2] = p2[2][:4] + [7] + p2[2][5:]                  # a row whose prompt changes inside the old prefix
+    from taboo_brittleness_amd.pipelines.token_forcing import _lcp
+
+    keep = [_lcp(x, y) for x, y in zip(p2, p1)]
+    assert keep[2] == 4 and keep[0] == len(p1[0])
+    r = a.generate(p2, 8, graph_key="t", keep=keep)
+    f = Generator(mg, len(p1), S, use_graphs=True, stop_ids=(100_000,)).generate(p2, 8, graph_key="t")
+    for i in range(len(p2)):
+        assert r.response_ids(i) == f.response_ids(i)
+    assert torch.equal(r.tok_nll[:, :8], f.tok_nll[:, :8])
+
+
+def test_generate_shared_bitwise(gpu, tb_gemm):
+    """Generator.generate_shared on the GPU (each group's common prefix prefilled once, its K/V copied for the
+    members' suffix prefill, the decode reading the prefix from the group's first slot through the shared-prefix
+    attention) gives BIT-identical tokens and NLLs to generate() prefilling every prompt whole."""
+    _, mg = _models(gpu)
+    g = torch.Generator().manual_seed(6)
+    hist = [[2] + torch.randint(3, SPEC.vocab_size, (n,), generator=g).tolist() for n in (40, 25)]
+    prompts, groups = [], []
+    for gi, h in enumerate(hist):
+        for k in range(5):
+            prompts.append(h + torch.randint(3, SPEC.vocab_size, (3 + k,), generator=g).tolist())
+            groups.append(gi)
+    prompts.append([2] + torch.randint(3, SPEC.vocab_size, (12,), generator=g).tolist())
+    groups.append(9)
+    S = 96
+    a = Generator(mg, len(prompts), S, use_graphs=True, stop_ids=(100_000,)).generate(prompts, 10, graph_key="s")
+    gb = Generator(mg, len(prompts), S, use_graphs=True, stop_ids=(100_000,))
+    for _ in range(2):                                   # capture, then replay
+        b = gb.generate_shared(prompts, groups, 10, graph_key="s")
+        for i in range(len(prompts)):
+            assert a.response_ids(i) == b.response_ids(i)
+        assert torch.equal(a.tok_nll[:, :10], b.tok_nll[:, :10])
+    assert gb.kv_prefix is not None and gb.kv_prefix.k is gb.cache.k
+    c = gb.generate(prompts, 10, graph_key="s")           # plain generate after it: prefix lengths reset
+    assert [c.response_ids(i) for i in range(len(prompts))] == [a.response_ids(i) for i in range(len(prompts))]
+
+
 def test_sae_encode_matches_fp32(gpu):
     from taboo_brittleness_amd.interp.sae import JumpReLUSAE
 

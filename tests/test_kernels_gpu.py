@@ -925,6 +925,45 @@ def test_attention_decode_shared_prefix_buckets(gpu, HD):
         _close(og, orf, atol=2e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("G,S", [(2, 96), (2, 700), (4, 300)])
+def test_attention_decode_split_bitequal(gpu, G, S):
+    """The 4-wave-per-(row, kv head) decode kernel (few rows) is BIT-identical to the one-wave kernel per row: own
+    keys, shared-prefix keys, a padding row, a sliding window, with and without a rowmap -- so the row count that
+    picks between them never changes a result."""
+    torch.manual_seed(19)
+    Hkv, HD, B, P = 4, 256, 37, 5
+    d = lambda t: t.to(gpu)                               # noqa: E731
+    kc = d(torch.randn(B, Hkv, S, HD, dtype=BF))
+    vc = d(torch.randn(B, Hkv, S, HD, dtype=BF))
+    pk = d(torch.randn(P, Hkv, S, HD, dtype=BF))
+    pv = d(torch.randn(P, Hkv, S, HD, dtype=BF))
+    q = d(torch.randn(B, Hkv * G, HD, dtype=BF) * 2)
+    slot = torch.randperm(B).to(torch.int32)
+    pos = torch.randint(0, S + 8, (B,), dtype=torch.int32)   # incl. positions past the cache (clamped keys)
+    pos[3] = -1
+    ps = torch.randint(0, P, (B,), dtype=torch.int32)
+    pl = torch.minimum(torch.randint(0, S, (B,), dtype=torch.int32), pos.clamp(min=0))
+    rm = ops.attn_rowmap(d(ps), d(pl), None, B)
+    k = ops._k()
+    old = (k.attention_split_rows(-1, False), k.attention_split_rows(-1, True))
+    try:
+        for window, pre in ((0, False), (24, False), (0, True), (40, True)):
+            args = (q, kc, vc, d(pos), d(slot), B, 1, HD ** -0.5, 50.0, window)
+            outs = []
+            for split in (0, 1 << 20):
+                k.attention_split_rows(split, pre)
+                if pre:
+                    outs.append(ops.attention(*args, prefix=(pk, pv, d(ps), d(pl))))
+                    outs.append(ops.attention(*args, prefix=(pk, pv, d(ps), d(pl), rm)))
+                else:
+                    outs.append(ops.attention(*args))
+            for o in outs[1:]:
+                assert torch.equal(o, outs[0]), (window, pre, (o.float() - outs[0].float()).abs().max().item())
+    finally:
+        k.attention_split_rows(old[0], False)
+        k.attention_split_rows(old[1], True)
+
+
 @pytest.mark.parametrize("nb", [61, 5000])
 def test_attention_decode_rowmap(gpu, nb):
     """ops.attn_rowmap: a permutation of the rows grouped by prefix slot (rows without a prefix last); decode

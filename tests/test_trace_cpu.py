@@ -86,6 +86,11 @@ def test_forcing_shared_prefix_matches_full_prefill(monkeypatch):
         monkeypatch.setattr(TF, "SHARE_PREFIX", share)
         got[share] = TF.run_forcing_settings(cfg, m, tok, settings, "postgame", sae, 1, chunk_rows=16)
     assert got[False] == got[True]
+    # warm-up turns resumed behind the previous turn's cached prompt K/V (RESUME_TURNS) == each turn prefilled whole
+    monkeypatch.setattr(TF, "RESUME_TURNS", False)
+    whole = TF.run_forcing_settings(cfg, m, tok, settings, "postgame", sae, 1, chunk_rows=16)
+    monkeypatch.setattr(TF, "RESUME_TURNS", True)
+    assert whole == got[True]
     comps = {}
     for share in (False, True):
         monkeypatch.setattr(TF, "SHARE_PREFIX", share)

@@ -31,6 +31,9 @@ def main():
     ap.add_argument("--prompt", type=int, default=17)
     ap.add_argument("--gen", type=int, default=50)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--own", action="store_true",
+                    help="rows with their own keys only (no shared prefix: the token-forcing decode): one-wave vs "
+                         "4-wave kernel")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     Hq, Hkv, HD, S = 16, 8, 256, args.S
@@ -79,6 +82,14 @@ def main():
         variants["map_sorted"]()
         torch.cuda.synchronize()
         biteq = bool(torch.equal(out, out_x))
+        kx = ops._k()
+        old_split = (kx.attention_split_rows(0, False), kx.attention_split_rows(0, True))
+        if args.own:
+            def _plain(n):
+                kx.attention_split_rows(n, False)
+                ops.attention(q, kc, vc, pos_d, slot, M, 1, HD ** -0.5, 50.0, 0, out=out)
+                kx.attention_split_rows(0, False)
+            variants = {"wave": lambda: _plain(0), "split": lambda: _plain(1 << 20)}
         res = {}
         for name, f in variants.items():
             for _ in range(3):
@@ -91,7 +102,18 @@ def main():
             b.record()
             torch.cuda.synchronize()
             res[name] = a.elapsed_time(b) / args.reps * 1e3
+        kx.attention_split_rows(old_split[0], False)
+        kx.attention_split_rows(old_split[1], True)
         us = res["wave"]
+        if args.own:
+            own_b = float((pos + 1).sum()) * Hkv * HD * 2 * 2
+            print(json.dumps({"rows": M, "own_keys": True, "wave_us": round(us, 1), "split_us": round(res["split"], 1),
+                              "mean_keys": round(float(pos.float().mean()) + 1, 1),
+                              "wave_TBps": round(own_b / us / 1e6, 2),
+                              "split_TBps": round(own_b / res["split"] / 1e6, 2)}), flush=True)
+            del kc, vc, pk, pv, q, out
+            torch.cuda.empty_cache()
+            continue
         row_b = Hkv * HD * 2 * 2                                           # K + V bytes per key, all kv heads
         streamed = float((pos + 1).sum()) * row_b
         pref = {}
