@@ -27,13 +27,11 @@ int tb_attention_lds_bytes(int HD);
 // kernel), for rows without / with a shared prefix; n < 0: query only; returns the previous value
 int tb_attention_split_rows(int n, bool prefix);
 // pkc/pvc/pslot/plen (decode only, T == 1; nullptr = none): row b reads keys [0, plen[b]) from slot
-// pslot[b] of the shared prefix cache (pkc, pvc) [P, Hkv, S, HD] instead of its own slot.  rowmap (decode, S <= 2048,
-// nullptr = identity): a permutation of [0, B) -- workgroup x computes row rowmap[x] (the order only moves work
-// between XCDs: every row's output is the same bits).
+// pslot[b] of the shared prefix cache (pkc, pvc) [P, Hkv, S, HD] instead of its own slot.
 void tb_attention(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, uint16_t* out, const int32_t* pos,
                   const int32_t* slot, int B, int T, int Hq, int Hkv, int HD, int S, float scale, float softcap,
                   int window, hipStream_t st, const uint16_t* pkc = nullptr, const uint16_t* pvc = nullptr,
-                  const int32_t* pslot = nullptr, const int32_t* plen = nullptr, const int32_t* rowmap = nullptr);
+                  const int32_t* pslot = nullptr, const int32_t* plen = nullptr);
 // blk [nblk, bw]: (first row, rows, slot) (bw = 3) or + (prefix slot, prefix length) (bw = 5, keys below the
 // prefix length read from that slot of pkc/pvc).
 void tb_attention_varlen(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, uint16_t* out, const int32_t* pos,
@@ -50,7 +48,10 @@ void tb_gather_probs(const uint16_t* logits, const float* lse, const int32_t* id
 void tb_lens_colsum(const uint16_t* logits, const float* lse, const uint8_t* mask, const int32_t* excl, float* acc,
                     int B, int T, int V, int accumulate, int round_bf16, const int32_t* offs, float* cum,
                     const int32_t* rowmap, hipStream_t st);
-void tb_topk_rows(const float* x, float* vals, int32_t* idx, int R, int V, int K, hipStream_t st);
+// (chunked when C > 1: workspaces wv / wi of R * C * K entries; C from tb_topk_chunks)
+int tb_topk_chunks(int R, int V);
+void tb_topk_rows(const float* x, float* vals, int32_t* idx, int R, int V, int K, float* wv, int32_t* wi, int C,
+                  hipStream_t st);
 void tb_xent_rows(const uint16_t* logits, const int32_t* tgt, float* nll, int R, int V, float cap, int emulate_bf16,
                   hipStream_t st);
 void tb_register_softcap_table(float cap, const uint16_t* tab);   // [32768] bf16 softcap of +bf16 bit patterns
@@ -133,10 +134,6 @@ void tb_capture_rows(uint16_t* store, const uint16_t* h, const int32_t* pos, con
                      int D, hipStream_t st);
 void tb_row_gather(uint16_t* out, const uint16_t* src, const void* idx, bool idx64, int n, int D, hipStream_t st);
 int tb_share_group_max_rows();
-// rowmap[0..nb) = rows 0..nb counting-sorted by prefix slot pslot (rows with len_a == 0 (and len_b == 0 / nullptr)
-// last): the shared-prefix decode attention's launch order (tb_attention rowmap)
-void tb_attn_rowmap(const int32_t* pslot, const int32_t* len_a, const int32_t* len_b, int32_t* rowmap, int nb,
-                    hipStream_t st);
 void tb_share_group(int64_t* gid, const int32_t* tok, int64_t* rep, int64_t* grp, int32_t* src, int64_t* U, int nb,
                     int act, int first, int64_t V, hipStream_t st);
 

@@ -532,16 +532,14 @@ __global__ void __launch_bounds__(256) attn_decode_wave_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
     uint16_t* __restrict__ out, const int32_t* __restrict__ pos, const int32_t* __restrict__ slot, int Hq, int Hkv,
     int S, float scale, float softcap, int window, const uint16_t* __restrict__ pkc, const uint16_t* __restrict__ pvc,
-    const int32_t* __restrict__ pslot, const int32_t* __restrict__ plen, const int32_t* __restrict__ rowmap) {
+    const int32_t* __restrict__ pslot, const int32_t* __restrict__ plen) {
   constexpr int KS = HD / 32;
   constexpr int DPL = HD / 64;
   constexpr int VCH = VCH_;              // V rows per prefetch chunk
   using VT = typename vrow_t<DPL>::type;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nwh = blockDim.x >> 6;
-  // rowmap (optional): workgroup x runs row rowmap[x] -- rows sharing a prefix slot placed on one XCD (attn_row_order)
-  const int b = rowmap != nullptr ? rowmap[blockIdx.x] : (int)blockIdx.x, hy = blockIdx.y;
-  if ((unsigned)b >= gridDim.x) return;
+  const int b = blockIdx.x, hy = blockIdx.y;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int kh = hy * nwh + w;
   const int grp = lane >> 4, col = lane & 15;
@@ -714,7 +712,7 @@ __global__ void __launch_bounds__(256) attn_decode_split_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
     uint16_t* __restrict__ out, const int32_t* __restrict__ pos, const int32_t* __restrict__ slot, int Hq, int Hkv,
     int S, float scale, float softcap, int window, const uint16_t* __restrict__ pkc, const uint16_t* __restrict__ pvc,
-    const int32_t* __restrict__ pslot, const int32_t* __restrict__ plen, const int32_t* __restrict__ rowmap) {
+    const int32_t* __restrict__ pslot, const int32_t* __restrict__ plen) {
   constexpr int KS = HD / 32;
   constexpr int PARTS = 4 / G;                 // waves per head in the P V phase
   constexpr int DPW = HD / PARTS / 64;         // output dims per lane
@@ -722,8 +720,7 @@ __global__ void __launch_bounds__(256) attn_decode_split_kernel(
   static_assert(PARTS * G == 4 && (DPW == 2 || DPW == 4), "geometry");
   using VT = typename vrow_t<DPW>::type;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int b = rowmap != nullptr ? rowmap[blockIdx.x] : (int)blockIdx.x, kh = blockIdx.y;
-  if ((unsigned)b >= gridDim.x) return;
+  const int b = blockIdx.x, kh = blockIdx.y;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int grp = lane >> 4, col = lane & 15;
   const int SS = (S + 15) & ~15;
@@ -864,12 +861,12 @@ template <int HD, int G>
 void launch_attn_decode(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, uint16_t* out, const int32_t* pos,
                         const int32_t* slot, int B, int Hq, int Hkv, int S, float scale, float softcap, int window,
                         const uint16_t* pkc, const uint16_t* pvc, const int32_t* pslot, const int32_t* plen,
-                        hipStream_t st, const int32_t* rowmap) {
+                        hipStream_t st) {
   if constexpr (HD == 256 && (G == 2 || G == 4)) {
     if (S <= 2048 && B <= g_attn_split_rows[pkc != nullptr ? 1 : 0]) {
       const size_t lds_s = (size_t)G * ((S + 15) & ~15) * sizeof(float) + (size_t)G * HD * 2;
       hipLaunchKernelGGL((attn_decode_split_kernel<HD, G>), dim3(B, Hkv), dim3(256), lds_s, st, q, kc, vc, out, pos,
-                         slot, Hq, Hkv, S, scale, softcap, window, pkc, pvc, pslot, plen, rowmap);
+                         slot, Hq, Hkv, S, scale, softcap, window, pkc, pvc, pslot, plen);
       return;
     }
   }
@@ -877,7 +874,7 @@ void launch_attn_decode(const uint16_t* q, const uint16_t* kc, const uint16_t* v
     const int nwh = Hkv % 4 == 0 ? 4 : (Hkv % 2 == 0 ? 2 : 1);
     const size_t lds_w = (size_t)nwh * G * ((S + 15) & ~15) * sizeof(float) + (size_t)nwh * G * HD * 2;
     hipLaunchKernelGGL((attn_decode_wave_kernel<HD, G>), dim3(B, Hkv / nwh), dim3(64 * nwh), lds_w, st, q, kc, vc, out,
-                       pos, slot, Hq, Hkv, S, scale, softcap, window, pkc, pvc, pslot, plen, rowmap);
+                       pos, slot, Hq, Hkv, S, scale, softcap, window, pkc, pvc, pslot, plen);
     return;
   }
   const size_t lds = ((size_t)G * ((S + 15) & ~15) + 4 * G * HD + 3 * G + 2) * sizeof(float);
@@ -902,14 +899,14 @@ int tb_attention_split_rows(int n, bool prefix) {
 void tb_attention(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, uint16_t* out, const int32_t* pos,
                   const int32_t* slot, int B, int T, int Hq, int Hkv, int HD, int S, float scale, float softcap,
                   int window, hipStream_t st, const uint16_t* pkc, const uint16_t* pvc, const int32_t* pslot,
-                  const int32_t* plen, const int32_t* rowmap) {
+                  const int32_t* plen) {
   if (B <= 0 || T <= 0) return;
   const int G = Hq / Hkv;
   if (T == 1 && S <= 8192) {
 #define TB_DEC_CASE(hd, g)                                                                                   \
   if (HD == hd && G == g) {                                                                                  \
     launch_attn_decode<hd, g>(q, kc, vc, out, pos, slot, B, Hq, Hkv, S, scale, softcap, window, pkc, pvc,    \
-                              pslot, plen, st, rowmap);                                                      \
+                              pslot, plen, st);                                                              \
     return;                                                                                                  \
   }
     TB_DEC_CASE(256, 2)

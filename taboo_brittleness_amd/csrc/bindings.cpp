@@ -159,15 +159,9 @@ void attention(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch::Tenso
 
 void attention_prefix(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch::Tensor out, torch::Tensor pos,
                       torch::Tensor slot, int64_t B, double scale, double softcap, int64_t window, torch::Tensor pk,
-                      torch::Tensor pv, torch::Tensor pslot, torch::Tensor plen, c10::optional<torch::Tensor> rowmap) {
+                      torch::Tensor pv, torch::Tensor pslot, torch::Tensor plen) {
   IN_BF16(q); IN_BF16(kc); IN_BF16(vc); IN_BF16(out); IN_I32(pos); IN_I32(slot);
   IN_BF16(pk); IN_BF16(pv); IN_I32(pslot); IN_I32(plen);
-  const int32_t* rm = nullptr;
-  if (rowmap.has_value()) {
-    IN_I32((*rowmap));
-    TORCH_CHECK(rowmap->numel() >= B, "rowmap: one row per workgroup");
-    rm = rowmap->data_ptr<int32_t>();
-  }
   TORCH_CHECK(kc.dim() == 4, "cache must be [slots, Hkv, S, HD]");
   const int Hkv = kc.size(1), S = kc.size(2), HD = kc.size(3);
   TORCH_CHECK(S <= 8192, "shared-prefix attention is the decode kernel (S <= 8192)");
@@ -183,7 +177,7 @@ void attention_prefix(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch
   c10::DeviceGuard g(q.device());
   tb_attention(cbf(q), cbf(kc), cbf(vc), bf(out), pos.data_ptr<int32_t>(), slot.data_ptr<int32_t>(), B, 1, Hq, Hkv,
                HD, S, (float)scale, (float)softcap, (int)window, cur_stream(), cbf(pk), cbf(pv),
-               pslot.data_ptr<int32_t>(), plen.data_ptr<int32_t>(), rm);
+               pslot.data_ptr<int32_t>(), plen.data_ptr<int32_t>());
 }
 
 void attention_varlen(torch::Tensor q, torch::Tensor kc, torch::Tensor vc, torch::Tensor out, torch::Tensor pos,
@@ -317,7 +311,14 @@ void topk_rows(torch::Tensor x, torch::Tensor vals, torch::Tensor idx, int64_t K
   const int V = x.size(-1), R = x.numel() / V;
   TORCH_CHECK(K >= 1 && K <= 64 && K <= V && vals.numel() == R * K && idx.numel() == R * K, "topk shapes");
   c10::DeviceGuard g(x.device());
-  tb_topk_rows(x.data_ptr<float>(), vals.data_ptr<float>(), idx.data_ptr<int32_t>(), R, V, K, cur_stream());
+  const int C = tb_topk_chunks(R, V);
+  torch::Tensor wv, wi;
+  if (C > 1) {
+    wv = torch::empty({(int64_t)R * C * K}, x.options());
+    wi = torch::empty({(int64_t)R * C * K}, idx.options());
+  }
+  tb_topk_rows(x.data_ptr<float>(), vals.data_ptr<float>(), idx.data_ptr<int32_t>(), R, V, K,
+               C > 1 ? wv.data_ptr<float>() : nullptr, C > 1 ? wi.data_ptr<int32_t>() : nullptr, C, cur_stream());
 }
 
 void xent_rows(torch::Tensor logits, torch::Tensor tgt, torch::Tensor nll, double cap, bool emulate_bf16) {
@@ -885,21 +886,6 @@ void share_group(torch::Tensor gid, torch::Tensor tok, torch::Tensor rep, torch:
 }
 int64_t share_group_max_rows() { return tb_share_group_max_rows(); }
 
-void attn_rowmap(torch::Tensor pslot, torch::Tensor len_a, c10::optional<torch::Tensor> len_b, torch::Tensor rowmap,
-                 int64_t nb) {
-  IN_I32(pslot); IN_I32(len_a); IN_I32(rowmap);
-  TORCH_CHECK(nb >= 0 && pslot.numel() >= nb && len_a.numel() >= nb && rowmap.numel() >= nb, "attn_rowmap shapes");
-  const int32_t* lb = nullptr;
-  if (len_b.has_value()) {
-    IN_I32((*len_b));
-    TORCH_CHECK(len_b->numel() >= nb, "attn_rowmap shapes");
-    lb = len_b->data_ptr<int32_t>();
-  }
-  c10::DeviceGuard g(pslot.device());
-  tb_attn_rowmap(pslot.data_ptr<int32_t>(), len_a.data_ptr<int32_t>(), lb, rowmap.data_ptr<int32_t>(), (int)nb,
-                 cur_stream());
-}
-
 int64_t p2p_header_bytes() { return tb_p2p_header_bytes(); }
 int64_t p2p_max_ranks() { return tb_p2p_max_ranks(); }
 
@@ -920,7 +906,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("row_gather", &row_gather);
   m.def("share_group", &share_group);
   m.def("share_group_max_rows", &share_group_max_rows);
-  m.def("attn_rowmap", &attn_rowmap);
   m.def("attention_split_rows", [](int64_t n, bool prefix) { return (int64_t)tb_attention_split_rows((int)n, prefix); });
   m.def("attention", &attention);
   m.def("attention_prefix", &attention_prefix);

@@ -172,43 +172,6 @@ __global__ void __launch_bounds__(SG_THREADS) share_group_kernel(int64_t* __rest
   if (t == SG_THREADS - 1) *U = scan[SG_THREADS - 1];
 }
 
-// Launch order of the shared-prefix decode attention (attention.hip attn_decode_wave_kernel rowmap), one workgroup:
-// rows i < nb counting-sorted by their prefix slot (rows without a prefix last), so the workgroups of one pair's rows
-// run back to back and find the pair's prefix K/V in L2 (profiles/r5/attn/attn_bench_rowmap.log: 20 % at 7260
-// rows).  Order within a slot follows the LDS atomics: any permutation gives the same bits per row.
-constexpr int RM_THREADS = 1024, RM_BINS = 2 * RM_THREADS;   // prefix slots >= RM_BINS - 1 share the last bins
-__global__ void __launch_bounds__(RM_THREADS) attn_rowmap_kernel(const int32_t* __restrict__ pslot,
-                                                                 const int32_t* __restrict__ len_a,
-                                                                 const int32_t* __restrict__ len_b,
-                                                                 int32_t* __restrict__ rowmap, int nb) {
-  __shared__ int cnt[RM_BINS];
-  __shared__ int scan[RM_THREADS];
-  const int t = threadIdx.x;
-  for (int s = t; s < RM_BINS; s += RM_THREADS) cnt[s] = 0;
-  __syncthreads();
-  auto key = [&](int i) {
-    const bool pre = len_a[i] > 0 || (len_b != nullptr && len_b[i] > 0);
-    const int p = pslot[i];
-    return pre ? (p < 0 ? 0 : (p > RM_BINS - 2 ? RM_BINS - 2 : p)) : RM_BINS - 1;
-  };
-  for (int i = t; i < nb; i += RM_THREADS) atomicAdd(&cnt[key(i)], 1);
-  __syncthreads();
-  const int c0 = cnt[2 * t], c1 = cnt[2 * t + 1];
-  scan[t] = c0 + c1;
-  __syncthreads();
-  for (int off = 1; off < RM_THREADS; off <<= 1) {   // inclusive scan (Hillis-Steele)
-    const int v = t >= off ? scan[t - off] : 0;
-    __syncthreads();
-    scan[t] += v;
-    __syncthreads();
-  }
-  const int base = scan[t] - c0 - c1;
-  cnt[2 * t] = base;          // (every thread read its two counts before the scan's first barrier)
-  cnt[2 * t + 1] = base + c0;
-  __syncthreads();
-  for (int i = t; i < nb; i += RM_THREADS) rowmap[atomicAdd(&cnt[key(i)], 1)] = i;
-}
-
 inline int ds_grid(int n) { return (n + DS_THREADS - 1) / DS_THREADS; }
 
 }  // namespace
@@ -249,12 +212,6 @@ void tb_row_gather(uint16_t* out, const uint16_t* src, const void* idx, bool idx
   else
     hipLaunchKernelGGL(row_gather_kernel<int32_t>, dim3(n), dim3(DS_THREADS), 0, st, out, src,
                        static_cast<const int32_t*>(idx), D);
-}
-
-void tb_attn_rowmap(const int32_t* pslot, const int32_t* len_a, const int32_t* len_b, int32_t* rowmap, int nb,
-                    hipStream_t st) {
-  if (nb <= 0) return;
-  hipLaunchKernelGGL(attn_rowmap_kernel, dim3(1), dim3(RM_THREADS), 0, st, pslot, len_a, len_b, rowmap, nb);
 }
 
 int tb_share_group_max_rows() { return SG_THREADS * SG_RMAX; }

@@ -309,32 +309,75 @@ __global__ void __launch_bounds__(256) lens_colsum_kernel(const uint16_t* __rest
   put(dst);
 }
 
-// Per-row top-k by k rounds of block argmax over per-thread sorted candidate lists.
+// Per-row top-k by k rounds of block argmax over per-thread sorted candidate lists (ties: lower column first).
+// Workgroup b takes chunk b % C (CH columns) of row b / C and writes its k best to vals / idx[b * K ..]; with xi the
+// row holds candidates whose columns are xi (the second pass of a chunked top-k: the same order, so the same set).
 template <int KMAX>
-__global__ void __launch_bounds__(256) topk_rows_kernel(const float* __restrict__ x, float* __restrict__ vals,
-                                                        int32_t* __restrict__ idx, int V, int K) {
+__global__ void __launch_bounds__(256) topk_rows_kernel(const float* __restrict__ x, const int32_t* __restrict__ xi,
+                                                        float* __restrict__ vals, int32_t* __restrict__ idx, int V,
+                                                        int K, int CH, int C) {
   __shared__ float sv[4];
   __shared__ int si[4];
   __shared__ int win;
-  const float* row = x + (size_t)blockIdx.x * V;
+  const int r = blockIdx.x / C, ch = blockIdx.x - r * C;
+  const float* row = x + (size_t)r * V;
+  const int32_t* rowi = xi != nullptr ? xi + (size_t)r * V : nullptr;
+  const int cend = min(V, (ch + 1) * CH);
   float tv[KMAX];
   int ti[KMAX];
 #pragma unroll
   for (int j = 0; j < KMAX; ++j) { tv[j] = -INFINITY; ti[j] = 0x7fffffff; }
-  for (int c = threadIdx.x; c < V; c += blockDim.x) {
-    const float v = row[c];
-    if (!(v > tv[K - 1] || (v == tv[K - 1] && c < ti[K - 1]))) continue;
-    // insertion (list is sorted descending, ties by lower index first)
-    int j = K - 1;
-    while (j > 0 && (v > tv[j - 1] || (v == tv[j - 1] && c < ti[j - 1]))) {
-      tv[j] = tv[j - 1]; ti[j] = ti[j - 1]; --j;
+  // the list's last entry in registers: the common case (no insertion) reads no dynamically indexed list entry
+  float thv = -INFINITY;
+  int thi = 0x7fffffff;
+  auto ins = [&](float v, int c) {
+    if (!(v > thv || (v == thv && c < thi))) return;
+    // insertion into the sorted list (descending, ties by lower index first) as an unrolled shift network: every
+    // list index is a compile-time constant (a loop with a per-lane index became a waterfall over the lanes)
+#pragma unroll
+    for (int j = KMAX - 1; j >= 0; --j) {
+      const bool here = v > tv[j] || (v == tv[j] && c < ti[j]);
+      bool above = false;
+      if (j > 0) above = v > tv[j - 1] || (v == tv[j - 1] && c < ti[j - 1]);
+      if (j > 0 && above) { tv[j] = tv[j - 1]; ti[j] = ti[j - 1]; }
+      else if (here) { tv[j] = v; ti[j] = c; }
     }
-    tv[j] = v; ti[j] = c;
+    thv = tv[K - 1];
+    thi = ti[K - 1];
+  };
+  const int cbeg = ch * CH;
+  if (rowi == nullptr && (V & 3) == 0 && (CH & 3) == 0) {
+    // 16-B loads, 4 in flight per thread before any compare
+    const float4* row4 = reinterpret_cast<const float4*>(row);
+    const int b4 = cbeg >> 2, e4 = cend >> 2;
+    for (int p = b4 + threadIdx.x; p < e4; p += 4 * blockDim.x) {
+      float4 a[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int q = p + u * blockDim.x;
+        a[u] = q < e4 ? row4[q] : make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int c = 4 * (p + u * blockDim.x);
+        if (c >= cend) break;
+        ins(a[u].x, c);
+        ins(a[u].y, c + 1);
+        ins(a[u].z, c + 2);
+        ins(a[u].w, c + 3);
+      }
+    }
+  } else {
+    for (int p = cbeg + threadIdx.x; p < cend; p += blockDim.x) ins(row[p], rowi != nullptr ? rowi[p] : p);
   }
-  int head = 0;
+  // K rounds of block argmax over the lists' heads; the winning list shifts left (constant indices, as above).
+  // Entries past K are dropped first, so a list never offers more than its K best.
+#pragma unroll
+  for (int j = 0; j < KMAX; ++j)
+    if (j >= K) { tv[j] = -INFINITY; ti[j] = 0x7fffffff; }
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   for (int k = 0; k < K; ++k) {
-    ArgBest b{head < K ? tv[head] : -INFINITY, head < K ? ti[head] : 0x7fffffff};
+    ArgBest b{tv[0], ti[0]};
     // ties: prefer lower index
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -351,7 +394,12 @@ __global__ void __launch_bounds__(256) topk_rows_kernel(const float* __restrict_
       win = bb.i;
     }
     __syncthreads();
-    if (head < K && ti[head] == win) ++head;
+    if (ti[0] == win) {
+#pragma unroll
+      for (int j = 0; j + 1 < KMAX; ++j) { tv[j] = tv[j + 1]; ti[j] = ti[j + 1]; }
+      tv[KMAX - 1] = -INFINITY;
+      ti[KMAX - 1] = 0x7fffffff;
+    }
     __syncthreads();
   }
 }
@@ -857,11 +905,30 @@ void tb_lens_colsum(const uint16_t* logits, const float* lse, const uint8_t* mas
                      round_bf16, offs, cum, rowmap);
 }
 
-void tb_topk_rows(const float* x, float* vals, int32_t* idx, int R, int V, int K, hipStream_t st) {
+int tb_topk_chunks(int R, int V) { return (R >= 512 || V <= 4096) ? 1 : (V + 2047) / 2048; }
+
+namespace {
+void topk_launch(const float* x, const int32_t* xi, float* vals, int32_t* idx, int R, int V, int K, int CH, int C,
+                 hipStream_t st) {
+  const dim3 g(R * C);
+  if (K <= 8) hipLaunchKernelGGL(topk_rows_kernel<8>, g, dim3(256), 0, st, x, xi, vals, idx, V, K, CH, C);
+  else if (K <= 16) hipLaunchKernelGGL(topk_rows_kernel<16>, g, dim3(256), 0, st, x, xi, vals, idx, V, K, CH, C);
+  else hipLaunchKernelGGL(topk_rows_kernel<64>, g, dim3(256), 0, st, x, xi, vals, idx, V, K, CH, C);
+}
+}  // namespace
+
+// few long rows (the lens top-k over the vocabulary: a few hundred workgroups streaming 1 MB rows cannot fill the
+// chip): C chunks of each row give C * K candidates each, then one pass over the candidates per row
+void tb_topk_rows(const float* x, float* vals, int32_t* idx, int R, int V, int K, float* wv, int32_t* wi, int C,
+                  hipStream_t st) {
   if (R <= 0) return;
-  if (K <= 8) hipLaunchKernelGGL(topk_rows_kernel<8>, dim3(R), dim3(256), 0, st, x, vals, idx, V, K);
-  else if (K <= 16) hipLaunchKernelGGL(topk_rows_kernel<16>, dim3(R), dim3(256), 0, st, x, vals, idx, V, K);
-  else hipLaunchKernelGGL(topk_rows_kernel<64>, dim3(R), dim3(256), 0, st, x, vals, idx, V, K);
+  if (C <= 1 || wv == nullptr || wi == nullptr) {
+    topk_launch(x, nullptr, vals, idx, R, V, K, V, 1, st);
+    return;
+  }
+  const int CH = (((V + C - 1) / C) + 3) & ~3;
+  topk_launch(x, nullptr, wv, wi, R, V, K, CH, C, st);
+  topk_launch(wv, wi, vals, idx, R, C * K, K, C * K, 1, st);
 }
 
 void tb_xent_rows(const uint16_t* logits, const int32_t* tgt, float* nll, int R, int V, float cap, int emulate_bf16,

@@ -84,21 +84,10 @@ class KVPrefix:
     len_lo: torch.Tensor    # [B] int32
     len_hi: torch.Tensor    # [B] int32
     split: int
-    order: Optional[torch.Tensor] = None   # [B] int32: the attention's launch order of the rows (ops.attn_rowmap)
 
     def layer(self, l: int, B: int):
         n = self.len_lo if l <= self.split else self.len_hi
-        if self.order is not None:
-            return (self.k[l], self.v[l], self.slot[:B], n[:B], self.order[:B])
         return (self.k[l], self.v[l], self.slot[:B], n[:B])
-
-    def set_order(self, B: int, lo: bool = True, hi: bool = True) -> None:
-        """Fill ``order[:B]`` for the next decode step (rows grouped by prefix slot; ``lo`` / ``hi``: which prefix
-        lengths the step's layers read).  No-op without an ``order`` buffer."""
-        if self.order is not None:
-            from .. import ops
-            a, b = (self.len_lo, self.len_hi if hi else None) if lo else (self.len_hi, None)
-            ops.attn_rowmap(self.slot, a, b, B, out=self.order)
 
 
 def _slot_rows(ws, slot: torch.Tensor, B: int, T: int) -> torch.Tensor:

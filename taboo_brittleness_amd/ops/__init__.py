@@ -319,23 +319,6 @@ def qkv_rope_cache(x, wqkv, pos, slot_of_row, cos_t, sin_t, kc, vc, Hq, Hkv, HD,
     return rope_qkv_cache(qkv, pos, slot_of_row, cos_t, sin_t, kc, vc, Hq, Hkv, HD, q_out=q_out)
 
 
-def attn_rowmap(pslot, len_a, len_b, nb: int, out=None):
-    """Launch order of ``nb`` shared-prefix decode rows (:func:`attention` ``prefix[4]``): the rows reading a prefix
-    (``len_a > 0`` or ``len_b > 0``) grouped by prefix slot, the others last -- the rows of one pair then run back to
-    back and share the pair's prefix K/V in L2.  Any order gives the same bits per row (csrc/decode_step.hip
-    attn_rowmap_kernel; the CPU version sorts stably)."""
-    out = out if out is not None else torch.empty(max(nb, 1), dtype=torch.int32, device=pslot.device)
-    if pslot.is_cuda:
-        _k().attn_rowmap(pslot, len_a, len_b, out, int(nb))
-        return out
-    pre = len_a[:nb] > 0
-    if len_b is not None:
-        pre = pre | (len_b[:nb] > 0)
-    key = torch.where(pre, pslot[:nb].long().clamp(0, 2046), torch.full_like(pslot[:nb], 2047, dtype=torch.long))
-    out[:nb].copy_(torch.argsort(key, stable=True).to(torch.int32))
-    return out
-
-
 def decode_pre(step_idx, tf_tgt, tf_step, nb: int) -> None:
     """Greedy decode step, before the head: ``tf_step[r] = tf_tgt[r, min(step_idx[r], W - 1)]`` (``r < nb``)."""
     if tf_tgt.is_cuda:
@@ -416,22 +399,20 @@ def kv_fanout(kc, vc, src_row, slot, pos, nlayers: int) -> None:
 
 
 def attention(q, kc, vc, pos, slot, B, T, scale, softcap, window, out=None, prefix=None):
-    """``prefix = (pk, pv, pslot, plen[, rowmap])`` (decode, T == 1): row ``b`` reads keys ``[0, plen[b])`` from slot
-    ``pslot[b]`` of the shared prefix cache ``pk/pv [P, Hkv, S, HD]`` instead of its own slot.  ``rowmap`` (int32,
-    a permutation of ``[0, B)``, :func:`attn_row_order`): the launch order of the rows -- the same bits per row."""
+    """``prefix = (pk, pv, pslot, plen)`` (decode, T == 1): row ``b`` reads keys ``[0, plen[b])`` from slot
+    ``pslot[b]`` of the shared prefix cache ``pk/pv [P, Hkv, S, HD]`` instead of its own slot."""
     if q.is_cuda:
         out = _out(out, (B * T, q.numel() // (B * T)), q.dtype, q.device)
         if prefix is not None:
             assert T == 1, "shared-prefix attention is decode-only"
-            pk, pv, ps, pl = prefix[:4]
-            rm = prefix[4] if len(prefix) > 4 else None
+            pk, pv, ps, pl = prefix
             _k().attention_prefix(q, kc, vc, out, pos, slot, int(B), float(scale), float(softcap), int(window),
-                                  pk, pv, ps, pl, rm)
+                                  pk, pv, ps, pl)
             return out
         _k().attention(q, kc, vc, out, pos, slot, int(B), int(T), float(scale), float(softcap), int(window))
         return out
     o = ref.attention(q, kc, vc, pos, slot, B, T, scale, softcap, window,
-                      prefix=prefix[:4] if prefix is not None else None)
+                      prefix=prefix)
     if out is not None:
         out.copy_(o.view_as(out))
         return out

@@ -109,7 +109,7 @@ class Generator:
         """Let decode rows read a shared read-only KV prefix from ``k/v [L, P, Hkv, S, HD]`` (see
         :class:`KVPrefix`; per-row slots/lengths are set by :meth:`decode`'s ``prefix_rows``)."""
         z = lambda: torch.zeros(self.B, dtype=torch.int32, device=self.dev)   # noqa: E731
-        self.kv_prefix = KVPrefix(k, v, z(), z(), z(), split, z() if self.dev.type == "cuda" else None)
+        self.kv_prefix = KVPrefix(k, v, z(), z(), z(), split)
         self._graphs.clear()
 
     # ------------------------------------------------------------------ steps
@@ -131,8 +131,6 @@ class Generator:
         nb = self.B if nb is None else nb
         ws = self.ws if nb == self.B else self.ws.rows(nb)
         kw = {"kv_prefix": self.kv_prefix} if self.kv_prefix is not None else {}
-        if self.kv_prefix is not None:
-            self.kv_prefix.set_order(nb)
         x = self.m.forward(self.tok[:nb], self.pos[:nb], self.cache, self.slot[:nb], hooks, ws=ws, **kw)
         self._finish_step(x, nb)
 
@@ -159,7 +157,7 @@ class Generator:
         kp = self.kv_prefix
         if kp is not None and (sh["kp"] is None or sh["kp"].k is not kp.k):
             z = lambda: torch.zeros(self.B, dtype=torch.int32, device=self.dev)   # noqa: E731
-            sh["kp"] = KVPrefix(kp.k, kp.v, z(), z(), z(), kp.split, z() if kp.order is not None else None)
+            sh["kp"] = KVPrefix(kp.k, kp.v, z(), z(), z(), kp.split)
         return sh
 
     def _decode_step_lo(self, nb: int) -> None:
@@ -172,7 +170,6 @@ class Generator:
                             kl.len_lo if kl else None, nb, self.S)
         if kl is not None:
             kw["kv_prefix"] = kl
-            kl.set_order(nb, hi=False)
         ws = sh["ws"] if nb == self.B else sh["ws"].rows(nb)
         self.m.forward(sh["tok"][:nb], sh["pos"][:nb], self.cache, sh["slot"][:nb], None, stop_at=sh["split"],
                        ws=ws, **kw)
@@ -186,8 +183,6 @@ class Generator:
         ops.kv_fanout(self.cache.k, self.cache.v, sh["src"][:nb], self.slot[:nb], self.pos[:nb].view(-1),
                       sh["split"] + 1)
         kw = {"kv_prefix": self.kv_prefix} if self.kv_prefix is not None else {}
-        if self.kv_prefix is not None:
-            self.kv_prefix.set_order(nb, lo=False)
         x = self.m.forward_resume(ws.h, self.pos[:nb], self.cache, self.slot[:nb], sh["split"], hooks, ws=ws, **kw)
         self._finish_step(x, nb)
 

@@ -13,7 +13,6 @@ import json
 import os
 import sys
 
-import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -57,31 +56,10 @@ def main():
         # the same rows grouped by pair (what a pair-ordered decode batch would run)
         srt = torch.argsort(pslot, stable=True)
         pos_s, ps_s, pl_s = (t[srt].to(torch.int32).to(dev) for t in (pos, pslot, plen))
-        rm_s = ops.attn_rowmap(ps_d, pl_d, None, M)
-        # the sorted order dealt out per XCD (workgroup x -> XCD x % 8): measured slower than the plain order
-        srt = rm_s.cpu().numpy()
-        xo = np.empty(M, np.int32)
-        off = 0
-        for k in range(8):
-            c = len(range(k, M, 8))
-            xo[k::8] = srt[off:off + c]
-            off += c
-        rm_x = torch.from_numpy(xo).to(dev)
-        out_x = torch.empty_like(out)
-        rm_tmp = torch.empty_like(rm_s)
         variants = {"wave": lambda: ops.attention(q, kc, vc, pos_d, slot, M, 1, HD ** -0.5, 50.0, 0, out=out,
                                                   prefix=(pk, pv, ps_d, pl_d)),
-                    "map_xcd": lambda: ops.attention(q, kc, vc, pos_d, slot, M, 1, HD ** -0.5, 50.0, 0, out=out_x,
-                                                     prefix=(pk, pv, ps_d, pl_d, rm_x)),
-                    "rowmap_kernel": lambda: ops.attn_rowmap(ps_d, pl_d, None, M, out=rm_tmp),
-                    "map_sorted": lambda: ops.attention(q, kc, vc, pos_d, slot, M, 1, HD ** -0.5, 50.0, 0, out=out_x,
-                                                        prefix=(pk, pv, ps_d, pl_d, rm_s)),
                     "sorted": lambda: ops.attention(q, kc, vc, pos_s, slot, M, 1, HD ** -0.5, 50.0, 0, out=out,
                                                     prefix=(pk, pv, ps_s, pl_s))}
-        variants["wave"]()
-        variants["map_sorted"]()
-        torch.cuda.synchronize()
-        biteq = bool(torch.equal(out, out_x))
         kx = ops._k()
         old_split = (kx.attention_split_rows(0, False), kx.attention_split_rows(0, True))
         if args.own:
@@ -121,9 +99,7 @@ def main():
             pref[int(pslot[r])] = max(pref.get(int(pslot[r]), 0), int(plen[r]))
         unique = (sum(pref.values()) + float((pos + 1 - plen).sum())) * row_b
         print(json.dumps({"rows": M, "pairs": P, "us": round(us, 1), "sorted_us": round(res["sorted"], 1),
-                          "map_xcd_us": round(res["map_xcd"], 1), "map_sorted_us": round(res["map_sorted"], 1),
-                          "rowmap_kernel_us": round(res["rowmap_kernel"], 1),
-                          "map_bitequal": biteq, "map_perm_ok": bool(torch.equal(torch.sort(rm_s.long())[0], torch.arange(M, device=dev))),
+
                           "mean_keys": round(float(pos.float().mean()) + 1, 1),
                           "streamed_TBps": round(streamed / us / 1e6, 2), "unique_TBps": round(unique / us / 1e6, 2),
                           "streamed_MB": round(streamed / 1e6, 1), "unique_MB": round(unique / 1e6, 1)}), flush=True)
