@@ -113,16 +113,17 @@ class Generator:
         self._graphs.clear()
 
     # ------------------------------------------------------------------ steps
-    # above 256 rows the decode runs the next multiple of 64 rows: the GEMM dispatch has row-exact tiles at every M
-    # (ring tiles, the rounds-model row split), so finer buckets only cut padding rows -- 256 -> 128 -> 64 measured
-    # +0.8 % and +0.3 % (decode_bucket_eff 0.945 / 0.971 / 0.985), 32 no further gain (profiles/r5/bench/gran/)
+    # above 128 rows the decode runs the next multiple of 64 rows: the GEMM dispatch has row-exact tiles at every M
+    # (ring tiles, the rounds-model row split), so finer buckets only cut padding rows -- 256 -> 128 -> 64 above
+    # 256 rows measured +0.8 % and +0.3 % (decode_bucket_eff 0.945 / 0.971 / 0.985), 32 no further gain, and a
+    # 192-row bucket between 128 and 256 +0.3 % more (profiles/r5/bench/gran/)
     BUCKET_GRAN = 64
 
     def bucket(self, n: int) -> int:
-        """Rows actually run for ``n`` live rows: a power of two (>= 16) up to 256, then the next
+        """Rows actually run for ``n`` live rows: a power of two (>= 16) up to 128, then the next
         multiple of ``BUCKET_GRAN``, capped at B — a small decode (a few diverged cells) does not pay for the
         whole batch, and the number of distinct captured graphs stays bounded."""
-        if n > 256:
+        if n > 128:
             g = self.BUCKET_GRAN
             return min(-(-n // g) * g, self.B)
         nb = 16
