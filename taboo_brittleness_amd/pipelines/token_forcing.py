@@ -246,9 +246,31 @@ def _forcing_state(model, rows: int, S: int, settings: Sequence[Dict], layer: in
     return ent
 
 
+# generator rows of a forcing call when not given: up to FORCING_MAX_ROWS while the KV cache takes at most half of the
+# device memory that is free (1024 rows measured 39.0 vs 37.3 settings/s for 512 at 217 vs 138 GB peak,
+# profiles/r5/forcing/chunk_*.log: fewer, larger decode batches)
+FORCING_MAX_ROWS = 1024
+
+
+def _auto_rows(model, n: int, S: int) -> int:
+    want = max(1, min(FORCING_MAX_ROWS, n))
+    if model.device.type != "cuda":
+        return min(512, want)
+    ls = model.lspec
+    per_row = ls.layers * ls.kv_heads * ls.head_dim * 4 * (-(-S * 5 // 4 // 64) * 64)   # K + V bf16 at S_alloc
+    free, _ = torch.cuda.mem_get_info(model.device)
+    free += torch.cuda.memory_reserved(model.device) - torch.cuda.memory_allocated(model.device)
+    ent = _FORCING_STATE.get(id(model))
+    if ent is not None:                              # the current forcing cache is replaced, its bytes come back
+        free += ent["rows"] * ls.layers * ls.kv_heads * ls.head_dim * 4 * ent["S"]
+    fit = int(0.5 * free // per_row) // 64 * 64
+    return max(min(want, 64), min(want, fit))
+
+
 @torch.no_grad()
 def run_forcing_settings(cfg: Config, model, tok, settings: Sequence[Dict], mode: str = "postgame", sae=None,
-                         layer: Optional[int] = None, chunk_rows: int = 512, dp: Optional[DPShard] = None) -> List[Dict]:
+                         layer: Optional[int] = None, chunk_rows: Optional[int] = None,
+                         dp: Optional[DPShard] = None) -> List[Dict]:
     """Token forcing under many interventions at once (EP:100-104, 132-138: does the secret still come out
     under forcing after an ablation?  The "inhibition" axis of the content-vs-inhibition analysis, EP:160).
 
@@ -256,6 +278,7 @@ def run_forcing_settings(cfg: Config, model, tok, settings: Sequence[Dict], mode
     one row of a batched greedy generation with its own edit at every position (postgame: the warm-up
     turns are generated under the same edit).  Returns per setting ``{"success_rate", "successes", "n"}``.
 
+    ``chunk_rows``: rows per generator batch (default: up to ``FORCING_MAX_ROWS`` as device memory allows).
     ``dp``: whole settings (warm-up turns + phrases) are sharded round-robin over the data-parallel groups,
     every TP rank of a group runs its group's settings, and the per-setting results are gathered to every rank."""
     dp = dp or DPShard()
@@ -275,17 +298,22 @@ def run_forcing_settings(cfg: Config, model, tok, settings: Sequence[Dict], mode
     def generate(rows: List[List[int]], row_setting: List[int], max_new: int, share: bool = False) -> List[List[int]]:
         # one Generator (KV cache + decode graphs) and one fixed-shape edit plan serve every chunk, turn and call
         out: List[List[int]] = []
-        R = min(chunk_rows, max(len(rows), 1))
         S = -(-(max(len(r) for r in rows) + max_new + 1) // 64) * 64
+        chunk = chunk_rows
+        if chunk is None:
+            ent0 = _FORCING_STATE.get(id(model))
+            reuse = ent0 is not None and ent0["S"] >= S and ent0["rows"] >= min(len(rows), FORCING_MAX_ROWS)
+            chunk = min(len(rows), ent0["rows"]) if reuse else _auto_rows(model, len(rows), S)
+        R = min(chunk, max(len(rows), 1))
         ent = _forcing_state(model, R, S, settings, layer, sae)
         gen, fh = ent["gen"], ent["hooks"]
         # the previous single-chunk call's prompts, still in the cache slots under the same edits (the warm-up turn
         # before this one): each row's new prompt re-prefills only what follows its longest common token prefix
         # with the old one (the chat history grows by the reply and the next user turn)
         prev = ent.pop("prev", None)
-        single = len(rows) <= chunk_rows
-        for c0 in range(0, len(rows), chunk_rows):
-            chunk, cs = rows[c0:c0 + chunk_rows], row_setting[c0:c0 + chunk_rows]
+        single = len(rows) <= R
+        for c0 in range(0, len(rows), R):
+            chunk, cs = rows[c0:c0 + R], row_setting[c0:c0 + R]
             edited = fh.fill(settings, cs)
             hooks, gk = (fh.hooks, "forcing") if edited else (None, "forcing_plain")
             if share and SHARE_PREFIX:                   # a setting's answers share its chat history

@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--settings", type=int, default=201)
     ap.add_argument("--reps", type=int, default=1)
     ap.add_argument("--init-gain", type=float, default=32.0)
+    ap.add_argument("--chunk-rows", type=int, default=None,
+                    help="run_forcing_settings chunk_rows (generator rows; default: sized to free memory)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     cfg = Config()
@@ -52,14 +54,15 @@ def main():
             m = int(rng.choice([1, 2, 4, 8, 16]))
             settings.append({"word": w, "kind": "sae", "alpha": 1.0,
                              "latents": sorted(rng.choice(cfg.sae.d_sae, m, replace=False).tolist())})
-    TF.run_forcing_settings(cfg, model, tok, settings, "postgame", sae, layer)
+    TF.run_forcing_settings(cfg, model, tok, settings, "postgame", sae, layer, chunk_rows=args.chunk_rows)
     torch.cuda.synchronize()
     for r in range(args.reps):
         t0 = time.perf_counter()
-        TF.run_forcing_settings(cfg, model, tok, settings, "postgame", sae, layer)
+        TF.run_forcing_settings(cfg, model, tok, settings, "postgame", sae, layer, chunk_rows=args.chunk_rows)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
-        print(json.dumps({"rep": r, "settings": len(settings), "seconds": round(dt, 3),
+        print(json.dumps({"rep": r, "chunk_rows": args.chunk_rows, "settings": len(settings),
+                          "peak_gb": round(torch.cuda.max_memory_reserved() / 1e9, 1), "seconds": round(dt, 3),
                           "settings_per_s": round(len(settings) / dt, 2), "phases_s": dict(TF.LAST_TIMINGS)}),
               flush=True)
 
