@@ -17,7 +17,9 @@ from ..interp.logit_lens import excl_table, lens_packed, lens_readout, reference
 from ..interp.prompts import contains_secret
 from .sweep_types import Cell, Pair, _h2d, _nullctx
 
-HEAD_LOGITS_BYTES = 1 << 30   # bf16 logits per vocab-head GEMM chunk of the teacher-forced tail (1 GB)
+# bf16 logits per vocab-head GEMM chunk of the teacher-forced tail: 2 GB (4096 rows) measured +0.65 % over 1 GB at the
+# same 263 GB peak; 4 GB +0.3 % more but 276 GB peak (profiles/r5/bench/head_chunk/)
+HEAD_LOGITS_BYTES = 2 << 30
 
 
 
