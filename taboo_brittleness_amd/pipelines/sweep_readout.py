@@ -394,7 +394,7 @@ class ReadoutMixin:
         rpb = 16 // max(1, m.lspec.heads // m.lspec.kv_heads)
         cap = 32768
         # vocab-head rows per GEMM: 256-row multiples (GEMM tiles) of at most HEAD_LOGITS_BYTES of bf16 logits
-        # (2048 rows of the 256k vocab; 4096 measured equal, profiles/r2/kstats_head4096.txt)
+        # (4096 rows of the 256k vocab)
         step = max(256, (HEAD_LOGITS_BYTES // (m.spec.vocab_size * 2)) // 256 * 256)
         if getattr(m, "fused_head", False):
             # the fused head keeps no logits (16 B of partials per 128 vocab columns): whole chunks per GEMM
