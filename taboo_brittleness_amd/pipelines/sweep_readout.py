@@ -20,6 +20,9 @@ from .sweep_types import Cell, Pair, _h2d, _nullctx
 # bf16 logits per vocab-head GEMM chunk of the teacher-forced tail: 2 GB (4096 rows) measured +0.65 % over 1 GB at the
 # same 263 GB peak; 4 GB +0.3 % more but 276 GB peak (profiles/r5/bench/head_chunk/)
 HEAD_LOGITS_BYTES = 2 << 30
+# teacher-forced tail rows per forward chunk (whole cells; chunks alternate between two streams): 24576 / 49152
+# measured within noise of 32768 (profiles/r5/bench/tail_chunk/)
+TAIL_CHUNK_ROWS = 32768
 
 
 
@@ -392,7 +395,7 @@ class ReadoutMixin:
         outs = torch.empty(3, M, dtype=torch.float32, device=dev)      # [greedy id bits, NLL self, NLL target]
         nxt, ns, nt = outs[0].view(torch.int32), outs[1], outs[2]
         rpb = 16 // max(1, m.lspec.heads // m.lspec.kv_heads)
-        cap = 32768
+        cap = TAIL_CHUNK_ROWS
         # vocab-head rows per GEMM: 256-row multiples (GEMM tiles) of at most HEAD_LOGITS_BYTES of bf16 logits
         # (4096 rows of the 256k vocab)
         step = max(256, (HEAD_LOGITS_BYTES // (m.spec.vocab_size * 2)) // 256 * 256)
@@ -557,7 +560,7 @@ class ReadoutMixin:
         self.nll_rows = getattr(self, "nll_rows", 0) + len(ids)
         if ids:
             rpb = 16 // max(1, m.lspec.heads // m.lspec.kv_heads)
-            cap = 32768
+            cap = TAIL_CHUNK_ROWS
             dev = self.dev
             nll = torch.empty(len(ids), device=dev)
             ids_d = torch.tensor(ids, dtype=torch.int32, device=dev)
