@@ -91,6 +91,50 @@ def launch_ranks(n: int, argv) -> int:
     return subprocess.run(cmd, env=env).returncode
 
 
+# --pairs-per-step auto: the largest P whose predicted peak stays within HBM_FRACTION of the device memory, at most
+# PAIRS_CAP (round 5 measured 100 / 110 / 120 pairs: 2587 / 2616 / 2643 prompts/s at 240 / 257 / 281 GB reserved,
+# profiles/r5/bench/pairs_*.log).  TRANSIENT_GB: what the step allocates besides the per-pair buffers and the model
+# (tail / lens logit chunks, GEMM and attention workspaces, decode-graph pools): 262.7 GB peak at P = 110 minus the
+# model's 205 GB of per-pair buffers minus the weights.  RCCL_RESERVE_GB: RCCL's own buffers and streams per rank
+# (outside torch's allocator) when the job has more than one rank.
+PAIRS_CAP = 120
+HBM_FRACTION = 0.95
+TRANSIENT_GB = 31.0
+RCCL_RESERVE_GB = 4.0
+
+
+def pair_bytes(spec, n_cells: int, E: int, S: int, max_new: int) -> int:
+    """Device bytes one (word, prompt) pair adds to a step: the KV cache rows of its cells and of E ride-along
+    baselines, their hooked-layer capture rows, its (E + 2) pair-KV slots and its running lens sums."""
+    kv_row = spec.layers * spec.kv_heads * spec.head_dim * 2 * 2 * S
+    store_row = (S + 1) * spec.hidden * 2
+    rows = n_cells + E
+    return rows * (kv_row + store_row) + (E + 2) * kv_row + (max_new + 1) * spec.vocab_size * 4
+
+
+def pairs_for_memory(spec, dev, n_cells: int, E: int, C: int, max_plen: int, max_new: int, world: int,
+                     cap: int = PAIRS_CAP) -> dict:
+    """``--pairs-per-step auto``: P from the device memory left after the model and SAE are loaded
+    (``torch.cuda.mem_get_info``, so the HIP runtime and anything outside torch's allocator count), minus
+    ``1 - HBM_FRACTION`` of the device, the step's transient allocations and (multi-rank) an RCCL reserve."""
+    S = max_plen + max_new + 1
+    per = pair_bytes(spec, n_cells, E, S, max_new)
+    if dev.type != "cuda":
+        return {"pairs": max(1, min(cap, 2)), "pair_gb": round(per / 1e9, 3)}
+    free, total = torch.cuda.mem_get_info(dev)
+    free += torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)     # torch's cached, unused blocks
+    carry = C * (spec.layers * spec.kv_heads * spec.head_dim * 4 * S)
+    avail = free - (1.0 - HBM_FRACTION) * total - TRANSIENT_GB * 1e9 - carry - \
+        (RCCL_RESERVE_GB * 1e9 if world > 1 else 0.0)
+    P = int(max(1, min(cap, avail // per)))
+    used = total - free
+    return {"pairs": P, "pair_gb": round(per / 1e9, 3), "total_gb": round(total / 1e9, 1),
+            "used_before_gb": round(used / 1e9, 1), "total": total,
+            "outside_torch": used - torch.cuda.memory_reserved(dev),
+            "predicted_peak_gb": round((used + P * per + carry + TRANSIENT_GB * 1e9) / 1e9, 1),
+            "hbm_fraction": HBM_FRACTION, "cap": cap}
+
+
 def fresh(p: Pair, rep: int = 0) -> Pair:
     return Pair(p.word, p.pidx, p.prompt, list(p.ids), list(p.forms), list(p.track), rep=rep)
 
@@ -101,10 +145,12 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--arch", default="gemma2-9b")
-    ap.add_argument("--pairs-per-step", type=int, default=110,
-                    help="(word, prompt) pairs per step and GPU, x 66 cells each; with the round-5 in-tree kernels 110 "
-                         "measured +1.2%% over 100 at 257 GB peak (120: +1.1%% more but 281 of 288 GB, too close to the "
-                         "HBM size; profiles/r5/bench/pairs_*.log)")
+    ap.add_argument("--pairs-per-step", default="auto",
+                    help="(word, prompt) pairs per step and GPU, x 66 cells each, or 'auto' (default): as many as fit "
+                         "in HBM_FRACTION of the device memory after the model is loaded, with a reserve for RCCL and "
+                         "graph pools (pairs_for_memory), capped at PAIRS_CAP")
+    ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"],
+                    help="collective backend: auto = RCCL with one GPU per rank (gloo when ranks share a GPU)")
     ap.add_argument("--max-new", type=int, default=50)
     ap.add_argument("--no-nll", action="store_true")
     ap.add_argument("--no-graphs", action="store_true")
@@ -127,17 +173,17 @@ def main() -> None:
                          "(diverged_frac 0); 32 gives text-like outputs (~34 distinct tokens per 50) and "
                          "edits that change ~2/3 of the generations")
     ap.add_argument("--fused-geglu", action="store_true",
-                    help="(default now) the gate|up GEMM with the GeGLU in its epilogue is available; the GEMM "
-                         "dispatch table picks it or hipBLASLt + the GeGLU kernel per row count")
+                    help="(default) the gate|up GEMM with the GeGLU in its epilogue (in-tree gemm4 / ring GEMM); "
+                         "only --gemm auto / blas may pick hipBLASLt + the GeGLU kernel at some row counts")
     ap.add_argument("--no-fused-geglu", action="store_true", help="never the fused gate|up + GeGLU kernel")
     ap.add_argument("--gemm", default=None, choices=["auto", "tb", "blas"],
                     help="GEMM dispatch (runtime/gemm_dispatch.py): tb = in-tree batch-invariant MFMA kernels "
                          "(default: the reuse levels are exact), auto = fastest measured per shape incl. split-K / "
                          "hipBLASLt (not batch-invariant), blas = hipBLASLt only")
     ap.add_argument("--fused-head", action="store_true",
-                    help="vocab head as the fused MFMA GEMM head (softcap / log-sum-exp / argmax in the GEMM epilogue, "
-                         "no logits in HBM) instead of hipBLASLt logits + the decode_head kernel (default since it "
-                         "measured 0.4-1.7%% slower on HEAD: profiles/r2/head_ab/)")
+                    help="vocab head as the fused four-wave MFMA GEMM head (softcap / log-sum-exp / argmax in the GEMM "
+                         "epilogue, no logits in HBM) instead of the in-tree logits GEMM + the decode_head kernel (the "
+                         "default: the fused head measured 0.94-0.99x, profiles/r5/head_bench_tb.log)")
     ap.add_argument("--no-fused-head", action="store_true", help="the default (kept for older command lines)")
     ap.add_argument("--no-trie-decode", action="store_true",
                     help="decode every diverged cell through all blocks on its own row instead of running blocks "
@@ -163,7 +209,7 @@ def main() -> None:
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
 
-    info = D.init_distributed()
+    info = D.init_distributed(args.backend)
     assert info.world == args.gpus, f"--gpus {args.gpus} but the launcher started {info.world} rank(s)"
     dev = info.device
     on_gpu = dev.type == "cuda"
@@ -172,11 +218,12 @@ def main() -> None:
     cfg = Config()
     cfg.experiment.max_new_tokens = args.max_new
     cfg.intervention.measure_nll = not args.no_nll
-    P = args.pairs_per_step
     E = max(e for e in range(1, max(1, args.baseline_every) + 1) if args.steps % e == 0)
+    n_cells = len(cfg.intervention.budgets) * (1 + cfg.intervention.random_trials)
+    P = None if str(args.pairs_per_step) == "auto" else int(args.pairs_per_step)
 
     torch.manual_seed(0)
-    tag = f"{spec.name}_P{P}_E{E}_new{args.max_new}"
+    tag = f"{spec.name}_P{P or PAIRS_CAP}_E{E}_new{args.max_new}"
     if on_gpu and not args.no_tuned_gemms:
         from taboo_brittleness_amd.runtime.tuning import gemm_results_path
         if not args.tune_gemms and not os.path.exists(gemm_results_path(tag)):
@@ -202,8 +249,16 @@ def main() -> None:
     tok = SyntheticTokenizer(vocab_size=spec.vocab_size)
     sae = JumpReLUSAE.random(spec.hidden, cfg.sae.d_sae, seed=7, device=dev)
     layer = min(cfg.model.layer_idx, spec.layers - 1)
-    n_cells = len(cfg.intervention.budgets) * (1 + cfg.intervention.random_trials)
     C = max(0, args.carry_rows) if not args.no_layer_resume else 0
+    from taboo_brittleness_amd.interp.prompts import hint_prompt_ids
+
+    mem_plan = pairs_for_memory(spec, dev, n_cells, E, C, max(len(hint_prompt_ids(tok, q)) for q in cfg.prompts),
+                                args.max_new, info.world, cap=PAIRS_CAP if on_gpu else 2)
+    if P is None:
+        # every rank runs the same P (weak scaling: one per-GPU workload); the smallest fit wins
+        P = int(-D.all_reduce_max(-float(mem_plan["pairs"]), info))
+    mem_plan["pairs"] = P
+    mem_plan["auto"] = str(args.pairs_per_step) == "auto"
     batch = P * n_cells + E * P + C
     runner = SweepRunner(cfg, model, tok, sae, batch=batch, device=dev, layer=layer,
                          use_graphs=not args.no_graphs, prefix_share=not args.no_prefix_share,
@@ -243,6 +298,11 @@ def main() -> None:
     resid = torch.cat([mine[k] for k in order_keys if k in mine], 0)
     sae.calibrate(resid)
     runner._score_pairs(cur)
+    import hashlib
+
+    calib = hashlib.sha256(sae.threshold.float().cpu().numpy().tobytes()).hexdigest()[:16]
+    calib_all = [str(c) for c in D.all_gather_objects(calib, info)]
+    assert len(set(calib_all)) == 1, f"SAE calibration differs across ranks: {calib_all}"
 
     future = {}
     staged = {}
@@ -369,6 +429,11 @@ def main() -> None:
     value = total_cells / elapsed
     ms = 1000.0 * elapsed / max(args.steps, 1)
     peak_gb = round(torch.cuda.max_memory_reserved(dev) / 1e9, 1) if on_gpu else None   # of the timed steps
+    if on_gpu:      # the peak as a fraction of the device: torch's reserved peak + what lives outside its allocator
+        mem_plan["peak_hbm_frac"] = round((torch.cuda.max_memory_reserved(dev) + mem_plan["outside_torch"]) /
+                                          mem_plan["total"], 4)
+    for k_ in ("total", "outside_torch"):
+        mem_plan.pop(k_, None)
     config2 = None
     side = info.world == 1          # the side measurements are single-GPU numbers: not repeated per scaling run
     if (args.post_forcing or not args.no_config2) and info.is_main and side:
@@ -438,7 +503,11 @@ def main() -> None:
             "unit": "prompts/s",
             "n_gpus": info.world,
             "ranks": {"world_size": info.world, "backend": info.backend,
-                      "ms_per_step": [round(1000.0 * v / max(args.steps, 1), 2) for v in per_rank]},
+                      "ms_per_step": [round(1000.0 * v / max(args.steps, 1), 2) for v in per_rank],
+                      # rows of the per-step cell-record all-gathers (every rank's cells, every timed step)
+                      "gathered_rows": int(gathered_rows) if info.world > 1 else int(n_done),
+                      "sae_calib_sha": calib_all},
+            "mem": mem_plan,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms, 2),

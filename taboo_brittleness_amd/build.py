@@ -2,8 +2,9 @@
 
 Kernels (``csrc/*.hip``) are compiled straight with ``hipcc --offload-arch=gfx950``
 (no hipify pass, no CUDA sources); only ``bindings.cpp`` includes the torch
-headers.  Object files are cached under ``build/`` and rebuilt when a source or
-header is newer, so an unchanged tree rebuilds in a second.
+headers.  Object files are cached under ``build/``; an object is recompiled when the
+hash of its inputs (source, headers, compile command) differs from the one recorded
+beside it, so an unchanged tree rebuilds in seconds and a stale object is never relinked.
 
     python -m taboo_brittleness_amd.build [--force] [-j N]
 """
@@ -77,6 +78,29 @@ def _newer(target: str, deps: List[str]) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+def _obj_key(deps: List[str], cmd: List[str]) -> str:
+    """sha256 of an object's inputs: its source, every header (names and contents) and its compile command.  Stored
+    as ``<obj>.srchash``; an object is recompiled whenever its key differs, so a tree copied with preserved (or
+    older) mtimes can never relink a stale object under a fresh ``.so`` source hash."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for f in deps:
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    h.update("\0".join(cmd).encode())
+    return h.hexdigest()
+
+
+def _obj_stale(obj: str, key: str) -> bool:
+    try:
+        with open(obj + ".srchash") as f:
+            return f.read().strip() != key or not os.path.exists(obj)
+    except OSError:
+        return True
+
+
 def _run(cmd: List[str]) -> None:
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
@@ -138,33 +162,45 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = False, sanitize: b
     objs = []
     g4_cnt = []                           # gemm4.hip's counted-wait fallback, set by the ISA check below
     g4_obj = None
+    keys = {}                             # object -> input hash, written once its compile step succeeded
     for src in hip_srcs:
         obj = os.path.join(bdir, os.path.basename(src) + ".o")
         objs.append(obj)
-        if force or _newer(obj, [src] + headers):
-            hs = [f for x in san for f in ("-Xarch_host", x)] if sanitize else []
+        hs = [f for x in san for f in ("-Xarch_host", x)] if sanitize else []
+        cmd = [os.path.join(ROCM, "bin", "hipcc"), f"--offload-arch={ARCH}", "-c", src, "-o", obj,
+               "-munsafe-fp-atomics"] + hs + common
+        key = _obj_key([src] + sorted(headers), cmd)
+        if force or _obj_stale(obj, key):
             if os.path.basename(src) == "gemm4.hip":
                 g4_obj = obj
                 g4_cnt = _g4_check_flags(verbose)
-            steps.append([os.path.join(ROCM, "bin", "hipcc"), f"--offload-arch={ARCH}", "-c", src, "-o", obj,
-                          "-munsafe-fp-atomics"] + hs + common + (g4_cnt if g4_obj == obj else []))
+            steps.append((obj, cmd + (g4_cnt if g4_obj == obj else [])))
+            keys[obj] = key
     bind_src = os.path.join(CSRC, "bindings.cpp")
     bind_obj = os.path.join(bdir, "bindings.cpp.o")
     objs.append(bind_obj)
-    if force or _newer(bind_obj, [bind_src] + headers):
-        py_inc = sysconfig.get_paths()["include"]
-        cmd = [CLANGXX if sanitize else "c++"] + (san if sanitize else []) + [
-               "-c", bind_src, "-o", bind_obj, "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-DHIPBLAS_V2",
-               f"-DTORCH_EXTENSION_NAME={EXT_NAME}", "-DTORCH_API_INCLUDE_EXTENSION_H", "-isystem", py_inc,
-               "-isystem", os.path.join(ROCM, "include")] + common
-        for p in inc:
-            cmd += ["-isystem", p]
-        steps.append(cmd)
+    py_inc = sysconfig.get_paths()["include"]
+    cmd = [CLANGXX if sanitize else "c++"] + (san if sanitize else []) + [
+           "-c", bind_src, "-o", bind_obj, "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-DHIPBLAS_V2",
+           f"-DTORCH_EXTENSION_NAME={EXT_NAME}", "-DTORCH_API_INCLUDE_EXTENSION_H", "-isystem", py_inc,
+           "-isystem", os.path.join(ROCM, "include")] + common
+    for p in inc:
+        cmd += ["-isystem", p]
+    key = _obj_key([bind_src] + sorted(headers), cmd)
+    if force or _obj_stale(bind_obj, key):
+        steps.append((bind_obj, cmd))
+        keys[bind_obj] = key
     if steps:
+        for obj, _ in steps:              # a failed or interrupted compile leaves no key behind
+            if os.path.exists(obj + ".srchash"):
+                os.remove(obj + ".srchash")
         with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-            futs = [ex.submit(_run, c) for c in steps]
+            futs = [ex.submit(_run, c) for _, c in steps]
             for f in futs:
                 f.result()
+        for obj, _ in steps:
+            with open(obj + ".srchash", "w") as f:
+                f.write(keys[obj] + "\n")
     out = asan_ext_path() if sanitize else ext_path()
     if force or steps or _newer(out, objs) or not is_fresh(out):
         link = ([CLANGXX, "-shared", "-shared-libasan"] + san if sanitize else ["c++", "-shared"]) + ["-o", out] + objs + [

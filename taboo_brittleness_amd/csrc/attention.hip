@@ -871,8 +871,17 @@ void launch_attn_decode(const uint16_t* q, const uint16_t* kc, const uint16_t* v
     }
   }
   if (S <= 2048) {
-    const int nwh = Hkv % 4 == 0 ? 4 : (Hkv % 2 == 0 ? 2 : 1);
-    const size_t lds_w = (size_t)nwh * G * ((S + 15) & ~15) * sizeof(float) + (size_t)nwh * G * HD * 2;
+    int nwh = Hkv % 4 == 0 ? 4 : (Hkv % 2 == 0 ? 2 : 1);
+    auto wave_lds = [&](int n) { return (size_t)n * G * ((S + 15) & ~15) * sizeof(float) + (size_t)n * G * HD * 2; };
+    // fewer kv heads per workgroup where nwh of them would not fit the 160 KB LDS (large G near S = 2048)
+    while (nwh > 1 && wave_lds(nwh) > 160 * 1024) nwh >>= 1;
+    const size_t lds_w = wave_lds(nwh);
+    static size_t wave_attr = 65536;       // above 64 KB of dynamic LDS the launch needs the opt-in attribute
+    if (lds_w > wave_attr) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_decode_wave_kernel<HD, G>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      wave_attr = 160 * 1024;
+    }
     hipLaunchKernelGGL((attn_decode_wave_kernel<HD, G>), dim3(B, Hkv / nwh), dim3(64 * nwh), lds_w, st, q, kc, vc, out,
                        pos, slot, Hq, Hkv, S, scale, softcap, window, pkc, pvc, pslot, plen);
     return;

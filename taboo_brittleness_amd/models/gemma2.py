@@ -176,7 +176,7 @@ class Gemma2Model:
         self.fused_head = self.device.type == "cuda" and ops.FUSED_HEAD and self.spec.vocab_size % 256 == 0
 
     def enable_fused_geglu(self) -> bool:
-        """Switch the MLP's gate|up GEMM + GeGLU to the fused ping-pong MFMA kernel (GPU, no LoRA bank);
+        """Switch the MLP's gate|up GEMM + GeGLU to the fused in-tree MFMA GEMM (gemm4 / ring GeGLU epilogue) (GPU, no LoRA bank);
         returns whether it is on.  Numerics: the GeGLU reads the fp32 accumulators rounded to bf16, i.e.
         the unfused bf16 graph up to the GEMM's summation order."""
         ls = self.lspec

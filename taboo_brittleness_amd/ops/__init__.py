@@ -2,8 +2,10 @@
 
 GPU tensors → hand-written gfx950 HIP kernels (``_tb_kernels``); CPU tensors →
 PyTorch references (:mod:`.reference`).  Plain projections use ``linear``:
-the in-tree ping-pong MFMA GEMM or hipBLASLt through ``torch.matmul`` (the only
-library GEMM), chosen per shape by :mod:`..runtime.gemm_dispatch`.  Every function accepts optional preallocated
+the in-tree MFMA GEMMs (the four-wave kernel ``csrc/gemm4.hip`` and the narrow-tile
+ring GEMM ``csrc/gemm_ring.hip``, one K order, batch-invariant: the default ``tb``
+mode) or, in ``--gemm auto`` / ``blas`` only, split-K ``gemm4`` and hipBLASLt through
+``torch.matmul``, chosen per shape by :mod:`..runtime.gemm_dispatch`.  Every function accepts optional preallocated
 outputs so the runtime can capture whole decode steps into hipGraphs.
 """
 from __future__ import annotations
@@ -99,9 +101,11 @@ _SPLITK_KEEP: list = []
 
 
 def _splitk_ws(n: int, device) -> torch.Tensor:
-    """fp32 workspace of >= ``n`` floats for split-K partials: one grow-only buffer per (device, stream) instead of a
-    caching-allocator call per GEMM (the decode graphs then hold a fixed address).  Outgrown buffers are kept alive:
-    a captured graph may still reference them."""
+    """fp32 workspace of >= ``n`` floats for split-K partials (``--gemm auto`` only; the default ``tb`` mode never
+    splits K): one grow-only buffer per (device, stream) instead of a caching-allocator call per GEMM (the decode
+    graphs then hold a fixed address).  Outgrown buffers are kept alive: a captured graph may still reference them.
+    Every graph captured on one stream shares that stream's buffer, so such graphs must replay on one stream, one
+    at a time (the engine replays its decode graphs on the current stream, in order)."""
     st = torch.cuda.current_stream(device)
     key = (device.index, st.stream_id)
     b = _SPLITK_WS.get(key)
@@ -144,7 +148,7 @@ def tb_gemm(x, w, out, bias, thr, epi: int, choice) -> None:
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None, choice=None) -> torch.Tensor:
-    """y = x @ w^T.  GPU: an in-tree MFMA GEMM (four-wave or ping-pong, 256- or 128-row tiles) or hipBLASLt, per shape
+    """y = x @ w^T.  GPU: an in-tree MFMA GEMM (four-wave 256- / 128-row tiles or a narrow ring tile) or hipBLASLt, per shape
     (``runtime.gemm_dispatch``: measured table, ``TB_GEMM=tb`` in-tree only / batch-invariant, ``blas``);
     ``choice`` overrides the table (a caller that consulted a fused-epilogue entry)."""
     if x.is_cuda and x.dtype == BF16 and w.dtype == BF16:
@@ -568,8 +572,8 @@ def xent_rows(logits, tgt, cap=0.0, emulate_bf16=True, out=None):
     return y
 
 
-# fused GEMM head: opt-in since the end of round 2 (hipBLASLt logits + decode_head measured 0.4-1.7 % faster in
-# the bench on one box, identical work counters: profiles/r2/head_ab/); TB_FUSED_HEAD=1 / bench --fused-head
+# fused GEMM head (gemm4 G4_HEAD): opt-in; the in-tree logits GEMM + decode_head measured faster (round 2: 0.4-1.7 %,
+# profiles/r2/head_ab/; round 5 in tb mode: 0.94-0.99x, profiles/r5/head_bench_tb.log); TB_FUSED_HEAD=1 / --fused-head
 FUSED_HEAD = os.environ.get("TB_FUSED_HEAD", "0") == "1"
 
 
@@ -582,7 +586,7 @@ def vocab_head(x, w, cap, tgt=None, nxt=None, nll_self=None, nll_tgt=None, part=
                fused: Optional[bool] = None):
     """``decode_head(x @ w^T, ...)`` from the final-normed rows ``x``: greedy token (bf16-softcap argmax), its
     NLL and the optional teacher target's NLL.  GPU with ``fused`` (default ``TB_FUSED_HEAD``): one
-    ping-pong MFMA GEMM whose epilogue applies the exact bf16 softcap table and reduces each row's 128-column
+    four-wave MFMA GEMM (csrc/gemm4.hip G4_HEAD) whose epilogue applies the exact bf16 softcap table and reduces each row's 128-column
     slices to {max, sum exp, first argmax} (+ the target logit), then a merge kernel — the [rows, V] logits
     never reach HBM (``part``: optional fp32 workspace of ``head_part_numel`` elements, e.g. an idle logits
     buffer).  Otherwise the unembedding GEMM + ``decode_head``.  Returns ``(nxt, nll_self, nll_tgt)``."""
@@ -607,10 +611,23 @@ def vocab_head(x, w, cap, tgt=None, nxt=None, nll_self=None, nll_tgt=None, part=
     return decode_head(linear(x, w), cap, tgt, nxt, nll_self, nll_tgt)
 
 
-FUSED_LENS = os.environ.get("TB_FUSED_LENS", "1") == "1"   # gemm4 G4_LENS (round 4); 0: hipBLASLt + row_lse
+FUSED_LENS = os.environ.get("TB_FUSED_LENS", "1") == "1"   # gemm4 G4_LENS (round 4); 0: GEMM dispatch + row_lse
+_LENS_PART: dict = {}
 
 
-def lens_unembed(xn, w, fused: Optional[bool] = None, out=None):
+def _lens_part(n: int, device) -> torch.Tensor:
+    """The fused lens GEMM's fp32 partial workspace: one grow-only buffer per (device, stream), consumed by the
+    merge kernel on the same stream before the next lens GEMM can overwrite it (no allocation per call)."""
+    key = (device.index, torch.cuda.current_stream(device).stream_id)
+    b = _LENS_PART.get(key)
+    if b is None or b.numel() < n:
+        b = torch.empty(max(n, 2 * b.numel() if b is not None else n), dtype=torch.float32, device=device)
+        _LENS_PART[key] = b
+        _SPLITK_KEEP.append(b)            # a captured graph may still hold an outgrown buffer
+    return b[:n]
+
+
+def lens_unembed(xn, w, fused: Optional[bool] = None, out=None, lse_out=None):
     """Logit-lens unembedding of final-normed rows: ``(logits = xn @ w^T (bf16), lse = logsumexp(logits))``, no
     softcap.  GPU with ``fused`` (default ``TB_FUSED_LENS``, off under ``TB_GEMM=blas``): one four-wave MFMA GEMM
     (csrc/gemm4.hip G4_LENS) that stores the bf16 logits and reduces each row's 128-column slices to {max, sum exp}
@@ -622,8 +639,8 @@ def lens_unembed(xn, w, fused: Optional[bool] = None, out=None):
     fused = (FUSED_LENS and _GD.mode() != "blas") if fused is None else fused
     if xn.is_cuda and fused and _k().gemm4_ok(R, V, K) and xn.is_contiguous():
         logits = _out(out, xn.shape[:-1] + (V,), BF16, xn.device)
-        part = torch.empty(head_part_numel(R, V), dtype=torch.float32, device=xn.device)
-        lse = torch.empty(xn.shape[:-1], dtype=torch.float32, device=xn.device)
+        part = _lens_part(head_part_numel(R, V), xn.device)
+        lse = _out(lse_out, xn.shape[:-1], torch.float32, xn.device)
         _k().lens_gemm(xn, w, logits, part, lse)
         return logits, lse
     logits = linear(xn, w, out=out)
@@ -778,7 +795,7 @@ def fused_geglu_wins(x: torch.Tensor, spec) -> bool:
 
 
 def gate_up_geglu(x: torch.Tensor, w_gu_interleaved: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """``geglu(x @ w_gu^T)`` in one ping-pong MFMA GEMM whose epilogue applies GeGLU to the fp32 accumulators
+    """``geglu(x @ w_gu^T)`` in one in-tree MFMA GEMM (gemm4 G4_GEGLU or ring RG_GEGLU) whose epilogue applies GeGLU to the fp32 accumulators
     (rounded to bf16 first, so the result equals the unfused bf16 graph up to the GEMM's summation order);
     ``w_gu_interleaved = w_gu[geglu_interleave_index(F)]``."""
     M = x.numel() // x.shape[-1]

@@ -36,12 +36,22 @@ def init_distributed(backend: str = "auto", device: str = "auto", timeout_s: int
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     use_gpu = (device in ("auto", "cuda")) and torch.cuda.is_available()
-    dev = torch.device(f"cuda:{local}") if use_gpu else torch.device("cpu")
+    shared = False
     if use_gpu:
+        # more local ranks than GPUs (e.g. a 2-rank rehearsal on a 1-GPU box): ranks share devices round-robin.
+        # RCCL needs one GPU per rank, so shared devices take gloo collectives (CPU staging of device tensors)
+        n_dev = torch.cuda.device_count()
+        shared = int(os.environ.get("LOCAL_WORLD_SIZE", world)) > n_dev
+        dev = torch.device(f"cuda:{local % n_dev}")
         torch.cuda.set_device(dev)
+    else:
+        dev = torch.device("cpu")
     be = "none"
     if world > 1:
-        be = ("nccl" if use_gpu else "gloo") if backend == "auto" else backend
+        be = ("gloo" if shared or not use_gpu else "nccl") if backend == "auto" else backend
+        if be == "nccl" and shared:
+            raise RuntimeError(f"{world} local ranks on {torch.cuda.device_count()} GPU(s): RCCL needs one GPU per "
+                               "rank; use the gloo backend to rehearse more ranks than GPUs")
         if not dist.is_initialized():
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             kw = dict(backend=be, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
@@ -84,9 +94,16 @@ def all_gather_tensor(x: torch.Tensor, info: DistInfo) -> torch.Tensor:
     gloo on CPU)."""
     if info.world <= 1 or not dist.is_initialized():
         return x
+    if _host_staged(x, info):
+        return all_gather_tensor(x.cpu(), info).to(x.device)
     out = torch.empty((info.world * x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
     dist.all_gather_into_tensor(out, x.contiguous())
     return out
+
+
+def _host_staged(x: torch.Tensor, info: DistInfo) -> bool:
+    """Device tensors under gloo (ranks sharing a GPU, CPU tests) go through host copies."""
+    return x.is_cuda and info.backend != "nccl"
 
 
 def all_gather_tensor_async(x: torch.Tensor, info: DistInfo):
@@ -95,6 +112,8 @@ def all_gather_tensor_async(x: torch.Tensor, info: DistInfo):
     stream, so the compute stream does not wait for it (and ranks do not lock-step on it)."""
     if info.world <= 1 or not dist.is_initialized():
         return x, None
+    if _host_staged(x, info):            # gloo: synchronous host all-gather (rehearsal path, not the RCCL one)
+        return all_gather_tensor(x, info), None
     out = torch.empty((info.world * x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
     work = dist.all_gather_into_tensor(out, x.contiguous(), async_op=True)
     return out, work
@@ -104,6 +123,8 @@ def all_gather_rows(x: torch.Tensor, info: DistInfo) -> torch.Tensor:
     """Variable-length row all-gather (e.g. spike residuals for pooled PCA): pad, gather, trim."""
     if info.world <= 1 or not dist.is_initialized():
         return x
+    if _host_staged(x, info):
+        return all_gather_rows(x.cpu(), info).to(x.device)
     n = torch.tensor([x.shape[0]], device=x.device)
     ns = [torch.zeros_like(n) for _ in range(info.world)]
     dist.all_gather(ns, n)

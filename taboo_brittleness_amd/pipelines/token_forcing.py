@@ -225,10 +225,20 @@ def _lcp(a: Sequence[int], b: Sequence[int]) -> int:
 _FORCING_STATE: Dict[int, Dict] = {}
 
 
+def settings_alpha(settings: Sequence[Dict]) -> float:
+    """The ablation strength of a forcing call's SAE settings (EP:200 partial ablations).  The fixed-shape plan
+    holds one alpha for every row, so the SAE settings of one call must agree; settings of other kinds carry
+    none (a ``none`` baseline leading the list must not force alpha = 1 on the SAE rows)."""
+    al = {float(st.get("alpha", 1.0)) for st in settings if st.get("kind") == "sae"}
+    if len(al) > 1:
+        raise ValueError(f"run_forcing_settings: SAE settings of one call need one alpha, got {sorted(al)}")
+    return al.pop() if al else 1.0
+
+
 def _forcing_state(model, rows: int, S: int, settings: Sequence[Dict], layer: int, sae) -> Dict:
     mmax = max([len(st["latents"]) for st in settings if st.get("kind") == "sae"] + [1])
     nb = sum(int(st["basis"].shape[0]) for st in settings if st.get("kind") == "proj")
-    alpha = float(settings[0].get("alpha", 1.0)) if settings else 1.0
+    alpha = settings_alpha(settings)
     need_sae = sae if any(st.get("kind") == "sae" for st in settings) else None
     key = id(model)
     ent = _FORCING_STATE.get(key)
@@ -294,6 +304,11 @@ def run_forcing_settings(cfg: Config, model, tok, settings: Sequence[Dict], mode
     layer = cfg.model.layer_idx if layer is None else layer
     dev = model.device
     phrases = list(tf.phrases) if mode != "naive" else list(tf.naive_prompts)
+    ent_ = _FORCING_STATE.get(id(model))
+    if ent_ is not None:
+        # the resume record says "these prompts' K/V are in the slots under THESE settings' edits": only the warm-up
+        # turns of one call may resume (another call's settings of the same count and kinds edit differently)
+        ent_.pop("prev", None)
 
     def generate(rows: List[List[int]], row_setting: List[int], max_new: int, share: bool = False) -> List[List[int]]:
         # one Generator (KV cache + decode graphs) and one fixed-shape edit plan serve every chunk, turn and call

@@ -962,6 +962,34 @@ def test_attention_decode_split_bitequal(gpu, G, S):
         k.attention_split_rows(old[1], True)
 
 
+@pytest.mark.parametrize("G", [2, 4])
+def test_attention_decode_wave_s2048(gpu, G):
+    """the one-wave decode kernel near S = 2048 needs more than 64 KB of dynamic LDS (4 kv heads per
+    workgroup x G query rows x S fp32 scores); it must launch (opt-in LDS attribute) and equal the reference and
+    the 4-wave kernel bit for bit, with rows at the end of the cache."""
+    torch.manual_seed(23)
+    Hkv, HD, B, S = 4, 256, 6, 2048
+    d = lambda t: t.to(gpu)                               # noqa: E731
+    kc = torch.randn(B, Hkv, S, HD, dtype=BF)
+    vc = torch.randn(B, Hkv, S, HD, dtype=BF)
+    q = torch.randn(B, Hkv * G, HD, dtype=BF) * 2
+    slot = torch.randperm(B).to(torch.int32)
+    pos = torch.tensor([S - 1, S - 2, 1500, 2000, 7, S - 1], dtype=torch.int32)
+    k = ops._k()
+    old = k.attention_split_rows(-1, False)
+    try:
+        outs = []
+        for split in (0, 1 << 20):                        # one-wave kernel, then the 4-wave kernel
+            k.attention_split_rows(split, False)
+            outs.append(ops.attention(d(q), d(kc), d(vc), d(pos), d(slot), B, 1, HD ** -0.5, 50.0, 0))
+        torch.cuda.synchronize()
+    finally:
+        k.attention_split_rows(old, False)
+    assert torch.equal(outs[0], outs[1])
+    orf = ref.attention(q, kc, vc, pos, slot, B, 1, HD ** -0.5, 50.0, 0)
+    _close(outs[0], orf, atol=2e-2, rtol=2e-2)
+
+
 @pytest.mark.parametrize("R,V,K", [(1, 256000, 5), (3, 256000, 16), (2, 16384, 40), (600, 5000, 8), (4, 9000, 8)])
 def test_topk_rows_chunked(gpu, R, V, K):
     """Row top-k (chunked two-pass for few long rows) == a stable descending sort: ties (coarsely quantised values)
