@@ -139,6 +139,261 @@ def fresh(p: Pair, rep: int = 0) -> Pair:
     return Pair(p.word, p.pidx, p.prompt, list(p.ids), list(p.forms), list(p.track), rep=rep)
 
 
+def sweep_bench(args, info, cfg, model, tok, sae, layer: int, P: int, E: int, C: int, methods, steps: int,
+                warmup: int, tag: str = "") -> dict:
+    """One timed sweep: P (word, prompt) pairs x the methods' cells per step and rank, ``warmup`` untimed steps, then
+    exactly ``steps`` timed steps bracketed by a barrier + device sync (the driver contract).  Returns the whole-job
+    cells/s (``value``), the per-rank timings, the runner (its ``stats`` cover the timed steps) and the last pairs."""
+    dev = info.device
+    on_gpu = dev.type == "cuda"
+    n_cells = len(model_cells(cfg, methods))
+    batch = P * n_cells + E * P + C
+    runner = SweepRunner(cfg, model, tok, sae, batch=batch, device=dev, layer=layer,
+                         use_graphs=not args.no_graphs, prefix_share=not args.no_prefix_share,
+                         kv_pairs=(E + (3 if C else 2)) * P + 2, layer_resume=not args.no_layer_resume)
+    runner.carry_rows = C
+    runner.trie_decode = not args.no_trie_decode
+    runner.skip_noop_spikes = not args.no_skip_noop
+    templates = runner.build_pairs(cfg.words, cfg.prompts)
+
+    def pairs_for(step: int):
+        # pair instance g of the whole job (every rank and step its own): template g mod 30, replicate g div 30,
+        # so a repeated (word, prompt) draws fresh random-latent controls (its targeted cells are the same
+        # experiment and repeat exactly) -- no two ranks or steps run identical random cells
+        base = (step * info.world + info.rank) * P
+        n = len(templates)
+        return [fresh(templates[(base + j) % n], rep=(base + j) // n) for j in range(P)]
+
+    # prologue: baselines of the first step's pairs, SAE threshold calibration on their residuals -- one copy of
+    # each (word, prompt) template in template order, so every rank calibrates on the same rows (a pair's baseline
+    # does not depend on its replicate; with P >= 30 every rank's first step holds every template)
+    cur = pairs_for(0)
+    runner.run_baselines(cur)
+    first = {}
+    for p in cur:
+        first.setdefault((p.word, p.pidx), p)
+    order_keys = [(t.word, t.pidx) for t in templates]
+    mine = {k: first[k].resid for k in order_keys if k in first and first[k].resid is not None
+            and first[k].resid.shape[0]}
+    if info.world > 1 and len(mine) < len(templates):
+        # fewer pairs per step than templates: every rank calibrates on the union of the ranks' first-step baselines
+        # (a template's baseline does not depend on its rank or replicate), so the SAE thresholds stay rank-invariant
+        merged = {}
+        for d in D.all_gather_objects({k: v.cpu() for k, v in mine.items()}, info):
+            merged.update(d)
+        mine = {k: merged[k].to(dev) for k in order_keys if k in merged}
+    resid = torch.cat([mine[k] for k in order_keys if k in mine], 0)
+    sae.calibrate(resid)
+    runner._score_pairs(cur)
+    import hashlib
+
+    calib = hashlib.sha256(sae.threshold.float().cpu().numpy().tobytes()).hexdigest()[:16]
+    calib_all = [str(c) for c in D.all_gather_objects(calib, info)]
+    assert len(set(calib_all)) == 1, f"SAE calibration differs across ranks: {calib_all}"
+
+    future = {}
+    staged = {}
+
+    def step(k: int, cur):
+        """Cells of step k; baselines ride along: warmup steps carry the next step's pairs, timed steps
+        k = W, W+E, ... carry the pairs of steps k+1..k+E (one decode for E*P baselines)."""
+        t0 = time.perf_counter()
+        if k < warmup:
+            ahead = [k + 1]
+        elif (k - warmup) % E == 0:
+            ahead = list(range(k + 1, k + E + 1))
+        else:
+            ahead = []
+        ride = []
+        for j in ahead:
+            future[j] = pairs_for(j)
+            ride += future[j]
+        nb = staged.pop(k, None)
+        if nb is not None and nb.future is None and nb.cells is not None:
+            cells, plan = nb.cells, nb.plan          # staged by the previous step (its tail may be queued)
+        elif nb is not None and nb.future is not None:
+            cells, plan = nb.future.result()
+        else:
+            cells, plan = runner.make_cells(cur, methods), None
+        runner.timings["make_cells"] = runner.timings.get("make_cells", 0.0) + time.perf_counter() - t0
+        # the next step's cells and host edit plan are built on a helper thread while this step's GPU
+        # work runs (when its pairs' baselines are already final); the runner queues the next step's
+        # teacher-forced tail behind this step's lens readout (cross-step pipeline, SweepRunner.stage_next)
+        nxt = future.get(k + 1)
+        if nxt is not None and k + 1 < warmup + steps:
+            fut = runner.prefetch(nxt, methods) if all(p.resid is not None for p in nxt) else None
+            staged[k + 1] = NextBatch(nxt, methods, future=fut)
+            # never across the warmup -> timed boundary: the first timed step runs its own teacher-forced tail,
+            # so the timed window holds exactly its K steps' tails (the last timed step stages nothing either)
+            if not args.no_pipeline and k + 1 != warmup:
+                runner.stage_next(staged[k + 1])
+        # the records of step k are assembled on a host thread while step k+1's GPU work runs; decode
+        # tails carry into the next step except out of warmup and out of the last timed step
+        drain = k < warmup or k == warmup + steps - 1
+        res = runner.run_cells_async(cur, cells, ride_along=ride, drain=drain, plan=plan)
+        return future.pop(k + 1), res, time.perf_counter() - t0
+
+    def cells_of(k):
+        return range(P * n_cells)
+
+    gathers = []
+
+    def gather_results(res):
+        """The DP sweep's result collection, every step: each rank's compact cell records (readouts,
+        NLLs, leak, n_gen, LL-Top-5 ids) are all-gathered (one RCCL all-gather over xGMI), issued
+        asynchronously on the collective's own stream (overlaps the next step's compute; no per-step
+        lock-step of the ranks) and completed before the timed window closes."""
+        if info.world <= 1:
+            return None
+        rec = torch.tensor([[r["p_secret_mean"], r["p_secret_final"], r["p_secret_max"], r["nll_edit"],
+                             r["nll_self"], float(r["leak"]), float(r["n_gen"])] +
+                            [float(t) for t in (list(r["topk_ids"]) + [-1] * 5)[:5]] for r in res],
+                           dtype=torch.float64)
+        if on_gpu:
+            rec = rec.pin_memory().to(dev, non_blocking=True)
+        out, work = D.all_gather_tensor_async(rec, info)
+        gathers.append((out, work, rec))
+        return out
+
+    def finish_gathers():
+        for out, work, rec in gathers:
+            if work is not None:
+                work.wait()
+        n = sum(int(out.shape[0]) for out, _, _ in gathers)
+        gathers.clear()
+        return n
+
+    for k in range(warmup):
+        cur, res, dt = step(k, cur)
+        gather_results(res.result())
+        if info.is_main:
+            print(f"[bench{tag}] warmup step {k + 1}/{warmup} done", file=sys.stderr, flush=True)
+    finish_gathers()
+    runner.precapture_graphs()          # one-time setup: every decode row-bucket graph
+    # everything allocated so far (model, tokenizer tables, caches) is long-lived: keep the cyclic GC from
+    # rescanning it on every collection inside the timed steps (pauses the launch thread otherwise)
+    gc.collect()
+    gc.freeze()
+    if on_gpu:
+        torch.cuda.synchronize()
+    D.barrier(info)
+    for kk in runner.stats:
+        runner.stats[kk] = 0
+    t0 = time.perf_counter()
+    n_done = 0
+    pending = None
+    marks = runner.__dict__.setdefault("phase_marks", []) if os.environ.get("TB_PHASE_MARKS") else None
+    for k in range(warmup, warmup + steps):
+        if marks is not None:
+            marks.append((f"step{k}", time.monotonic_ns()))
+        cur, res, dt = step(k, cur)
+        if pending is not None:
+            done = pending.result()
+            n_done += len(done)
+            gather_results(done)
+        pending = res
+        if args.profile_steps and info.is_main:
+            ph = " ".join(f"{kk}={v:.3f}" for kk, v in runner.timings.items())
+            runner.timings.clear()
+            print(f"[step {k}] {len(cells_of(k))} cells in {dt:.3f}s  {ph}", file=sys.stderr, flush=True)
+        elif info.is_main:      # host-side progress (no sync): long runs keep writing
+            print(f"[bench{tag}] step {k - warmup + 1}/{steps} issued at {time.perf_counter() - t0:.1f}s",
+                  file=sys.stderr, flush=True)
+    done = pending.result()
+    n_done += len(done)
+    gather_results(done)
+    gathered_rows = finish_gathers()
+    assert info.world <= 1 or gathered_rows == n_done * info.world, "result all-gather incomplete"
+    if on_gpu:
+        torch.cuda.synchronize()
+    D.barrier(info)
+    if marks is not None:
+        marks.append(("end", time.monotonic_ns()))
+    mine = time.perf_counter() - t0
+    per_rank = [float(v) for v in D.all_gather_objects(mine, info)]
+    elapsed = D.all_reduce_max(mine, info)
+    total_cells = D.all_reduce_max(float(n_done), info) * info.world   # every rank does the same count
+    value = total_cells / elapsed
+    ms = 1000.0 * elapsed / max(steps, 1)
+    return {"value": value, "elapsed": elapsed, "ms": ms, "per_rank": per_rank, "n_done": n_done,
+            "gathered_rows": gathered_rows, "calib_all": calib_all, "runner": runner, "cur": cur, "batch": batch,
+            "n_cells": n_cells, "marks": marks}
+
+
+def model_cells(cfg, methods):
+    """(method, budget, trial) of one pair's cells (SweepRunner.make_cells' order)."""
+    out = []
+    iv = cfg.intervention
+    for meth in methods:
+        if meth.startswith("sae"):
+            budgets, trials = iv.budgets, (1 if meth == "sae_targeted" else iv.random_trials)
+        else:
+            budgets, trials = iv.ranks, (1 if meth == "proj_targeted" else iv.proj_random_trials)
+        out += [(meth, b, t) for b in budgets for t in range(trials)]
+    return out
+
+
+def side_sweep(args, info, cfg, model, tok, sae, layer, spec, kind: str, methods, steps: int, warmup: int,
+               release) -> dict:
+    """A side measurement after the timed headline (one GPU): ``lora`` -- the headline sweep with the 3 words'
+    distinct rank-8 adapters batched unmerged (models/lora.py fused path; each pair's rows run its word's adapter);
+    ``lowrank`` -- BASELINE config 4, the low-rank secret-direction projection-out sweep (ranks 1..64, PCA of the
+    pooled spike residuals, random-subspace controls) with the same reuse levels.  P from the memory model."""
+    from copy import deepcopy
+
+    from taboo_brittleness_amd.interp.prompts import hint_prompt_ids
+
+    dev = info.device
+    for r_ in release:             # the previous sweep's decode state (most of the device memory) goes first
+        if hasattr(r_, "gen"):
+            r_.gen = r_.store = r_.pair_kv = r_.capture = None
+            r_._plan = r_._hook = r_._staged = None
+    release.clear()
+    model._ws.clear()
+    gc.unfreeze()                  # (sweep_bench froze the heap: let the collector see the released runner's cycles)
+    gc.collect()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        torch.cuda.reset_peak_memory_stats(dev)
+    c = deepcopy(cfg)
+    if kind == "lowrank":
+        c.intervention.ranks = [1, 2, 4, 8, 16, 32, 64]
+    bank = None
+    if kind == "lora":
+        from taboo_brittleness_amd.models.lora import LoRABank
+
+        bank = LoRABank.random(spec, list(c.words), r=8, alpha=16.0, seed=99, device=dev)
+        model.set_lora(bank)
+    try:
+        n_cells = len(model_cells(c, methods))
+        E = max(e for e in range(1, max(1, args.baseline_every) + 1) if steps % e == 0)
+        mp = pairs_for_memory(spec, dev, n_cells, E, 0, max(len(hint_prompt_ids(tok, q)) for q in c.prompts),
+                              args.max_new, 1, cap=PAIRS_CAP if dev.type == "cuda" else 2)
+        t0 = time.perf_counter()
+        R = sweep_bench(args, info, c, model, tok, sae, layer, mp["pairs"], E, 0, methods, steps, warmup, tag=f" {kind}")
+        run = R["runner"]
+        st = dict(run.stats)
+        out = {"metric": ("multi-adapter SAE-ablation sweep prompts/s (3 distinct rank-8 per-word LoRA adapters, "
+                          "unmerged, fused into the in-tree GEMMs)" if kind == "lora" else
+                          "low-rank projection-out sweep prompts/s (BASELINE config 4: ranks 1..64 x (1 targeted PCA "
+                          "+ 5 random subspaces), 50 new tokens)"),
+               "value": round(R["value"], 3), "unit": "prompts/s", "n_gpus": 1, "steps": steps, "warmup": warmup,
+               "ms_per_step": round(R["ms"], 2), "pairs_per_step": mp["pairs"], "cells_per_pair": n_cells,
+               "diverged_frac": round(st["diverged"] / max(1, st["cells"]), 4),
+               "decode_row_steps_per_cell": round(st["decode_row_steps"] / max(1, st["cells"]), 2),
+               "peak_mem_gb": round(torch.cuda.max_memory_reserved(dev) / 1e9, 1) if dev.type == "cuda" else None,
+               "wall_s": round(time.perf_counter() - t0, 1)}
+        if kind == "lora":
+            out["adapters"] = {"n": bank.n, "rank": bank.r, "kp": int(bank.KP), "words": list(bank.names)}
+        release += [R["runner"], R["cur"]]
+        return out
+    finally:
+        if bank is not None:
+            model.set_lora(None)
+            model.enable_fused_geglu()
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -201,6 +456,12 @@ def main() -> None:
     ap.add_argument("--no-config2", action="store_true",
                     help="skip the BASELINE config-2 side measurement (LL-Top-k baseline: batched greedy hints + "
                          "42-layer lens over 3 words x 10 prompts), reported as 'config2' after the timed steps")
+    ap.add_argument("--no-lora-side", action="store_true",
+                    help="skip the multi-adapter side measurement ('lora': the same sweep with 3 distinct rank-8 "
+                         "per-word adapters batched unmerged through the fused LoRA GEMMs, same steps / warmup)")
+    ap.add_argument("--no-lowrank-side", action="store_true",
+                    help="skip the BASELINE config-4 side measurement ('lowrank': projection-out cells, ranks 1..64)")
+    ap.add_argument("--lowrank-steps", type=int, default=4, help="timed steps of the lowrank side measurement")
     ap.add_argument("--tune-gemms", action="store_true",
                     help="run TunableOp over every GEMM shape and save configs/tunableop/<tag>.csv")
     ap.add_argument("--no-tuned-gemms", action="store_true", help="ignore the saved TunableOp results")
@@ -259,175 +520,11 @@ def main() -> None:
         P = int(-D.all_reduce_max(-float(mem_plan["pairs"]), info))
     mem_plan["pairs"] = P
     mem_plan["auto"] = str(args.pairs_per_step) == "auto"
-    batch = P * n_cells + E * P + C
-    runner = SweepRunner(cfg, model, tok, sae, batch=batch, device=dev, layer=layer,
-                         use_graphs=not args.no_graphs, prefix_share=not args.no_prefix_share,
-                         kv_pairs=(E + (3 if C else 2)) * P + 2, layer_resume=not args.no_layer_resume)
-    runner.carry_rows = C
-    runner.trie_decode = not args.no_trie_decode
-    runner.skip_noop_spikes = not args.no_skip_noop
-    templates = runner.build_pairs(cfg.words, cfg.prompts)
     methods = ("sae_targeted", "sae_random")
-
-    def pairs_for(step: int):
-        # pair instance g of the whole job (every rank and step its own): template g mod 30, replicate g div 30,
-        # so a repeated (word, prompt) draws fresh random-latent controls (its targeted cells are the same
-        # experiment and repeat exactly) -- no two ranks or steps run identical random cells
-        base = (step * info.world + info.rank) * P
-        n = len(templates)
-        return [fresh(templates[(base + j) % n], rep=(base + j) // n) for j in range(P)]
-
-    # prologue: baselines of the first step's pairs, SAE threshold calibration on their residuals -- one copy of
-    # each (word, prompt) template in template order, so every rank calibrates on the same rows (a pair's baseline
-    # does not depend on its replicate; with P >= 30 every rank's first step holds every template)
-    cur = pairs_for(0)
-    runner.run_baselines(cur)
-    first = {}
-    for p in cur:
-        first.setdefault((p.word, p.pidx), p)
-    order_keys = [(t.word, t.pidx) for t in templates]
-    mine = {k: first[k].resid for k in order_keys if k in first and first[k].resid is not None
-            and first[k].resid.shape[0]}
-    if info.world > 1 and len(mine) < len(templates):
-        # fewer pairs per step than templates: every rank calibrates on the union of the ranks' first-step baselines
-        # (a template's baseline does not depend on its rank or replicate), so the SAE thresholds stay rank-invariant
-        merged = {}
-        for d in D.all_gather_objects({k: v.cpu() for k, v in mine.items()}, info):
-            merged.update(d)
-        mine = {k: merged[k].to(dev) for k in order_keys if k in merged}
-    resid = torch.cat([mine[k] for k in order_keys if k in mine], 0)
-    sae.calibrate(resid)
-    runner._score_pairs(cur)
-    import hashlib
-
-    calib = hashlib.sha256(sae.threshold.float().cpu().numpy().tobytes()).hexdigest()[:16]
-    calib_all = [str(c) for c in D.all_gather_objects(calib, info)]
-    assert len(set(calib_all)) == 1, f"SAE calibration differs across ranks: {calib_all}"
-
-    future = {}
-    staged = {}
-
-    def step(k: int, cur):
-        """Cells of step k; baselines ride along: warmup steps carry the next step's pairs, timed steps
-        k = W, W+E, ... carry the pairs of steps k+1..k+E (one decode for E*P baselines)."""
-        t0 = time.perf_counter()
-        if k < args.warmup:
-            ahead = [k + 1]
-        elif (k - args.warmup) % E == 0:
-            ahead = list(range(k + 1, k + E + 1))
-        else:
-            ahead = []
-        ride = []
-        for j in ahead:
-            future[j] = pairs_for(j)
-            ride += future[j]
-        nb = staged.pop(k, None)
-        if nb is not None and nb.future is None and nb.cells is not None:
-            cells, plan = nb.cells, nb.plan          # staged by the previous step (its tail may be queued)
-        elif nb is not None and nb.future is not None:
-            cells, plan = nb.future.result()
-        else:
-            cells, plan = runner.make_cells(cur, methods), None
-        runner.timings["make_cells"] = runner.timings.get("make_cells", 0.0) + time.perf_counter() - t0
-        # the next step's cells and host edit plan are built on a helper thread while this step's GPU
-        # work runs (when its pairs' baselines are already final); the runner queues the next step's
-        # teacher-forced tail behind this step's lens readout (cross-step pipeline, SweepRunner.stage_next)
-        nxt = future.get(k + 1)
-        if nxt is not None and k + 1 < args.warmup + args.steps:
-            fut = runner.prefetch(nxt, methods) if all(p.resid is not None for p in nxt) else None
-            staged[k + 1] = NextBatch(nxt, methods, future=fut)
-            # never across the warmup -> timed boundary: the first timed step runs its own teacher-forced tail,
-            # so the timed window holds exactly its K steps' tails (the last timed step stages nothing either)
-            if not args.no_pipeline and k + 1 != args.warmup:
-                runner.stage_next(staged[k + 1])
-        # the records of step k are assembled on a host thread while step k+1's GPU work runs; decode
-        # tails carry into the next step except out of warmup and out of the last timed step
-        drain = k < args.warmup or k == args.warmup + args.steps - 1
-        res = runner.run_cells_async(cur, cells, ride_along=ride, drain=drain, plan=plan)
-        return future.pop(k + 1), res, time.perf_counter() - t0
-
-    def cells_of(k):
-        return range(P * n_cells)
-
-    gathers = []
-
-    def gather_results(res):
-        """The DP sweep's result collection, every step: each rank's compact cell records (readouts,
-        NLLs, leak, n_gen, LL-Top-5 ids) are all-gathered (one RCCL all-gather over xGMI), issued
-        asynchronously on the collective's own stream (overlaps the next step's compute; no per-step
-        lock-step of the ranks) and completed before the timed window closes."""
-        if info.world <= 1:
-            return None
-        rec = torch.tensor([[r["p_secret_mean"], r["p_secret_final"], r["p_secret_max"], r["nll_edit"],
-                             r["nll_self"], float(r["leak"]), float(r["n_gen"])] +
-                            [float(t) for t in (list(r["topk_ids"]) + [-1] * 5)[:5]] for r in res],
-                           dtype=torch.float64)
-        if on_gpu:
-            rec = rec.pin_memory().to(dev, non_blocking=True)
-        out, work = D.all_gather_tensor_async(rec, info)
-        gathers.append((out, work, rec))
-        return out
-
-    def finish_gathers():
-        for out, work, rec in gathers:
-            if work is not None:
-                work.wait()
-        n = sum(int(out.shape[0]) for out, _, _ in gathers)
-        gathers.clear()
-        return n
-
-    for k in range(args.warmup):
-        cur, res, dt = step(k, cur)
-        gather_results(res.result())
-        if info.is_main:
-            print(f"[bench] warmup step {k + 1}/{args.warmup} done", file=sys.stderr, flush=True)
-    finish_gathers()
-    runner.precapture_graphs()          # one-time setup: every decode row-bucket graph
-    # everything allocated so far (model, tokenizer tables, caches) is long-lived: keep the cyclic GC from
-    # rescanning it on every collection inside the timed steps (pauses the launch thread otherwise)
-    gc.collect()
-    gc.freeze()
-    if on_gpu:
-        torch.cuda.synchronize()
-    D.barrier(info)
-    for kk in runner.stats:
-        runner.stats[kk] = 0
-    t0 = time.perf_counter()
-    n_done = 0
-    pending = None
-    marks = runner.__dict__.setdefault("phase_marks", []) if os.environ.get("TB_PHASE_MARKS") else None
-    for k in range(args.warmup, args.warmup + args.steps):
-        if marks is not None:
-            marks.append((f"step{k}", time.monotonic_ns()))
-        cur, res, dt = step(k, cur)
-        if pending is not None:
-            done = pending.result()
-            n_done += len(done)
-            gather_results(done)
-        pending = res
-        if args.profile_steps and info.is_main:
-            ph = " ".join(f"{kk}={v:.3f}" for kk, v in runner.timings.items())
-            runner.timings.clear()
-            print(f"[step {k}] {len(cells_of(k))} cells in {dt:.3f}s  {ph}", file=sys.stderr, flush=True)
-        elif info.is_main:      # host-side progress (no sync): long runs keep writing
-            print(f"[bench] step {k - args.warmup + 1}/{args.steps} issued at {time.perf_counter() - t0:.1f}s",
-                  file=sys.stderr, flush=True)
-    done = pending.result()
-    n_done += len(done)
-    gather_results(done)
-    gathered_rows = finish_gathers()
-    assert info.world <= 1 or gathered_rows == n_done * info.world, "result all-gather incomplete"
-    if on_gpu:
-        torch.cuda.synchronize()
-    D.barrier(info)
-    if marks is not None:
-        marks.append(("end", time.monotonic_ns()))
-    mine = time.perf_counter() - t0
-    per_rank = [float(v) for v in D.all_gather_objects(mine, info)]
-    elapsed = D.all_reduce_max(mine, info)
-    total_cells = D.all_reduce_max(float(n_done), info) * info.world   # every rank does the same count
-    value = total_cells / elapsed
-    ms = 1000.0 * elapsed / max(args.steps, 1)
+    R = sweep_bench(args, info, cfg, model, tok, sae, layer, P, E, C, methods, args.steps, args.warmup)
+    value, elapsed, ms, per_rank = R["value"], R["elapsed"], R["ms"], R["per_rank"]
+    n_done, gathered_rows, calib_all, runner, cur, batch = (R["n_done"], R["gathered_rows"], R["calib_all"],
+                                                            R["runner"], R["cur"], R["batch"])
     peak_gb = round(torch.cuda.max_memory_reserved(dev) / 1e9, 1) if on_gpu else None   # of the timed steps
     if on_gpu:      # the peak as a fraction of the device: torch's reserved peak + what lives outside its allocator
         mem_plan["peak_hbm_frac"] = round((torch.cuda.max_memory_reserved(dev) + mem_plan["outside_torch"]) /
@@ -543,6 +640,8 @@ def main() -> None:
             },
             "config2": config2,
             "post_forcing": forcing,
+            "lora": None,
+            "lowrank": None,
             # work actually done in the timed steps (rank 0): cells whose greedy tokens left their
             # baseline's decode from the divergence through all blocks; the rest are exact replays of
             # the blocks after the hooked layer (see pipelines/sweep.py::_run_batch_resume)
@@ -573,11 +672,23 @@ def main() -> None:
                                                   for p in cur) / max(1, sum(len(p.gen_toks) - 1 for p in cur))), 3),
             },
         }
+        phase_marks = list(getattr(runner, "phase_marks", []))
+        if side:
+            # after the headline's records are taken: the multi-adapter and low-rank sweeps (each its own P, warmup
+            # and timed steps; the headline's decode state is released first)
+            rel = [runner, cur]
+            runner = cur = None
+            if not args.no_lora_side and args.lora_rank == 0:
+                out["lora"] = side_sweep(args, info, cfg, model, tok, sae, layer, spec, "lora",
+                                         ("sae_targeted", "sae_random"), args.steps, args.warmup, rel)
+            if not args.no_lowrank_side:
+                out["lowrank"] = side_sweep(args, info, cfg, model, tok, sae, layer, spec, "lowrank",
+                                            ("proj_targeted", "proj_random"), args.lowrank_steps, 1, rel)
         print(json.dumps(out), flush=True)
     marks_path = os.environ.get("TB_PHASE_MARKS")
     if marks_path and info.is_main:
         with open(marks_path, "w") as f:
-            json.dump(getattr(runner, "phase_marks", []), f)
+            json.dump(phase_marks, f)
     if args.tune_gemms:
         flush_tuned_gemms()
     D.destroy(info)

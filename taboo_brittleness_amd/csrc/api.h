@@ -68,9 +68,11 @@ void tb_head_fused4(const uint16_t* A, const uint16_t* W, float* part, float cap
                     float* tgt_logit, int32_t* nxt, float* nll_self, float* nll_tgt, int M, int N, int K, hipStream_t st);
 // cs: the RoPE table as bf16 (cos, sin) pairs [max_pos, 128, 2] (the fp32 tables rounded once: the epilogue rounds
 // them to bf16 anyway, rope.hip's chain)
+// a2 / k0 (multi-adapter LoRA): the GEMM's A operand is [A (k0 columns) | a2 (K - k0 columns)] (two sources, no copy)
 void tb_gemm4_qkv_rope(const uint16_t* A, const uint16_t* W, const int32_t* pos, const int32_t* slot_of_row,
                        const uint16_t* cs, uint16_t* q_out, uint16_t* kc, uint16_t* vc, int M, int K,
-                       int Hq, int Hkv, int S, int max_pos, int tile_rows, hipStream_t st);
+                       int Hq, int Hkv, int S, int max_pos, int tile_rows, hipStream_t st, const uint16_t* a2 = nullptr,
+                       int k0 = 0);
 bool tb_register_softcap_compact(float cap, const uint16_t* tab, int lo, int hi, float sat);
 bool tb_softcap_compact(const uint16_t* x, float* y, int n, float cap, hipStream_t st);
 bool tb_gemm4_ok(int M, int N, int K);
@@ -82,7 +84,7 @@ void tb_add_rmsnorm2_part(uint16_t* h, const float* part, int ks, const uint16_t
 void tb_gemm4_splitk(const uint16_t* A, const uint16_t* W, uint16_t* out, float* ws, int M, int N, int K, int ldo,
                      int epi, int tile_rows, int ks, hipStream_t st);
 void tb_gemm4(const uint16_t* A, const uint16_t* W, void* C, const float* bias, const float* thr, int M, int N, int K,
-              int ldc, int epi, int tile_rows, hipStream_t st);
+              int ldc, int epi, int tile_rows, hipStream_t st, const uint16_t* a2 = nullptr, int k0 = 0);
 void tb_gemm_nt(const uint16_t* A, const uint16_t* W, void* C, const float* bias, const float* thr, int M, int N,
                 int K, int ldc, int epi, hipStream_t st);
 void tb_lowrank_edit(uint16_t* h, uint16_t* x_next, const uint8_t* apply, const int32_t* idx, const int32_t* cnt,
@@ -141,7 +143,13 @@ void tb_share_group(int64_t* gid, const int32_t* tok, int64_t* rep, int64_t* grp
 bool tb_gemm_ring_ok(int M, int N, int K, int epi, int bm, int bn, int var);
 int tb_gemm_ring_tiles(int epi, int* bm, int* bn, int cap);
 void tb_gemm_ring(const uint16_t* A, const uint16_t* W, uint16_t* C, int M, int N, int K, int ldc, int epi, int bm,
-                  int bn, int var, hipStream_t st);
+                  int bn, int var, hipStream_t st, const uint16_t* a2 = nullptr, int k0 = 0);
 void tb_gemm_ring_qkv_rope(const uint16_t* A, const uint16_t* W, const int32_t* pos, const int32_t* slot_of_row,
                            const uint16_t* cs, uint16_t* q_out, uint16_t* kc, uint16_t* vc, int M,
-                           int K, int Hq, int Hkv, int S, int max_pos, int bm, int bn, int var, hipStream_t st);
+                           int K, int Hq, int Hkv, int S, int max_pos, int bm, int bn, int var, hipStream_t st,
+                           const uint16_t* a2 = nullptr, int k0 = 0);
+// multi-adapter LoRA down-projection: T[m, c] = bf16(x[m] . A_all[c]) where column c belongs to the row's adapter
+// (c < nsr and (c % nr) / r == adapter[m]), else 0; T is [M, N] (N = A_all rows, the padded LoRA width)
+bool tb_lora_t_ok(int M, int N, int K, int bm, int bn);
+void tb_lora_t(const uint16_t* x, const uint16_t* a_all, uint16_t* t, const int32_t* adapter, int M, int N, int K,
+               int nsr, int nr, int r, int bm, int bn, hipStream_t st);

@@ -41,16 +41,15 @@ __device__ __forceinline__ v4i16 ds_read_tr16(const uint16_t* lds_ptr) {
 
 __device__ __forceinline__ bf16x8 as_bf16x8(const uint4& u) { return __builtin_bit_cast(bf16x8, u); }
 
-// SPLIT = true: the 4 waves of a workgroup split one (query block, kv head) item's key range and merge
-// through LDS (long contexts).  SPLIT = false (block-table mode only): every wave owns its own item and
-// walks all of its keys — for short contexts (the sweep's teacher-forced tails: <= ~100 keys) where
-// a 4-way key split leaves waves idle and the merge costs more than it saves.
-template <int HD, int G, bool SPLIT = true>
+// The 4 waves of a workgroup split one (query block, kv head) item's key range and merge through LDS.  Prefill
+// (dense [B, T]) and long packed contexts; short packed rows (the sweep's teacher-forced tails) run
+// attn_tail_exact_kernel, the decode's numerics.
+template <int HD, int G>
 __global__ void __launch_bounds__(256) attn_cache_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
     uint16_t* __restrict__ out, const int32_t* __restrict__ pos, const int32_t* __restrict__ slot, int T, int Hq,
-    int Hkv, int S, float scale, float softcap, int window, const int32_t* __restrict__ blk, int nitems = 0,
-    int bw = 3, const uint16_t* __restrict__ pkc = nullptr, const uint16_t* __restrict__ pvc = nullptr) {
+    int Hkv, int S, float scale, float softcap, int window, const int32_t* __restrict__ blk, int bw = 3,
+    const uint16_t* __restrict__ pkc = nullptr, const uint16_t* __restrict__ pvc = nullptr) {
   constexpr int P = 16 / G;        // query positions per workgroup
   constexpr int KS = HD / 32;      // MFMA k-steps over head_dim
   constexpr int DT = HD / 16;      // 16-wide output dim tiles
@@ -66,18 +65,9 @@ __global__ void __launch_bounds__(256) attn_cache_kernel(
   // {first row, rows (<= P), cache slot} over packed rows (varlen prefill / teacher forcing).
   // bw = 5: blk[i] also holds (prefix slot, prefix length): keys [0, plen) are read from that slot of
   // the shared prefix cache (pkc, pvc) — the pair's baseline KV — instead of the row's own slot.
-  int kh = blockIdx.y;
+  const int kh = blockIdx.y;
   int rbase, nvalid, cs, ps = 0, np = 0;
-  if constexpr (!SPLIT) {
-    const int item = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (item >= nitems) return;                 // wave-uniform; no workgroup barrier in this variant
-    const int bi = item / Hkv;
-    kh = item % Hkv;
-    rbase = blk[bw * bi];
-    nvalid = blk[bw * bi + 1];
-    cs = blk[bw * bi + 2];
-    if (bw == 5) { ps = blk[bw * bi + 3]; np = blk[bw * bi + 4]; }
-  } else if (blk != nullptr) {
+  if (blk != nullptr) {
     rbase = blk[bw * blockIdx.x];
     nvalid = blk[bw * blockIdx.x + 1];
     cs = blk[bw * blockIdx.x + 2];
@@ -145,7 +135,7 @@ __global__ void __launch_bounds__(256) attn_cache_kernel(
   uint16_t* plds = plds_all + wid * 16 * PSTR;
   const float inv_cap = softcap > 0.f ? 1.f / softcap : 0.f;
 
-  for (int kb = kstart + (SPLIT ? wid * 32 : 0); kb <= kmax; kb += (SPLIT ? 4 * 32 : 32)) {
+  for (int kb = kstart + wid * 32; kb <= kmax; kb += 4 * 32) {
     // ---- stage V block (32 keys x HD) into this wave's LDS, coalesced 1 KB per instruction
     constexpr int VCH = HD / 8;                // 16-B chunks per key row
     constexpr int VIT = 32 * VCH / 64;         // instructions per lane
@@ -242,28 +232,6 @@ __global__ void __launch_bounds__(256) attn_cache_kernel(
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
 
-  if constexpr (!SPLIT) {
-    // own item: normalise in registers, transpose through this wave's staging LDS, 16-B stores
-    uint16_t* ob = vlds;                                  // [16][HD] bf16 <= 32 * VSTR halves
-    float inv[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) inv[i] = l_r[i] > 0.f ? 1.f / l_r[i] : 0.f;
-#pragma unroll
-    for (int d = 0; d < DT; ++d)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) ob[(4 * grp + i) * HD + d * 16 + col] = f2bf(o_acc[d][i] * inv[i]);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    for (int e = lane; e < 16 * (HD / 8); e += 64) {
-      const int r = e / (HD / 8), c8 = (e % (HD / 8)) * 8;
-      const int t = r / G, h = kh * G + (r % G);
-      if (t < nvalid)
-        *reinterpret_cast<uint4*>(out + (((size_t)rbase + t) * Hq + h) * HD + c8) =
-            *reinterpret_cast<const uint4*>(ob + r * HD + c8);
-    }
-    return;
-  }
   // ---- merge the 4 waves: publish (m, l) and O (fp32, reusing the V staging area)
   __syncthreads();
   float* ofin = reinterpret_cast<float*>(smem);   // [4][16][HD] fp32 = 64 KB for HD=256
@@ -306,43 +274,6 @@ __global__ void __launch_bounds__(256) attn_cache_kernel(
     *reinterpret_cast<uint4*>(out + (((size_t)rbase + t) * Hq + h) * HD + c8) = pack8(o8);
   }
 }
-
-template <int HD, int G>
-void launch_attn(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, uint16_t* out, const int32_t* pos,
-                 const int32_t* slot, int B, int T, int Hq, int Hkv, int S, float scale, float softcap, int window,
-                 hipStream_t st, const int32_t* blk = nullptr, int nblk = 0, int bw = 3,
-                 const uint16_t* pkc = nullptr, const uint16_t* pvc = nullptr) {
-  constexpr int P = 16 / G;
-  const size_t lds = (size_t)tb_attention_lds_bytes(HD);
-  static bool attr_set = false;   // > 64 KB dynamic LDS needs the opt-in (first call is never captured)
-  if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_cache_kernel<HD, G>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr_set = true;
-  }
-  if (blk != nullptr && S <= 512) {
-    static bool attr_short = false;
-    if (!attr_short) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_cache_kernel<HD, G, false>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      attr_short = true;
-    }
-    const int nitems = nblk * Hkv;
-    hipLaunchKernelGGL((attn_cache_kernel<HD, G, false>), dim3((nitems + 3) / 4), dim3(256), lds, st, q, kc, vc, out,
-                       pos, slot, T, Hq, Hkv, S, scale, softcap, window, blk, nitems, bw, pkc, pvc);
-    return;
-  }
-  if (blk != nullptr) {
-    dim3 grid(nblk, Hkv, 1);
-    hipLaunchKernelGGL((attn_cache_kernel<HD, G>), grid, dim3(256), lds, st, q, kc, vc, out, pos, slot, T, Hq, Hkv,
-                       S, scale, softcap, window, blk, 0, bw, pkc, pvc);
-    return;
-  }
-  dim3 grid((T + P - 1) / P, Hkv, B);
-  hipLaunchKernelGGL((attn_cache_kernel<HD, G>), grid, dim3(256), lds, st, q, kc, vc, out, pos, slot, T, Hq, Hkv, S,
-                     scale, softcap, window, (const int32_t*)nullptr, 0);
-}
-
 
 // ---------------------------------------------------------------------------
 // Decode (one query position per sequence): one workgroup per (sequence, kv
@@ -699,6 +630,194 @@ __global__ void __launch_bounds__(256) attn_decode_wave_kernel(
 }
 
 
+// Packed rows (block-table mode: the sweep's teacher-forced tails and NLL passes) with the DECODE kernel's numerics,
+// bit for bit.  A tail row at position p is the same query the greedy decode computes at p (the reuse levels replay
+// positions >= a cell's first edit as one packed forward instead of one decode step each), so the tail must round
+// exactly like attn_decode_wave_kernel or a resumed cell's records drift from a from-scratch generation's
+// (tests/test_exact_9b_gpu.py).  Per (block of P = 16 / G positions of one sequence, kv head) one wave:
+//  * scores: the decode's MFMA chain (Q fragment A, K fragment B, head_dim in 32-deep steps) for the block's 16
+//    (position, head) rows at once -- an MFMA output row depends on its own A row only, so every row's scores are
+//    the decode's; scaled, softcapped and masked (keys in [kmin_r, pos_r]) per row, into LDS key-major;
+//  * softmax per row as the decode does it: exact max, p = rbf(exp(s - m)), l = the lane-strided sum from kmin_r +
+//    wave butterfly, in the same order;
+//  * O = sum_j p_j v_j on the VALU in ascending key order, one fp32 FMA chain per (row, dim) -- the decode's chain;
+//    keys outside a row's range carry p = 0, and adding +-0 leaves an fp32 sum unchanged;
+//  * out = O * (1 / l), bf16.
+// Each wave reads the block's K / V once for its 16 rows (the decode kernel would read them once per row).
+template <int HD, int G>
+__global__ void __launch_bounds__(256) attn_tail_exact_kernel(
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
+    uint16_t* __restrict__ out, const int32_t* __restrict__ pos, int Hq, int Hkv, int S, float scale, float softcap,
+    int window, const int32_t* __restrict__ blk, int nitems, int bw, const uint16_t* __restrict__ pkc,
+    const uint16_t* __restrict__ pvc) {
+  constexpr int P = 16 / G;
+  constexpr int KS = HD / 32;
+  constexpr int DPL = HD / 64;
+  constexpr int VCH = 8;
+  using VT = typename vrow_t<DPL>::type;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int item = blockIdx.x * 4 + wid;
+  if (item >= nitems) return;                     // wave-uniform; the waves never synchronise
+  const int SS = (S + 15) & ~15;
+  float* sc = reinterpret_cast<float*>(smem) + (size_t)wid * 16 * SS;   // key-major [SS][16] scores / weights
+  const int bi = item / Hkv, kh = item % Hkv;
+  const int rbase = blk[bw * bi], nvalid = blk[bw * bi + 1], cs = blk[bw * bi + 2];
+  const int ps = bw == 5 ? blk[bw * bi + 3] : 0, np = bw == 5 ? blk[bw * bi + 4] : 0;
+  const int grp = lane >> 4, col = lane & 15;
+  const uint16_t* kbase = kc + ((size_t)cs * Hkv + kh) * (size_t)S * HD;
+  const uint16_t* vbase = vc + ((size_t)cs * Hkv + kh) * (size_t)S * HD;
+  const uint16_t* kpre = kbase;
+  const uint16_t* vpre = vbase;
+  if (np > 0) {
+    kpre = pkc + ((size_t)ps * Hkv + kh) * (size_t)S * HD;
+    vpre = pvc + ((size_t)ps * Hkv + kh) * (size_t)S * HD;
+  }
+  // row r = (position t = r / G, head kh * G + r % G); per-row key range [kmin_r, kmax_r] as the decode computes it
+  auto rpos = [&](int r) -> int { return (r / G) < nvalid ? pos[(size_t)rbase + r / G] : -1; };
+  auto rkmax = [&](int p) -> int { return p < S ? p : S - 1; };
+  auto rkmin = [&](int p) -> int {
+    int k = 0;
+    if (window > 0) { k = p - window + 1; if (k < 0) k = 0; }
+    return k;
+  };
+  int kmaxb = -1, kminb = 1 << 30;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int p = rpos(r);
+    if (p >= 0) { kmaxb = max(kmaxb, rkmax(p)); kminb = min(kminb, rkmin(p)); }
+  }
+  uint16_t* orow0 = out + (size_t)rbase * Hq * HD;
+  if (kmaxb < 0) {                                  // every row is padding: zeros, as the decode writes them
+    for (int e = lane; e < nvalid * G * HD; e += 64) {
+      const int t = e / (G * HD), rem = e % (G * HD);
+      orow0[(size_t)t * Hq * HD + kh * G * HD + rem] = 0;
+    }
+    return;
+  }
+  // ---- scores (the decode's MFMA operands: query row (r) fragments, key rows clamped into [kminb, kmaxb])
+  const int pA = rpos(col);                         // this lane's A row
+  bf16x8 qa[KS];
+  {
+    const uint16_t* qrow = q + (((size_t)rbase + col / G) * Hq + kh * G + col % G) * HD + grp * 8;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      uint4 u = {0, 0, 0, 0};
+      if (pA >= 0) u = *reinterpret_cast<const uint4*>(qrow + ks * 32);
+      qa[ks] = as_bf16x8(u);
+    }
+  }
+  int pC[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) pC[i] = rpos(4 * grp + i);
+  const float inv_cap = softcap > 0.f ? 1.f / softcap : 0.f;
+  for (int t = kminb >> 4; t <= kmaxb >> 4; ++t) {
+    const int kk = t * 16 + col;
+    const int kr = kk < kminb ? kminb : (kk > kmaxb ? kmaxb : kk);
+    const uint16_t* krow = (kr < np ? kpre : kbase) + (size_t)kr * HD + grp * 8;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[ks], as_bf16x8(*reinterpret_cast<const uint4*>(krow + ks * 32)),
+                                                    acc, 0, 0, 0);
+    float sv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float s = acc[i] * scale;
+      if (softcap > 0.f) s = tanhf(s * inv_cap) * softcap;
+      const int p = pC[i];
+      sv[i] = (p >= 0 && kk >= rkmin(p) && kk <= rkmax(p)) ? s : -INFINITY;
+    }
+    if (kk < SS) *reinterpret_cast<float4*>(sc + (size_t)kk * 16 + 4 * grp) = make_float4(sv[0], sv[1], sv[2], sv[3]);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // ---- softmax weights per row, the decode's order; keys of the block's range outside the row's get p = 0
+  float inv_l[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int p = rpos(r);
+    inv_l[r] = 0.f;
+    if (p < 0) {
+      for (int j = kminb + lane; j <= kmaxb; j += 64) sc[(size_t)j * 16 + r] = 0.f;
+      continue;
+    }
+    const int k0 = rkmin(p), k1 = rkmax(p);
+    float m = -INFINITY;
+    for (int j = k0 + lane; j <= k1; j += 64) m = fmaxf(m, sc[(size_t)j * 16 + r]);
+    m = wave_max(m);
+    float l = 0.f;
+    for (int j = k0 + lane; j <= k1; j += 64) {
+      const float pw = m > -INFINITY ? rbf(__expf(sc[(size_t)j * 16 + r] - m)) : 0.f;
+      sc[(size_t)j * 16 + r] = pw;
+      l += pw;
+    }
+    l = wave_sum(l);
+    inv_l[r] = l > 0.f ? 1.f / l : 0.f;
+    for (int j = kminb + lane; j <= kmaxb; j += 64)
+      if (j < k0 || j > k1) sc[(size_t)j * 16 + r] = 0.f;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // ---- O = sum_j p_j v_j: each lane owns DPL dims of all 16 rows, keys ascending, V rows prefetched VCH ahead
+  float o[16][DPL];
+#pragma unroll
+  for (int r = 0; r < 16; ++r)
+#pragma unroll
+    for (int d = 0; d < DPL; ++d) o[r][d] = 0.f;
+  auto vload = [&](int j, VT (&v)[VCH]) {
+#pragma unroll
+    for (int u = 0; u < VCH; ++u) {
+      const int jj = j + u <= kmaxb ? j + u : kmaxb;
+      v[u] = *reinterpret_cast<const VT*>((jj < np ? vpre : vbase) + (size_t)jj * HD + lane * DPL);
+    }
+  };
+  auto accum = [&](int j, const VT (&v)[VCH]) {
+#pragma unroll
+    for (int u = 0; u < VCH; ++u) {
+      if (j + u > kmaxb) break;
+      float vf[DPL];
+      vrow_t<DPL>::unpack(v[u], vf);
+      const float4* pr = reinterpret_cast<const float4*>(sc + (size_t)(j + u) * 16);
+#pragma unroll
+      for (int r4 = 0; r4 < 4; ++r4) {
+        const float4 pw4 = pr[r4];
+        const float pwv[4] = {pw4.x, pw4.y, pw4.z, pw4.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int d = 0; d < DPL; ++d) o[4 * r4 + i][d] += pwv[i] * vf[d];
+      }
+    }
+  };
+  VT va[VCH], vb[VCH];
+  vload(kminb, va);
+  for (int j = kminb; j <= kmaxb; j += 2 * VCH) {
+    if (j + VCH <= kmaxb) vload(j + VCH, vb);
+    accum(j, va);
+    if (j + VCH <= kmaxb) {
+      if (j + 2 * VCH <= kmaxb) vload(j + 2 * VCH, va);
+      accum(j + VCH, vb);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    if (r / G >= nvalid) continue;
+    float v[DPL];
+#pragma unroll
+    for (int d = 0; d < DPL; ++d) v[d] = o[r][d] * inv_l[r];
+    uint16_t* dst = out + (((size_t)rbase + r / G) * Hq + kh * G + r % G) * HD + lane * DPL;
+    if constexpr (DPL == 4) {
+      *reinterpret_cast<uint2*>(dst) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+    } else {
+      *reinterpret_cast<uint32_t*>(dst) = pack2(v[0], v[1]);
+    }
+  }
+}
+
+
 // Decode, one 4-wave workgroup per (row, kv head): attn_decode_wave_kernel's arithmetic spread over 4 waves, for the
 // small decode buckets (<= 64 rows: 2 or fewer waves per SIMD in the wave kernel, each walking its keys alone).
 // Bit-identical to the wave kernel per row (so switching kernels by row count keeps the decode batch-invariant):
@@ -850,6 +969,45 @@ __global__ void __launch_bounds__(256) attn_decode_split_kernel(
     *reinterpret_cast<uint32_t*>(dst) = pack2(r[0], r[1]);
   }
 }
+
+template <int HD, int G>
+void launch_attn(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, uint16_t* out, const int32_t* pos,
+                 const int32_t* slot, int B, int T, int Hq, int Hkv, int S, float scale, float softcap, int window,
+                 hipStream_t st, const int32_t* blk = nullptr, int nblk = 0, int bw = 3,
+                 const uint16_t* pkc = nullptr, const uint16_t* pvc = nullptr) {
+  constexpr int P = 16 / G;
+  const size_t lds = (size_t)tb_attention_lds_bytes(HD);
+  static bool attr_set = false;   // > 64 KB dynamic LDS needs the opt-in (first call is never captured)
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_cache_kernel<HD, G>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_set = true;
+  }
+  if (blk != nullptr && S <= 512) {
+    // packed tails / NLL passes: the decode's numerics (attn_tail_exact_kernel), 4 independent waves per workgroup
+    const size_t lds_t = (size_t)4 * 16 * ((S + 15) & ~15) * sizeof(float);
+    static size_t attr_tail = 65536;
+    if (lds_t > attr_tail) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_tail_exact_kernel<HD, G>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      attr_tail = 160 * 1024;
+    }
+    const int nitems = nblk * Hkv;
+    hipLaunchKernelGGL((attn_tail_exact_kernel<HD, G>), dim3((nitems + 3) / 4), dim3(256), lds_t, st, q, kc, vc, out,
+                       pos, Hq, Hkv, S, scale, softcap, window, blk, nitems, bw, pkc, pvc);
+    return;
+  }
+  if (blk != nullptr) {
+    dim3 grid(nblk, Hkv, 1);
+    hipLaunchKernelGGL((attn_cache_kernel<HD, G>), grid, dim3(256), lds, st, q, kc, vc, out, pos, slot, T, Hq, Hkv,
+                       S, scale, softcap, window, blk, bw, pkc, pvc);
+    return;
+  }
+  dim3 grid((T + P - 1) / P, Hkv, B);
+  hipLaunchKernelGGL((attn_cache_kernel<HD, G>), grid, dim3(256), lds, st, q, kc, vc, out, pos, slot, T, Hq, Hkv, S,
+                     scale, softcap, window, (const int32_t*)nullptr);
+}
+
 
 // rows at or below which the decode (S <= 2048, HD 256, G 2 / 4) runs attn_decode_split_kernel (same bits), for rows
 // with their own keys only / rows reading a shared prefix: at 64 rows 15-18 % faster than the one-wave kernel (too

@@ -546,6 +546,103 @@ void gemm4_qkv_rope(torch::Tensor x, torch::Tensor w, torch::Tensor pos, torch::
                     (int)tile_rows, cur_stream());
 }
 
+// ---- multi-adapter LoRA (models/lora.py): two-source A operands [x (k0 columns) | T (K - k0 columns)] of the in-tree
+// GEMMs (gemm4 / ring, same K chain as one [M, K] operand: batch-invariant, every fused epilogue kept) and the masked
+// down-projection T = x A_all^T (only the row's adapter's columns, ring RG_LMASK)
+static void l2a_check(const torch::Tensor& x, const torch::Tensor& a2, const torch::Tensor& W, int& M, int& K, int& k0) {
+  IN_BF16(x); IN_BF16(a2); IN_BF16(W);
+  TORCH_CHECK(W.dim() == 2, "l2a: W must be [N, K]");
+  k0 = x.size(-1);
+  M = x.numel() / k0;
+  K = W.size(1);
+  TORCH_CHECK(a2.numel() == (int64_t)M * (K - k0), "l2a: a2 must be [M, K - k0]");
+  TORCH_CHECK(k0 > 0 && k0 < K && k0 % 128 == 0 && K % 128 == 0, "l2a: k0 and K must be multiples of 128, k0 < K");
+}
+
+void gemm4_l2a(torch::Tensor x, torch::Tensor a2, torch::Tensor W, torch::Tensor C, int64_t epi, int64_t tile_rows) {
+  int M, K, k0;
+  l2a_check(x, a2, W, M, K, k0);
+  IN_BF16(C);
+  const int N = W.size(0);
+  TORCH_CHECK(tb_gemm4_ok(M, N, K) && (epi == 0 || epi == 3) && (tile_rows == 256 || tile_rows == 128),
+              "gemm4_l2a: N % 256, epi 0 | 3, tile_rows 256 | 128");
+  const int64_t ncols = epi == 3 ? N / 2 : N;
+  TORCH_CHECK(C.numel() == (int64_t)M * ncols, "gemm4_l2a: C shape");
+  c10::DeviceGuard g(x.device());
+  tb_gemm4(cbf(x), cbf(W), C.data_ptr(), nullptr, nullptr, M, N, K, (int)ncols, (int)epi, (int)tile_rows, cur_stream(),
+           cbf(a2), k0);
+}
+
+void gemm_ring_l2a(torch::Tensor x, torch::Tensor a2, torch::Tensor W, torch::Tensor C, int64_t epi, int64_t bm,
+                   int64_t bn) {
+  int M, K, k0;
+  l2a_check(x, a2, W, M, K, k0);
+  IN_BF16(C);
+  const int N = W.size(0);
+  TORCH_CHECK((epi == 0 || epi == 3) && tb_gemm_ring_ok(M, N, K, (int)epi, (int)bm, (int)bn, 1),
+              "gemm_ring_l2a: unsupported tile / shape (144 KB ring)");
+  const int64_t ncols = epi == 3 ? N / 2 : N;
+  TORCH_CHECK(C.numel() == (int64_t)M * ncols, "gemm_ring_l2a: C shape");
+  c10::DeviceGuard g(x.device());
+  tb_gemm_ring(cbf(x), cbf(W), bf(C), M, N, K, (int)ncols, (int)epi, (int)bm, (int)bn, 1, cur_stream(), cbf(a2), k0);
+}
+
+static void qkv_l2a_check(const torch::Tensor& pos, const torch::Tensor& slot_of_row, const torch::Tensor& cs,
+                          const torch::Tensor& q_out, const torch::Tensor& kc, const torch::Tensor& vc, int M, int64_t Hq,
+                          int64_t Hkv, const torch::Tensor& W) {
+  IN_I32(pos); IN_I32(slot_of_row); IN_BF16(cs); IN_BF16(q_out); IN_BF16(kc); IN_BF16(vc);
+  TORCH_CHECK(pos.numel() == M && slot_of_row.numel() == M, "qkv_l2a: pos / slot_of_row numel");
+  TORCH_CHECK(W.size(0) == (Hq + 2 * Hkv) * 256, "qkv_l2a: w rows");
+  TORCH_CHECK(q_out.numel() == (int64_t)M * Hq * 256, "qkv_l2a: q_out shape");
+  TORCH_CHECK(kc.dim() == 4 && kc.size(1) == Hkv && kc.size(3) == 256 && vc.sizes() == kc.sizes(),
+              "qkv_l2a: cache shape [slots, Hkv, S, 256]");
+  TORCH_CHECK(cs.dim() == 3 && cs.size(1) == 128 && cs.size(2) == 2, "qkv_l2a: rope table [max_pos, 128, 2]");
+}
+
+void gemm4_qkv_rope_l2a(torch::Tensor x, torch::Tensor a2, torch::Tensor w, torch::Tensor pos, torch::Tensor slot_of_row,
+                        torch::Tensor cs, torch::Tensor q_out, torch::Tensor kc, torch::Tensor vc, int64_t Hq,
+                        int64_t Hkv, int64_t tile_rows) {
+  int M, K, k0;
+  l2a_check(x, a2, w, M, K, k0);
+  qkv_l2a_check(pos, slot_of_row, cs, q_out, kc, vc, M, Hq, Hkv, w);
+  TORCH_CHECK(tile_rows == 256 || tile_rows == 128, "gemm4_qkv_rope_l2a: tile_rows must be 256 or 128");
+  c10::DeviceGuard g(x.device());
+  tb_gemm4_qkv_rope(cbf(x), cbf(w), pos.data_ptr<int32_t>(), slot_of_row.data_ptr<int32_t>(), cbf(cs), bf(q_out),
+                    bf(kc), bf(vc), M, K, Hq, Hkv, kc.size(2), cs.size(0), (int)tile_rows, cur_stream(), cbf(a2), k0);
+}
+
+void gemm_ring_qkv_rope_l2a(torch::Tensor x, torch::Tensor a2, torch::Tensor w, torch::Tensor pos,
+                            torch::Tensor slot_of_row, torch::Tensor cs, torch::Tensor q_out, torch::Tensor kc,
+                            torch::Tensor vc, int64_t Hq, int64_t Hkv, int64_t bm, int64_t bn) {
+  int M, K, k0;
+  l2a_check(x, a2, w, M, K, k0);
+  qkv_l2a_check(pos, slot_of_row, cs, q_out, kc, vc, M, Hq, Hkv, w);
+  TORCH_CHECK(tb_gemm_ring_ok(M, w.size(0), K, 4, (int)bm, (int)bn, 1), "gemm_ring_qkv_rope_l2a: unsupported tile");
+  c10::DeviceGuard g(x.device());
+  tb_gemm_ring_qkv_rope(cbf(x), cbf(w), pos.data_ptr<int32_t>(), slot_of_row.data_ptr<int32_t>(), cbf(cs), bf(q_out),
+                        bf(kc), bf(vc), M, K, Hq, Hkv, kc.size(2), cs.size(0), (int)bm, (int)bn, 1, cur_stream(),
+                        cbf(a2), k0);
+}
+
+// T [M, N] = the row's adapter's columns of x A_all^T (A_all [N, K] = the bank's stacked down-projections, zero-padded
+// rows), every other column 0; adapter [M] int32 (-1: base model, T = 0)
+void lora_t(torch::Tensor x, torch::Tensor a_all, torch::Tensor t, torch::Tensor adapter, int64_t nsr, int64_t nr,
+            int64_t r, int64_t bm, int64_t bn) {
+  IN_BF16(x); IN_BF16(a_all); IN_BF16(t); IN_I32(adapter);
+  const int K = x.size(-1), M = x.numel() / K, N = a_all.size(0);
+  TORCH_CHECK(a_all.dim() == 2 && a_all.size(1) == K, "lora_t: A_all must be [N, K]");
+  TORCH_CHECK(t.numel() == (int64_t)M * N && adapter.numel() == M, "lora_t: T [M, N], adapter [M]");
+  TORCH_CHECK(nsr <= N && nr > 0 && r > 0 && nr % r == 0, "lora_t: widths");
+  TORCH_CHECK(tb_lora_t_ok(M, N, K, (int)bm, (int)bn), "lora_t: unsupported tile / shape");
+  c10::DeviceGuard g(x.device());
+  tb_lora_t(cbf(x), cbf(a_all), bf(t), adapter.data_ptr<int32_t>(), M, N, K, (int)nsr, (int)nr, (int)r, (int)bm,
+            (int)bn, cur_stream());
+}
+
+bool lora_t_ok(int64_t M, int64_t N, int64_t K, int64_t bm, int64_t bn) {
+  return tb_lora_t_ok((int)M, (int)N, (int)K, (int)bm, (int)bn);
+}
+
 // Logit-lens unembedding on the four-wave GEMM (gemm4.hip G4_LENS): bf16 logits and their per-row
 // log-sum-exp (no softcap), so the lens needs no separate row_lse pass.  part: f32 >= M * (V / 128) * 4.
 void lens_gemm(torch::Tensor x, torch::Tensor W, torch::Tensor logits, torch::Tensor part, torch::Tensor lse) {
@@ -935,6 +1032,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm4_splitk_part", &gemm4_splitk_part);
   m.def("add_rmsnorm2_part", &add_rmsnorm2_part);
   m.def("gemm4_qkv_rope", &gemm4_qkv_rope);
+  m.def("gemm4_l2a", &gemm4_l2a);
+  m.def("gemm_ring_l2a", &gemm_ring_l2a);
+  m.def("gemm4_qkv_rope_l2a", &gemm4_qkv_rope_l2a);
+  m.def("gemm_ring_qkv_rope_l2a", &gemm_ring_qkv_rope_l2a);
+  m.def("lora_t", &lora_t);
+  m.def("lora_t_ok", &lora_t_ok);
   m.def("head_fused", &head_fused);
   m.def("lens_gemm", &lens_gemm);
   m.def("lowrank_edit", &lowrank_edit);

@@ -141,10 +141,16 @@ struct G4Rope {
   // split-K (G4_F32 only, tb_gemm4_splitk): the K tiles are cut into ksplit ranges of kchunk tiles; virtual tile v is
   // (split v / nwg, output tile v % nwg) and split s writes its fp32 partial tile to C + s * M * ldc
   int ksplit, kchunk;
+  // two-source A (the L2A instantiations, multi-adapter LoRA): columns [0, k0) of the GEMM's A operand are A (row
+  // stride k0), columns [k0, K) are a2 (row stride K - k0); W is [N, K].  K tiles below k0 / 64 stage from A, the
+  // rest from a2 -- the same K chain as one contiguous [M, K] operand, so the result is the GEMM of the
+  // concatenation [A | a2] bit for bit, with no copy of A
+  const uint16_t* a2;
+  int k0;
 };
 constexpr int G4_CTAB_N = 32768;
 
-template <int BM, int EPI>
+template <int BM, int EPI, bool L2A = false>
 __global__ void __launch_bounds__(G4_THREADS, 1)
 gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, void* __restrict__ C,
              const float* __restrict__ bias, const float* __restrict__ thr, int M, int N, int K, int ldc, G4Rope rp) {
@@ -198,23 +204,31 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
   // holds logical chunk (lane%8) ^ ((row>>1)&7) = (lane%8) ^ ((4*wid + lane/16) & 7) (the same for every i)
   const int lchunk = (lane & 7) ^ ((4 * wid + (lane >> 4)) & 7);
   const int wbytes = G4_BN * K * 2;
-  uint32_t vp[PI], vq[QI];
+  // A's row stride (L2A: the first source's k0 columns; the second source a2 holds the other K - k0)
+  const int KA = L2A ? rp.k0 : K, K2 = K - KA, NT0 = KA >> 6;
+  uint32_t vp[PI], vq[QI], vq2[L2A ? QI : 1];
 #pragma unroll
   for (int i = 0; i < PI; ++i) vp[i] = (uint32_t)((8 * (4 * i + wid) + (lane >> 3)) * K + lchunk * 8) * 2u;
-  int mrows, abytes, nt;
-  void *wtile, *atile;
+  int mrows, abytes, abytes2 = 0, nt;
+  void *wtile, *atile, *atile2 = nullptr;
 #define G4_DESC()                                                                                 \
   do {                                                                                            \
     mrows = min(BM, M - m0);                                                                      \
     wtile = (void*)(W + (size_t)n0 * K + sk * KC * 64);                                           \
-    atile = (void*)(A + (size_t)m0 * K + sk * KC * 64);                                           \
+    atile = (void*)(A + (size_t)m0 * KA + sk * KC * 64);                                          \
     nt = min(KC, NT - sk * KC);                                                                   \
-    abytes = mrows * K * 2;                                                                       \
+    abytes = mrows * KA * 2;                                                                      \
     int ln_ = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));   /* opaque copy: the offsets are recomputed per tile, not hoisted and spilled */ \
     asm volatile("" : "+v"(ln_));                                                                 \
     const int lc_ = (ln_ & 7) ^ ((4 * wid + (ln_ >> 4)) & 7);                                     \
     _Pragma("unroll") for (int i = 0; i < QI; ++i)                                                \
-      vq[i] = (uint32_t)(min(8 * (4 * i + wid) + (ln_ >> 3), mrows - 1) * K + lc_ * 8) * 2u;      \
+      vq[i] = (uint32_t)(min(8 * (4 * i + wid) + (ln_ >> 3), mrows - 1) * KA + lc_ * 8) * 2u;     \
+    if constexpr (L2A) {                                                                          \
+      atile2 = (void*)(rp.a2 + (size_t)m0 * K2);                                                  \
+      abytes2 = mrows * K2 * 2;                                                                   \
+      _Pragma("unroll") for (int i = 0; i < QI; ++i)                                              \
+        vq2[L2A ? i : 0] = (uint32_t)(min(8 * (4 * i + wid) + (ln_ >> 3), mrows - 1) * K2 + lc_ * 8) * 2u; \
+    }                                                                                             \
   } while (0)
   G4_DESC();
 
@@ -246,6 +260,10 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
     if ((g) < PI)                                                                                                  \
       __builtin_amdgcn_raw_ptr_buffer_load_lds(__builtin_amdgcn_make_buffer_rsrc(wtile, 0, wbytes, 0x00020000),    \
                                                (g4_lds_t*)(d_ + (g) * 4096), 16, vp[(g) < PI ? (g) : 0], (t) * 128, 0, 0); \
+    else if (L2A && (t) >= NT0)           /* the second A source: its own descriptor, row offsets, K offset */    \
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(__builtin_amdgcn_make_buffer_rsrc(atile2, 0, abytes2, 0x00020000),  \
+                                               (g4_lds_t*)(d_ + PIMG + ((g) - PI) * 4096), 16,                      \
+                                               vq2[L2A && (g) >= PI ? (g) - PI : 0], ((t) - NT0) * 128, 0, 0);      \
     else                                                                                                           \
       __builtin_amdgcn_raw_ptr_buffer_load_lds(__builtin_amdgcn_make_buffer_rsrc(atile, 0, abytes, 0x00020000),    \
                                                (g4_lds_t*)(d_ + PIMG + ((g) - PI) * 4096), 16,                      \
@@ -754,11 +772,14 @@ bool tb_gemm4_ok(int M, int N, int K) { return M > 0 && N > 0 && N % G4_BN == 0 
 
 // tile_rows: 256 or 128 (output rows per tile; identical numerics)
 void tb_gemm4(const uint16_t* A, const uint16_t* W, void* C, const float* bias, const float* thr, int M, int N, int K,
-              int ldc, int epi, int tile_rows, hipStream_t st) {
+              int ldc, int epi, int tile_rows, hipStream_t st, const uint16_t* a2, int k0) {
   if (M <= 0 || N <= 0) return;
-  const G4Rope rp{};
+  G4Rope rp{};
 #define G4_GO(BM_, E_)                                                                                          \
   hipLaunchKernelGGL((gemm4_kernel<BM_, E_>), dim3(g4_grid((N / G4_BN) * ((M + (BM_) - 1) / (BM_)))),            \
+                     dim3(G4_THREADS), 0, st, A, W, C, bias, thr, M, N, K, ldc, rp)
+#define G4_GO2(BM_, E_)                                                                                         \
+  hipLaunchKernelGGL((gemm4_kernel<BM_, E_, true>), dim3(g4_grid((N / G4_BN) * ((M + (BM_) - 1) / (BM_)))),      \
                      dim3(G4_THREADS), 0, st, A, W, C, bias, thr, M, N, K, ldc, rp)
 #define G4_EPI(BM_)                                   \
   switch (epi) {                                      \
@@ -766,6 +787,18 @@ void tb_gemm4(const uint16_t* A, const uint16_t* W, void* C, const float* bias, 
     case G4_F32: G4_GO(BM_, G4_F32); break;           \
     case G4_JUMPRELU: G4_GO(BM_, G4_JUMPRELU); break; \
     default: G4_GO(BM_, G4_GEGLU);                    \
+  }
+  if (a2 != nullptr) {     // two-source A (host-checked: epi 0 / 3, 0 < k0 < K, both multiples of 64)
+    rp.a2 = a2;
+    rp.k0 = k0;
+    if (tile_rows == 128) {
+      if (epi == G4_GEGLU) G4_GO2(128, G4_GEGLU);
+      else G4_GO2(128, G4_BF16);
+    } else {
+      if (epi == G4_GEGLU) G4_GO2(256, G4_GEGLU);
+      else G4_GO2(256, G4_BF16);
+    }
+    return;
   }
   if (tile_rows == 128) {
     G4_EPI(128)
@@ -873,16 +906,24 @@ void tb_lens_gemm4(const uint16_t* A, const uint16_t* W, uint16_t* logits, float
 
 void tb_gemm4_qkv_rope(const uint16_t* A, const uint16_t* W, const int32_t* pos, const int32_t* slot_of_row,
                        const uint16_t* cs, uint16_t* q_out, uint16_t* kc, uint16_t* vc, int M, int K,
-                       int Hq, int Hkv, int S, int max_pos, int tile_rows, hipStream_t st) {
+                       int Hq, int Hkv, int S, int max_pos, int tile_rows, hipStream_t st, const uint16_t* a2, int k0) {
   if (M <= 0) return;
   const int N = (Hq + 2 * Hkv) * 256, ldc = 0;
   void* C = nullptr;
   const float* bias = nullptr;
   const float* thr = nullptr;
-  const G4Rope rp{pos, slot_of_row, cs, q_out, kc, vc, Hq, Hkv, S, max_pos};
+  G4Rope rp{pos, slot_of_row, cs, q_out, kc, vc, Hq, Hkv, S, max_pos};
+  if (a2 != nullptr) {
+    rp.a2 = a2;
+    rp.k0 = k0;
+    if (tile_rows == 128) G4_GO2(128, G4_ROPE);
+    else G4_GO2(256, G4_ROPE);
+    return;
+  }
   if (tile_rows == 128) G4_GO(128, G4_ROPE);
   else G4_GO(256, G4_ROPE);
 #undef G4_GO
+#undef G4_GO2
 }
 
 namespace {

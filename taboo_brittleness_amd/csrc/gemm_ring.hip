@@ -46,7 +46,7 @@ namespace {
 typedef __attribute__((address_space(3))) void rg_lds_t;
 typedef const __attribute__((address_space(1))) void rg_gbl_t;
 
-enum { RG_BF16 = 0, RG_GEGLU = 3, RG_ROPE = 4 };
+enum { RG_BF16 = 0, RG_GEGLU = 3, RG_ROPE = 4, RG_LMASK = 5 };
 
 struct RingArgs {   // RG_ROPE operands (gemm4.hip G4Rope's subset)
   const int32_t* pos;
@@ -56,6 +56,14 @@ struct RingArgs {   // RG_ROPE operands (gemm4.hip G4Rope's subset)
   uint16_t* kc;
   uint16_t* vc;
   int Hq, Hkv, S, max_pos;
+  // two-source A (L2A instantiations, multi-adapter LoRA; gemm4.hip G4Rope::a2): columns [0, k0) of A from A (row
+  // stride k0), [k0, K) from a2 (row stride K - k0)
+  const uint16_t* a2;
+  int k0;
+  // RG_LMASK (the LoRA down-projection T = x A_all^T of the multi-adapter bank, models/lora.py): output column c is
+  // kept only where it belongs to the row's adapter -- c < nsr and (c % nr) / r == adapter[m] -- else 0
+  const int32_t* adapter;
+  int nsr, nr, r;
 };
 
 template <int N_>
@@ -119,11 +127,11 @@ constexpr int rg_ns(int BM, int BN, int KU, int LKB) {
   return ns;
 }
 
-template <int BM, int BN, int EPI, int KU, int LKB>
+template <int BM, int BN, int EPI, int KU, int LKB, bool L2A = false>
 __global__ void __launch_bounds__(256, LKB <= 80 ? 2 : 1)
 gemm_ring_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, uint16_t* __restrict__ C, int M,
                  int N, int K, int ldc, RingArgs ra) {
-  constexpr bool PAIR = EPI != RG_BF16;
+  constexpr bool PAIR = EPI == RG_GEGLU || EPI == RG_ROPE;
   constexpr int WGN = rg_wgn(BM, BN, PAIR), WGM = rg_wgm(BM, BN, PAIR), NS = rg_ns(BM, BN, KU, LKB);
   constexpr int R = BN + BM, IB = R * 128, SB = KU * IB, NI = R / 8, GLO = NI / 4, GX = NI % 4, GMAX = GLO + (GX ? 1 : 0);
   constexpr int TM = BM / WGM, TN = BN / WGN, FM = TM / 16, FN = TN / 16;
@@ -159,13 +167,23 @@ gemm_ring_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W,
 
   // ---- staging sources: instruction j = wid + 4 q covers image rows 8j .. 8j+7; lane -> row 8j + lane/8, physical
   // chunk lane % 8 holding logical chunk (lane % 8) ^ ((row >> 1) & 7)
+  // (L2A: A rows have stride k0 and K tiles from k0 / 64 on come from a2; an instruction's 8 image rows are all W or
+  // all A rows, BN % 8 == 0)
+  const int KA = L2A ? ra.k0 : K, K2 = K - KA, NT0 = KA >> 6;
   const uint16_t* src[GMAX];
+  const uint16_t* src2[L2A ? GMAX : 1];
+  bool isa[L2A ? GMAX : 1];
 #pragma unroll
   for (int q = 0; q < GMAX; ++q) {
     const int j = wid + 4 * q, lr = min(8 * j + (lane >> 3), R - 1);
     const int lc = (lane & 7) ^ ((lr >> 1) & 7);
-    const uint16_t* row = lr < BN ? W + (size_t)wrow(lr) * K : A + (size_t)min(m0 + lr - BN, M - 1) * K;
+    const int am = min(m0 + lr - BN, M - 1);
+    const uint16_t* row = lr < BN ? W + (size_t)wrow(lr) * K : A + (size_t)am * KA;
     src[q] = row + lc * 8;
+    if constexpr (L2A) {
+      isa[q] = 8 * j >= BN;
+      src2[q] = ra.a2 + (size_t)(isa[q] ? am : 0) * K2 + lc * 8;
+    }
   }
   const bool gx = wid < GX;   // this wave issues GLO + 1 instructions per K tile
   auto issue = [&](int t, int stg) {
@@ -173,9 +191,15 @@ gemm_ring_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W,
     for (int kk = 0; kk < KU; ++kk)
 #pragma unroll
       for (int q = 0; q < GMAX; ++q) {
-        if (q < GLO || gx)
-          __builtin_amdgcn_global_load_lds((rg_gbl_t*)(src[q] + (t * KU + kk) * 64),
+        if (q < GLO || gx) {
+          const int kt = t * KU + kk;
+          const uint16_t* p = src[q] + kt * 64;
+          if constexpr (L2A) {
+            if (isa[q] && kt >= NT0) p = src2[q] + (kt - NT0) * 64;
+          }
+          __builtin_amdgcn_global_load_lds((rg_gbl_t*)p,
                                            (rg_lds_t*)(smem + stg * SB + kk * IB + (wid + 4 * q) * 1024), 16, 0, 0);
+        }
       }
   };
   auto wait_tiles = [&](int n) {   // n stages of this wave's staging left in flight
@@ -272,6 +296,24 @@ gemm_ring_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W,
               make_uint2(pack2(acc[i][j][0], acc[i][j][1]), pack2(acc[i][j][2], acc[i][j][3]));
       }
     }
+  } else if constexpr (EPI == RG_LMASK) {
+#pragma unroll
+    for (int j = 0; j < FM; ++j) {
+      const int m = mb + j * 16;
+      if (m >= M) continue;
+      const int ad = ra.adapter[m];
+#pragma unroll
+      for (int i = 0; i < FN; ++i) {
+        const int n = n0 + wn * TN + i * 16 + 4 * (lane >> 4);
+        float o[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int c = n + q;
+          o[q] = (ad >= 0 && c < ra.nsr && (c % ra.nr) / ra.r == ad) ? acc[i][j][q] : 0.f;
+        }
+        *reinterpret_cast<uint2*>(C + (size_t)m * ldc + n) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
+      }
+    }
   } else if constexpr (EPI == RG_GEGLU) {
     // gate|up rounded to bf16 first: the result equals geglu(bf16 gate|up GEMM output), as gemm4's G4_GEGLU
 #pragma unroll
@@ -360,6 +402,12 @@ void rg_launch(int var, const uint16_t* A, const uint16_t* W, uint16_t* C, int M
                const RingArgs& ra, hipStream_t st) {
   const int tiles = ((M + BM - 1) / BM) * (N / BN);
   constexpr int KU1 = rg_ku1(BM, BN), KU2 = rg_ku2(BM, BN);
+  if (ra.a2 != nullptr) {   // two-source A (multi-adapter LoRA): the 144 KB ring only (host-checked)
+    if constexpr (EPI != RG_LMASK)
+      hipLaunchKernelGGL((gemm_ring_kernel<BM, BN, EPI, KU1, RG_LKB1, true>), dim3(tiles), dim3(256), 0, st, A, W, C, M,
+                         N, K, ldc, ra);
+    return;
+  }
   if (var == 2) {
     if constexpr (KU2 > KU1)
       hipLaunchKernelGGL((gemm_ring_kernel<BM, BN, EPI, KU2, 144>), dim3(tiles), dim3(256), 0, st, A, W, C, M, N, K, ldc,
@@ -374,11 +422,15 @@ void rg_launch(int var, const uint16_t* A, const uint16_t* W, uint16_t* C, int M
 bool rg_has_var2(int bm, int bn) { return rg_ku2(bm, bn) > rg_ku1(bm, bn); }
 
 template <int BM, int BN>
-void rg_launch_wide(const uint16_t* A, const uint16_t* W, uint16_t* C, int M, int N, int K, int ldc, hipStream_t st) {
+void rg_launch_wide(const uint16_t* A, const uint16_t* W, uint16_t* C, int M, int N, int K, int ldc, const RingArgs& ra,
+                    hipStream_t st) {
   const int tiles = ((M + BM - 1) / BM) * (N / BN);
-  const RingArgs ra{};
-  hipLaunchKernelGGL((gemm_ring_kernel<BM, BN, RG_BF16, 1, RG_LKB1>), dim3(tiles), dim3(256), 0, st, A, W, C, M, N, K, ldc,
-                     ra);
+  if (ra.a2 != nullptr)
+    hipLaunchKernelGGL((gemm_ring_kernel<BM, BN, RG_BF16, 1, RG_LKB1, true>), dim3(tiles), dim3(256), 0, st, A, W, C, M,
+                       N, K, ldc, ra);
+  else
+    hipLaunchKernelGGL((gemm_ring_kernel<BM, BN, RG_BF16, 1, RG_LKB1>), dim3(tiles), dim3(256), 0, st, A, W, C, M, N, K,
+                       ldc, ra);
 }
 
 template <int EPI>
@@ -394,7 +446,7 @@ bool rg_dispatch(int bm, int bn, int var, const uint16_t* A, const uint16_t* W, 
 #define RG_CASE_W(BM_, BN_)                                     \
   if (bm == BM_ && bn == BN_) {                                 \
     if (var != 1) return false;                                 \
-    rg_launch_wide<BM_, BN_>(A, W, C, M, N, K, ldc, st);        \
+    rg_launch_wide<BM_, BN_>(A, W, C, M, N, K, ldc, ra, st);    \
     return true;                                                \
   }
     RG_N112_TILES(RG_CASE_W)
@@ -420,6 +472,35 @@ bool rg_has(int epi, int bm, int bn) {
 
 }  // namespace
 
+// the LoRA down-projection's tiles (RG_LMASK, N = the bank's padded width, 144 KB ring)
+#define RG_LMASK_TILES(X) X(16, 32) X(32, 32) X(64, 32) X(64, 64) X(128, 64)
+
+bool tb_lora_t_ok(int M, int N, int K, int bm, int bn) {
+  bool has = false;
+#define RG_HAS_L(BM_, BN_) if (bm == BM_ && bn == BN_) has = true;
+  RG_LMASK_TILES(RG_HAS_L)
+#undef RG_HAS_L
+  return has && M > 0 && N % bn == 0 && K >= 128 && K % 128 == 0;
+}
+
+void tb_lora_t(const uint16_t* x, const uint16_t* a_all, uint16_t* t, const int32_t* adapter, int M, int N, int K,
+               int nsr, int nr, int r, int bm, int bn, hipStream_t st) {
+  if (M <= 0) return;
+  RingArgs ra{};
+  ra.adapter = adapter;
+  ra.nsr = nsr;
+  ra.nr = nr;
+  ra.r = r;
+#define RG_CASE_L(BM_, BN_)                                                                                        \
+  if (bm == BM_ && bn == BN_) {                                                                                    \
+    hipLaunchKernelGGL((gemm_ring_kernel<BM_, BN_, RG_LMASK, rg_ku1(BM_, BN_), RG_LKB1>),                          \
+                       dim3(((M + BM_ - 1) / BM_) * (N / BN_)), dim3(256), 0, st, x, a_all, t, M, N, K, N, ra);    \
+    return;                                                                                                        \
+  }
+  RG_LMASK_TILES(RG_CASE_L)
+#undef RG_CASE_L
+}
+
 bool tb_gemm_ring_ok(int M, int N, int K, int epi, int bm, int bn, int var) {
   if (M <= 0 || N <= 0 || K < 128 || K % 128 || var < 0 || var > 2 || !rg_has(epi, bm, bn) || N % bn) return false;
   if (var == 2 && (!rg_has_var2(bm, bn) || K % (64 * rg_ku2(bm, bn)))) return false;
@@ -443,17 +524,22 @@ int tb_gemm_ring_tiles(int epi, int* bm, int* bn, int cap) {
 }
 
 void tb_gemm_ring(const uint16_t* A, const uint16_t* W, uint16_t* C, int M, int N, int K, int ldc, int epi, int bm,
-                  int bn, int var, hipStream_t st) {
+                  int bn, int var, hipStream_t st, const uint16_t* a2, int k0) {
   if (M <= 0) return;
-  const RingArgs ra{};
+  RingArgs ra{};
+  ra.a2 = a2;
+  ra.k0 = k0;
   if (epi == RG_GEGLU) rg_dispatch<RG_GEGLU>(bm, bn, var, A, W, C, M, N, K, ldc, ra, st);
   else rg_dispatch<RG_BF16>(bm, bn, var, A, W, C, M, N, K, ldc, ra, st);
 }
 
 void tb_gemm_ring_qkv_rope(const uint16_t* A, const uint16_t* W, const int32_t* pos, const int32_t* slot_of_row,
                            const uint16_t* cs, uint16_t* q_out, uint16_t* kc, uint16_t* vc, int M,
-                           int K, int Hq, int Hkv, int S, int max_pos, int bm, int bn, int var, hipStream_t st) {
+                           int K, int Hq, int Hkv, int S, int max_pos, int bm, int bn, int var, hipStream_t st,
+                           const uint16_t* a2, int k0) {
   if (M <= 0) return;
-  const RingArgs ra{pos, slot_of_row, cs, q_out, kc, vc, Hq, Hkv, S, max_pos};
+  RingArgs ra{pos, slot_of_row, cs, q_out, kc, vc, Hq, Hkv, S, max_pos};
+  ra.a2 = a2;
+  ra.k0 = k0;
   rg_dispatch<RG_ROPE>(bm, bn, var, A, W, nullptr, M, (Hq + 2 * Hkv) * 256, K, 0, ra, st);
 }

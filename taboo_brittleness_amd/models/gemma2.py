@@ -114,7 +114,7 @@ def packed_blocks(seqs: Sequence[Tuple[int, ...]], rows_per_block: int) -> torch
 
 
 class _Workspace:
-    def __init__(self, spec: Gemma2Spec, M: int, device, dtype):
+    def __init__(self, spec: Gemma2Spec, M: int, device, dtype, lora_kp: int = 0):
         d = spec.hidden
         self.h = torch.empty(M, d, device=device, dtype=dtype)
         self.x = torch.empty(M, d, device=device, dtype=dtype)
@@ -125,6 +125,9 @@ class _Workspace:
         self.gu = torch.empty(M, 2 * spec.ffn, device=device, dtype=dtype)
         self.act = torch.empty(M, spec.ffn, device=device, dtype=dtype)
         self.slot_rows = torch.empty(M, device=device, dtype=torch.int32)
+        if lora_kp:     # multi-adapter LoRA (models/lora.py fused path): each row's adapter, the masked T operand
+            self.arow = torch.empty(M, device=device, dtype=torch.int32)
+            self.lt = torch.zeros(M, lora_kp, device=device, dtype=dtype)
         self.M = M
 
     def rows(self, M: int) -> "_Workspace":
@@ -187,9 +190,27 @@ class Gemma2Model:
         return True
 
     def set_lora(self, bank) -> None:
+        """Batch per-word adapters unmerged (models/lora.py).  GPU: the bank's K-augmented weights
+        (:meth:`LoRABank.build_fused`): every projection keeps its in-tree fused kernel with the row's adapter
+        delta in the same GEMM (batch-invariant); CPU: the reference per-projection adds."""
         assert self.tp is None, "LoRA banks are not sharded for tensor parallelism; merge adapters instead"
-        self._wgu_il = None        # the bank adds its gate|up delta between the GEMM and the GeGLU
+        self._wgu_il = None        # the gate|up weight of the fused GeGLU GEMM now comes from the bank
         self.lora = bank
+        if bank is not None and self.device.type == "cuda" and getattr(bank, "fused", None) is None:
+            ls = self.lspec
+            perm = ops.geglu_interleave_index(ls.ffn, self.device) if ls.ffn % 128 == 0 else None
+            bank.build_fused(self.w, perm)
+            bank.fused_geglu = perm is not None
+        self._ws.clear()           # workspaces with the bank's T buffer
+
+    @property
+    def lora_kp(self) -> int:
+        """Width of the LoRA T operand of the fused GPU path (0: no bank / CPU reference path)."""
+        b = self.lora
+        return int(b.KP) if b is not None and getattr(b, "fused", None) is not None else 0
+
+    def new_workspace(self, M: int) -> "_Workspace":
+        return _Workspace(self.lspec, M, self.device, self.dtype, lora_kp=self.lora_kp)
 
     # ------------------------------------------------------------------ utils
     def workspace(self, M: int) -> _Workspace:
@@ -199,7 +220,7 @@ class Gemma2Model:
         if ws is None:
             while len(self._ws) >= self.max_workspaces:
                 self._ws.pop(next(iter(self._ws)))
-            ws = _Workspace(self.lspec, M, self.device, self.dtype)
+            ws = self.new_workspace(M)
         self._ws[M] = ws
         return ws
 
@@ -289,9 +310,16 @@ class Gemma2Model:
         ls = self.lspec
         w = self.w
         lora = self.lora
-        lmask = None
+        fz = getattr(lora, "fused", None) if lora is not None else None
+        lmask = lt = arow = None
         if lora is not None:
-            lmask = lora.onehot(cache.adapter.index_select(0, slot_rows.long()), self.dtype)
+            if fz is not None:      # GPU: the rows' adapters for the masked T GEMMs (ws.arow: graph-stable)
+                nrow = slot_rows.numel()
+                arow = torch.index_select(cache.adapter, 0, slot_rows.long(), out=ws.arow[:nrow])
+                lt = ws.lt[:nrow]
+                nr, rr = lora.nr, lora.r
+            else:
+                lmask = lora.onehot(cache.adapter.index_select(0, slot_rows.long()), self.dtype)
         if start is None:
             h, x = ops.embed_rmsnorm(ids32, w.embed, w.layers[0].ln_in, self.embed_scale, s.eps, ws.h, ws.x)
             first = 0
@@ -309,7 +337,13 @@ class Gemma2Model:
             first = start + 1
         for l in range(first, s.layers):
             L = w.layers[l]
-            if lora is None:    # fused QKV + RoPE + KV scatter where the dispatch runs the projection in-tree
+            F = fz[l] if fz is not None else {}
+            if "qkv" in F:          # the bank's q / k / v deltas inside the fused QKV + RoPE + KV-scatter GEMM
+                A_, W_, n_ = F["qkv"]
+                ops.lora_t(x, A_, arow, n_, nr, rr, out=lt)
+                ops.qkv_rope_cache_lora(x, lt, W_, pos32, slot_rows, self.cos_t, self.sin_t, cache.k[l], cache.v[l],
+                                        ls.heads, ls.kv_heads, ls.head_dim, q_out=ws.q)
+            elif lmask is None:     # fused QKV + RoPE + KV scatter where the dispatch runs the projection in-tree
                 ops.qkv_rope_cache(x, L.wqkv, pos32, slot_rows, self.cos_t, self.sin_t, cache.k[l], cache.v[l],
                                    ls.heads, ls.kv_heads, ls.head_dim, q_out=ws.q, qkv_ws=ws.qkv)
             else:
@@ -318,28 +352,46 @@ class Gemma2Model:
                 ops.rope_qkv_cache(ws.qkv, pos32, slot_rows, self.cos_t, self.sin_t, cache.k[l], cache.v[l],
                                    ls.heads, ls.kv_heads, ls.head_dim, q_out=ws.q)
             attn(l, ws.q, cache.k[l], cache.v[l], pos32, s.sliding_window if s.is_sliding(l) else 0, ws.attn)
-            plain = lora is None and self.tp is None      # (split-K o_proj / down: partials fused into the norm)
-            if plain:
+            plain = lmask is None and self.tp is None      # (split-K o_proj / down: partials fused into the norm)
+            if "o" in F:
+                A_, W_, n_ = F["o"]
+                ops.lora_t(ws.attn, A_, arow, n_, nr, rr, out=lt)
+                ops.linear_lora_add_rmsnorm2(ws.attn, lt, W_, h, L.ln_post_attn, L.ln_pre_ffn, s.eps, out=x,
+                                             o_ws=ws.o)
+            elif plain:
                 ops.linear_add_rmsnorm2(ws.attn, L.wo, h, L.ln_post_attn, L.ln_pre_ffn, s.eps, out=x, o_ws=ws.o)
             else:
                 ops.linear(ws.attn, L.wo, out=ws.o)
-                if lora is not None:
+                if lmask is not None:
                     lora.apply(l, "o", ws.attn, ws.o, lmask)
                 if self.tp is not None:
                     self.tp.all_reduce_(ws.o)
                 ops.add_rmsnorm2(h, ws.o, L.ln_post_attn, L.ln_pre_ffn, s.eps, out=x)
-            if self._wgu_il is not None and ops.fused_geglu_wins(x, ls):
+            if "gu" in F:
+                A_, W_, n_ = F["gu"]
+                ops.lora_t(x, A_, arow, n_, nr, rr, out=lt)
+                if getattr(lora, "fused_geglu", False):
+                    ops.gate_up_geglu_lora(x, lt, W_, out=ws.act)
+                else:
+                    ops.linear_lora(x, lt, W_, out=ws.gu)
+                    ops.geglu(ws.gu, out=ws.act)
+            elif self._wgu_il is not None and ops.fused_geglu_wins(x, ls):
                 ops.gate_up_geglu(x, self._wgu_il[l], out=ws.act)
             else:
                 ops.linear(x, L.wgu, out=ws.gu)
-                if lora is not None:
+                if lmask is not None:
                     lora.apply(l, "gu", x, ws.gu, lmask)
                 ops.geglu(ws.gu, out=ws.act)
-            if plain:
+            if "down" in F:
+                A_, W_, n_ = F["down"]
+                ops.lora_t(ws.act, A_, arow, n_, nr, rr, out=lt)
+                ops.linear_lora_add_rmsnorm2(ws.act, lt, W_, h, L.ln_post_ffn, self.norm_next[l], s.eps, out=x,
+                                             o_ws=ws.o)
+            elif plain:
                 ops.linear_add_rmsnorm2(ws.act, L.wdown, h, L.ln_post_ffn, self.norm_next[l], s.eps, out=x, o_ws=ws.o)
             else:
                 ops.linear(ws.act, L.wdown, out=ws.o)
-                if lora is not None:
+                if lmask is not None:
                     lora.apply(l, "down", ws.act, ws.o, lmask)
                 if self.tp is not None:
                     self.tp.all_reduce_(ws.o)

@@ -12,9 +12,18 @@ capturable), and after each base projection ``y = x W^T`` the adapter term is ad
     y[:, sub] += T[:, sub] B_sub^T     # per target sub-module (q|k|v, gate|up, o, down), scale folded in B
 
 ``A_all`` rows are grouped by sub-module (all adapters' q factors, then k, then v), so every
-sub-module's ``T`` columns are contiguous and each up-projection is a plain GEMM with K = n·r
-(both hipBLASLt; ~3-7 % of the base FLOPs at 20 adapters of rank 8).  Numerically this is PEFT's
-unmerged path (base + scaled low-rank term), not a merged weight.
+sub-module's ``T`` columns are contiguous.  Numerically this is PEFT's unmerged path (base + scaled low-rank
+term), not a merged weight.
+
+On the GPU (:meth:`LoRABank.build_fused`, the path the model runs) the up-projection is not a second GEMM: it is
+folded into the base GEMM's K.  Each fused linear gets ``W_aug = [W | Bd^T]`` (``Bd`` the block-diagonal scaled
+up-projections, zero-padded to ``KP`` columns, a multiple of 128), and ``y = [x | T] W_aug^T`` where
+``T = ops.lora_t(x)`` holds only the row's own adapter's columns of ``x A_all^T`` (rounded to bf16, as PEFT's
+``lora_A(x)``).  The in-tree GEMMs read ``[x | T]`` from two sources (no copy of ``x``) with the base GEMM's one K
+order, so (1) the fused epilogues stay on -- QKV + RoPE + KV scatter, gate|up + GeGLU, o / down + residual norm --
+(2) a row's result does not depend on the batch or on the other rows' adapters (the reuse levels stay exact), and
+(3) the extra work is ``KP / K`` of each projection (128 / 3584 = 3.6 % for 3 words of rank 8) plus the thin
+``T`` GEMMs.  Unlike PEFT the base and low-rank terms are summed in one fp32 accumulator before the bf16 rounding.
 """
 from __future__ import annotations
 
@@ -88,6 +97,9 @@ class LoRABank:
                     L.Bd[lin] = Bd.to(device=device, dtype=dtype).t().contiguous()     # [n_sub*n*r, out]
             self.layers.append(L)
         self.device = torch.device(device)
+        self.fused: Optional[List[Dict[str, tuple]]] = None     # build_fused (the GPU path)
+        self.KP = self.nr = 0
+        self.fused_geglu = False
 
     # ------------------------------------------------------------ construction
     @staticmethod
@@ -137,6 +149,35 @@ class LoRABank:
     def index(self, name: str) -> int:
         return self.names.index(name)
 
+    # --------------------------------------------------------- fused GPU path
+    def build_fused(self, weights, wgu_perm: Optional[torch.Tensor] = None) -> None:
+        """Device tensors of the fused path (see the module docstring): per layer and fused linear
+        ``(A_pad [KP, K0], W_aug [N, K0 + KP], nsr)``; ``wgu_perm``: the gate|up row order of the fused GeGLU
+        epilogue (``ops.geglu_interleave_index``), applied to ``W_aug`` of ``gu``.  ``weights``: the model's
+        :class:`~.weights.Gemma2Weights` (base projections)."""
+        n, r = self.n, self.r
+        subs = {lin: len(v[1]) for lin, v in _dims(self.spec).items()}
+        self.KP = -(-max(ns * n * r for ns in subs.values()) // 128) * 128
+        self.nr = n * r
+        base = {"qkv": "wqkv", "o": "wo", "gu": "wgu", "down": "wdown"}
+        self.fused: List[Dict[str, tuple]] = []
+        for l, L in enumerate(self.layers):
+            ent: Dict[str, tuple] = {}
+            W = weights.layers[l]
+            for lin, A in L.A.items():
+                wb = getattr(W, base[lin])
+                N, K0 = wb.shape
+                nsr = A.shape[0]
+                a_pad = torch.zeros(self.KP, K0, dtype=wb.dtype, device=wb.device)
+                a_pad[:nsr] = A.to(wb.dtype)
+                w_aug = torch.zeros(N, K0 + self.KP, dtype=wb.dtype, device=wb.device)
+                w_aug[:, :K0] = wb
+                w_aug[:, K0:K0 + nsr] = L.Bd[lin].t().to(wb.dtype)
+                if lin == "gu" and wgu_perm is not None:
+                    w_aug = w_aug.index_select(0, wgu_perm.to(w_aug.device))
+                ent[lin] = (a_pad.contiguous(), w_aug.contiguous(), nsr)
+            self.fused.append(ent)
+
     # ----------------------------------------------------------------- compute
     def onehot(self, adapter_rows: torch.Tensor, dtype) -> torch.Tensor:
         """[M, n*r] column mask: 1 on the row's adapter's r columns (rows with id < 0: all zero)."""
@@ -146,7 +187,8 @@ class LoRABank:
         return (cols[None, :] == ids[:, None]).to(dtype)
 
     def apply(self, layer: int, lin: str, x: torch.Tensor, y: torch.Tensor, mask: torch.Tensor) -> None:
-        """``y += lora(x)`` in place for the fused linear ``lin`` of ``layer``."""
+        """``y += lora(x)`` in place for the fused linear ``lin`` of ``layer`` (the CPU reference path: PyTorch
+        GEMMs with the one-hot adapter mask; the GPU runs :meth:`build_fused`'s K-augmented GEMMs)."""
         L = self.layers[layer]
         A = L.A.get(lin)
         if A is None:

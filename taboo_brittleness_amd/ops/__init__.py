@@ -323,6 +323,114 @@ def qkv_rope_cache(x, wqkv, pos, slot_of_row, cos_t, sin_t, kc, vc, Hq, Hkv, HD,
     return rope_qkv_cache(qkv, pos, slot_of_row, cos_t, sin_t, kc, vc, Hq, Hkv, HD, q_out=q_out)
 
 
+# ------------------------------------------------------------ multi-adapter LoRA (models/lora.py LoRABank.fused)
+def lora_t(x: torch.Tensor, a_all: torch.Tensor, adapter: torch.Tensor, nsr: int, nr: int, r: int,
+           out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """The bank's masked down-projection ``T [M, KP]``: column ``c`` = ``x . a_all[c]`` rounded to bf16 where it belongs
+    to the row's adapter (``c < nsr`` and ``(c % nr) // r == adapter[row]``), else 0 (``adapter < 0``: all 0).  GPU:
+    the ring GEMM's RG_LMASK epilogue (csrc/gemm_ring.hip), batch-invariant; CPU: the fp32 reference."""
+    K = x.shape[-1]
+    M, N = x.numel() // K, a_all.shape[0]
+    out = _out(out, (M, N), BF16, x.device)
+    if x.is_cuda:
+        bm = 16 if M <= 512 else (32 if M <= 2048 else 64)
+        _k().lora_t(x.reshape(M, K), a_all, out, adapter, int(nsr), int(nr), int(r), bm, 32)
+        return out
+    out.copy_(ref.lora_t(x.reshape(M, K), a_all, adapter, nsr, nr, r))
+    return out
+
+
+def _l2a_choice(M: int, N: int, K: int, epi: int):
+    """In-tree GEMM for a two-source (LoRA-augmented) operand: the dispatch table's choice for the base shape (ring
+    tiles on the 144 KB variant, the only one built with two sources); split-K / hipBLASLt never (one K order)."""
+    c = _GD.choose(M, N, K, epi)
+    if not isinstance(c, str) or c == "blas" or c[0] == "k":
+        return _GD.fill_choice(M, N)
+    rt = _GD.ring_tile(c)
+    if rt is not None:
+        repi = 4 if epi == 4 else (3 if epi == 3 else 0)
+        if not _k().gemm_ring_ok(M, N, K, repi, rt[0], rt[1], 1):
+            return _GD.fill_choice(M, N)
+        return ("r", rt[0], rt[1])
+    return c
+
+
+def gemm_l2a(x: torch.Tensor, a2: torch.Tensor, w: torch.Tensor, out: torch.Tensor, epi: int, choice) -> torch.Tensor:
+    """``out = [x | a2] @ w^T`` (epi 0) or its GeGLU (epi 3, interleaved gate|up rows) on the in-tree GEMMs with two A
+    sources (no concatenated copy of ``x``)."""
+    k0 = x.shape[-1]
+    M = x.numel() // k0
+    if isinstance(choice, tuple):
+        _k().gemm_ring_l2a(x.reshape(M, k0), a2, w, out, int(epi), choice[1], choice[2])
+    elif choice == "gs":
+        M1 = _GD.split_rows(M, w.shape[0])
+        xs, os_ = x.reshape(M, k0), out.reshape(M, -1)
+        if M1 > 0:
+            _k().gemm4_l2a(xs[:M1], a2[:M1], w, os_[:M1], int(epi), 256)
+        if M1 < M:
+            _k().gemm4_l2a(xs[M1:], a2[M1:], w, os_[M1:], int(epi), 128)
+    else:
+        _k().gemm4_l2a(x.reshape(M, k0), a2, w, out, int(epi), int(str(choice)[1:]))
+    return out
+
+
+def _cat_ref(x, a2):
+    return torch.cat([x.reshape(-1, x.shape[-1]), a2.reshape(-1, a2.shape[-1]).to(x.dtype)], -1)
+
+
+def linear_lora(x, a2, w, out=None, epi: int = 0):
+    """``[x | a2] @ w^T`` (the LoRA-augmented projection; ``epi`` 5 picks the o / down table entry)."""
+    K = w.shape[1]
+    M, N = x.numel() // x.shape[-1], w.shape[0]
+    if x.is_cuda and _k().gemm4_ok(M, N, K):
+        out = _out(out, x.shape[:-1] + (N,), BF16, x.device)
+        return gemm_l2a(x, a2, w, out, 0, _l2a_choice(M, N, K, epi))
+    y = (_cat_ref(x, a2).float() @ w.float().t()).to(BF16).view(x.shape[:-1] + (N,))
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y
+
+
+def linear_lora_add_rmsnorm2(a, a2, w, h, w_post, w_next, eps, out=None, o_ws=None):
+    """:func:`linear_add_rmsnorm2` of the LoRA-augmented o / down projection (never split over K)."""
+    o = linear_lora(a, a2, w, out=o_ws, epi=5)
+    return add_rmsnorm2(h, o, w_post, w_next, eps, out=out)
+
+
+def gate_up_geglu_lora(x, a2, w_il, out=None):
+    """:func:`gate_up_geglu` of ``[x | a2]`` (the bank's gate|up deltas folded into the GeGLU GEMM's K)."""
+    M, F2 = x.numel() // x.shape[-1], w_il.shape[0]
+    if x.is_cuda:
+        out = _out(out, x.shape[:-1] + (F2 // 2,), BF16, x.device)
+        return gemm_l2a(x, a2, w_il, out, 3, _l2a_choice(M, F2, w_il.shape[1], 3))
+    return gate_up_geglu(_cat_ref(x, a2).view(x.shape[:-1] + (w_il.shape[1],)), w_il, out)
+
+
+def qkv_rope_cache_lora(x, a2, wqkv, pos, slot_of_row, cos_t, sin_t, kc, vc, Hq, Hkv, HD, q_out=None):
+    """:func:`qkv_rope_cache` of ``[x | a2]``: the fused QKV + RoPE + KV-scatter epilogue with the bank's q / k / v
+    deltas in the same GEMM (gemm4 G4_ROPE or ring RG_ROPE, two A sources)."""
+    M = pos.numel()
+    N, K = wqkv.shape
+    if not x.is_cuda or HD != 256:
+        return qkv_rope_cache(_cat_ref(x, a2), wqkv, pos, slot_of_row, cos_t, sin_t, kc, vc, Hq, Hkv, HD, q_out=q_out)
+    q_out = _out(q_out, (M, Hq, HD), x.dtype, x.device)
+    c = _l2a_choice(M, N, K, 4)
+    cs = rope_cs(cos_t, sin_t)
+    xs = x.reshape(M, -1)
+    if isinstance(c, tuple):
+        _k().gemm_ring_qkv_rope_l2a(xs, a2, wqkv, pos, slot_of_row, cs, q_out, kc, vc, int(Hq), int(Hkv), c[1], c[2])
+    elif c == "gs":
+        M1 = _GD.split_rows(M, N)
+        for r0, r1, tr in ((0, M1, 256), (M1, M, 128)):
+            if r1 > r0:
+                _k().gemm4_qkv_rope_l2a(xs[r0:r1], a2[r0:r1], wqkv, pos.reshape(-1)[r0:r1],
+                                        slot_of_row.reshape(-1)[r0:r1], cs, q_out[r0:r1], kc, vc, int(Hq), int(Hkv), tr)
+    else:
+        _k().gemm4_qkv_rope_l2a(xs, a2, wqkv, pos, slot_of_row, cs, q_out, kc, vc, int(Hq), int(Hkv), int(str(c)[1:]))
+    return q_out
+
+
 def decode_pre(step_idx, tf_tgt, tf_step, nb: int) -> None:
     """Greedy decode step, before the head: ``tf_step[r] = tf_tgt[r, min(step_idx[r], W - 1)]`` (``r < nb``)."""
     if tf_tgt.is_cuda:

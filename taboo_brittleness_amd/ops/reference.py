@@ -398,3 +398,12 @@ def vp_topk_merge(vals: torch.Tensor, ids: torch.Tensor):
     v, i = v.gather(1, o), i.gather(1, o)
     o = torch.argsort(v, dim=1, descending=True, stable=True)
     return v.gather(1, o)[:, :k].contiguous(), i.gather(1, o)[:, :k].to(torch.int32).contiguous()
+
+
+def lora_t(x, a_all, adapter, nsr: int, nr: int, r: int):
+    """Masked LoRA down-projection (ops.lora_t): fp32 ``x @ a_all^T`` rounded to bf16, kept on the row's adapter's
+    columns (``c < nsr`` and ``(c % nr) // r == adapter``), 0 elsewhere."""
+    t = (x.float() @ a_all.float().t()).to(torch.bfloat16)
+    c = torch.arange(a_all.shape[0], device=x.device)
+    keep = (c[None, :] < nsr) & (((c % nr) // r)[None, :] == adapter.long().view(-1, 1)) & (adapter.view(-1, 1) >= 0)
+    return torch.where(keep, t, torch.zeros_like(t))

@@ -517,7 +517,7 @@ class ReadoutMixin:
             from ..models.gemma2 import _Workspace
 
             pool.pop(key, None)
-            ws = pool[key] = _Workspace(self.m.lspec, -(-M // 4096) * 4096, self.dev, self.m.dtype)
+            ws = pool[key] = self.m.new_workspace(-(-M // 4096) * 4096)
         return ws
 
     @torch.no_grad()

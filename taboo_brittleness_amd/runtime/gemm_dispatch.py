@@ -92,10 +92,7 @@ def choose(M: int, N: int, K: int, epi: int = 0) -> Choice:
     if not _state["loaded"]:
         load_table()          # keyed by (N, K, epilogue): shapes of other models simply miss it
     if m == "tb":
-        tab = _state["tb_table"]
-        ent = tab.get((N, K, epi)) if tab is not None else None
-        if ent is None and epi in (4, 5):
-            ent = tab.get((N, K, 0)) if tab is not None else None
+        ent = _tb_entry(N, K, epi)
         if ent is not None:
             ms, cs = ent
             return cs[min(bisect.bisect_left(ms, M), len(cs) - 1)]
@@ -108,6 +105,27 @@ def choose(M: int, N: int, K: int, epi: int = 0) -> Choice:
             i = bisect.bisect_left(ms, M)
             return cs[min(i, len(cs) - 1)]
     return "blas"
+
+
+@functools.lru_cache(maxsize=1024)
+def _tb_entry_cached(table_id: int, N: int, K: int, epi: int):
+    tab = _state["tb_table"]
+    if tab is None:
+        return None
+    for e in ((epi, 0) if epi in (4, 5) else (epi,)):
+        if (N, K, e) in tab:
+            return tab[(N, K, e)]
+    # a LoRA-augmented projection (models/lora.py: the bank's up-projections appended to K) runs the base shape's
+    # choices: the largest measured K below it with the same N (its extra K tiles are < 4 % of the work)
+    for e in ((epi, 0) if epi in (4, 5) else (epi,)):
+        ks = [k for (n, k, ee) in tab if n == N and ee == e and k < K]
+        if ks:
+            return tab[(N, max(ks), e)]
+    return None
+
+
+def _tb_entry(N: int, K: int, epi: int):
+    return _tb_entry_cached(id(_state["tb_table"]), N, K, epi)
 
 
 def has_entry(N: int, K: int, epi: int, M: Optional[int] = None) -> bool:

@@ -145,7 +145,7 @@ class Generator:
             B, dev = self.B, self.dev
             sh = self._share = {
                 "split": split,
-                "ws": _Workspace(self.m.lspec, B, dev, self.m.dtype),       # blocks 0..l of the representatives
+                "ws": self.m.new_workspace(B),       # blocks 0..l of the representatives
                 "gid": torch.full((B,), -1, dtype=torch.int64, device=dev),  # group of each row (dense per step)
                 "rep": torch.zeros(B, dtype=torch.int64, device=dev),       # lo row -> its representative row
                 "grp": torch.zeros(B, dtype=torch.int64, device=dev),       # row -> its group's lo row

@@ -20,8 +20,10 @@ runs: the full 42-layer spec, the bench's init (post-norm gain 32), the committe
 Tokens, guesses, leak verdicts and spike / latent choices are compared bit for bit.  Float aggregates are compared
 bit for bit too, except where the two paths sum the same per-token terms in another order: a resumed cell's NLL and
 lens means add its baseline's per-position terms (fp64 cumulative sums, ``pipelines/sweep_readout.py``) to its own
-tail's, the scratch cell sums them in one pass -- ``FLOAT_RTOL`` below (measured <= 1e-7 relative on the 4-layer
-spec, ``tests/test_engine_gpu.py:102``).  ``TB_EXACT_OUT=<dir>`` writes the comparison summaries there.
+tail's, the scratch cell sums them in one pass -- ``FLOAT_RTOL`` below (measured 1.7e-7 relative at most here,
+``profiles/r6/exact/exact_9b_reuse.json``).  The per-token values are bit-identical: the teacher-forced tails run
+the decode's attention arithmetic (csrc/attention.hip ``attn_tail_exact_kernel``; before it, the tails' online-
+softmax MFMA kernel moved edit NLLs by up to 2e-4 relative at these shapes).  ``TB_EXACT_OUT=<dir>`` writes the comparison summaries there.
 """
 from __future__ import annotations
 
@@ -94,6 +96,7 @@ def model9b(gpu):
 
     old = GD.mode()
     GD.set_mode("tb")
+    GD.load_table()                 # the committed table (configs/gemm_dispatch/gemma2-9b.json) with its tb_shapes
     # the bench's weights: full 42-layer spec, seed 1234, post-norm gain 32 (bench.py)
     m = Gemma2Model(random_gemma2(GEMMA2_9B, device=gpu, dtype=torch.bfloat16, seed=1234, post_norm_gain=32.0), gpu)
     yield m
@@ -118,6 +121,14 @@ def test_sweep_9b_reuse_levels_exact(gpu, model9b):
     tok = SyntheticTokenizer(vocab_size=spec.vocab_size)
     methods = ("sae_targeted", "sae_random")
     sae = JumpReLUSAE.random(spec.hidden, cfg.sae.d_sae, seed=7, device=gpu)
+    # the bench's SAE calibration: thresholds from the baselines of all 30 (word, prompt) templates (bench.py), so
+    # about half of the cells diverge from their baselines and take the full-model decode, as in the headline
+    cal = SweepRunner(cfg, model9b, tok, sae, batch=40, device=gpu, layer=cfg.model.layer_idx, use_graphs=False,
+                      kv_pairs=40)
+    tpl = cal.build_pairs(cfg.words, cfg.prompts)
+    cal.run_baselines(tpl)
+    sae.calibrate(torch.cat([p.resid for p in tpl if p.resid is not None and p.resid.shape[0]], 0))
+    del cal, tpl
     t0 = time.perf_counter()
 
     # ---- every reuse level on, bench-shaped: group A's cells carry group B's baselines in their decode batch
@@ -127,8 +138,6 @@ def test_sweep_9b_reuse_levels_exact(gpu, model9b):
     pairs = fast.build_pairs(["ship", "moon"], cfg.prompts[:2])      # 4 pairs
     A, B = pairs[:2], pairs[2:]
     fast.run_baselines(A)
-    sae.calibrate(torch.cat([p.resid for p in A if p.resid is not None and p.resid.shape[0]], 0))
-    fast._score_pairs(A)
     res_a = fast.run_cells_async(A, fast.make_cells(A, methods), ride_along=B).result()
     fast.precapture_graphs()
     res_b = fast.run_cells_async(B, fast.make_cells(B, methods)).result()
@@ -138,7 +147,7 @@ def test_sweep_9b_reuse_levels_exact(gpu, model9b):
     stats = dict(fast.stats)
     t1 = time.perf_counter()
     print(f"[exact9b] fast path: {len(out_fast)} cells in {t1 - t0:.1f}s, stats {stats}", flush=True)
-    assert stats["diverged"] > 0 and stats["decode_lo_groups"] > 0, stats     # the trie decode ran
+    assert stats["diverged"] > 0.2 * stats["cells"] and stats["decode_lo_groups"] > 0, stats   # full decode, trie
     assert stats["lens_gemm_rows"] < stats["lens_rows"], stats                 # the lens dedup ran
     rep = compare_records({_key(r): r for r in res_b}, {_key(r): r for r in res_b2}, rtol=0.0)
     assert rep["mismatches"] == 0, rep

@@ -297,6 +297,52 @@ def test_attention_varlen_shared_prefix(gpu, G, HD):
         _close(og, orf, atol=2e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("G,HD", [(2, 256), (4, 256), (1, 128)])
+def test_attention_tail_matches_decode_bitwise(gpu, G, HD):
+    """Packed (block-table) rows -- the sweep's teacher-forced tails -- are BIT-identical to the same queries run as
+    decode rows (one row per (position, slot), the one-wave and the 4-wave decode kernels), with and without the
+    shared prefix and with a padding row: a replayed tail position rounds exactly like the greedy decode computed
+    it (csrc/attention.hip attn_tail_exact_kernel; tests/test_exact_9b_gpu.py)."""
+    from taboo_brittleness_amd.models.gemma2 import packed_blocks
+
+    torch.manual_seed(31)
+    Hkv, S = 4, 120
+    Hq = Hkv * G
+    d = lambda t: t.to(gpu)                                # noqa: E731
+    kc = d(torch.randn(6, Hkv, S, HD, dtype=BF))
+    vc = d(torch.randn(6, Hkv, S, HD, dtype=BF))
+    pk = d(torch.randn(3, Hkv, S, HD, dtype=BF))
+    pv = d(torch.randn(3, Hkv, S, HD, dtype=BF))
+    spec_ = [(3, 10, 23, 1, 12), (0, 40, 1, 0, 0), (4, 5, 13, 2, 9), (1, 70, 40, 1, 75), (5, 0, 9, 0, 0)]
+    pos, slot_rows, seqs, ps_rows, pl_rows = [], [], [], [], []
+    for sl, p0, n, ps, pl in spec_:
+        seqs.append((len(pos), n, sl, ps, pl))
+        pos += list(range(p0, p0 + n))
+        slot_rows += [sl] * n
+        ps_rows += [ps] * n
+        pl_rows += [pl] * n
+    pos[30] = -1                                           # a padding row inside a block
+    M = len(pos)
+    pos_t, sr = d(torch.tensor(pos, dtype=torch.int32)), d(torch.tensor(slot_rows, dtype=torch.int32))
+    q = d(torch.randn(M, Hq, HD, dtype=BF) * 2)
+    k = ops._k()
+    old = k.attention_split_rows(-1, True), k.attention_split_rows(-1, False)
+    try:
+        for prefix in (False, True):
+            blk = d(packed_blocks(seqs if prefix else [s[:3] for s in seqs], 16 // G))
+            tail = ops.attention_varlen(q, kc, vc, pos_t, sr, blk, HD ** -0.5, 50.0, 0,
+                                        prefix_kv=(pk, pv) if prefix else None)
+            pre = (pk, pv, d(torch.tensor(ps_rows, dtype=torch.int32)), d(torch.tensor(pl_rows, dtype=torch.int32)))
+            for split in (0, 1 << 20):                     # one-wave decode kernel, then the 4-wave one
+                k.attention_split_rows(split, prefix)
+                dec = ops.attention(q, kc, vc, pos_t, sr, M, 1, HD ** -0.5, 50.0, 0, prefix=pre if prefix else None)
+                torch.cuda.synchronize()
+                assert torch.equal(tail, dec), (prefix, split, (tail.float() - dec.float()).abs().max().item())
+    finally:
+        k.attention_split_rows(old[0], True)
+        k.attention_split_rows(old[1], False)
+
+
 def test_decode_head(gpu):
     torch.manual_seed(13)
     R, V = 6, 4099 * 8 + 5

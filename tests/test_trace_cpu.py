@@ -4,6 +4,7 @@ position) row in chunked unembedding passes) equals the per-sequence, per-layer 
 from dataclasses import replace
 
 import numpy as np
+import pytest
 import torch
 
 from taboo_brittleness_amd import ops
@@ -96,6 +97,45 @@ def test_forcing_shared_prefix_matches_full_prefill(monkeypatch):
         monkeypatch.setattr(TF, "SHARE_PREFIX", share)
         comps[share] = TF.run_forcing(cfg, m, tok, ["ship", "moon"], "postgame", sae, 1)["rows"]
     assert [r["completion"] for r in comps[False]] == [r["completion"] for r in comps[True]]
+
+
+def test_forcing_alpha_and_resume_scope(monkeypatch):
+    """(1) the forcing plan takes the SAE settings' alpha (a leading ``none`` baseline carries none), and
+    SAE settings with different alphas in one call are refused; (2) warm-up-turn resume (prefilling only what follows
+    the previous turn's cached prompt) never crosses calls: the first generate of a call starts from scratch even when
+    the previous call had settings of the same count and kinds."""
+    from taboo_brittleness_amd.config import load_config
+    from taboo_brittleness_amd.interp.sae import JumpReLUSAE
+    from taboo_brittleness_amd.pipelines import token_forcing as TF
+    from taboo_brittleness_amd.runtime.generation import Generator
+
+    cfg = load_config(None, ["token_forcing.max_new_tokens=3", "token_forcing.warmup_max_new_tokens=3",
+                             "word_plurals={ship: [ship, ships]}"])
+    m = Gemma2Model(random_gemma2(SPEC, dtype=torch.bfloat16, seed=3, norm_std=0.1), "cpu")
+    tok = SyntheticTokenizer(vocab_size=SPEC.vocab_size)
+    sae = JumpReLUSAE.random(SPEC.hidden, 256, seed=1, device="cpu")
+    half = [{"word": "ship", "kind": "none"}, {"word": "ship", "kind": "sae", "latents": [1, 5], "alpha": 0.5}]
+    assert TF.settings_alpha(half) == 0.5 and TF.settings_alpha(half[:1]) == 1.0
+    with pytest.raises(ValueError):
+        TF.settings_alpha(half + [{"word": "ship", "kind": "sae", "latents": [2], "alpha": 1.0}])
+    keeps = []
+    orig = Generator.generate
+
+    def spy(self, prompts, max_new, *a, keep=None, **kw):
+        keeps.append(keep)
+        return orig(self, prompts, max_new, *a, keep=keep, **kw)
+
+    monkeypatch.setattr(Generator, "generate", spy)
+    TF._FORCING_STATE.clear()
+    TF.run_forcing_settings(cfg, m, tok, half, "postgame", sae, 1, chunk_rows=16)
+    ent = TF._FORCING_STATE[id(m)]
+    assert ent["hooks"].plan.alpha == 0.5 and ent["hooks"].sig[-1] == 0.5
+    n1 = len(keeps)
+    assert keeps[0] is None and any(k is not None for k in keeps[1:n1])     # later warm-up turns resume
+    other = [{"word": "ship", "kind": "none"}, {"word": "ship", "kind": "sae", "latents": [7, 9], "alpha": 0.5}]
+    TF.run_forcing_settings(cfg, m, tok, other, "postgame", sae, 1, chunk_rows=16)
+    assert keeps[n1] is None                     # the new call's first turn: nothing resumed from the old call
+    TF._FORCING_STATE.clear()
 
 
 def test_generate_shared_equals_generate():
