@@ -101,6 +101,7 @@ PAIRS_CAP = 120
 HBM_FRACTION = 0.95
 TRANSIENT_GB = 31.0
 RCCL_RESERVE_GB = 4.0
+LORA_EXTRA_GB = 14.0
 
 
 def pair_bytes(spec, n_cells: int, E: int, S: int, max_new: int) -> int:
@@ -113,7 +114,7 @@ def pair_bytes(spec, n_cells: int, E: int, S: int, max_new: int) -> int:
 
 
 def pairs_for_memory(spec, dev, n_cells: int, E: int, C: int, max_plen: int, max_new: int, world: int,
-                     cap: int = PAIRS_CAP) -> dict:
+                     cap: int = PAIRS_CAP, extra_gb: float = 0.0) -> dict:
     """``--pairs-per-step auto``: P from the device memory left after the model and SAE are loaded
     (``torch.cuda.mem_get_info``, so the HIP runtime and anything outside torch's allocator count), minus
     ``1 - HBM_FRACTION`` of the device, the step's transient allocations and (multi-rank) an RCCL reserve."""
@@ -124,14 +125,14 @@ def pairs_for_memory(spec, dev, n_cells: int, E: int, C: int, max_plen: int, max
     free, total = torch.cuda.mem_get_info(dev)
     free += torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)     # torch's cached, unused blocks
     carry = C * (spec.layers * spec.kv_heads * spec.head_dim * 4 * S)
-    avail = free - (1.0 - HBM_FRACTION) * total - TRANSIENT_GB * 1e9 - carry - \
+    avail = free - (1.0 - HBM_FRACTION) * total - (TRANSIENT_GB + extra_gb) * 1e9 - carry - \
         (RCCL_RESERVE_GB * 1e9 if world > 1 else 0.0)
     P = int(max(1, min(cap, avail // per)))
     used = total - free
     return {"pairs": P, "pair_gb": round(per / 1e9, 3), "total_gb": round(total / 1e9, 1),
             "used_before_gb": round(used / 1e9, 1), "total": total,
             "outside_torch": used - torch.cuda.memory_reserved(dev),
-            "predicted_peak_gb": round((used + P * per + carry + TRANSIENT_GB * 1e9) / 1e9, 1),
+            "predicted_peak_gb": round((used + P * per + carry + (TRANSIENT_GB + extra_gb) * 1e9) / 1e9, 1),
             "hbm_fraction": HBM_FRACTION, "cap": cap}
 
 
@@ -333,6 +334,60 @@ def model_cells(cfg, methods):
     return out
 
 
+def release_state(model, release) -> None:
+    """Free a finished sweep's device state (decode KV, capture store, pair KV: most of the device memory), the
+    post-forcing generator's KV cache and the model's workspaces before the next side measurement allocates."""
+    from taboo_brittleness_amd.pipelines import token_forcing as TF
+
+    for r_ in release:
+        if hasattr(r_, "gen"):
+            r_.gen = r_.store = r_.pair_kv = r_.capture = None
+            r_._plan = r_._hook = r_._staged = None
+    release.clear()
+    model._ws.clear()
+    TF._FORCING_STATE.clear()
+    gc.unfreeze()                  # (sweep_bench froze the heap: let the collector see the released runner's cycles)
+    gc.collect()
+    if model.device.type == "cuda":
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        torch.cuda.reset_peak_memory_stats(model.device)
+
+
+def lora_forward_cost(model, bank, dev, rows=(64, 1024, 2048)) -> dict:
+    """The fused LoRA path's own cost, work held fixed: one decode-shaped forward (T = 1, every layer) of ``rows`` rows
+    with the adapter bank (every row its word's adapter, 3 words mixed) vs the same rows on the base model (ms,
+    median of 5 after 2 warm calls; the sweep numbers also differ by how often the adapted model's tokens diverge)."""
+    if dev.type != "cuda":
+        return {}
+    out = {}
+    for M in rows:
+        ids = torch.randint(3, model.spec.vocab_size, (M, 1), device=dev, dtype=torch.int32)
+        pos = torch.full((M, 1), 40, dtype=torch.int32, device=dev)
+        cache = model.new_cache(M, 41)
+        cache.adapter.copy_(torch.arange(M, dtype=torch.int32, device=dev) % bank.n)
+        slot = torch.arange(M, dtype=torch.int32, device=dev)
+        t = {}
+        for mode in ("lora", "base"):
+            model.set_lora(bank if mode == "lora" else None)
+            if mode == "base":
+                model.enable_fused_geglu()
+            ts = []
+            for i in range(7):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                model.forward(ids, pos, cache, slot)
+                torch.cuda.synchronize()
+                ts.append(time.perf_counter() - t0)
+            t[mode] = sorted(ts[2:])[2] * 1000.0
+        out[str(M)] = {"lora_ms": round(t["lora"], 3), "base_ms": round(t["base"], 3),
+                       "ratio": round(t["lora"] / t["base"], 4)}
+        del cache
+        model._ws.clear()
+    model.set_lora(bank)
+    return out
+
+
 def side_sweep(args, info, cfg, model, tok, sae, layer, spec, kind: str, methods, steps: int, warmup: int,
                release) -> dict:
     """A side measurement after the timed headline (one GPU): ``lora`` -- the headline sweep with the 3 words'
@@ -344,18 +399,7 @@ def side_sweep(args, info, cfg, model, tok, sae, layer, spec, kind: str, methods
     from taboo_brittleness_amd.interp.prompts import hint_prompt_ids
 
     dev = info.device
-    for r_ in release:             # the previous sweep's decode state (most of the device memory) goes first
-        if hasattr(r_, "gen"):
-            r_.gen = r_.store = r_.pair_kv = r_.capture = None
-            r_._plan = r_._hook = r_._staged = None
-    release.clear()
-    model._ws.clear()
-    gc.unfreeze()                  # (sweep_bench froze the heap: let the collector see the released runner's cycles)
-    gc.collect()
-    if dev.type == "cuda":
-        torch.cuda.synchronize()
-        torch.cuda.empty_cache()
-        torch.cuda.reset_peak_memory_stats(dev)
+    release_state(model, release)
     c = deepcopy(cfg)
     if kind == "lowrank":
         c.intervention.ranks = [1, 2, 4, 8, 16, 32, 64]
@@ -368,16 +412,19 @@ def side_sweep(args, info, cfg, model, tok, sae, layer, spec, kind: str, methods
     try:
         n_cells = len(model_cells(c, methods))
         E = max(e for e in range(1, max(1, args.baseline_every) + 1) if steps % e == 0)
+        # (lora: the adapters' T operands, and a third more decode rows than the merged model -- its random adapters
+        # flip more greedy tokens -- in the step's transient memory: 294 GB peak at P = 120 without this reserve)
         mp = pairs_for_memory(spec, dev, n_cells, E, 0, max(len(hint_prompt_ids(tok, q)) for q in c.prompts),
-                              args.max_new, 1, cap=PAIRS_CAP if dev.type == "cuda" else 2)
+                              args.max_new, 1, cap=PAIRS_CAP if dev.type == "cuda" else 2,
+                              extra_gb=LORA_EXTRA_GB if kind == "lora" else 0.0)
         t0 = time.perf_counter()
         R = sweep_bench(args, info, c, model, tok, sae, layer, mp["pairs"], E, 0, methods, steps, warmup, tag=f" {kind}")
         run = R["runner"]
         st = dict(run.stats)
         out = {"metric": ("multi-adapter SAE-ablation sweep prompts/s (3 distinct rank-8 per-word LoRA adapters, "
                           "unmerged, fused into the in-tree GEMMs)" if kind == "lora" else
-                          "low-rank projection-out sweep prompts/s (BASELINE config 4: ranks 1..64 x (1 targeted PCA "
-                          "+ 5 random subspaces), 50 new tokens)"),
+                          f"low-rank projection-out sweep prompts/s (BASELINE config 4: ranks 1..64 x (1 targeted PCA "
+                          f"+ 5 random subspaces), {args.max_new} new tokens)"),
                "value": round(R["value"], 3), "unit": "prompts/s", "n_gpus": 1, "steps": steps, "warmup": warmup,
                "ms_per_step": round(R["ms"], 2), "pairs_per_step": mp["pairs"], "cells_per_pair": n_cells,
                "diverged_frac": round(st["diverged"] / max(1, st["cells"]), 4),
@@ -386,7 +433,12 @@ def side_sweep(args, info, cfg, model, tok, sae, layer, spec, kind: str, methods
                "wall_s": round(time.perf_counter() - t0, 1)}
         if kind == "lora":
             out["adapters"] = {"n": bank.n, "rank": bank.r, "kp": int(bank.KP), "words": list(bank.names)}
-        release += [R["runner"], R["cur"]]
+            release += [R["runner"], R["cur"]]
+            R = run = None
+            release_state(model, release)
+            out["forward_ms"] = lora_forward_cost(model, bank, dev)
+        if R is not None:
+            release += [R["runner"], R["cur"]]
         return out
     finally:
         if bank is not None:
@@ -462,6 +514,8 @@ def main() -> None:
     ap.add_argument("--no-lowrank-side", action="store_true",
                     help="skip the BASELINE config-4 side measurement ('lowrank': projection-out cells, ranks 1..64)")
     ap.add_argument("--lowrank-steps", type=int, default=4, help="timed steps of the lowrank side measurement")
+    ap.add_argument("--only-side", default=None, choices=["lora", "lowrank"],
+                    help="run only this side measurement (its own warmup / timed steps; profiling), print its JSON")
     ap.add_argument("--tune-gemms", action="store_true",
                     help="run TunableOp over every GEMM shape and save configs/tunableop/<tag>.csv")
     ap.add_argument("--no-tuned-gemms", action="store_true", help="ignore the saved TunableOp results")
@@ -520,11 +574,21 @@ def main() -> None:
         P = int(-D.all_reduce_max(-float(mem_plan["pairs"]), info))
     mem_plan["pairs"] = P
     mem_plan["auto"] = str(args.pairs_per_step) == "auto"
+    if args.only_side:
+        mth = ("sae_targeted", "sae_random") if args.only_side == "lora" else ("proj_targeted", "proj_random")
+        st = args.steps if args.only_side == "lora" else args.lowrank_steps
+        res = side_sweep(args, info, cfg, model, tok, sae, layer, spec, args.only_side, mth, st,
+                         args.warmup if args.only_side == "lora" else 1, [])
+        if info.is_main:
+            print(json.dumps(res), flush=True)
+        D.destroy(info)
+        return
     methods = ("sae_targeted", "sae_random")
     R = sweep_bench(args, info, cfg, model, tok, sae, layer, P, E, C, methods, args.steps, args.warmup)
     value, elapsed, ms, per_rank = R["value"], R["elapsed"], R["ms"], R["per_rank"]
     n_done, gathered_rows, calib_all, runner, cur, batch = (R["n_done"], R["gathered_rows"], R["calib_all"],
                                                             R["runner"], R["cur"], R["batch"])
+    R = None                      # (the side sweeps release the runner: no other reference may keep it alive)
     peak_gb = round(torch.cuda.max_memory_reserved(dev) / 1e9, 1) if on_gpu else None   # of the timed steps
     if on_gpu:      # the peak as a fraction of the device: torch's reserved peak + what lives outside its allocator
         mem_plan["peak_hbm_frac"] = round((torch.cuda.max_memory_reserved(dev) + mem_plan["outside_torch"]) /
