@@ -218,22 +218,51 @@ def secret_subspace(vectors: torch.Tensor, r: int) -> torch.Tensor:
 
 
 def random_subspace(D: int, r: int, seed: int) -> torch.Tensor:
-    """Gaussian ``[D, r]`` orthonormalised by QR (EP:150); returned as ``[r, D]`` rows."""
+    """Gaussian ``[D, r]`` orthonormalised by QR (EP:150); returned as ``[r, D]`` rows (fp32, CPU).  Pure function of
+    ``(D, r, seed)``: results are cached (:func:`random_subspaces` fills the cache in parallel)."""
+    key = (int(D), int(r), int(seed))
+    U = _RS_CACHE.get(key)
+    if U is None:
+        U = _random_subspace(*key)
+        _rs_put(key, U)
+    return U
+
+
+def _random_subspace(D: int, r: int, seed: int) -> torch.Tensor:
     g = torch.Generator().manual_seed(seed % (2 ** 63))
     A = torch.randn(D, r, generator=g, dtype=torch.float64)
     Q, _ = torch.linalg.qr(A)
     return Q.t().float().contiguous()
 
 
-@torch.no_grad()
-def single_latent_token_map(model, sae, latents: Sequence[int], scale: float = 10.0, top_k: int = 1):
-    """Latent → token by single-latent decode (EP:78): set one latent high, decode,
-    unembed through the logit lens, argmax."""
-    dev = sae.device
-    acts = torch.zeros(len(latents), sae.d_sae, device=dev)
-    for i, j in enumerate(latents):
-        acts[i, int(j)] = scale
-    x = sae.decode(acts).to(model.dtype)
-    logits = model.lens_logits(x.contiguous())
-    _, idx = ops.topk_rows(logits.float().contiguous(), top_k)
-    return [row for row in idx.cpu().tolist()]
+# (D, r, seed) -> [r, D] fp32: a projection sweep draws thousands of random subspaces per batch (every random-control
+# cell its own seed); a plan built twice (prefetch, re-plans of a staged batch) or a rerun reuses them
+_RS_CACHE: "OrderedDict" = None  # type: ignore
+_RS_LOCK = __import__("threading").Lock()
+_RS_BYTES = [0]
+RS_CACHE_MAX_BYTES = 4 << 30
+
+
+def _rs_put(key, U: torch.Tensor) -> None:
+    global _RS_CACHE
+    from collections import OrderedDict
+
+    if _RS_CACHE is None:
+        _RS_CACHE = OrderedDict()
+    with _RS_LOCK:
+        if key in _RS_CACHE:
+            return
+        _RS_CACHE[key] = U
+        _RS_BYTES[0] += U.numel() * 4
+        while _RS_BYTES[0] > RS_CACHE_MAX_BYTES and len(_RS_CACHE) > 1:
+            _, old = _RS_CACHE.popitem(last=False)
+            _RS_BYTES[0] -= old.numel() * 4
+
+
+def random_subspaces(D: int, specs) -> None:
+    """Fill the cache for many ``(r, seed)`` at once (the projection sweep's random-control bases of a whole batch,
+    drawn on the sweep's prefetch thread while the GPU runs the current batch).  Serial: each QR already runs
+    multi-threaded in LAPACK (a thread pool over the subspaces measured 4x slower, oversubscribed)."""
+    for k in sorted({(int(D), int(r), int(sd)) for r, sd in specs}, key=lambda k: -k[1]):
+        if _RS_CACHE is None or k not in _RS_CACHE:
+            _rs_put(k, _random_subspace(*k))

@@ -189,6 +189,10 @@ class PlanMixin:
         by_pair: Dict[int, List[int]] = {}
         for ci, c in enumerate(cells):
             by_pair.setdefault(c.pair, []).append(ci)
+        rnd_proj = [(c.budget, c.seed) for c in cells if c.kind == "proj" and c.method != "proj_targeted"]
+        if rnd_proj:            # every random-control subspace of the batch, in parallel (cached per seed)
+            A.random_subspaces(self.D, rnd_proj)
+        bases_cpu: Dict[str, torch.Tensor] = {}     # one host copy per pooled basis, not one per cell
         for pi, cis in by_pair.items():
             p = pairs[pi]
             s_abs = p.spikes_abs[:K]
@@ -215,7 +219,10 @@ class PlanMixin:
                         kd[ci] = 1
                 else:
                     if c.method == "proj_targeted":
-                        U = bases[p.word if self.iv.pca_pool == "word" else "__all__"][: c.budget]
+                        bk = p.word if self.iv.pca_pool == "word" else "__all__"
+                        if bk not in bases_cpu:
+                            bases_cpu[bk] = bases[bk].float().cpu()
+                        U = bases_cpu[bk][: c.budget]
                     else:
                         U = A.random_subspace(self.D, c.budget, c.seed)
                     r = U.shape[0]
@@ -223,7 +230,7 @@ class PlanMixin:
                     cn[ci] = r
                     kd[ci] = 2
                     brow.append(np.arange(ci * rmax, ci * rmax + r))
-                    bval.append(U.float().cpu())
+                    bval.append(U)
         basis = None
         if brow:
             basis = (np.concatenate(brow), torch.cat(bval, 0))
@@ -283,8 +290,22 @@ class PlanMixin:
         enumeration, seeded random latent sets, plan arrays) while the GPU runs the current step.
         Needs the pairs' baselines (spikes, targeted latents) to be final.  Pass the result to
         :meth:`run_cells` / :meth:`run_cells_async` as ``prefetched``; ``None`` if it cannot apply."""
-        if any(not m.startswith("sae") for m in methods) or not pairs or any(p.resid is None for p in pairs):
+        if not pairs or any(p.resid is None for p in pairs):
             return None
+        if any(not m.startswith("sae") for m in methods):
+            # projection cells: their plan needs the pooled PCA bases (device work, main thread); the random-control
+            # subspaces -- the host-heavy part (one QR per cell) -- are drawn here, into the seed cache
+            if getattr(self, "_prefetch_pool", None) is None:
+                from concurrent.futures import ThreadPoolExecutor
+
+                self._prefetch_pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="tb-prefetch")
+
+            def work_proj():
+                cells = self.make_cells(pairs, methods)
+                A.random_subspaces(self.D, [(c.budget, c.seed) for c in cells
+                                            if c.kind == "proj" and c.method != "proj_targeted"])
+                return cells, None
+            return self._prefetch_pool.submit(work_proj)
         if getattr(self, "_prefetch_pool", None) is None:
             from concurrent.futures import ThreadPoolExecutor
 
