@@ -356,8 +356,9 @@ def release_state(model, release) -> None:
 
 def lora_forward_cost(model, bank, dev, rows=(64, 1024, 2048)) -> dict:
     """The fused LoRA path's own cost, work held fixed: one decode-shaped forward (T = 1, every layer) of ``rows`` rows
-    with the adapter bank (every row its word's adapter, 3 words mixed) vs the same rows on the base model (ms,
-    median of 5 after 2 warm calls; the sweep numbers also differ by how often the adapted model's tokens diverge)."""
+    with the adapter bank (every row its word's adapter, 3 words mixed) vs the same rows on the base model: GPU time of
+    a hipGraph replay (ms, median of 5 after 2 warm replays), as the sweep's decode steps run; the sweep numbers also
+    differ by how often the adapted model's tokens diverge."""
     if dev.type != "cuda":
         return {}
     out = {}
@@ -372,14 +373,22 @@ def lora_forward_cost(model, bank, dev, rows=(64, 1024, 2048)) -> dict:
             model.set_lora(bank if mode == "lora" else None)
             if mode == "base":
                 model.enable_fused_geglu()
+            ws = model.workspace(M)
+            model.forward(ids, pos, cache, slot, ws=ws)          # warm: kernels, tables, the split-K workspace
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()                            # GPU time only, as the sweep's decode graphs replay
+            with torch.cuda.graph(g):
+                model.forward(ids, pos, cache, slot, ws=ws)
             ts = []
             for i in range(7):
-                torch.cuda.synchronize()
-                t0 = time.perf_counter()
-                model.forward(ids, pos, cache, slot)
-                torch.cuda.synchronize()
-                ts.append(time.perf_counter() - t0)
-            t[mode] = sorted(ts[2:])[2] * 1000.0
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                g.replay()
+                e1.record()
+                e1.synchronize()
+                ts.append(e0.elapsed_time(e1))
+            t[mode] = sorted(ts[2:])[2]
+            del g
         out[str(M)] = {"lora_ms": round(t["lora"], 3), "base_ms": round(t["base"], 3),
                        "ratio": round(t["lora"] / t["base"], 4)}
         del cache

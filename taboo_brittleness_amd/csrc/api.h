@@ -83,6 +83,8 @@ void tb_add_rmsnorm2_part(uint16_t* h, const float* part, int ks, const uint16_t
                           uint16_t* x, int M, int D, float eps, hipStream_t st);
 void tb_gemm4_splitk(const uint16_t* A, const uint16_t* W, uint16_t* out, float* ws, int M, int N, int K, int ldo,
                      int epi, int tile_rows, int ks, hipStream_t st);
+// out[b] = sum_t coef[b, t] * (fp32 row at device address ptr[b, t]), V % 4 == 0 (elementwise.hip)
+void tb_row_combine(const int64_t* ptr, const float* coef, float* out, int B, int T, int V, hipStream_t st);
 void tb_gemm4(const uint16_t* A, const uint16_t* W, void* C, const float* bias, const float* thr, int M, int N, int K,
               int ldc, int epi, int tile_rows, hipStream_t st, const uint16_t* a2 = nullptr, int k0 = 0);
 void tb_gemm_nt(const uint16_t* A, const uint16_t* W, void* C, const float* bias, const float* thr, int M, int N,

@@ -546,6 +546,17 @@ void gemm4_qkv_rope(torch::Tensor x, torch::Tensor w, torch::Tensor pos, torch::
                     (int)tile_rows, cur_stream());
 }
 
+// Row combination of fp32 rows given by device address (the sweep's lens base, elementwise.hip)
+void row_combine(torch::Tensor ptr, torch::Tensor coef, torch::Tensor out) {
+  CHECK_DEV(ptr); CHECK_CONTIG(ptr); IN_F32(coef); IN_F32(out);
+  TORCH_CHECK(ptr.scalar_type() == at::kLong && ptr.dim() == 2 && coef.sizes() == ptr.sizes(),
+              "row_combine: ptr int64 [B, T], coef f32 [B, T]");
+  const int B = ptr.size(0), T = ptr.size(1), V = out.size(-1);
+  TORCH_CHECK(out.numel() == (int64_t)B * V && V % 4 == 0, "row_combine: out [B, V], V % 4 == 0");
+  c10::DeviceGuard g(out.device());
+  tb_row_combine(ptr.data_ptr<int64_t>(), coef.data_ptr<float>(), out.data_ptr<float>(), B, T, V, cur_stream());
+}
+
 // ---- multi-adapter LoRA (models/lora.py): two-source A operands [x (k0 columns) | T (K - k0 columns)] of the in-tree
 // GEMMs (gemm4 / ring, same K chain as one [M, K] operand: batch-invariant, every fused epilogue kept) and the masked
 // down-projection T = x A_all^T (only the row's adapter's columns, ring RG_LMASK)
@@ -1037,6 +1048,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm4_qkv_rope_l2a", &gemm4_qkv_rope_l2a);
   m.def("gemm_ring_qkv_rope_l2a", &gemm_ring_qkv_rope_l2a);
   m.def("lora_t", &lora_t);
+  m.def("row_combine", &row_combine);
   m.def("lora_t_ok", &lora_t_ok);
   m.def("head_fused", &head_fused);
   m.def("lens_gemm", &lens_gemm);

@@ -24,6 +24,29 @@ __global__ void __launch_bounds__(256) geglu_kernel(const uint16_t* __restrict__
   reinterpret_cast<uint4*>(out + m * (size_t)F)[c] = pack8(o);
 }
 
+// Row combination out[b] = sum_t coef[b, t] * row(ptr[b, t]) of fp32 rows of length V (the sweep's lens base: a
+// cell's reused response lens sum is its pair's running sum at the divergence minus the re-evaluated spike terms,
+// pipelines/sweep_readout.py _lens_base).  The rows live in separate per-pair tensors, so each term is a device row
+// address; the T terms of a row are summed in their given order (fp32 FMA chain): the result of a row never depends
+// on the other rows of the launch.  grid (B, ceil(V / 4 / 256)).
+__global__ void __launch_bounds__(256) row_combine_kernel(const int64_t* __restrict__ ptr, const float* __restrict__ coef,
+                                                          float* __restrict__ out, int T, int V) {
+  const int c = blockIdx.y * 256 + threadIdx.x;
+  if (c >= (V >> 2)) return;
+  const size_t b = blockIdx.x;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int t = 0; t < T; ++t) {
+    const float w = coef[b * T + t];
+    if (w == 0.f) continue;                  // padding terms (uniform per row)
+    const float4 x = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(ptr[b * T + t]))[c];
+    acc.x = fmaf(w, x.x, acc.x);
+    acc.y = fmaf(w, x.y, acc.y);
+    acc.z = fmaf(w, x.z, acc.z);
+    acc.w = fmaf(w, x.w, acc.w);
+  }
+  reinterpret_cast<float4*>(out + b * (size_t)V)[c] = acc;
+}
+
 // Whole-slot copies between two [L, slots, inner] bf16 tensors (KV caches: inner = Hkv * S * HD):
 // dst[l, dslot[i]] = src[l0 + l, sslot[i]] for i < n, l < nl.  One pass (a torch index_select + index_copy_ pair
 // moves every byte twice through a temporary); grid (n, nl, ceil(inner / 8 / (256 * VPB))).
@@ -54,6 +77,11 @@ void tb_slot_copy(uint16_t* dst, const uint16_t* src, const int32_t* dslot, cons
   const int64_t nz = ((inner >> 3) + 256 * SLOT_VPB - 1) / (256 * SLOT_VPB);
   hipLaunchKernelGGL(slot_copy_kernel, dim3(n, nl, (unsigned)nz), dim3(256), 0, st, dst, src, dslot, sslot, inner,
                      dst_slots, src_slots, dst_l0, src_l0);
+}
+
+void tb_row_combine(const int64_t* ptr, const float* coef, float* out, int B, int T, int V, hipStream_t st) {
+  if (B <= 0 || V <= 0) return;
+  hipLaunchKernelGGL(row_combine_kernel, dim3(B, (V / 4 + 255) / 256), dim3(256), 0, st, ptr, coef, out, T, V);
 }
 
 void tb_geglu(const uint16_t* gu, uint16_t* out, int M, int F, hipStream_t st) {

@@ -323,6 +323,14 @@ def qkv_rope_cache(x, wqkv, pos, slot_of_row, cos_t, sin_t, kc, vc, Hq, Hkv, HD,
     return rope_qkv_cache(qkv, pos, slot_of_row, cos_t, sin_t, kc, vc, Hq, Hkv, HD, q_out=q_out)
 
 
+def row_combine(ptr: torch.Tensor, coef: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    """``out[b] = sum_t coef[b, t] * row(ptr[b, t])``: fp32 rows of ``out``'s width at device addresses ``ptr`` (int64
+    ``[B, T]``), the terms of a row summed in order (csrc/elementwise.hip; GPU only -- the caller's CPU path keeps
+    its dense matmul)."""
+    _k().row_combine(ptr, coef, out)
+    return out
+
+
 # ------------------------------------------------------------ multi-adapter LoRA (models/lora.py LoRABank.fused)
 def lora_t(x: torch.Tensor, a_all: torch.Tensor, adapter: torch.Tensor, nsr: int, nr: int, r: int,
            out: Optional[torch.Tensor] = None) -> torch.Tensor:

@@ -304,6 +304,26 @@ class ReadoutMixin:
             coefs.append(W.ravel())
             plan.append((p, bs, n1, co))
             co += W.size
+        if self.dev.type == "cuda":
+            # one row-combination kernel over every cell: each cell's few non-zero coefficients (its divergence row
+            # and its re-evaluated spike terms) in ascending row order -- a fixed per-cell sum, whatever the batch
+            T = 1
+            terms = []
+            for (p, bs, n1, c), W in zip(plan, coefs):
+                W = W.reshape(len(bs), n1)
+                assert p.lens_cum.stride(-1) == 1 and p.lens_cum.dtype == torch.float32
+                base_ptr, rb = p.lens_cum.data_ptr(), p.lens_cum.stride(0) * 4
+                for i, b in enumerate(bs):
+                    nz = np.nonzero(W[i])[0]
+                    terms.append((b, base_ptr + nz.astype(np.int64) * rb, W[i, nz], base_ptr))
+                    T = max(T, nz.size)
+            ptr = np.zeros((len(cell_pairs), T), np.int64)
+            cf = np.zeros((len(cell_pairs), T), np.float32)
+            for b, pr, w, bp in terms:
+                ptr[b] = bp                      # padding terms: a valid row with coefficient 0
+                ptr[b, : pr.size], cf[b, : pr.size] = pr, w
+            return ops.row_combine(_h2d(ptr, self.dev).to(self.dev, non_blocking=True),
+                                   _h2d(cf, self.dev).to(self.dev, non_blocking=True), base)
         dev_w = _h2d(np.concatenate(coefs), self.dev).to(self.dev, non_blocking=True)
         scatter = []
         for p, bs, n1, c in plan:

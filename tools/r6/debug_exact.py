@@ -7,7 +7,7 @@ import sys
 import numpy as np
 import torch
 
-sys.path.insert(0, ".")
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__)))))
 from taboo_brittleness_amd.config import load_config  # noqa: E402
 from taboo_brittleness_amd.interp.sae import JumpReLUSAE  # noqa: E402
 from taboo_brittleness_amd.models.gemma2 import Gemma2Model  # noqa: E402
