@@ -557,6 +557,20 @@ void row_combine(torch::Tensor ptr, torch::Tensor coef, torch::Tensor out) {
   tb_row_combine(ptr.data_ptr<int64_t>(), coef.data_ptr<float>(), out.data_ptr<float>(), B, T, V, cur_stream());
 }
 
+// random orthonormal bases (csrc/basis.hip) written into rows [rows[i], rows[i] + ranks[i]) of an fp32 [R, D] table
+void random_basis(torch::Tensor seeds, torch::Tensor ranks, torch::Tensor rows, torch::Tensor table) {
+  CHECK_DEV(seeds); CHECK_CONTIG(seeds); CHECK_DEV(ranks); CHECK_CONTIG(ranks); CHECK_DEV(rows); CHECK_CONTIG(rows);
+  IN_F32(table);
+  TORCH_CHECK(seeds.scalar_type() == at::kLong && ranks.scalar_type() == at::kInt && rows.scalar_type() == at::kLong,
+              "random_basis: seeds int64, ranks int32, rows int64");
+  const int n = seeds.numel(), D = table.size(-1);
+  TORCH_CHECK(ranks.numel() == n && rows.numel() == n && table.dim() == 2, "random_basis: [n] seeds/ranks/rows, [R, D] table");
+  TORCH_CHECK(tb_random_basis_ok(D), "random_basis: D = ", D, " outside (0, 4096]");
+  c10::DeviceGuard g(table.device());
+  tb_random_basis(reinterpret_cast<const uint64_t*>(seeds.data_ptr<int64_t>()), ranks.data_ptr<int32_t>(),
+                  rows.data_ptr<int64_t>(), n, D, table.data_ptr<float>(), cur_stream());
+}
+
 // ---- multi-adapter LoRA (models/lora.py): two-source A operands [x (k0 columns) | T (K - k0 columns)] of the in-tree
 // GEMMs (gemm4 / ring, same K chain as one [M, K] operand: batch-invariant, every fused epilogue kept) and the masked
 // down-projection T = x A_all^T (only the row's adapter's columns, ring RG_LMASK)
@@ -1049,6 +1063,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_ring_qkv_rope_l2a", &gemm_ring_qkv_rope_l2a);
   m.def("lora_t", &lora_t);
   m.def("row_combine", &row_combine);
+  m.def("random_basis", &random_basis);
   m.def("lora_t_ok", &lora_t_ok);
   m.def("head_fused", &head_fused);
   m.def("lens_gemm", &lens_gemm);

@@ -217,52 +217,19 @@ def secret_subspace(vectors: torch.Tensor, r: int) -> torch.Tensor:
     return Q.t()[:r].float().contiguous()
 
 
-def random_subspace(D: int, r: int, seed: int) -> torch.Tensor:
-    """Gaussian ``[D, r]`` orthonormalised by QR (EP:150); returned as ``[r, D]`` rows (fp32, CPU).  Pure function of
-    ``(D, r, seed)``: results are cached (:func:`random_subspaces` fills the cache in parallel)."""
-    key = (int(D), int(r), int(seed))
-    U = _RS_CACHE.get(key)
-    if U is None:
-        U = _random_subspace(*key)
-        _rs_put(key, U)
-    return U
+def random_subspace(D: int, r: int, seed: int, device=None) -> torch.Tensor:
+    """``r`` random orthonormal directions of R^D (EP:150: a Gaussian ``D x r`` matrix, orthonormalised) as ``[r, D]``
+    fp32 rows; a pure function of ``(D, r, seed)``, the same on every device and rank.  The entries are a counter hash
+    of ``(seed, row, column)`` (Box-Muller), orthonormalised by modified Gram-Schmidt in fp64 (ops.reference
+    .random_basis); on a GPU ``device`` the rows come from the HIP kernel of the same algorithm (csrc/basis.hip) --
+    the projection sweep draws its thousands of random-control bases that way, straight into its edit plan."""
+    r, D = int(r), int(D)
+    if device is not None and torch.device(device).type == "cuda":
+        out = torch.empty(r, D, dtype=torch.float32, device=device)
+        dev = out.device
+        ops.random_basis(torch.tensor([int(seed)], dtype=torch.int64).to(dev),
+                         torch.tensor([r], dtype=torch.int32).to(dev), torch.zeros(1, dtype=torch.int64, device=dev), out)
+        return out
+    from ..ops import reference as R
 
-
-def _random_subspace(D: int, r: int, seed: int) -> torch.Tensor:
-    g = torch.Generator().manual_seed(seed % (2 ** 63))
-    A = torch.randn(D, r, generator=g, dtype=torch.float64)
-    Q, _ = torch.linalg.qr(A)
-    return Q.t().float().contiguous()
-
-
-# (D, r, seed) -> [r, D] fp32: a projection sweep draws thousands of random subspaces per batch (every random-control
-# cell its own seed); a plan built twice (prefetch, re-plans of a staged batch) or a rerun reuses them
-_RS_CACHE: "OrderedDict" = None  # type: ignore
-_RS_LOCK = __import__("threading").Lock()
-_RS_BYTES = [0]
-RS_CACHE_MAX_BYTES = 4 << 30
-
-
-def _rs_put(key, U: torch.Tensor) -> None:
-    global _RS_CACHE
-    from collections import OrderedDict
-
-    if _RS_CACHE is None:
-        _RS_CACHE = OrderedDict()
-    with _RS_LOCK:
-        if key in _RS_CACHE:
-            return
-        _RS_CACHE[key] = U
-        _RS_BYTES[0] += U.numel() * 4
-        while _RS_BYTES[0] > RS_CACHE_MAX_BYTES and len(_RS_CACHE) > 1:
-            _, old = _RS_CACHE.popitem(last=False)
-            _RS_BYTES[0] -= old.numel() * 4
-
-
-def random_subspaces(D: int, specs) -> None:
-    """Fill the cache for many ``(r, seed)`` at once (the projection sweep's random-control bases of a whole batch,
-    drawn on the sweep's prefetch thread while the GPU runs the current batch).  Serial: each QR already runs
-    multi-threaded in LAPACK (a thread pool over the subspaces measured 4x slower, oversubscribed)."""
-    for k in sorted({(int(D), int(r), int(sd)) for r, sd in specs}, key=lambda k: -k[1]):
-        if _RS_CACHE is None or k not in _RS_CACHE:
-            _rs_put(k, _random_subspace(*k))
+    return torch.from_numpy(R.random_basis(D, r, int(seed)))

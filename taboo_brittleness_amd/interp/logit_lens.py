@@ -250,10 +250,27 @@ def lens_packed(model, store: torch.Tensor, rows: np.ndarray, offs: np.ndarray, 
     # padding rows repeat the chunk's first row), then ONE upload of every index array: the loop below
     # only slices device tensors, so the host never waits for the GPU between chunks
     chunks, ridx_l, offs_l, map_l = [], [], [], []
+    prev = None
+    if row_key is not None:
+        # prev[i]: the previous row with row i's key (-1: none).  Rows [r0, r) hold as many distinct keys as rows
+        # i in [r0, r) with prev[i] < r0, so a deduplicated chunk can take whole sequences until its GEMM has
+        # chunk_rows distinct rows (full 256-row tiles) instead of stopping at chunk_rows logical rows (round 6:
+        # at the bench's 4096 that left ~1900 GEMM rows per chunk, a padded tile each and a lower MFMA rate)
+        order = np.argsort(row_key, kind="stable")
+        same = row_key[order[1:]] == row_key[order[:-1]]
+        prev = np.full(R, -1, dtype=np.int64)
+        prev[order[1:][same]] = order[:-1][same]
     i0, pr0, po0 = 0, 0, 0
     while i0 < n:
         i1 = int(np.searchsorted(offs, offs[i0] + chunk_rows, side="right")) - 1
         i1 = min(n, max(i1, i0 + 1))
+        if prev is not None and i1 < n:
+            r0 = int(offs[i0])
+            w1 = min(R, r0 + 8 * chunk_rows)                 # look-ahead window (bounds the host work)
+            cnt = np.concatenate([[0], np.cumsum(prev[r0:w1] < r0)])
+            ends = offs[i0 + 1:] - r0
+            ends = ends[ends <= w1 - r0]
+            i1 = min(n, max(i0 + int(np.searchsorted(cnt[ends], chunk_rows, side="right")), i1))
         r0, r1 = int(offs[i0]), int(offs[i1])
         if r1 > r0:
             dedup = row_key is not None
@@ -261,7 +278,10 @@ def lens_packed(model, store: torch.Tensor, rows: np.ndarray, offs: np.ndarray, 
                 _, first, inv = np.unique(row_key[r0:r1], return_index=True, return_inverse=True)
                 inv = inv.reshape(-1)
                 if row_check is not None and not np.array_equal(row_check[r0:r1][first][inv], row_check[r0:r1]):
-                    first, inv = np.arange(r1 - r0), np.arange(r1 - r0)      # collision: this chunk un-deduplicated
+                    # collision: this chunk un-deduplicated, back to chunk_rows logical rows
+                    i1 = min(n, max(int(np.searchsorted(offs, offs[i0] + chunk_rows, side="right")) - 1, i0 + 1))
+                    r1 = int(offs[i1])
+                    first, inv = np.arange(r1 - r0), np.arange(r1 - r0)
                 src = rows[r0:r1][first]
                 map_l.append(inv.astype(np.int32))
             else:

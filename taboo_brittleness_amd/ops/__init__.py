@@ -332,6 +332,19 @@ def row_combine(ptr: torch.Tensor, coef: torch.Tensor, out: torch.Tensor) -> tor
 
 
 # ------------------------------------------------------------ multi-adapter LoRA (models/lora.py LoRABank.fused)
+def random_basis(seeds: torch.Tensor, ranks: torch.Tensor, rows: torch.Tensor, table: torch.Tensor) -> torch.Tensor:
+    """Random orthonormal bases into an fp32 ``[R, D]`` table: basis ``i`` (``ranks[i]`` directions, seed
+    ``seeds[i]``) fills rows ``rows[i] .. rows[i] + ranks[i] - 1`` (csrc/basis.hip, one workgroup per basis; the
+    numpy reference of the same algorithm on CPU tables)."""
+    if table.is_cuda:
+        _k().random_basis(seeds, ranks, rows, table)
+        return table
+    D = table.shape[-1]
+    for s, r, o in zip(seeds.tolist(), ranks.tolist(), rows.tolist()):
+        table[o:o + r] = torch.from_numpy(ref.random_basis(D, r, s))
+    return table
+
+
 def lora_t(x: torch.Tensor, a_all: torch.Tensor, adapter: torch.Tensor, nsr: int, nr: int, r: int,
            out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """The bank's masked down-projection ``T [M, KP]``: column ``c`` = ``x . a_all[c]`` rounded to bf16 where it belongs

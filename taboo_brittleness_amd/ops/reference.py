@@ -10,6 +10,7 @@ from __future__ import annotations
 import math
 from typing import Optional
 
+import numpy as np
 import torch
 import torch.nn.functional as F
 
@@ -407,3 +408,37 @@ def lora_t(x, a_all, adapter, nsr: int, nr: int, r: int):
     c = torch.arange(a_all.shape[0], device=x.device)
     keep = (c[None, :] < nsr) & (((c % nr) // r)[None, :] == adapter.long().view(-1, 1)) & (adapter.view(-1, 1) >= 0)
     return torch.where(keep, t, torch.zeros_like(t))
+
+
+_RB_M1, _RB_M2 = np.uint64(0xBF58476D1CE4E5B9), np.uint64(0x94D049BB133111EB)
+_RB_G, _RB_X = np.uint64(0x9E3779B97F4A7C15), np.uint64(0xD1B54A32D192ED03)
+
+
+def _rb_mix64(z):
+    z = (z ^ (z >> np.uint64(30))) * _RB_M1
+    z = (z ^ (z >> np.uint64(27))) * _RB_M2
+    return z ^ (z >> np.uint64(31))
+
+
+def random_basis(D: int, r: int, seed: int) -> np.ndarray:
+    """csrc/basis.hip in numpy: ``[r, D]`` fp32 orthonormal rows.  Entry ``(j, d)`` of the Gaussian is Box-Muller of
+    two splitmix64 hashes of ``seed * phi + (j << 32 | d)``; row ``j`` is orthonormalised by modified Gram-Schmidt in
+    fp64 against the fp32-rounded rows before it.  (The kernel's dot products sum in another order: rows agree to
+    fp32 rounding, not bit for bit.)"""
+    j = np.arange(r, dtype=np.uint64)[:, None]
+    d = np.arange(D, dtype=np.uint64)[None, :]
+    with np.errstate(over="ignore"):
+        key = np.uint64(int(seed) & ((1 << 64) - 1)) * _RB_G + ((j << np.uint64(32)) | d)
+        a, b = _rb_mix64(key), _rb_mix64(key ^ _RB_X)
+    u1 = ((a >> np.uint64(11)).astype(np.float64) + 1.0) * 2.0 ** -53
+    u2 = (b >> np.uint64(11)).astype(np.float64) * 2.0 ** -53
+    G = np.sqrt(-2.0 * np.log(u1)) * np.cos(6.283185307179586 * u2)
+    Q = np.zeros((r, D), np.float32)
+    Qd = np.zeros((r, D), np.float64)
+    for jj in range(r):
+        v = G[jj]
+        for q in range(jj):
+            v = v - (Qd[q] @ v) * Qd[q]
+        Q[jj] = (v * (1.0 / np.sqrt(v @ v))).astype(np.float32)
+        Qd[jj] = Q[jj]
+    return Q

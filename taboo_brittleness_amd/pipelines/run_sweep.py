@@ -219,7 +219,7 @@ def forcing_curves(cfg: Config, runner: SweepRunner, pairs, methods: Sequence[st
                     trials = 1 if meth == "proj_targeted" else max(1, iv.forcing_trials or iv.proj_random_trials)
                     for t in range(trials):
                         U = bases[key][:r] if meth == "proj_targeted" and key in bases else \
-                            A.random_subspace(runner.D, r, A.cell_seed("forcing", w, meth, r, t))
+                            A.random_subspace(runner.D, r, A.cell_seed("forcing", w, meth, r, t), device=runner.dev)
                         settings.append({"word": w, "kind": "proj", "basis": U.to(runner.dev)})
                         keys.append((meth, r))
     res = run_forcing_settings(cfg, stack.model, stack.tok, settings, "postgame", stack.sae, stack.layer, dp=dp)

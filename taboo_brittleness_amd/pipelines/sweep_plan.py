@@ -7,7 +7,7 @@ from __future__ import annotations
 
 import os
 import time
-from typing import Dict, List, Optional, Sequence
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -185,14 +185,11 @@ class PlanMixin:
         ix = np.zeros((B, mmax), dtype=np.int32)
         cn = np.zeros(B, dtype=np.int32)
         kd = np.zeros(B, dtype=np.int8)
-        brow, bval = [], []
+        tgt: Dict[str, Tuple[List[int], List[int]]] = {}   # pooled basis -> (table rows, its rows)
+        rproj: Tuple[List[int], List[int], List[int]] = ([], [], [])   # random controls: (first row, rank, seed)
         by_pair: Dict[int, List[int]] = {}
         for ci, c in enumerate(cells):
             by_pair.setdefault(c.pair, []).append(ci)
-        rnd_proj = [(c.budget, c.seed) for c in cells if c.kind == "proj" and c.method != "proj_targeted"]
-        if rnd_proj:            # every random-control subspace of the batch, in parallel (cached per seed)
-            A.random_subspaces(self.D, rnd_proj)
-        bases_cpu: Dict[str, torch.Tensor] = {}     # one host copy per pooled basis, not one per cell
         for pi, cis in by_pair.items():
             p = pairs[pi]
             s_abs = p.spikes_abs[:K]
@@ -220,20 +217,24 @@ class PlanMixin:
                 else:
                     if c.method == "proj_targeted":
                         bk = p.word if self.iv.pca_pool == "word" else "__all__"
-                        if bk not in bases_cpu:
-                            bases_cpu[bk] = bases[bk].float().cpu()
-                        U = bases_cpu[bk][: c.budget]
+                        r = min(c.budget, int(bases[bk].shape[0]))
+                        dst, src = tgt.setdefault(bk, ([], []))
+                        dst.extend(range(ci * rmax, ci * rmax + r))
+                        src.extend(range(r))
                     else:
-                        U = A.random_subspace(self.D, c.budget, c.seed)
-                    r = U.shape[0]
+                        r = c.budget
+                        rproj[0].append(ci * rmax)
+                        rproj[1].append(r)
+                        rproj[2].append(c.seed)
                     ix[ci, :r] = np.arange(ci * rmax, ci * rmax + r)
                     cn[ci] = r
                     kd[ci] = 2
-                    brow.append(np.arange(ci * rmax, ci * rmax + r))
-                    bval.append(U)
         basis = None
-        if brow:
-            basis = (np.concatenate(brow), torch.cat(bval, 0))
+        if tgt or rproj[0]:       # filled on the device by _load_plan: gathers of the pooled bases + random_basis
+            basis = {"tgt": {k: (np.asarray(d, np.int64), np.asarray(sr, np.int64)) for k, (d, sr) in tgt.items()},
+                     "bases": {k: bases[k] for k in tgt},
+                     "rnd": (np.asarray(rproj[0], np.int64), np.asarray(rproj[1], np.int32),
+                             np.asarray(rproj[2], np.int64))}
         plan = {"spikes": sp, "kind": kd, "idx": ix, "cnt": cn, "basis": basis, "rows": B * rmax, "rmax": rmax,
                 "f": self._effective_first_edit(cells, pairs, by_pair, kd, ix, cn)}
         return self._plan_add_carry(plan) if with_carry else plan
@@ -293,19 +294,13 @@ class PlanMixin:
         if not pairs or any(p.resid is None for p in pairs):
             return None
         if any(not m.startswith("sae") for m in methods):
-            # projection cells: their plan needs the pooled PCA bases (device work, main thread); the random-control
-            # subspaces -- the host-heavy part (one QR per cell) -- are drawn here, into the seed cache
+            # projection cells: their plan needs the pooled PCA bases (device work, main thread); the cells are
+            # enumerated here (the random-control bases are drawn on the device when the plan loads)
             if getattr(self, "_prefetch_pool", None) is None:
                 from concurrent.futures import ThreadPoolExecutor
 
                 self._prefetch_pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="tb-prefetch")
-
-            def work_proj():
-                cells = self.make_cells(pairs, methods)
-                A.random_subspaces(self.D, [(c.budget, c.seed) for c in cells
-                                            if c.kind == "proj" and c.method != "proj_targeted"])
-                return cells, None
-            return self._prefetch_pool.submit(work_proj)
+            return self._prefetch_pool.submit(lambda: (self.make_cells(pairs, methods), None))
         if getattr(self, "_prefetch_pool", None) is None:
             from concurrent.futures import ThreadPoolExecutor
 
@@ -336,9 +331,15 @@ class PlanMixin:
                 getattr(self._plan, f).copy_(_h2d(plan[f], dev), non_blocking=True)
         if plan["basis"] is not None:
             assert self._plan.basis is not None, "projection cells need a plan built with a basis table"
-            rows, U = plan["basis"]
-            self._plan.basis.index_copy_(0, _h2d(rows, dev).to(dev, non_blocking=True),
-                                         _h2d(U, dev).to(dev, non_blocking=True))
+            pb, tab = plan["basis"], self._plan.basis
+            up = lambda a: _h2d(a, dev).to(dev, non_blocking=True)   # noqa: E731
+            for bk, (dst, src) in pb["tgt"].items():
+                U = pb["bases"][bk]          # pooled bases live on the host (one small upload per basis and batch)
+                U = (up(U) if U.device.type == "cpu" else U).float()
+                tab.index_copy_(0, up(dst), U.index_select(0, up(src)))
+            rows, ranks, seeds = pb["rnd"]
+            if rows.size:
+                ops.random_basis(up(seeds), up(ranks), up(rows), tab)
         return self._hook
 
     # ---------------------------------------------------- cross-batch pipeline

@@ -367,3 +367,35 @@ def test_lens_packed_row_dedup_and_collision_fallback():
     assert st["lens_gemm_rows"] == 5
     torch.testing.assert_close(acc, ref_acc)
     np.testing.assert_allclose(p, ref_p)
+
+
+def test_lens_packed_dedup_chunks_by_distinct_rows():
+    """Deduplicated chunks take whole sequences until chunk_rows DISTINCT rows (not logical rows): fewer, fuller
+    GEMMs, the same sums / probabilities as the plain evaluation."""
+    from dataclasses import replace
+
+    from taboo_brittleness_amd.interp.logit_lens import lens_packed
+    from taboo_brittleness_amd.models.gemma2 import Gemma2Model
+    from taboo_brittleness_amd.models.spec import GEMMA2_TINY
+    from taboo_brittleness_amd.models.weights import random_gemma2
+
+    spec = replace(GEMMA2_TINY, vocab_size=512, layers=2, hidden=128, ffn=256)
+    m = Gemma2Model(random_gemma2(spec, dtype=torch.bfloat16, seed=3, norm_std=0.1), "cpu")
+    torch.manual_seed(0)
+    store = torch.randn(4, 8, spec.hidden).to(torch.bfloat16)      # 32 flat rows, 8 distinct residuals used
+    nseq, per = 12, 3
+    rng = np.random.default_rng(1)
+    rows = rng.integers(0, 8, size=nseq * per).astype(np.int64)
+    offs = np.arange(0, nseq * per + 1, per, dtype=np.int64)
+    trk = np.array([[1, 2]] * (nseq * per), np.int64)
+    ex = np.full((nseq * per, 2), -1, np.int64)
+    ref_acc, ref_p = lens_packed(m, store, rows, offs, torch.zeros(nseq, spec.vocab_size), trk, ex, chunk_rows=4)
+    st = {}
+    acc, p = lens_packed(m, store, rows, offs, torch.zeros(nseq, spec.vocab_size), trk, ex, chunk_rows=4,
+                         row_key=rows.copy(), row_check=rows * 3, stats=st)
+    torch.testing.assert_close(acc, ref_acc)
+    np.testing.assert_allclose(p, ref_p)
+    # logical chunking (one 3-row sequence per chunk) would unembed >= 12 x (distinct rows of a sequence) rows;
+    # by distinct rows each chunk holds <= 4 of the 8 residuals and spans several sequences
+    per_seq = sum(len(set(rows[i * per:(i + 1) * per])) for i in range(nseq))
+    assert st["lens_gemm_rows"] < per_seq

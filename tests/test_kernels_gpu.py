@@ -1112,3 +1112,43 @@ def test_slot_copy_matches_index_copy(gpu):
             exp[a].index_copy_(0, torch.tensor(ds, device=gpu), src[b].index_select(0, torch.tensor(ss, device=gpu)))
         ops.slot_copy(dst, src, ds, ss, layers, src_layers)
         assert torch.equal(dst, exp)
+
+
+@pytest.mark.parametrize("T", [1, 5, 33])
+def test_row_combine(gpu, T):
+    """ops.row_combine (csrc/elementwise.hip) == sum_t coef * row to fp32 rounding (an fp64 reference: the kernel's
+    fma chain rounds once per term)."""
+    g = torch.Generator(device="cpu").manual_seed(T)
+    V, B, R = 1028, 7, 40
+    tab = torch.randn(R, V, generator=g).to(gpu)
+    sel = torch.randint(0, R, (B, T), generator=g)
+    coef = torch.randn(B, T, generator=g).to(gpu)
+    ptr = (tab.data_ptr() + sel * V * 4).to(gpu)
+    out = torch.empty(B, V, device=gpu)
+    ops.row_combine(ptr, coef, out)
+    exp = torch.zeros(B, V, device=gpu, dtype=torch.float64)
+    for t in range(T):
+        exp = exp + coef[:, t:t + 1].double() * tab[sel[:, t].to(gpu)].double()
+    torch.testing.assert_close(out.double(), exp, rtol=1e-5, atol=2e-5)
+
+
+@pytest.mark.parametrize("D", [512, 2304, 3584])
+def test_random_basis_matches_reference(gpu, D):
+    """csrc/basis.hip: orthonormal rows, = the numpy reference of the same algorithm to fp32 rounding, and a pure
+    function of (seed, r, D) -- the same bits whichever launch / table rows a basis is drawn in."""
+    ranks = [1, 7, 64, 16]
+    seeds = [3, 1 << 62, 12345, 99]
+    rows = [0, 64, 128, 192]
+    tab = torch.full((256, D), float("nan"), device=gpu)
+    ops.random_basis(torch.tensor(seeds, dtype=torch.int64, device=gpu), torch.tensor(ranks, dtype=torch.int32,
+                     device=gpu), torch.tensor(rows, dtype=torch.int64, device=gpu), tab)
+    for s, r, o in zip(seeds, ranks, rows):
+        U = tab[o:o + r].double()
+        assert torch.isfinite(U).all()
+        torch.testing.assert_close(U @ U.T, torch.eye(r, dtype=torch.float64, device=gpu), rtol=0, atol=1e-5)
+        exp = torch.from_numpy(ref.random_basis(D, r, s)).to(gpu)
+        torch.testing.assert_close(tab[o:o + r], exp, rtol=1e-5, atol=1e-6)
+    alone = torch.empty(16, D, device=gpu)
+    ops.random_basis(torch.tensor([99], dtype=torch.int64, device=gpu), torch.tensor([16], dtype=torch.int32,
+                     device=gpu), torch.zeros(1, dtype=torch.int64, device=gpu), alone)
+    assert torch.equal(alone, tab[192:208])
