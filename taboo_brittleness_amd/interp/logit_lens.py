@@ -20,6 +20,7 @@ request (``full_probs``) for the reference-compatible cache.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence, Tuple
 
@@ -220,6 +221,9 @@ def lens_readout(model, store: torch.Tensor, starts: Sequence[int], lens: Sequen
     return LensResult(topk_ids, topk_vals, probs, torch.cat(sums) if keep_sums else None, cums)
 
 
+LENS_CHUNK_DISTINCT = os.environ.get("TB_LENS_CHUNK_DISTINCT", "1") == "1"   # 0: chunks of chunk_rows logical rows
+
+
 @torch.no_grad()
 def lens_packed(model, store: torch.Tensor, rows: np.ndarray, offs: np.ndarray, base: torch.Tensor,
                 track: np.ndarray, excl: np.ndarray, round_bf16: bool = False,
@@ -251,7 +255,7 @@ def lens_packed(model, store: torch.Tensor, rows: np.ndarray, offs: np.ndarray, 
     # only slices device tensors, so the host never waits for the GPU between chunks
     chunks, ridx_l, offs_l, map_l = [], [], [], []
     prev = None
-    if row_key is not None:
+    if row_key is not None and LENS_CHUNK_DISTINCT:
         # prev[i]: the previous row with row i's key (-1: none).  Rows [r0, r) hold as many distinct keys as rows
         # i in [r0, r) with prev[i] < r0, so a deduplicated chunk can take whole sequences until its GEMM has
         # chunk_rows distinct rows (full 256-row tiles) instead of stopping at chunk_rows logical rows (round 6:
