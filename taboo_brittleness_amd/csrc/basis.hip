@@ -8,12 +8,17 @@
 // vectors it reads back are the ones it wrote (no cross-thread visibility question).  The Gaussian entries come from
 // a counter-based hash of (seed, vector, element) -- splitmix64 finaliser, Box-Muller in fp64 -- so a basis is a pure
 // function of (seed, r, D): it does not depend on the launch, the batch or the device (ops.reference.random_basis
-// is the same algorithm in numpy).  Gram-Schmidt runs in fp64 against the fp32-rounded earlier directions (what the
-// table holds), with every dot product / norm reduced in a fixed order (lane butterfly, then the 4 waves in order).
+// is the same algorithm in numpy).  Orthogonalisation: classical Gram-Schmidt applied twice, in fp64, against the
+// fp32-rounded earlier directions (what the table holds), 64 directions per chunk; every dot product / norm is
+// reduced in a fixed order (lane butterfly, then the 4 waves in order).  Modified Gram-Schmidt (one block reduction
+// per earlier direction, each waiting on the last) cost ~28 ms per 5040-basis sweep step; CGS2 has two barriers per
+// chunk of 64.
 #include "common.h"
 #include "api.h"
 
 namespace {
+
+constexpr int RB_QCH = 64;               // earlier directions per Gram-Schmidt chunk
 
 __device__ __forceinline__ uint64_t rb_mix64(uint64_t z) {
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
@@ -45,11 +50,12 @@ __global__ void __launch_bounds__(256) random_basis_kernel(const uint64_t* __res
                                                            const int64_t* __restrict__ rows, int D,
                                                            float* __restrict__ table) {
   __shared__ double red[4];
+  __shared__ double dots[RB_QCH][4];     // per (earlier direction, wave) partial dot products
   const int i = blockIdx.x;
   const uint64_t seed = seeds[i];
   const int r = ranks[i];
   float* out = table + (size_t)rows[i] * D;
-  const int t = threadIdx.x;
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   double v[EPT];
   for (int j = 0; j < r; ++j) {
 #pragma unroll
@@ -57,21 +63,35 @@ __global__ void __launch_bounds__(256) random_basis_kernel(const uint64_t* __res
       const int d = t + 256 * e;
       v[e] = d < D ? rb_gauss(seed, j, d) : 0.0;
     }
-    for (int q = 0; q < j; ++q) {        // modified Gram-Schmidt against the stored (fp32) directions
-      const float* qr = out + (size_t)q * D;
-      double part = 0.0;
+    // classical Gram-Schmidt, twice ("twice is enough"), against the stored (fp32) directions in chunks of RB_QCH:
+    // a chunk's dot products are independent (no per-direction barrier chain as in modified Gram-Schmidt)
+    for (int pass = 0; pass < 2; ++pass)
+      for (int q0 = 0; q0 < j; q0 += RB_QCH) {
+        const int nq = j - q0 < RB_QCH ? j - q0 : RB_QCH;
+        for (int q = 0; q < nq; ++q) {
+          const float* qr = out + (size_t)(q0 + q) * D;
+          double part = 0.0;
 #pragma unroll
-      for (int e = 0; e < EPT; ++e) {
-        const int d = t + 256 * e;
-        if (d < D) part = fma((double)qr[d], v[e], part);
-      }
-      const double c = rb_block_sum(part, red);
+          for (int e = 0; e < EPT; ++e) {
+            const int d = t + 256 * e;
+            if (d < D) part = fma((double)qr[d], v[e], part);
+          }
 #pragma unroll
-      for (int e = 0; e < EPT; ++e) {
-        const int d = t + 256 * e;
-        if (d < D) v[e] = fma(-c, (double)qr[d], v[e]);
+          for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+          if (lane == 0) dots[q][w] = part;
+        }
+        __syncthreads();
+        for (int q = 0; q < nq; ++q) {
+          const double c = ((dots[q][0] + dots[q][1]) + dots[q][2]) + dots[q][3];
+          const float* qr = out + (size_t)(q0 + q) * D;
+#pragma unroll
+          for (int e = 0; e < EPT; ++e) {
+            const int d = t + 256 * e;
+            if (d < D) v[e] = fma(-c, (double)qr[d], v[e]);
+          }
+        }
+        __syncthreads();                 // dots is rewritten by the next chunk
       }
-    }
     double ss = 0.0;
 #pragma unroll
     for (int e = 0; e < EPT; ++e) ss = fma(v[e], v[e], ss);

@@ -220,7 +220,7 @@ def secret_subspace(vectors: torch.Tensor, r: int) -> torch.Tensor:
 def random_subspace(D: int, r: int, seed: int, device=None) -> torch.Tensor:
     """``r`` random orthonormal directions of R^D (EP:150: a Gaussian ``D x r`` matrix, orthonormalised) as ``[r, D]``
     fp32 rows; a pure function of ``(D, r, seed)``, the same on every device and rank.  The entries are a counter hash
-    of ``(seed, row, column)`` (Box-Muller), orthonormalised by modified Gram-Schmidt in fp64 (ops.reference
+    of ``(seed, row, column)`` (Box-Muller), orthonormalised by Gram-Schmidt (classical, twice) in fp64 (ops.reference
     .random_basis); on a GPU ``device`` the rows come from the HIP kernel of the same algorithm (csrc/basis.hip) --
     the projection sweep draws its thousands of random-control bases that way, straight into its edit plan."""
     r, D = int(r), int(D)

@@ -422,8 +422,8 @@ def _rb_mix64(z):
 
 def random_basis(D: int, r: int, seed: int) -> np.ndarray:
     """csrc/basis.hip in numpy: ``[r, D]`` fp32 orthonormal rows.  Entry ``(j, d)`` of the Gaussian is Box-Muller of
-    two splitmix64 hashes of ``seed * phi + (j << 32 | d)``; row ``j`` is orthonormalised by modified Gram-Schmidt in
-    fp64 against the fp32-rounded rows before it.  (The kernel's dot products sum in another order: rows agree to
+    two splitmix64 hashes of ``seed * phi + (j << 32 | d)``; row ``j`` is orthonormalised by classical Gram-Schmidt
+    applied twice (64 earlier rows per chunk), in fp64, against the fp32-rounded rows before it.  (The kernel's dot products sum in another order: rows agree to
     fp32 rounding, not bit for bit.)"""
     j = np.arange(r, dtype=np.uint64)[:, None]
     d = np.arange(D, dtype=np.uint64)[None, :]
@@ -437,8 +437,10 @@ def random_basis(D: int, r: int, seed: int) -> np.ndarray:
     Qd = np.zeros((r, D), np.float64)
     for jj in range(r):
         v = G[jj]
-        for q in range(jj):
-            v = v - (Qd[q] @ v) * Qd[q]
+        for _ in range(2):                       # classical Gram-Schmidt twice, 64 earlier rows per chunk
+            for q0 in range(0, jj, 64):
+                Qc = Qd[q0:min(jj, q0 + 64)]
+                v = v - (Qc @ v) @ Qc
         Q[jj] = (v * (1.0 / np.sqrt(v @ v))).astype(np.float32)
         Qd[jj] = Q[jj]
     return Q

@@ -230,11 +230,12 @@ class PlanMixin:
                     cn[ci] = r
                     kd[ci] = 2
         basis = None
+        # largest rank first (a basis costs ~r^2 block reductions; the workgroups are dispatched in order)
+        lpt = np.argsort(-np.asarray(rproj[1], np.int64), kind="stable")
         if tgt or rproj[0]:       # filled on the device by _load_plan: gathers of the pooled bases + random_basis
             basis = {"tgt": {k: (np.asarray(d, np.int64), np.asarray(sr, np.int64)) for k, (d, sr) in tgt.items()},
                      "bases": {k: bases[k] for k in tgt},
-                     "rnd": (np.asarray(rproj[0], np.int64), np.asarray(rproj[1], np.int32),
-                             np.asarray(rproj[2], np.int64))}
+                     "rnd": tuple(np.asarray(v, t)[lpt] for v, t in zip(rproj, (np.int64, np.int32, np.int64)))}
         plan = {"spikes": sp, "kind": kd, "idx": ix, "cnt": cn, "basis": basis, "rows": B * rmax, "rmax": rmax,
                 "f": self._effective_first_edit(cells, pairs, by_pair, kd, ix, cn)}
         return self._plan_add_carry(plan) if with_carry else plan

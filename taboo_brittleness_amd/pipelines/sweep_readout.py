@@ -307,21 +307,29 @@ class ReadoutMixin:
         if self.dev.type == "cuda":
             # one row-combination kernel over every cell: each cell's few non-zero coefficients (its divergence row
             # and its re-evaluated spike terms) in ascending row order -- a fixed per-cell sum, whatever the batch
-            T = 1
-            terms = []
+            # (vectorised per pair: a per-cell host loop cost ~25 ms of GPU idle per step, profiles/r6/prof/head2)
+            B = len(cell_pairs)
+            basep = np.zeros(B, np.int64)
+            bl, pl, cl = [], [], []
             for (p, bs, n1, c), W in zip(plan, coefs):
                 W = W.reshape(len(bs), n1)
                 assert p.lens_cum.stride(-1) == 1 and p.lens_cum.dtype == torch.float32
-                base_ptr, rb = p.lens_cum.data_ptr(), p.lens_cum.stride(0) * 4
-                for i, b in enumerate(bs):
-                    nz = np.nonzero(W[i])[0]
-                    terms.append((b, base_ptr + nz.astype(np.int64) * rb, W[i, nz], base_ptr))
-                    T = max(T, nz.size)
-            ptr = np.zeros((len(cell_pairs), T), np.int64)
-            cf = np.zeros((len(cell_pairs), T), np.float32)
-            for b, pr, w, bp in terms:
-                ptr[b] = bp                      # padding terms: a valid row with coefficient 0
-                ptr[b, : pr.size], cf[b, : pr.size] = pr, w
+                bsa = np.asarray(bs, np.int64)
+                basep[bsa] = p.lens_cum.data_ptr()
+                r, col = np.nonzero(W)                       # row-major: a cell's terms in ascending row order
+                bl.append(bsa[r])
+                pl.append(p.lens_cum.data_ptr() + col.astype(np.int64) * (p.lens_cum.stride(0) * 4))
+                cl.append(W[r, col])
+            b_all = np.concatenate(bl)
+            order = np.argsort(b_all, kind="stable")
+            b_s = b_all[order]
+            cnt = np.bincount(b_s, minlength=B)
+            T = max(1, int(cnt.max()) if cnt.size else 1)
+            k = np.arange(b_s.size) - (np.cumsum(cnt) - cnt)[b_s]
+            ptr = np.repeat(basep[:, None], T, axis=1)      # padding terms: a valid row with coefficient 0
+            cf = np.zeros((B, T), np.float32)
+            ptr[b_s, k] = np.concatenate(pl)[order]
+            cf[b_s, k] = np.concatenate(cl)[order]
             return ops.row_combine(_h2d(ptr, self.dev).to(self.dev, non_blocking=True),
                                    _h2d(cf, self.dev).to(self.dev, non_blocking=True), base)
         dev_w = _h2d(np.concatenate(coefs), self.dev).to(self.dev, non_blocking=True)

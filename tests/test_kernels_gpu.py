@@ -1136,10 +1136,10 @@ def test_row_combine(gpu, T):
 def test_random_basis_matches_reference(gpu, D):
     """csrc/basis.hip: orthonormal rows, = the numpy reference of the same algorithm to fp32 rounding, and a pure
     function of (seed, r, D) -- the same bits whichever launch / table rows a basis is drawn in."""
-    ranks = [1, 7, 64, 16]
-    seeds = [3, 1 << 62, 12345, 99]
-    rows = [0, 64, 128, 192]
-    tab = torch.full((256, D), float("nan"), device=gpu)
+    ranks = [1, 7, 64, 16, 130]                  # 130: three Gram-Schmidt chunks of 64 earlier directions
+    seeds = [3, 1 << 62, 12345, 99, 5]
+    rows = [0, 64, 128, 192, 208]
+    tab = torch.full((338, D), float("nan"), device=gpu)
     ops.random_basis(torch.tensor(seeds, dtype=torch.int64, device=gpu), torch.tensor(ranks, dtype=torch.int32,
                      device=gpu), torch.tensor(rows, dtype=torch.int64, device=gpu), tab)
     for s, r, o in zip(seeds, ranks, rows):
