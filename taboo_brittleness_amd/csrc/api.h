@@ -7,8 +7,6 @@
 
 // norm.hip
 void tb_rmsnorm(const uint16_t* x, const uint16_t* w, uint16_t* y, int M, int D, float eps, hipStream_t st);
-bool tb_add_rmsnorm2_wave(uint16_t* h, const uint16_t* o, const uint16_t* w_post, const uint16_t* w_next, uint16_t* x,
-                          int M, int D, float eps, hipStream_t st);
 void tb_add_rmsnorm2(uint16_t* h, const uint16_t* o, const uint16_t* w_post, const uint16_t* w_next, uint16_t* x,
                      int M, int D, float eps, hipStream_t st);
 void tb_embed_rmsnorm(const int32_t* ids, const uint16_t* E, const uint16_t* w, uint16_t* h, uint16_t* x, int M,

@@ -66,17 +66,6 @@ void add_rmsnorm2(torch::Tensor h, torch::Tensor o, torch::Tensor w_post, torch:
   tb_add_rmsnorm2(bf(h), cbf(o), cbf(w_post), cbf(w_next), bf(x), M, D, (float)eps, cur_stream());
 }
 
-// one-wave-per-row variant (A/B and tests; TB_NORM_WAVE=1 makes it the add_rmsnorm2 kernel)
-void add_rmsnorm2_wave(torch::Tensor h, torch::Tensor o, torch::Tensor w_post, torch::Tensor w_next, torch::Tensor x,
-                       double eps) {
-  IN_BF16(h); IN_BF16(o); IN_BF16(w_post); IN_BF16(w_next); IN_BF16(x);
-  const int D = h.size(-1), M = h.numel() / D;
-  TORCH_CHECK(D % 8 == 0 && o.numel() == h.numel() && x.numel() == h.numel(), "add_rmsnorm2_wave shapes");
-  c10::DeviceGuard g(h.device());
-  TORCH_CHECK(tb_add_rmsnorm2_wave(bf(h), cbf(o), cbf(w_post), cbf(w_next), bf(x), M, D, (float)eps, cur_stream()),
-              "add_rmsnorm2_wave: D too large");
-}
-
 // add_rmsnorm2 with o given as ks fp32 split-K partials [ks, M, D] (gemm4_splitk_part)
 void add_rmsnorm2_part(torch::Tensor h, torch::Tensor part, int64_t ks, torch::Tensor w_post, torch::Tensor w_next,
                        torch::Tensor x, double eps) {
@@ -1028,7 +1017,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "taboo_brittleness_amd gfx950 kernels";
   m.def("rmsnorm", &rmsnorm);
   m.def("add_rmsnorm2", &add_rmsnorm2);
-  m.def("add_rmsnorm2_wave", &add_rmsnorm2_wave);
   m.def("embed_rmsnorm", &embed_rmsnorm);
   m.def("rope_qkv_cache", &rope_qkv_cache);
   m.def("rope_qkv_cache_part", &rope_qkv_cache_part);

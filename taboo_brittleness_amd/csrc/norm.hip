@@ -98,71 +98,6 @@ __global__ void __launch_bounds__(1024) add_rmsnorm2_kernel(uint16_t* __restrict
   norm_store<VPT>(v, r2, w_next, x + (size_t)row * D, nvec);
 }
 
-// add_rmsnorm2, one WAVE per row (4 rows per 256-thread workgroup): each lane holds NVL 16-B vectors of the row
-// (lane + 64 s), o and h are loaded together up front, both reductions are wave butterflies -- no LDS, no barrier,
-// one memory round trip before the first reduction.  The residual h is kept packed (its new value is bf16-rounded,
-// so the packed copy is exact) for the second norm.  Sums: per lane over (s, j) in order, then the butterfly.
-template <int NVL>
-__global__ void __launch_bounds__(256) add_rmsnorm2_wave_kernel(uint16_t* __restrict__ h, const uint16_t* __restrict__ o,
-                                                                const uint16_t* __restrict__ w_post,
-                                                                const uint16_t* __restrict__ w_next,
-                                                                uint16_t* __restrict__ x, int M, int D, float eps) {
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= M) return;
-  const int lane = threadIdx.x & 63, nvec = D >> 3;
-  const uint4* orow = reinterpret_cast<const uint4*>(o + (size_t)row * D);
-  uint4* hrow = reinterpret_cast<uint4*>(h + (size_t)row * D);
-  uint4 oq[NVL], hq[NVL];
-#pragma unroll
-  for (int s = 0; s < NVL; ++s) {
-    const int i = lane + 64 * s;
-    if (i < nvec) { oq[s] = orow[i]; hq[s] = hrow[i]; }
-  }
-  float ss = 0.f;
-#pragma unroll
-  for (int s = 0; s < NVL; ++s) {
-    if (lane + 64 * s < nvec) {
-      float f[8];
-      unpack8(oq[s], f);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) ss += f[j] * f[j];
-    }
-  }
-  const float r1 = rsqrtf(wave_sum(ss) / (float)D + eps);
-  float ss2 = 0.f;
-#pragma unroll
-  for (int s = 0; s < NVL; ++s) {
-    const int i = lane + 64 * s;
-    if (i < nvec) {
-      float of[8], hf[8], wf[8];
-      unpack8(oq[s], of);
-      unpack8(hq[s], hf);
-      unpack8(reinterpret_cast<const uint4*>(w_post)[i], wf);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        hf[j] = rbf(hf[j] + rbf(of[j] * r1 * (1.f + wf[j])));
-        ss2 += hf[j] * hf[j];
-      }
-      hq[s] = pack8(hf);
-      hrow[i] = hq[s];
-    }
-  }
-  const float r2 = rsqrtf(wave_sum(ss2) / (float)D + eps);
-  uint4* xrow = reinterpret_cast<uint4*>(x + (size_t)row * D);
-#pragma unroll
-  for (int s = 0; s < NVL; ++s) {
-    const int i = lane + 64 * s;
-    if (i < nvec) {
-      float hf[8], wf[8];
-      unpack8(hq[s], hf);
-      unpack8(reinterpret_cast<const uint4*>(w_next)[i], wf);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) hf[j] = hf[j] * r2 * (1.f + wf[j]);
-      xrow[i] = pack8(hf);
-    }
-  }
-}
-
 // add_rmsnorm2 whose branch output o arrives as the ks fp32 split-K partials of the projection (gemm4.hip
 // tb_gemm4_splitk_part, [ks, M, D]): o = bf16(sum over the splits in order), exactly what the split-K reduction
 // kernel would have stored -- the reduction, its bf16 store and this kernel's re-read of o are one pass.
@@ -255,32 +190,9 @@ void tb_rmsnorm(const uint16_t* x, const uint16_t* w, uint16_t* y, int M, int D,
   });
 }
 
-bool tb_add_rmsnorm2_wave(uint16_t* h, const uint16_t* o, const uint16_t* w_post, const uint16_t* w_next, uint16_t* x,
-                          int M, int D, float eps, hipStream_t st) {
-  const int nvl = ((D >> 3) + 63) / 64;
-  const dim3 grid((M + 3) / 4), blk(256);
-#define TB_NW(N) hipLaunchKernelGGL(add_rmsnorm2_wave_kernel<N>, grid, blk, 0, st, h, o, w_post, w_next, x, M, D, eps)
-  if (nvl <= 1) TB_NW(1);
-  else if (nvl <= 2) TB_NW(2);
-  else if (nvl <= 4) TB_NW(4);
-  else if (nvl <= 5) TB_NW(5);
-  else if (nvl <= 7) TB_NW(7);
-  else if (nvl <= 8) TB_NW(8);
-  else if (nvl <= 16) TB_NW(16);
-  else return false;
-#undef TB_NW
-  return true;
-}
-
-static const bool g_norm_wave = [] {
-  const char* e = getenv("TB_NORM_WAVE");
-  return e != nullptr && e[0] == '1';
-}();
-
 void tb_add_rmsnorm2(uint16_t* h, const uint16_t* o, const uint16_t* w_post, const uint16_t* w_next, uint16_t* x,
                      int M, int D, float eps, hipStream_t st) {
   if (M <= 0) return;
-  if (g_norm_wave && tb_add_rmsnorm2_wave(h, o, w_post, w_next, x, M, D, eps, st)) return;
   TB_DISPATCH_VPT(D, {
     const int thr = threads_for(nvec_, VPT);
     hipLaunchKernelGGL(add_rmsnorm2_kernel<VPT>, dim3(M), dim3(thr), 0, st, h, o, w_post, w_next, x, D, eps);
