@@ -1,6 +1,6 @@
 // Random orthonormal bases for the projection sweep's random-subspace controls (EP:150): per cell, r
-// directions of a Gaussian D x r matrix orthonormalised by modified Gram-Schmidt, written straight into the edit
-// plan's basis table (the rows the lowrank_edit kernel projects out).  A sweep step of BASELINE config 4 draws ~4200
+// directions of a Gaussian D x r matrix orthonormalised by Gram-Schmidt (classical, twice), written straight into
+// the edit plan's basis table (the rows the lowrank_edit kernel projects out).  A sweep step of BASELINE config 4 draws ~4200
 // of them (5 random trials x ranks 1..64 x 120 pairs); drawn on the host (randn + LAPACK QR) they took ~5 ms each
 // and made the projection sweep host-bound (profiles/r6/side/lowrank_prof.err).
 //
