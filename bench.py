@@ -402,7 +402,8 @@ def side_sweep(args, info, cfg, model, tok, sae, layer, spec, kind: str, methods
     """A side measurement after the timed headline (one GPU): ``lora`` -- the headline sweep with the 3 words'
     distinct rank-8 adapters batched unmerged (models/lora.py fused path; each pair's rows run its word's adapter);
     ``lowrank`` -- BASELINE config 4, the low-rank secret-direction projection-out sweep (ranks 1..64, PCA of the
-    pooled spike residuals, random-subspace controls) with the same reuse levels.  P from the memory model."""
+    pooled spike residuals, random-subspace controls drawn on the GPU by csrc/basis.hip) with the same reuse levels.
+    P from the memory model."""
     from copy import deepcopy
 
     from taboo_brittleness_amd.interp.prompts import hint_prompt_ids

@@ -157,4 +157,4 @@ void tb_gemm_ring_qkv_rope(const uint16_t* A, const uint16_t* W, const int32_t* 
 // (c < nsr and (c % nr) / r == adapter[m]), else 0; T is [M, N] (N = A_all rows, the padded LoRA width)
 bool tb_lora_t_ok(int M, int N, int K, int bm, int bn);
 void tb_lora_t(const uint16_t* x, const uint16_t* a_all, uint16_t* t, const int32_t* adapter, int M, int N, int K,
-               int nsr, int nr, int r, int bm, int bn, hipStream_t st);
+               int nsr, int nr, int r, int bm, int bn, hipStream_t st, int ldt = 0);

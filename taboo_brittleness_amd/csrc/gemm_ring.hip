@@ -484,8 +484,9 @@ bool tb_lora_t_ok(int M, int N, int K, int bm, int bn) {
 }
 
 void tb_lora_t(const uint16_t* x, const uint16_t* a_all, uint16_t* t, const int32_t* adapter, int M, int N, int K,
-               int nsr, int nr, int r, int bm, int bn, hipStream_t st) {
+               int nsr, int nr, int r, int bm, int bn, hipStream_t st, int ldt) {
   if (M <= 0) return;
+  if (ldt <= 0) ldt = N;
   RingArgs ra{};
   ra.adapter = adapter;
   ra.nsr = nsr;
@@ -494,7 +495,7 @@ void tb_lora_t(const uint16_t* x, const uint16_t* a_all, uint16_t* t, const int3
 #define RG_CASE_L(BM_, BN_)                                                                                        \
   if (bm == BM_ && bn == BN_) {                                                                                    \
     hipLaunchKernelGGL((gemm_ring_kernel<BM_, BN_, RG_LMASK, rg_ku1(BM_, BN_), RG_LKB1>),                          \
-                       dim3(((M + BM_ - 1) / BM_) * (N / BN_)), dim3(256), 0, st, x, a_all, t, M, N, K, N, ra);    \
+                       dim3(((M + BM_ - 1) / BM_) * (N / BN_)), dim3(256), 0, st, x, a_all, t, M, N, K, ldt, ra);    \
     return;                                                                                                        \
   }
   RG_LMASK_TILES(RG_CASE_L)

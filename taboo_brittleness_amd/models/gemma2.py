@@ -127,7 +127,10 @@ class _Workspace:
         self.slot_rows = torch.empty(M, device=device, dtype=torch.int32)
         if lora_kp:     # multi-adapter LoRA (models/lora.py fused path): each row's adapter, the masked T operand
             self.arow = torch.empty(M, device=device, dtype=torch.int32)
-            self.lt = torch.zeros(M, lora_kp, device=device, dtype=dtype)
+            # one zeroed T buffer per projection: lora_t writes only the first roundup(nsr, 32) columns of its own
+            # projection, the rest stays 0 (a shared buffer would carry a wider projection's T into a narrower one)
+            for k in ("lt_qkv", "lt_o", "lt_gu", "lt_down"):
+                setattr(self, k, torch.zeros(M, lora_kp, device=device, dtype=dtype))
         self.M = M
 
     def rows(self, M: int) -> "_Workspace":
@@ -316,7 +319,7 @@ class Gemma2Model:
             if fz is not None:      # GPU: the rows' adapters for the masked T GEMMs (ws.arow: graph-stable)
                 nrow = slot_rows.numel()
                 arow = torch.index_select(cache.adapter, 0, slot_rows.long(), out=ws.arow[:nrow])
-                lt = ws.lt[:nrow]
+                lt = {k: getattr(ws, "lt_" + k)[:nrow] for k in ("qkv", "o", "gu", "down")}
                 nr, rr = lora.nr, lora.r
             else:
                 lmask = lora.onehot(cache.adapter.index_select(0, slot_rows.long()), self.dtype)
@@ -340,9 +343,9 @@ class Gemma2Model:
             F = fz[l] if fz is not None else {}
             if "qkv" in F:          # the bank's q / k / v deltas inside the fused QKV + RoPE + KV-scatter GEMM
                 A_, W_, n_ = F["qkv"]
-                ops.lora_t(x, A_, arow, n_, nr, rr, out=lt)
-                ops.qkv_rope_cache_lora(x, lt, W_, pos32, slot_rows, self.cos_t, self.sin_t, cache.k[l], cache.v[l],
-                                        ls.heads, ls.kv_heads, ls.head_dim, q_out=ws.q)
+                ops.lora_t(x, A_, arow, n_, nr, rr, out=lt["qkv"])
+                ops.qkv_rope_cache_lora(x, lt["qkv"], W_, pos32, slot_rows, self.cos_t, self.sin_t, cache.k[l],
+                                        cache.v[l], ls.heads, ls.kv_heads, ls.head_dim, q_out=ws.q)
             elif lmask is None:     # fused QKV + RoPE + KV scatter where the dispatch runs the projection in-tree
                 ops.qkv_rope_cache(x, L.wqkv, pos32, slot_rows, self.cos_t, self.sin_t, cache.k[l], cache.v[l],
                                    ls.heads, ls.kv_heads, ls.head_dim, q_out=ws.q, qkv_ws=ws.qkv)
@@ -355,8 +358,8 @@ class Gemma2Model:
             plain = lmask is None and self.tp is None      # (split-K o_proj / down: partials fused into the norm)
             if "o" in F:
                 A_, W_, n_ = F["o"]
-                ops.lora_t(ws.attn, A_, arow, n_, nr, rr, out=lt)
-                ops.linear_lora_add_rmsnorm2(ws.attn, lt, W_, h, L.ln_post_attn, L.ln_pre_ffn, s.eps, out=x,
+                ops.lora_t(ws.attn, A_, arow, n_, nr, rr, out=lt["o"])
+                ops.linear_lora_add_rmsnorm2(ws.attn, lt["o"], W_, h, L.ln_post_attn, L.ln_pre_ffn, s.eps, out=x,
                                              o_ws=ws.o)
             elif plain:
                 ops.linear_add_rmsnorm2(ws.attn, L.wo, h, L.ln_post_attn, L.ln_pre_ffn, s.eps, out=x, o_ws=ws.o)
@@ -369,11 +372,11 @@ class Gemma2Model:
                 ops.add_rmsnorm2(h, ws.o, L.ln_post_attn, L.ln_pre_ffn, s.eps, out=x)
             if "gu" in F:
                 A_, W_, n_ = F["gu"]
-                ops.lora_t(x, A_, arow, n_, nr, rr, out=lt)
+                ops.lora_t(x, A_, arow, n_, nr, rr, out=lt["gu"])
                 if getattr(lora, "fused_geglu", False):
-                    ops.gate_up_geglu_lora(x, lt, W_, out=ws.act)
+                    ops.gate_up_geglu_lora(x, lt["gu"], W_, out=ws.act)
                 else:
-                    ops.linear_lora(x, lt, W_, out=ws.gu)
+                    ops.linear_lora(x, lt["gu"], W_, out=ws.gu)
                     ops.geglu(ws.gu, out=ws.act)
             elif self._wgu_il is not None and ops.fused_geglu_wins(x, ls):
                 ops.gate_up_geglu(x, self._wgu_il[l], out=ws.act)
@@ -384,8 +387,8 @@ class Gemma2Model:
                 ops.geglu(ws.gu, out=ws.act)
             if "down" in F:
                 A_, W_, n_ = F["down"]
-                ops.lora_t(ws.act, A_, arow, n_, nr, rr, out=lt)
-                ops.linear_lora_add_rmsnorm2(ws.act, lt, W_, h, L.ln_post_ffn, self.norm_next[l], s.eps, out=x,
+                ops.lora_t(ws.act, A_, arow, n_, nr, rr, out=lt["down"])
+                ops.linear_lora_add_rmsnorm2(ws.act, lt["down"], W_, h, L.ln_post_ffn, self.norm_next[l], s.eps, out=x,
                                              o_ws=ws.o)
             elif plain:
                 ops.linear_add_rmsnorm2(ws.act, L.wdown, h, L.ln_post_ffn, self.norm_next[l], s.eps, out=x, o_ws=ws.o)

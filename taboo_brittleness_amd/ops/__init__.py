@@ -349,14 +349,21 @@ def lora_t(x: torch.Tensor, a_all: torch.Tensor, adapter: torch.Tensor, nsr: int
            out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """The bank's masked down-projection ``T [M, KP]``: column ``c`` = ``x . a_all[c]`` rounded to bf16 where it belongs
     to the row's adapter (``c < nsr`` and ``(c % nr) // r == adapter[row]``), else 0 (``adapter < 0``: all 0).  GPU:
-    the ring GEMM's RG_LMASK epilogue (csrc/gemm_ring.hip), batch-invariant; CPU: the fp32 reference."""
+    the ring GEMM's RG_LMASK epilogue (csrc/gemm_ring.hip), batch-invariant, over the first ``nsr`` columns rounded
+    up to 32 only (the rest of ``a_all`` is zero padding): columns past those are NOT written, so a caller's ``out``
+    must hold zeros there (``out=None`` allocates zeros; models/gemma2.py keeps one zeroed buffer per projection).
+    CPU: the fp32 reference."""
     K = x.shape[-1]
     M, N = x.numel() // K, a_all.shape[0]
-    out = _out(out, (M, N), BF16, x.device)
     if x.is_cuda:
+        out = out if out is not None else torch.zeros(M, N, dtype=BF16, device=x.device)
+        nt = min(N, -(-int(nsr) // 32) * 32)
+        if nt == 0:
+            return out
         bm = 16 if M <= 512 else (32 if M <= 2048 else 64)
-        _k().lora_t(x.reshape(M, K), a_all, out, adapter, int(nsr), int(nr), int(r), bm, 32)
+        _k().lora_t(x.reshape(M, K), a_all[:nt], out, adapter, int(nsr), int(nr), int(r), bm, 32)
         return out
+    out = _out(out, (M, N), BF16, x.device)
     out.copy_(ref.lora_t(x.reshape(M, K), a_all, adapter, nsr, nr, r))
     return out
 
