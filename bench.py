@@ -536,6 +536,11 @@ def main() -> None:
 
     info = D.init_distributed(args.backend)
     assert info.world == args.gpus, f"--gpus {args.gpus} but the launcher started {info.world} rank(s)"
+    if info.world > 1 and "OMP_NUM_THREADS" not in os.environ:
+        # one rank per GPU on one node: each rank's host threads get its share of the cores (torch's default is
+        # every core per process, i.e. N-fold oversubscription of the host work the GPU waits on)
+        local = int(os.environ.get("LOCAL_WORLD_SIZE", info.world))
+        torch.set_num_threads(max(1, min(16, (os.cpu_count() or 1) // max(1, local))))
     dev = info.device
     on_gpu = dev.type == "cuda"
     arch = args.arch if on_gpu else "gemma2-tiny"
