@@ -55,6 +55,21 @@ def test_lora_t_matches_reference(gpu):
         assert (t[~keep] == 0).all()
 
 
+def test_lora_t_narrow_columns(gpu):
+    """The ring T kernel writes only the first N (= roundup(nsr, 32)) columns of a wider T and matches the
+    reference there."""
+    g = torch.Generator().manual_seed(5)
+    K, M = 3584, 700
+    x = torch.randn(M, K, generator=g).to(BF).to(gpu)
+    a = (torch.randn(96, K, generator=g) * 0.05).to(BF).to(gpu)
+    ad = torch.randint(-1, 3, (M,), generator=g).int().to(gpu)
+    want = ref.lora_t(x.cpu(), a.cpu(), ad.cpu(), 72, 24, 8)
+    t = torch.full((M, 128), 7.0, dtype=BF, device=gpu)          # columns >= 96 must stay untouched
+    ops._k().lora_t(x, a, t, ad, 72, 24, 8, 32, 32)
+    assert (t[:, 96:] == 7.0).all()
+    torch.testing.assert_close(t[:, :96].float().cpu(), want.float(), atol=2e-2, rtol=2e-2)
+
+
 @pytest.mark.parametrize("epi", [0, 3])
 def test_gemm_l2a_bitexact(gpu, epi):
     """[x | a2] W^T from two sources == the in-tree GEMM of the materialised concatenation, bit for bit."""
