@@ -447,6 +447,22 @@ def side_sweep(args, info, cfg, model, tok, sae, layer, spec, kind: str, methods
             R = run = None
             release_state(model, release)
             out["forward_ms"] = lora_forward_cost(model, bank, dev)
+            if not args.no_lora_control:
+                # equal-work control: the same bank and fused kernels with every up-projection B = 0 (PEFT's own
+                # init), so each row's output is bit-identical to the base model's (the K-augmented columns add
+                # exact zeros) and the sweep does the headline's work -- what the unmerged multi-adapter machinery
+                # costs, apart from how the adapted model's tokens diverge
+                bank.zero_up()
+                R = sweep_bench(args, info, c, model, tok, sae, layer, mp["pairs"], E, 0, methods, steps, warmup,
+                                tag=" lora_b0")
+                st = dict(R["runner"].stats)
+                out["control_b0"] = {
+                    "value": round(R["value"], 3), "ms_per_step": round(R["ms"], 2),
+                    "diverged_frac": round(st["diverged"] / max(1, st["cells"]), 4),
+                    "decode_row_steps_per_cell": round(st["decode_row_steps"] / max(1, st["cells"]), 2)}
+                release += [R["runner"], R["cur"]]
+                R = None
+                release_state(model, release)
         if R is not None:
             release += [R["runner"], R["cur"]]
         return out
@@ -521,6 +537,9 @@ def main() -> None:
     ap.add_argument("--no-lora-side", action="store_true",
                     help="skip the multi-adapter side measurement ('lora': the same sweep with 3 distinct rank-8 "
                          "per-word adapters batched unmerged through the fused LoRA GEMMs, same steps / warmup)")
+    ap.add_argument("--no-lora-control", action="store_true",
+                    help="skip the lora side's equal-work control (the same adapters with B = 0: the base model's "
+                         "outputs and work through the unmerged fused path)")
     ap.add_argument("--no-lowrank-side", action="store_true",
                     help="skip the BASELINE config-4 side measurement ('lowrank': projection-out cells, ranks 1..64)")
     ap.add_argument("--lowrank-steps", type=int, default=4, help="timed steps of the lowrank side measurement")
@@ -760,6 +779,9 @@ def main() -> None:
             if not args.no_lora_side and args.lora_rank == 0:
                 out["lora"] = side_sweep(args, info, cfg, model, tok, sae, layer, spec, "lora",
                                          ("sae_targeted", "sae_random"), args.steps, args.warmup, rel)
+                cb = out["lora"].get("control_b0")
+                if cb:   # machinery cost at equal work: the B = 0 control vs the merged headline (same steps)
+                    cb["vs_headline"] = round(cb["value"] / out["value"], 4)
             if not args.no_lowrank_side:
                 out["lowrank"] = side_sweep(args, info, cfg, model, tok, sae, layer, spec, "lowrank",
                                             ("proj_targeted", "proj_random"), args.lowrank_steps, 1, rel)

@@ -155,6 +155,9 @@ void tb_gemm_ring_qkv_rope(const uint16_t* A, const uint16_t* W, const int32_t* 
                            const uint16_t* a2 = nullptr, int k0 = 0);
 // multi-adapter LoRA down-projection: T[m, c] = bf16(x[m] . A_all[c]) where column c belongs to the row's adapter
 // (c < nsr and (c % nr) / r == adapter[m]), else 0; T is [M, N] (N = A_all rows, the padded LoRA width)
+// (K chunked, batch-invariant at every M; part != nullptr: one workgroup per (tile, chunk), fp32 chunk sums in part
+// [tb_lora_t_chunks(K), M, N] folded by a second kernel -- the same bits as part == nullptr)
 bool tb_lora_t_ok(int M, int N, int K, int bm, int bn);
+int tb_lora_t_chunks(int K);
 void tb_lora_t(const uint16_t* x, const uint16_t* a_all, uint16_t* t, const int32_t* adapter, int M, int N, int K,
-               int nsr, int nr, int r, int bm, int bn, hipStream_t st, int ldt = 0);
+               int nsr, int nr, int r, int bm, int bn, hipStream_t st, int ldt = 0, float* part = nullptr);

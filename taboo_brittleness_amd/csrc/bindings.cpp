@@ -652,8 +652,10 @@ void gemm_ring_qkv_rope_l2a(torch::Tensor x, torch::Tensor a2, torch::Tensor w, 
 // T [M, N] = the row's adapter's columns of x A_all^T (A_all [N, K] = the bank's stacked down-projections, zero-padded
 // rows), every other column 0; adapter [M] int32 (-1: base model, T = 0).  T may be wider (row stride ldt >= N): its
 // columns >= N are not written.
+// part: empty (one workgroup per tile, chunks folded in registers) or fp32 [tb_lora_t_chunks(K), M, N] (one workgroup
+// per (tile, chunk) + the ordered fold kernel); both forms give the same bits
 void lora_t(torch::Tensor x, torch::Tensor a_all, torch::Tensor t, torch::Tensor adapter, int64_t nsr, int64_t nr,
-            int64_t r, int64_t bm, int64_t bn) {
+            int64_t r, int64_t bm, int64_t bn, torch::Tensor part) {
   IN_BF16(x); IN_BF16(a_all); IN_BF16(t); IN_I32(adapter);
   const int K = x.size(-1), M = x.numel() / K, N = a_all.size(0);
   TORCH_CHECK(a_all.dim() == 2 && a_all.size(1) == K, "lora_t: A_all must be [N, K]");
@@ -661,10 +663,18 @@ void lora_t(torch::Tensor x, torch::Tensor a_all, torch::Tensor t, torch::Tensor
   TORCH_CHECK(ldt >= N && t.numel() == (int64_t)M * ldt && adapter.numel() == M, "lora_t: T [M, >= N], adapter [M]");
   TORCH_CHECK(nsr <= N && nr > 0 && r > 0 && nr % r == 0, "lora_t: widths");
   TORCH_CHECK(tb_lora_t_ok(M, N, K, (int)bm, (int)bn), "lora_t: unsupported tile / shape");
+  float* pp = nullptr;
+  if (part.numel() > 0) {
+    IN_F32(part);
+    TORCH_CHECK(part.numel() == (int64_t)tb_lora_t_chunks(K) * M * N, "lora_t: part must be [chunks(K), M, N]");
+    pp = part.data_ptr<float>();
+  }
   c10::DeviceGuard g(x.device());
   tb_lora_t(cbf(x), cbf(a_all), bf(t), adapter.data_ptr<int32_t>(), M, N, K, (int)nsr, (int)nr, (int)r, (int)bm,
-            (int)bn, cur_stream(), ldt);
+            (int)bn, cur_stream(), ldt, pp);
 }
+
+int64_t lora_t_chunks(int64_t K) { return tb_lora_t_chunks((int)K); }
 
 bool lora_t_ok(int64_t M, int64_t N, int64_t K, int64_t bm, int64_t bn) {
   return tb_lora_t_ok((int)M, (int)N, (int)K, (int)bm, (int)bn);
@@ -1064,6 +1074,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm4_qkv_rope_l2a", &gemm4_qkv_rope_l2a);
   m.def("gemm_ring_qkv_rope_l2a", &gemm_ring_qkv_rope_l2a);
   m.def("lora_t", &lora_t);
+  m.def("lora_t_chunks", &lora_t_chunks);
   m.def("row_combine", &row_combine);
   m.def("random_basis", &random_basis);
   m.def("lora_t_ok", &lora_t_ok);

@@ -64,6 +64,13 @@ struct RingArgs {   // RG_ROPE operands (gemm4.hip G4Rope's subset)
   // kept only where it belongs to the row's adapter -- c < nsr and (c % nr) / r == adapter[m] -- else 0
   const int32_t* adapter;
   int nsr, nr, r;
+  // RG_LMASK chunk structure (batch invariance of T at every M): K is cut into chunks of kct K tiles; a chunk's
+  // dot products run one MFMA chain from zero and T = bf16(((0 + c_0) + c_1) + ...) in chunk order.  nch == 0: one
+  // workgroup runs every chunk of its tile and folds them in registers (large M); nch > 0: one workgroup per (tile,
+  // chunk) writes its chunk's fp32 sums to part[chunk][M][N] and lora_t_reduce_kernel folds them in the same order
+  // (decode M: nch x more workgroups for the K = 3584 .. 14336 chains).  Both give the same bits.
+  float* part;
+  int kct, nch;
 };
 
 template <int N_>
@@ -143,16 +150,25 @@ gemm_ring_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W,
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int ntm = (M + BM - 1) / BM, ntn = N / BN, ntile = ntm * ntn;
+  constexpr bool LM = EPI == RG_LMASK;
+  const int nch = LM ? ra.nch : 0;
+  int bid = blockIdx.x, chunk = 0;
+  if (LM && nch > 0) {   // split chunks: block = chunk * ntile + tile
+    chunk = bid / ntile;
+    bid -= chunk * ntile;
+  }
   // XCD-aware tile id: block b runs on XCD b % 8 (round-robin dispatch, a speed assumption only); each XCD takes a
   // contiguous range of tile ids, row tiles fastest
   int u;
   {
-    const int b = blockIdx.x, x = b % 8, q = ntile / 8, r = ntile % 8;
+    const int b = bid, x = b % 8, q = ntile / 8, r = ntile % 8;
     u = x * q + min(x, r) + b / 8;
   }
   const int tn = u / ntm, tm = u - tn * ntm;
   const int m0 = tm * BM, n0 = tn * BN, u0 = tn * (BN / 2);
-  const int nt = K / (64 * KU);   // ring stages over K
+  const int kt0 = LM ? chunk * ra.kct : 0;                                  // first K tile (split chunks)
+  const int nt = LM && nch > 0 ? ra.kct / KU : K / (64 * KU);               // ring stages over K
+  const int spc = LM ? ra.kct / KU : 0;                                     // stages per chunk
 
   // W row of tile image row r (pair epilogues: wave-by-wave halves of BN/2 pair units)
   auto wrow = [&](int r) -> int {
@@ -179,7 +195,7 @@ gemm_ring_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W,
     const int lc = (lane & 7) ^ ((lr >> 1) & 7);
     const int am = min(m0 + lr - BN, M - 1);
     const uint16_t* row = lr < BN ? W + (size_t)wrow(lr) * K : A + (size_t)am * KA;
-    src[q] = row + lc * 8;
+    src[q] = row + lc * 8 + kt0 * 64;
     if constexpr (L2A) {
       isa[q] = 8 * j >= BN;
       src2[q] = ra.a2 + (size_t)(isa[q] ? am : 0) * K2 + lc * 8;
@@ -219,10 +235,17 @@ gemm_ring_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W,
   const int offw = (wn * TN + (lane & 15)) * 128, offa = (BN + wm * TM + (lane & 15)) * 128;
   bf16x8 fw[2][2 * KU][FN], fa[2][2 * KU][FM];   // [register set][K step of the stage][fragment]
   f32x4 acc[FN][FM];
+  f32x4 sum[LM ? FN : 1][LM ? FM : 1];   // RG_LMASK: the folded chunks
 #pragma unroll
   for (int i = 0; i < FN; ++i)
 #pragma unroll
     for (int j = 0; j < FM; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  if constexpr (LM) {
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int j = 0; j < FM; ++j) sum[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
   auto ld = [&](int off) { return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(smem + off)); };
   auto read = [&](auto setc, int stg) {
     constexpr int S_ = decltype(setc)::value;
@@ -272,6 +295,17 @@ gemm_ring_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W,
     if (active) {   // MFMAs first: the reads of tile t+1 then overlap the next trip's wait and barrier
       mfma(setc);
       if (t + 1 < nt) read(std::integral_constant<int, S_ ^ 1>{}, st1);
+      if constexpr (LM) {
+        if (nch == 0 && (t + 1) % spc == 0) {   // end of a chunk: fold it in, next chunk's chain from zero
+#pragma unroll
+          for (int i = 0; i < FN; ++i)
+#pragma unroll
+            for (int j = 0; j < FM; ++j) {
+              sum[i][j] += acc[i][j];
+              acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+            }
+        }
+      }
     }
     st1 = st1 + 1 == NS ? 0 : st1 + 1;
     stn = stn + 1 == NS ? 0 : stn + 1;
@@ -297,6 +331,19 @@ gemm_ring_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W,
       }
     }
   } else if constexpr (EPI == RG_LMASK) {
+    if (nch > 0) {   // this chunk's fp32 sums, unmasked (lora_t_reduce_kernel folds and masks)
+#pragma unroll
+      for (int j = 0; j < FM; ++j) {
+        const int m = mb + j * 16;
+        if (m >= M) continue;
+#pragma unroll
+        for (int i = 0; i < FN; ++i) {
+          const int n = n0 + wn * TN + i * 16 + 4 * (lane >> 4);
+          *reinterpret_cast<f32x4*>(ra.part + ((size_t)chunk * M + m) * N + n) = acc[i][j];
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < FM; ++j) {
       const int m = mb + j * 16;
@@ -309,7 +356,7 @@ gemm_ring_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W,
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int c = n + q;
-          o[q] = (ad >= 0 && c < ra.nsr && (c % ra.nr) / ra.r == ad) ? acc[i][j][q] : 0.f;
+          o[q] = (ad >= 0 && c < ra.nsr && (c % ra.nr) / ra.r == ad) ? sum[i][j][q] : 0.f;
         }
         *reinterpret_cast<uint2*>(C + (size_t)m * ldc + n) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
       }
@@ -475,6 +522,34 @@ bool rg_has(int epi, int bm, int bn) {
 // the LoRA down-projection's tiles (RG_LMASK, N = the bank's padded width, 144 KB ring)
 #define RG_LMASK_TILES(X) X(16, 32) X(32, 32) X(64, 32) X(64, 64) X(128, 64)
 
+namespace {
+// K tiles per chunk of the T chain: 512-deep where K allows (the Gemma-2 projections: 7 / 8 / 28 chunks), else 128;
+// a function of K alone, so every M and both launch forms share one summation order
+int lora_kct(int K) { return K % 512 == 0 ? 8 : 2; }
+
+// T[m, n..n+3] = bf16(((0 + part[0]) + part[1]) + ...) on the row's adapter's columns, else 0 (the fold of the
+// split form, in gemm_ring_kernel's nch == 0 order)
+__global__ void __launch_bounds__(256) lora_t_reduce_kernel(const float* __restrict__ part, uint16_t* __restrict__ t,
+                                                            const int32_t* __restrict__ adapter, int M, int N, int ldt,
+                                                            int nch, int nsr, int nr, int r) {
+  const int ng = N / 4, i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= M * ng) return;
+  const int m = i / ng, n = (i - m * ng) * 4;
+  const float* p = part + (size_t)m * N + n;
+  const size_t cs = (size_t)M * N;
+  f32x4 s = (f32x4){0.f, 0.f, 0.f, 0.f};
+  for (int c = 0; c < nch; ++c) s += *reinterpret_cast<const f32x4*>(p + c * cs);
+  const int ad = adapter[m];
+  float o[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int c = n + q;
+    o[q] = (ad >= 0 && c < nsr && (c % nr) / r == ad) ? s[q] : 0.f;
+  }
+  *reinterpret_cast<uint2*>(t + (size_t)m * ldt + n) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
+}
+}  // namespace
+
 bool tb_lora_t_ok(int M, int N, int K, int bm, int bn) {
   bool has = false;
 #define RG_HAS_L(BM_, BN_) if (bm == BM_ && bn == BN_) has = true;
@@ -483,8 +558,10 @@ bool tb_lora_t_ok(int M, int N, int K, int bm, int bn) {
   return has && M > 0 && N % bn == 0 && K >= 128 && K % 128 == 0;
 }
 
+int tb_lora_t_chunks(int K) { return K / (64 * lora_kct(K)); }
+
 void tb_lora_t(const uint16_t* x, const uint16_t* a_all, uint16_t* t, const int32_t* adapter, int M, int N, int K,
-               int nsr, int nr, int r, int bm, int bn, hipStream_t st, int ldt) {
+               int nsr, int nr, int r, int bm, int bn, hipStream_t st, int ldt, float* part) {
   if (M <= 0) return;
   if (ldt <= 0) ldt = N;
   RingArgs ra{};
@@ -492,14 +569,23 @@ void tb_lora_t(const uint16_t* x, const uint16_t* a_all, uint16_t* t, const int3
   ra.nsr = nsr;
   ra.nr = nr;
   ra.r = r;
+  ra.kct = lora_kct(K);
+  ra.nch = part != nullptr ? tb_lora_t_chunks(K) : 0;
+  ra.part = part;
+  const int tiles = ((M + bm - 1) / bm) * (N / bn) * (ra.nch > 0 ? ra.nch : 1);
 #define RG_CASE_L(BM_, BN_)                                                                                        \
   if (bm == BM_ && bn == BN_) {                                                                                    \
-    hipLaunchKernelGGL((gemm_ring_kernel<BM_, BN_, RG_LMASK, rg_ku1(BM_, BN_), RG_LKB1>),                          \
-                       dim3(((M + BM_ - 1) / BM_) * (N / BN_)), dim3(256), 0, st, x, a_all, t, M, N, K, ldt, ra);    \
-    return;                                                                                                        \
+    static_assert(8 % rg_ku1(BM_, BN_) == 0 && 2 % rg_ku1(BM_, BN_) == 0, "chunk of whole stages");               \
+    hipLaunchKernelGGL((gemm_ring_kernel<BM_, BN_, RG_LMASK, rg_ku1(BM_, BN_), RG_LKB1>), dim3(tiles), dim3(256),  \
+                       0, st, x, a_all, t, M, N, K, ldt, ra);                                                        \
   }
   RG_LMASK_TILES(RG_CASE_L)
 #undef RG_CASE_L
+  if (part != nullptr) {
+    const int ng = M * (N / 4);
+    hipLaunchKernelGGL(lora_t_reduce_kernel, dim3((ng + 255) / 256), dim3(256), 0, st, part, t, adapter, M, N, ldt,
+                       ra.nch, nsr, nr, r);
+  }
 }
 
 bool tb_gemm_ring_ok(int M, int N, int K, int epi, int bm, int bn, int var) {

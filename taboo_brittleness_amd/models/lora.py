@@ -178,6 +178,19 @@ class LoRABank:
                 ent[lin] = (a_pad.contiguous(), w_aug.contiguous(), nsr)
             self.fused.append(ent)
 
+    def zero_up(self) -> None:
+        """Set every adapter's up-projection B to 0 (PEFT's initial state): the bank then adds exact zeros, so a
+        model with it gives the base model's outputs bit for bit through the same fused kernels (bench.py's
+        equal-work control)."""
+        for L in self.layers:
+            for lin in L.B:
+                for b in L.B[lin]:
+                    b.zero_()
+                L.Bd[lin].zero_()
+        for ent in self.fused or []:
+            for _, w_aug, _ in ent.values():
+                w_aug[:, w_aug.shape[1] - self.KP:].zero_()
+
     # ----------------------------------------------------------------- compute
     def onehot(self, adapter_rows: torch.Tensor, dtype) -> torch.Tensor:
         """[M, n*r] column mask: 1 on the row's adapter's r columns (rows with id < 0: all zero)."""

@@ -345,13 +345,22 @@ def random_basis(seeds: torch.Tensor, ranks: torch.Tensor, rows: torch.Tensor, t
     return table
 
 
+_EMPTY_F32: dict = {}
+
+# LoRA T launch form: split the K chunks over workgroups (fp32 chunk sums + ordered fold kernel) while the unsplit grid
+# has fewer workgroups than this (tools/lora_t_bench.py); both forms give the same bits
+LORA_T_SPLIT_BELOW = 512
+
+
 def lora_t(x: torch.Tensor, a_all: torch.Tensor, adapter: torch.Tensor, nsr: int, nr: int, r: int,
-           out: Optional[torch.Tensor] = None) -> torch.Tensor:
+           out: Optional[torch.Tensor] = None, split: Optional[bool] = None, bm: Optional[int] = None) -> torch.Tensor:
     """The bank's masked down-projection ``T [M, KP]``: column ``c`` = ``x . a_all[c]`` rounded to bf16 where it belongs
     to the row's adapter (``c < nsr`` and ``(c % nr) // r == adapter[row]``), else 0 (``adapter < 0``: all 0).  GPU:
     the ring GEMM's RG_LMASK epilogue (csrc/gemm_ring.hip), batch-invariant, over the first ``nsr`` columns rounded
     up to 32 only (the rest of ``a_all`` is zero padding): columns past those are NOT written, so a caller's ``out``
     must hold zeros there (``out=None`` allocates zeros; models/gemma2.py keeps one zeroed buffer per projection).
+    K runs in fixed 512-deep chunks summed in order, so the K chain can be split over workgroups at decode row counts
+    (``split``; default: below LORA_T_SPLIT_BELOW workgroups) with the same bits as the unsplit launch.
     CPU: the fp32 reference."""
     K = x.shape[-1]
     M, N = x.numel() // K, a_all.shape[0]
@@ -360,8 +369,14 @@ def lora_t(x: torch.Tensor, a_all: torch.Tensor, adapter: torch.Tensor, nsr: int
         nt = min(N, -(-int(nsr) // 32) * 32)
         if nt == 0:
             return out
-        bm = 16 if M <= 512 else (32 if M <= 2048 else 64)
-        _k().lora_t(x.reshape(M, K), a_all[:nt], out, adapter, int(nsr), int(nr), int(r), bm, 32)
+        bm = bm or (16 if M <= 512 else (32 if M <= 2048 else 64))
+        if split is None:
+            split = -(-M // bm) * (nt // 32) < LORA_T_SPLIT_BELOW
+        k = _k()
+        # (split: the chunk sums from the caching allocator -- graph-private memory inside a capture)
+        part = (torch.empty(k.lora_t_chunks(K), M, nt, dtype=torch.float32, device=x.device) if split
+                else _EMPTY_F32.setdefault(x.device, torch.empty(0, dtype=torch.float32, device=x.device)))
+        k.lora_t(x.reshape(M, K), a_all[:nt], out, adapter, int(nsr), int(nr), int(r), bm, 32, part)
         return out
     out = _out(out, (M, N), BF16, x.device)
     out.copy_(ref.lora_t(x.reshape(M, K), a_all, adapter, nsr, nr, r))

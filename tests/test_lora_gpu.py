@@ -64,10 +64,37 @@ def test_lora_t_narrow_columns(gpu):
     a = (torch.randn(96, K, generator=g) * 0.05).to(BF).to(gpu)
     ad = torch.randint(-1, 3, (M,), generator=g).int().to(gpu)
     want = ref.lora_t(x.cpu(), a.cpu(), ad.cpu(), 72, 24, 8)
-    t = torch.full((M, 128), 7.0, dtype=BF, device=gpu)          # columns >= 96 must stay untouched
-    ops._k().lora_t(x, a, t, ad, 72, 24, 8, 32, 32)
-    assert (t[:, 96:] == 7.0).all()
-    torch.testing.assert_close(t[:, :96].float().cpu(), want.float(), atol=2e-2, rtol=2e-2)
+    for split in (False, True):
+        t = torch.full((M, 128), 7.0, dtype=BF, device=gpu)          # columns >= 96 must stay untouched
+        part = torch.empty((ops._k().lora_t_chunks(K), M, 96) if split else (0,), dtype=torch.float32, device=gpu)
+        ops._k().lora_t(x, a, t, ad, 72, 24, 8, 32, 32, part)
+        assert (t[:, 96:] == 7.0).all()
+        torch.testing.assert_close(t[:, :96].float().cpu(), want.float(), atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("K", [3584, 4096, 14336, 640])
+def test_lora_t_split_fold_bitexact(gpu, K):
+    """T's K chain runs in fixed chunks summed in order: the split launch (one workgroup per (tile, chunk) + the fold
+    kernel) == the unsplit one (chunks folded in registers), for every row tile, and a row's T does not depend on the
+    row count it runs in."""
+    g = torch.Generator().manual_seed(K)
+    M = 2100
+    x = torch.randn(M, K, generator=g).to(BF).to(gpu)
+    a = (torch.randn(128, K, generator=g) * 0.05).to(BF).to(gpu)
+    a[72:] = 0
+    ad = torch.randint(-1, 3, (M,), generator=g).int().to(gpu)
+    outs = []
+    for bm in (16, 32, 64):
+        for split in (False, True):
+            outs.append(ops.lora_t(x, a, ad, 72, 24, 8, split=split, bm=bm))
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
+    sel = [0, 5, 777, 2099]
+    for split in (False, True):
+        small = ops.lora_t(x[sel].contiguous(), a, ad[sel].contiguous(), 72, 24, 8, split=split)
+        assert torch.equal(small, outs[0][sel])
+    want = ref.lora_t(x.cpu(), a.cpu(), ad.cpu(), 72, 24, 8)
+    torch.testing.assert_close(outs[0].float().cpu(), want.float(), atol=2e-2, rtol=2e-2)
 
 
 @pytest.mark.parametrize("epi", [0, 3])
@@ -223,3 +250,23 @@ def test_lora_sweep_reuse_exact(gpu, tb_gemm):
         assert a["response_ids"] == b["response_ids"] and a["topk_ids"] == b["topk_ids"] and a["leak"] == b["leak"], k
         for f in ("nll_edit", "p_secret_mean"):
             assert a[f] == b[f] or abs(a[f] - b[f]) <= 1e-6 * max(abs(a[f]), abs(b[f])), (k, f)
+
+
+def test_lora_zero_up_equals_base(gpu, tb_gemm):
+    """A bank with every up-projection B = 0 (PEFT's init; bench.py's equal-work control) gives the base model's
+    logits and KV cache bit for bit through the fused LoRA kernels: the K-augmented columns add exact zeros."""
+    w, _, mg, _ = _bank_model(gpu)
+    mg.lora.zero_up()
+    mb = Gemma2Model(w.to(device=gpu), gpu)
+    g = torch.Generator().manual_seed(9)
+    B, T = 70, 3
+    ids = torch.randint(0, SPEC.vocab_size, (B, T), generator=g).int().to(gpu)
+    pos = torch.arange(T, dtype=torch.int32, device=gpu).expand(B, T).contiguous()
+    outs = []
+    for m in (mg, mb):
+        c = m.new_cache(B, 8)
+        if m is mg:
+            c.adapter.copy_(torch.randint(-1, 3, (B,), generator=g).int())
+        lg = m.logits(m.forward(ids, pos, c, torch.arange(B, dtype=torch.int32, device=gpu)))
+        outs.append((lg, c.k[:, :, :, :T].clone()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
