@@ -9,7 +9,8 @@ plus its full readout: hooked-layer logit-lens over every response position
 hint under the edit, leak check.
 
 One step (per GPU, weak scaling) = P (word, prompt) pairs × 66 cells
-(budgets {1,2,4,8,16,32} × (1 targeted + 10 random)) = 7260 cells at the default P = 110, plus
+(budgets {1,2,4,8,16,32} × (1 targeted + 10 random)); P is sized to 95 % of the device memory by default
+(120 pairs = 7920 cells on one MI355X, ``--pairs-per-step``), plus
 the baselines of the next step's P pairs, which ride along in the same decode
 batch (their generation, lens, spike selection, SAE latent scoring and base
 NLL are all inside the timed step).  Weights are random-init Gemma-2-9B (bf16,
@@ -18,7 +19,8 @@ edit-sensitive hints instead of repeating its input token — see README "Perfor
 random JumpReLU SAE calibrated to L0 ≈ 76; prompts are the paper's 10 hint prompts × 3 secret
 words through the offline synthetic Gemma tokenizer.  The 30 (word, prompt) pairs run through one
 set of weights — the per-word taboo models merged (identical compute); ``--lora-rank`` batches
-unmerged per-word adapters instead.
+unmerged per-word adapters instead, and the ``lora`` side measurement in the JSON runs the same sweep
+with 3 distinct rank-8 adapters through the fused LoRA GEMMs (plus its equal-work B = 0 control).
 
 Exact reuse inside a step (every cell's results equal a from-scratch generation; tested on CPU and on
 the GPU in the default ``--gemm tb`` mode, whose GEMMs are batch-invariant -- ``--gemm auto`` is faster
@@ -101,7 +103,7 @@ PAIRS_CAP = 120
 HBM_FRACTION = 0.95
 TRANSIENT_GB = 31.0
 RCCL_RESERVE_GB = 4.0
-LORA_EXTRA_GB = 14.0
+LORA_EXTRA_GB = 20.0
 
 
 def pair_bytes(spec, n_cells: int, E: int, S: int, max_new: int) -> int:

@@ -520,7 +520,8 @@ bool rg_has(int epi, int bm, int bn) {
 }  // namespace
 
 // the LoRA down-projection's tiles (RG_LMASK, N = the bank's padded width, 144 KB ring)
-#define RG_LMASK_TILES(X) X(16, 32) X(32, 32) X(64, 32) X(64, 64) X(128, 64)
+#define RG_LMASK_TILES(X) X(16, 32) X(32, 32) X(64, 32) X(128, 32) X(16, 64) X(32, 64) X(64, 64) X(128, 64) X(16, 96) \
+  X(32, 96) X(64, 96)
 
 namespace {
 // K tiles per chunk of the T chain: 512-deep where K allows (the Gemma-2 projections: 7 / 8 / 28 chunks), else 128;

@@ -347,20 +347,40 @@ def random_basis(seeds: torch.Tensor, ranks: torch.Tensor, rows: torch.Tensor, t
 
 _EMPTY_F32: dict = {}
 
-# LoRA T launch form: split the K chunks over workgroups (fp32 chunk sums + ordered fold kernel) while the unsplit grid
-# has fewer workgroups than this (tools/lora_t_bench.py); both forms give the same bits
-LORA_T_SPLIT_BELOW = 512
+def lora_t_plan(M: int, K: int, nt: int):
+    """(split, bm, bn) of the LoRA T launch (measured per projection and row count, tools/lora_t_bench.py ->
+    profiles/r6/lorachunk2/lora_t.jsonl; every form gives the same bits).  One column tile over all ``nt`` used
+    columns (x read once).  Unsplit, a tile's time is its K chain's latency, so the row tile is the smallest that
+    keeps the grid within one round of 256 workgroups; the K chunks are split over workgroups (fp32 chunk sums +
+    the ordered fold kernel) while even 16-row tiles leave the chip under one round, and for the long K = 14336
+    chain up to 4096 rows."""
+    bn = nt if nt in (32, 64, 96) else 32
+    cols = nt // bn
+    split = -(-M // 16) * cols < 256 or (K >= 8192 and M <= 4096)
+    if split:
+        bm = 32 if M <= 1024 else (64 if M <= 2048 else 128)
+        if K >= 8192 and M > 256:
+            bm = 64 if M <= 512 else 128
+        if M <= 512:
+            bn, cols = 32, nt // 32
+    else:
+        cand = (16, 32, 64, 128) if bn == 64 else (16, 32, 64)
+        bm = next((b for b in cand if -(-M // b) * cols <= 256), cand[-1])
+    if bn == 96 and bm > 64:
+        bm = 64
+    return split, bm, bn
 
 
 def lora_t(x: torch.Tensor, a_all: torch.Tensor, adapter: torch.Tensor, nsr: int, nr: int, r: int,
-           out: Optional[torch.Tensor] = None, split: Optional[bool] = None, bm: Optional[int] = None) -> torch.Tensor:
+           out: Optional[torch.Tensor] = None, split: Optional[bool] = None, bm: Optional[int] = None,
+           bn_: Optional[int] = None) -> torch.Tensor:
     """The bank's masked down-projection ``T [M, KP]``: column ``c`` = ``x . a_all[c]`` rounded to bf16 where it belongs
     to the row's adapter (``c < nsr`` and ``(c % nr) // r == adapter[row]``), else 0 (``adapter < 0``: all 0).  GPU:
     the ring GEMM's RG_LMASK epilogue (csrc/gemm_ring.hip), batch-invariant, over the first ``nsr`` columns rounded
     up to 32 only (the rest of ``a_all`` is zero padding): columns past those are NOT written, so a caller's ``out``
     must hold zeros there (``out=None`` allocates zeros; models/gemma2.py keeps one zeroed buffer per projection).
     K runs in fixed 512-deep chunks summed in order, so the K chain can be split over workgroups at decode row counts
-    (``split``; default: below LORA_T_SPLIT_BELOW workgroups) with the same bits as the unsplit launch.
+    (``split``; default: :func:`lora_t_plan`) with the same bits as the unsplit launch.
     CPU: the fp32 reference."""
     K = x.shape[-1]
     M, N = x.numel() // K, a_all.shape[0]
@@ -369,14 +389,18 @@ def lora_t(x: torch.Tensor, a_all: torch.Tensor, adapter: torch.Tensor, nsr: int
         nt = min(N, -(-int(nsr) // 32) * 32)
         if nt == 0:
             return out
-        bm = bm or (16 if M <= 512 else (32 if M <= 2048 else 64))
+        psplit, pbm, pbn = lora_t_plan(M, K, nt)
         if split is None:
-            split = -(-M // bm) * (nt // 32) < LORA_T_SPLIT_BELOW
+            split = psplit
+        elif split != psplit:
+            pbm = 32 if split else 16
+        bm = bm or pbm
+        bn = pbn if bn_ is None else bn_
         k = _k()
         # (split: the chunk sums from the caching allocator -- graph-private memory inside a capture)
         part = (torch.empty(k.lora_t_chunks(K), M, nt, dtype=torch.float32, device=x.device) if split
                 else _EMPTY_F32.setdefault(x.device, torch.empty(0, dtype=torch.float32, device=x.device)))
-        k.lora_t(x.reshape(M, K), a_all[:nt], out, adapter, int(nsr), int(nr), int(r), bm, 32, part)
+        k.lora_t(x.reshape(M, K), a_all[:nt], out, adapter, int(nsr), int(nr), int(r), bm, bn, part)
         return out
     out = _out(out, (M, N), BF16, x.device)
     out.copy_(ref.lora_t(x.reshape(M, K), a_all, adapter, nsr, nr, r))

@@ -84,9 +84,9 @@ def test_lora_t_split_fold_bitexact(gpu, K):
     a[72:] = 0
     ad = torch.randint(-1, 3, (M,), generator=g).int().to(gpu)
     outs = []
-    for bm in (16, 32, 64):
+    for bm, bn in ((16, 32), (32, 32), (64, 32), (128, 32), (16, 96), (32, 96), (64, 96)):
         for split in (False, True):
-            outs.append(ops.lora_t(x, a, ad, 72, 24, 8, split=split, bm=bm))
+            outs.append(ops.lora_t(x, a, ad, 72, 24, 8, split=split, bm=bm, bn_=bn))
     for o in outs[1:]:
         assert torch.equal(o, outs[0])
     sel = [0, 5, 777, 2099]

@@ -1,7 +1,7 @@
 """LoRA T = x A_all^T (ops.lora_t) launch forms at the Gemma-2-9B projection shapes: unsplit (one workgroup per tile,
 the K chunks folded in registers) vs split (one workgroup per (tile, chunk) + the ordered fold kernel), per row count
 and row tile.  GPU time per call from a hipGraph of 20 calls (no host launch cost), median of 5 replays.  Prints one
-JSON line per point; sets the split threshold ops.LORA_T_SPLIT_BELOW (in unsplit workgroups)."""
+JSON line per point; ops.lora_t_plan encodes the picks."""
 import json
 import sys
 
@@ -45,15 +45,19 @@ def main():
             out = torch.zeros(M, 128, dtype=BF, device=dev)
             res = {"proj": name, "M": M, "K": K}
             ref = None
-            for bm in (16, 32, 64):
-                for split in (False, True):
-                    f = lambda: ops.lora_t(x, a, ad, nsr, 24, 8, out=out, split=split, bm=bm)  # noqa: E731
-                    res[f"{'split' if split else 'fold'}{bm}"] = round(timed(f), 2)
-                    if ref is None:
-                        ref = out.clone()
-                    else:
-                        assert torch.equal(out, ref), (name, M, bm, split)
             nt = -(-nsr // 32) * 32
+            for bn in sorted({32, nt}):
+                for bm in (16, 32, 64, 128):
+                    if bm == 128 and bn == 96:
+                        continue
+                    for split in (False, True):
+                        f = lambda: ops.lora_t(x, a, ad, nsr, 24, 8, out=out, split=split, bm=bm, bn_=bn)  # noqa: E731
+                        res[f"{'split' if split else 'fold'}{bm}x{bn}"] = round(timed(f), 2)
+                        if ref is None:
+                            ref = out.clone()
+                        else:
+                            assert torch.equal(out, ref), (name, M, bm, bn, split)
+            res["auto"] = round(timed(lambda: ops.lora_t(x, a, ad, nsr, 24, 8, out=out)), 2)
             bm = 16 if M <= 512 else (32 if M <= 2048 else 64)
             res["unsplit_wgs"] = -(-M // bm) * (nt // 32)
             print(json.dumps(res), flush=True)
