@@ -50,10 +50,13 @@ def tail_forward_fp32(model, h: torch.Tensor, start: int) -> torch.Tensor:
         x1, x2 = x[..., :half], x[..., half:]
         return torch.cat([x1 * c - x2 * sn, x2 * c + x1 * sn], -1)
 
+    bw = getattr(model, "base_weight", None)
     for l in range(start, s.layers):
         L = w.layers[l]
+        wq, wo, wgu, wdn = ((bw(l, k) for k in ("qkv", "o", "gu", "down")) if bw is not None
+                            else (L.wqkv, L.wo, L.wgu, L.wdown))
         x = _rms(h, L.ln_in, s.eps)
-        qkv = x @ L.wqkv.float().t()
+        qkv = x @ wq.float().t()
         q = rope(qkv[:, : Hq * HD].view(T, Hq, HD))
         k = rope(qkv[:, Hq * HD:(Hq + Hkv) * HD].view(T, Hkv, HD))
         v = qkv[:, (Hq + Hkv) * HD:].view(T, Hkv, HD)
@@ -67,11 +70,11 @@ def tail_forward_fp32(model, h: torch.Tensor, start: int) -> torch.Tensor:
             mask = mask & (pos[:, None] - pos[None, :] < s.sliding_window)
         sc = sc.masked_fill(~mask[None], float("-inf"))
         att = torch.einsum("hts,shd->thd", torch.softmax(sc, -1), v).reshape(T, Hq * HD)
-        h = h + _rms(att @ L.wo.float().t(), L.ln_post_attn, s.eps)
+        h = h + _rms(att @ wo.float().t(), L.ln_post_attn, s.eps)
         x = _rms(h, L.ln_pre_ffn, s.eps)
-        gu = x @ L.wgu.float().t()
+        gu = x @ wgu.float().t()
         g, u = gu[:, : s.ffn], gu[:, s.ffn:]
-        h = h + _rms((F.gelu(g, approximate="tanh") * u) @ L.wdown.float().t(), L.ln_post_ffn, s.eps)
+        h = h + _rms((F.gelu(g, approximate="tanh") * u) @ wdn.float().t(), L.ln_post_ffn, s.eps)
     return _rms(h, w.norm_f, s.eps)
 
 

@@ -171,6 +171,7 @@ class Gemma2Model:
         self._ws: Dict[int, _Workspace] = {}
         self.max_workspaces = 4
         self.lora = None          # optional models.lora.LoRABank (multi-adapter batching)
+        self._released: list = []  # (layer, linear) base projections held only by the active bank
         # gate|up GEMM with the GeGLU in its epilogue (csrc/gemm4.hip / gemm_ring.hip): per-layer gate|up weights in the
         # kernel's interleaved row order (+2·ffn·d bf16 per layer); on by default on the GPU (the dispatch table /
         # TB_GEMM decides per M whether the fused kernel or hipBLASLt + the GeGLU kernel runs; bench
@@ -192,11 +193,17 @@ class Gemma2Model:
         self._wgu_il = [L.wgu.index_select(0, idx).contiguous() for L in self.w.layers]
         return True
 
+    _BASE_ATTR = {"qkv": "wqkv", "o": "wo", "gu": "wgu", "down": "wdown"}
+
     def set_lora(self, bank) -> None:
         """Batch per-word adapters unmerged (models/lora.py).  GPU: the bank's K-augmented weights
         (:meth:`LoRABank.build_fused`): every projection keeps its in-tree fused kernel with the row's adapter
-        delta in the same GEMM (batch-invariant); CPU: the reference per-projection adds."""
+        delta in the same GEMM (batch-invariant); CPU: the reference per-projection adds.  While a fused bank is
+        active, the plain base projections it covers are dropped (its ``W_aug = [W | B]`` holds them: 16.7 GB at
+        9B) and restored bit for bit from it when the bank is removed (``set_lora(None)``)."""
         assert self.tp is None, "LoRA banks are not sharded for tensor parallelism; merge adapters instead"
+        if self.lora is not None and bank is not self.lora:
+            self._restore_base()
         self._wgu_il = None        # the gate|up weight of the fused GeGLU GEMM now comes from the bank
         self.lora = bank
         if bank is not None and self.device.type == "cuda" and getattr(bank, "fused", None) is None:
@@ -204,7 +211,33 @@ class Gemma2Model:
             perm = ops.geglu_interleave_index(ls.ffn, self.device) if ls.ffn % 128 == 0 else None
             bank.build_fused(self.w, perm)
             bank.fused_geglu = perm is not None
+            bank.gu_perm = perm
+        if bank is not None and getattr(bank, "fused", None) is not None:
+            for l, ent in enumerate(bank.fused):
+                for lin in ent:
+                    setattr(self.w.layers[l], self._BASE_ATTR[lin], None)
+                    self._released.append((l, lin))
         self._ws.clear()           # workspaces with the bank's T buffer
+
+    def base_weight(self, l: int, lin: str) -> torch.Tensor:
+        """Base projection ``lin`` (qkv / o / gu / down) of layer ``l``: the plain tensor, or -- while a fused bank
+        holds it -- a copy taken from the bank's augmented weight (gate|up back in its natural row order)."""
+        w = getattr(self.w.layers[l], self._BASE_ATTR[lin])
+        if w is not None:
+            return w
+        b = self.lora
+        _, w_aug, _ = b.fused[l][lin]
+        v = w_aug[:, : w_aug.shape[1] - b.KP]
+        perm = getattr(b, "gu_perm", None)
+        if lin == "gu" and perm is not None:
+            out = torch.empty(v.shape, dtype=v.dtype, device=v.device)
+            return out.index_copy_(0, perm, v)
+        return v.contiguous()
+
+    def _restore_base(self) -> None:
+        rel, self._released = self._released, []
+        for l, lin in rel:
+            setattr(self.w.layers[l], self._BASE_ATTR[lin], self.base_weight(l, lin))
 
     @property
     def lora_kp(self) -> int:

@@ -270,3 +270,27 @@ def test_lora_zero_up_equals_base(gpu, tb_gemm):
         lg = m.logits(m.forward(ids, pos, c, torch.arange(B, dtype=torch.int32, device=gpu)))
         outs.append((lg, c.k[:, :, :, :T].clone()))
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+def test_lora_bank_holds_base_weights(gpu, tb_gemm):
+    """While a fused bank is active the plain base projections are dropped (the bank's W_aug holds them);
+    ``base_weight`` reads them back, and ``set_lora(None)`` restores them bit for bit (same logits as a fresh
+    base model, fused GeGLU back on)."""
+    w, _, mg, _ = _bank_model(gpu)
+    attrs = {"qkv": "wqkv", "o": "wo", "gu": "wgu", "down": "wdown"}
+    for l in range(SPEC.layers):
+        for lin, a in attrs.items():
+            assert getattr(mg.w.layers[l], a) is None
+            assert torch.equal(mg.base_weight(l, lin).cpu(), getattr(w.layers[l], a))
+    mg.set_lora(None)
+    assert mg.enable_fused_geglu()
+    for l in range(SPEC.layers):
+        for lin, a in attrs.items():
+            assert torch.equal(getattr(mg.w.layers[l], a).cpu(), getattr(w.layers[l], a))
+    mb = Gemma2Model(w.to(device=gpu), gpu)
+    B, T = 9, 4
+    ids = torch.randint(0, SPEC.vocab_size, (B, T), generator=torch.Generator().manual_seed(2)).int().to(gpu)
+    pos = torch.arange(T, dtype=torch.int32, device=gpu).expand(B, T).contiguous()
+    outs = [m.logits(m.forward(ids, pos, m.new_cache(B, 8), torch.arange(B, dtype=torch.int32, device=gpu)))
+            for m in (mg, mb)]
+    assert torch.equal(outs[0], outs[1])
