@@ -539,7 +539,16 @@ __global__ void __launch_bounds__(256) lora_t_reduce_kernel(const float* __restr
   const float* p = part + (size_t)m * N + n;
   const size_t cs = (size_t)M * N;
   f32x4 s = (f32x4){0.f, 0.f, 0.f, 0.f};
-  for (int c = 0; c < nch; ++c) s += *reinterpret_cast<const f32x4*>(p + c * cs);
+  int c = 0;
+  for (; c + 4 <= nch; c += 4) {   // four loads in flight, then the adds in chunk order
+    const f32x4 v0 = *reinterpret_cast<const f32x4*>(p + c * cs), v1 = *reinterpret_cast<const f32x4*>(p + (c + 1) * cs),
+                v2 = *reinterpret_cast<const f32x4*>(p + (c + 2) * cs), v3 = *reinterpret_cast<const f32x4*>(p + (c + 3) * cs);
+    s += v0;
+    s += v1;
+    s += v2;
+    s += v3;
+  }
+  for (; c < nch; ++c) s += *reinterpret_cast<const f32x4*>(p + c * cs);
   const int ad = adapter[m];
   float o[4];
 #pragma unroll
