@@ -426,13 +426,20 @@ def side_sweep(args, info, cfg, model, tok, sae, layer, spec, kind: str, methods
         E = max(e for e in range(1, max(1, args.baseline_every) + 1) if steps % e == 0)
         # (lora: the adapters' T operands, and a third more decode rows than the merged model -- its random adapters
         # flip more greedy tokens -- in the step's transient memory: 294 GB peak at P = 120 without this reserve)
+        # cap: the headline's cells per step (PAIRS_CAP pairs of 66 cells), so the lowrank side's 42-cell pairs run
+        # as large batches; its basis table (rmax = 64 fp32 rows per cell) is reserved on top of the model
+        cap = max(1, PAIRS_CAP * 66 // n_cells) if dev.type == "cuda" else 2
+        extra = LORA_EXTRA_GB if kind == "lora" else \
+            cap * (n_cells + E) * max(c.intervention.ranks) * spec.hidden * 4 / 1e9 + 2.0
         mp = pairs_for_memory(spec, dev, n_cells, E, 0, max(len(hint_prompt_ids(tok, q)) for q in c.prompts),
-                              args.max_new, 1, cap=PAIRS_CAP if dev.type == "cuda" else 2,
-                              extra_gb=LORA_EXTRA_GB if kind == "lora" else 0.0)
+                              args.max_new, 1, cap=cap, extra_gb=extra)
+        if args.side_pairs > 0:
+            mp["pairs"] = min(mp["pairs"], args.side_pairs)
         t0 = time.perf_counter()
         R = sweep_bench(args, info, c, model, tok, sae, layer, mp["pairs"], E, 0, methods, steps, warmup, tag=f" {kind}")
         run = R["runner"]
         st = dict(run.stats)
+        args.side_marks = list(getattr(run, "phase_marks", []))     # (--only-side with TB_PHASE_MARKS)
         out = {"metric": ("multi-adapter SAE-ablation sweep prompts/s (3 distinct rank-8 per-word LoRA adapters, "
                           "unmerged, fused into the in-tree GEMMs)" if kind == "lora" else
                           f"low-rank projection-out sweep prompts/s (BASELINE config 4: ranks 1..64 x (1 targeted PCA "
@@ -545,6 +552,9 @@ def main() -> None:
     ap.add_argument("--no-lowrank-side", action="store_true",
                     help="skip the BASELINE config-4 side measurement ('lowrank': projection-out cells, ranks 1..64)")
     ap.add_argument("--lowrank-steps", type=int, default=4, help="timed steps of the lowrank side measurement")
+    ap.add_argument("--side-pairs", type=int, default=0,
+                    help="at most this many pairs per step in the side sweeps (0: the memory model's P, capped at the "
+                         "headline's cells per step)")
     ap.add_argument("--only-side", default=None, choices=["lora", "lowrank"],
                     help="run only this side measurement (its own warmup / timed steps; profiling), print its JSON")
     ap.add_argument("--tune-gemms", action="store_true",
@@ -617,6 +627,9 @@ def main() -> None:
                          args.warmup if args.only_side == "lora" else 1, [])
         if info.is_main:
             print(json.dumps(res), flush=True)
+            if os.environ.get("TB_PHASE_MARKS"):
+                with open(os.environ["TB_PHASE_MARKS"], "w") as f:
+                    json.dump(getattr(args, "side_marks", []), f)
         D.destroy(info)
         return
     methods = ("sae_targeted", "sae_random")

@@ -87,7 +87,7 @@ void tb_gemm4_splitk(const uint16_t* A, const uint16_t* W, uint16_t* out, float*
 void tb_row_combine(const int64_t* ptr, const float* coef, float* out, int B, int T, int V, hipStream_t st);
 bool tb_random_basis_ok(int D);
 void tb_random_basis(const uint64_t* seeds, const int32_t* ranks, const int64_t* rows, int n, int D, float* table,
-                     hipStream_t st);
+                     hipStream_t st, int qu = 1);
 void tb_gemm4(const uint16_t* A, const uint16_t* W, void* C, const float* bias, const float* thr, int M, int N, int K,
               int ldc, int epi, int tile_rows, hipStream_t st, const uint16_t* a2 = nullptr, int k0 = 0);
 void tb_gemm_nt(const uint16_t* A, const uint16_t* W, void* C, const float* bias, const float* thr, int M, int N,

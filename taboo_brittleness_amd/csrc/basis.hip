@@ -44,7 +44,9 @@ __device__ __forceinline__ double rb_block_sum(double v, double* red) {
   return ((red[0] + red[1]) + red[2]) + red[3];
 }
 
-template <int EPT>
+// QU: earlier directions whose table rows are loaded together (each direction's own arithmetic and order unchanged,
+// so every QU gives the same bits; tools/basis_bench.py)
+template <int EPT, int QU>
 __global__ void __launch_bounds__(256) random_basis_kernel(const uint64_t* __restrict__ seeds,
                                                            const int32_t* __restrict__ ranks,
                                                            const int64_t* __restrict__ rows, int D,
@@ -68,26 +70,53 @@ __global__ void __launch_bounds__(256) random_basis_kernel(const uint64_t* __res
     for (int pass = 0; pass < 2; ++pass)
       for (int q0 = 0; q0 < j; q0 += RB_QCH) {
         const int nq = j - q0 < RB_QCH ? j - q0 : RB_QCH;
-        for (int q = 0; q < nq; ++q) {
-          const float* qr = out + (size_t)(q0 + q) * D;
-          double part = 0.0;
+        // dot products QU directions at a time: their table loads in flight together (each direction's own
+        // arithmetic and order unchanged, so the bits are those of one direction at a time)
+        for (int qb = 0; qb < nq; qb += QU) {
+          float a[QU][EPT];
 #pragma unroll
-          for (int e = 0; e < EPT; ++e) {
-            const int d = t + 256 * e;
-            if (d < D) part = fma((double)qr[d], v[e], part);
+          for (int u = 0; u < QU; ++u) {
+            const float* qr = out + (size_t)(q0 + (qb + u < nq ? qb + u : nq - 1)) * D;
+#pragma unroll
+            for (int e = 0; e < EPT; ++e) {
+              const int d = t + 256 * e;
+              a[u][e] = d < D ? qr[d] : 0.f;
+            }
           }
 #pragma unroll
-          for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
-          if (lane == 0) dots[q][w] = part;
+          for (int u = 0; u < QU; ++u) {
+            double part = 0.0;
+#pragma unroll
+            for (int e = 0; e < EPT; ++e) {
+              const int d = t + 256 * e;
+              if (d < D) part = fma((double)a[u][e], v[e], part);
+            }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+            if (lane == 0 && qb + u < nq) dots[qb + u][w] = part;
+          }
         }
         __syncthreads();
-        for (int q = 0; q < nq; ++q) {
-          const double c = ((dots[q][0] + dots[q][1]) + dots[q][2]) + dots[q][3];
-          const float* qr = out + (size_t)(q0 + q) * D;
+        for (int qb = 0; qb < nq; qb += QU) {   // v -= c_q q in direction order, loads batched likewise
+          float a[QU][EPT];
 #pragma unroll
-          for (int e = 0; e < EPT; ++e) {
-            const int d = t + 256 * e;
-            if (d < D) v[e] = fma(-c, (double)qr[d], v[e]);
+          for (int u = 0; u < QU; ++u) {
+            const float* qr = out + (size_t)(q0 + (qb + u < nq ? qb + u : nq - 1)) * D;
+#pragma unroll
+            for (int e = 0; e < EPT; ++e) {
+              const int d = t + 256 * e;
+              a[u][e] = d < D ? qr[d] : 0.f;
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < QU; ++u) {
+            if (qb + u >= nq) break;
+            const double c = ((dots[qb + u][0] + dots[qb + u][1]) + dots[qb + u][2]) + dots[qb + u][3];
+#pragma unroll
+            for (int e = 0; e < EPT; ++e) {
+              const int d = t + 256 * e;
+              if (d < D) v[e] = fma(-c, (double)a[u][e], v[e]);
+            }
           }
         }
         __syncthreads();                 // dots is rewritten by the next chunk
@@ -110,13 +139,21 @@ __global__ void __launch_bounds__(256) random_basis_kernel(const uint64_t* __res
 bool tb_random_basis_ok(int D) { return D > 0 && D <= 256 * 16; }
 
 void tb_random_basis(const uint64_t* seeds, const int32_t* ranks, const int64_t* rows, int n, int D, float* table,
-                     hipStream_t st) {
+                     hipStream_t st, int qu) {
   if (n <= 0) return;
   const int ept = (D + 255) / 256;
-  if (ept <= 4)
-    hipLaunchKernelGGL(random_basis_kernel<4>, dim3(n), dim3(256), 0, st, seeds, ranks, rows, D, table);
-  else if (ept <= 8)
-    hipLaunchKernelGGL(random_basis_kernel<8>, dim3(n), dim3(256), 0, st, seeds, ranks, rows, D, table);
-  else
-    hipLaunchKernelGGL(random_basis_kernel<16>, dim3(n), dim3(256), 0, st, seeds, ranks, rows, D, table);
+#define RB_GO(E_, Q_) hipLaunchKernelGGL((random_basis_kernel<E_, Q_>), dim3(n), dim3(256), 0, st, seeds, ranks, rows, D, table)
+#define RB_Q(E_)                  \
+  if (qu >= 4) RB_GO(E_, 4);      \
+  else if (qu == 2) RB_GO(E_, 2); \
+  else RB_GO(E_, 1);
+  if (ept <= 4) {
+    RB_Q(4)
+  } else if (ept <= 8) {
+    RB_Q(8)
+  } else {
+    RB_Q(16)
+  }
+#undef RB_Q
+#undef RB_GO
 }

@@ -558,7 +558,7 @@ void row_combine(torch::Tensor ptr, torch::Tensor coef, torch::Tensor out) {
 }
 
 // random orthonormal bases (csrc/basis.hip) written into rows [rows[i], rows[i] + ranks[i]) of an fp32 [R, D] table
-void random_basis(torch::Tensor seeds, torch::Tensor ranks, torch::Tensor rows, torch::Tensor table) {
+void random_basis(torch::Tensor seeds, torch::Tensor ranks, torch::Tensor rows, torch::Tensor table, int64_t qu) {
   CHECK_DEV(seeds); CHECK_CONTIG(seeds); CHECK_DEV(ranks); CHECK_CONTIG(ranks); CHECK_DEV(rows); CHECK_CONTIG(rows);
   IN_F32(table);
   TORCH_CHECK(seeds.scalar_type() == at::kLong && ranks.scalar_type() == at::kInt && rows.scalar_type() == at::kLong,
@@ -568,7 +568,7 @@ void random_basis(torch::Tensor seeds, torch::Tensor ranks, torch::Tensor rows, 
   TORCH_CHECK(tb_random_basis_ok(D), "random_basis: D = ", D, " outside (0, 4096]");
   c10::DeviceGuard g(table.device());
   tb_random_basis(reinterpret_cast<const uint64_t*>(seeds.data_ptr<int64_t>()), ranks.data_ptr<int32_t>(),
-                  rows.data_ptr<int64_t>(), n, D, table.data_ptr<float>(), cur_stream());
+                  rows.data_ptr<int64_t>(), n, D, table.data_ptr<float>(), cur_stream(), (int)qu);
 }
 
 // ---- multi-adapter LoRA (models/lora.py): two-source A operands [x (k0 columns) | T (K - k0 columns)] of the in-tree

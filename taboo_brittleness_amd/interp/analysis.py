@@ -191,27 +191,21 @@ def random_latents(d_sae: int, m: int, seed: int, exclude: Sequence[int] = (), p
 @torch.no_grad()
 def secret_subspace(vectors: torch.Tensor, r: int) -> torch.Tensor:
     """Top-``r`` principal directions of mean-centred spike residuals (EP:144-146). Returns ``[r, D]`` fp32 orthonormal rows."""
-    X = vectors.float()
+    X = vectors.double()
     X = X - X.mean(0, keepdim=True)
     n = X.shape[0]
     if n >= 2:
-        # Gram trick: N x N eigenproblem (N = pooled spike count << D)
-        G = X @ X.t()
-        evals, evecs = torch.linalg.eigh(G.double().cpu())
-        order = torch.argsort(evals, descending=True)
-        dirs = []
-        for j in order.tolist():
-            if evals[j] <= 1e-9 * max(float(evals.max()), 1e-30):
-                break
-            v = (X.t().double().cpu() @ evecs[:, j]) / float(evals[j]) ** 0.5
-            dirs.append(v)
-            if len(dirs) == r:
-                break
-        U = torch.stack(dirs, 0) if dirs else torch.zeros(0, X.shape[1], dtype=torch.float64)
+        # Gram trick: N x N eigenproblem (N = pooled spike count << D), in fp64 on the vectors' device: one host sync
+        # (the numerical rank) instead of a device -> host copy of X per direction
+        evals, evecs = torch.linalg.eigh(X @ X.t())
+        evals, order = torch.sort(evals, descending=True)
+        thr = 1e-9 * torch.clamp(evals[:1], min=1e-30)
+        k = min(r, int((evals > thr).sum()))        # the leading eigenvalues above the threshold
+        U = ((X.t() @ evecs[:, order[:k]]) / evals[:k].sqrt()).t()
     else:
-        U = torch.zeros(0, X.shape[1], dtype=torch.float64)
+        U = torch.zeros(0, X.shape[1], dtype=torch.float64, device=X.device)
     if U.shape[0] < r:   # pad a rank-deficient basis with random orthogonal directions
-        extra = random_subspace(X.shape[1], r - U.shape[0], seed=cell_seed("pad", n, r)).double()
+        extra = random_subspace(X.shape[1], r - U.shape[0], seed=cell_seed("pad", n, r)).double().to(X.device)
         U = torch.cat([U, extra], 0)
     Q, _ = torch.linalg.qr(U.t())
     return Q.t()[:r].float().contiguous()

@@ -332,12 +332,17 @@ def row_combine(ptr: torch.Tensor, coef: torch.Tensor, out: torch.Tensor) -> tor
 
 
 # ------------------------------------------------------------ multi-adapter LoRA (models/lora.py LoRABank.fused)
-def random_basis(seeds: torch.Tensor, ranks: torch.Tensor, rows: torch.Tensor, table: torch.Tensor) -> torch.Tensor:
+# earlier directions whose table rows the basis kernel loads together (1 / 2 / 4; the same bits; tools/basis_bench.py)
+RANDOM_BASIS_QU = 1
+
+
+def random_basis(seeds: torch.Tensor, ranks: torch.Tensor, rows: torch.Tensor, table: torch.Tensor,
+                 qu: Optional[int] = None) -> torch.Tensor:
     """Random orthonormal bases into an fp32 ``[R, D]`` table: basis ``i`` (``ranks[i]`` directions, seed
     ``seeds[i]``) fills rows ``rows[i] .. rows[i] + ranks[i] - 1`` (csrc/basis.hip, one workgroup per basis; the
     numpy reference of the same algorithm on CPU tables)."""
     if table.is_cuda:
-        _k().random_basis(seeds, ranks, rows, table)
+        _k().random_basis(seeds, ranks, rows, table, int(qu or RANDOM_BASIS_QU))
         return table
     D = table.shape[-1]
     for s, r, o in zip(seeds.tolist(), ranks.tolist(), rows.tolist()):
@@ -373,14 +378,15 @@ def lora_t_plan(M: int, K: int, nt: int):
 
 def lora_t(x: torch.Tensor, a_all: torch.Tensor, adapter: torch.Tensor, nsr: int, nr: int, r: int,
            out: Optional[torch.Tensor] = None, split: Optional[bool] = None, bm: Optional[int] = None,
-           bn_: Optional[int] = None) -> torch.Tensor:
+           bn: Optional[int] = None) -> torch.Tensor:
     """The bank's masked down-projection ``T [M, KP]``: column ``c`` = ``x . a_all[c]`` rounded to bf16 where it belongs
     to the row's adapter (``c < nsr`` and ``(c % nr) // r == adapter[row]``), else 0 (``adapter < 0``: all 0).  GPU:
     the ring GEMM's RG_LMASK epilogue (csrc/gemm_ring.hip), batch-invariant, over the first ``nsr`` columns rounded
     up to 32 only (the rest of ``a_all`` is zero padding): columns past those are NOT written, so a caller's ``out``
     must hold zeros there (``out=None`` allocates zeros; models/gemma2.py keeps one zeroed buffer per projection).
     K runs in fixed 512-deep chunks summed in order, so the K chain can be split over workgroups at decode row counts
-    (``split``; default: :func:`lora_t_plan`) with the same bits as the unsplit launch.
+    (``split``; default: :func:`lora_t_plan`, as are the tile ``bm`` x ``bn``) with the same bits as the unsplit
+    launch.
     CPU: the fp32 reference."""
     K = x.shape[-1]
     M, N = x.numel() // K, a_all.shape[0]
@@ -395,11 +401,15 @@ def lora_t(x: torch.Tensor, a_all: torch.Tensor, adapter: torch.Tensor, nsr: int
         elif split != psplit:
             pbm = 32 if split else 16
         bm = bm or pbm
-        bn = pbn if bn_ is None else bn_
+        bn = bn or pbn
         k = _k()
         # (split: the chunk sums from the caching allocator -- graph-private memory inside a capture)
-        part = (torch.empty(k.lora_t_chunks(K), M, nt, dtype=torch.float32, device=x.device) if split
-                else _EMPTY_F32.setdefault(x.device, torch.empty(0, dtype=torch.float32, device=x.device)))
+        if split:
+            part = torch.empty(k.lora_t_chunks(K), M, nt, dtype=torch.float32, device=x.device)
+        else:
+            part = _EMPTY_F32.get(x.device)
+            if part is None:
+                part = _EMPTY_F32[x.device] = torch.empty(0, dtype=torch.float32, device=x.device)
         k.lora_t(x.reshape(M, K), a_all[:nt], out, adapter, int(nsr), int(nr), int(r), bm, bn, part)
         return out
     out = _out(out, (M, N), BF16, x.device)

@@ -1152,3 +1152,8 @@ def test_random_basis_matches_reference(gpu, D):
     ops.random_basis(torch.tensor([99], dtype=torch.int64, device=gpu), torch.tensor([16], dtype=torch.int32,
                      device=gpu), torch.zeros(1, dtype=torch.int64, device=gpu), alone)
     assert torch.equal(alone, tab[192:208])
+    for qu in (1, 2, 4):      # table rows loaded 1 / 2 / 4 earlier directions at a time: the same bits
+        t2 = torch.full_like(tab, float("nan"))
+        ops.random_basis(torch.tensor(seeds, dtype=torch.int64, device=gpu), torch.tensor(ranks, dtype=torch.int32,
+                         device=gpu), torch.tensor(rows, dtype=torch.int64, device=gpu), t2, qu=qu)
+        assert torch.equal(t2, tab), qu

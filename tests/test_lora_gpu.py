@@ -86,7 +86,7 @@ def test_lora_t_split_fold_bitexact(gpu, K):
     outs = []
     for bm, bn in ((16, 32), (32, 32), (64, 32), (128, 32), (16, 96), (32, 96), (64, 96)):
         for split in (False, True):
-            outs.append(ops.lora_t(x, a, ad, 72, 24, 8, split=split, bm=bm, bn_=bn))
+            outs.append(ops.lora_t(x, a, ad, 72, 24, 8, split=split, bm=bm, bn=bn))
     for o in outs[1:]:
         assert torch.equal(o, outs[0])
     sel = [0, 5, 777, 2099]

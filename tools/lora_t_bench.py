@@ -51,7 +51,7 @@ def main():
                     if bm == 128 and bn == 96:
                         continue
                     for split in (False, True):
-                        f = lambda: ops.lora_t(x, a, ad, nsr, 24, 8, out=out, split=split, bm=bm, bn_=bn)  # noqa: E731
+                        f = lambda: ops.lora_t(x, a, ad, nsr, 24, 8, out=out, split=split, bm=bm, bn=bn)  # noqa: E731
                         res[f"{'split' if split else 'fold'}{bm}x{bn}"] = round(timed(f), 2)
                         if ref is None:
                             ref = out.clone()
