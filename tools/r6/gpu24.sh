@@ -3,7 +3,7 @@
 # the lora B = 0 control), then a kernel census of the lora side (4 / 1 steps, control off).
 set -o pipefail
 R=$GRAFT_REPO_ROOT; cd $R
-O=gpurun_out/r6/final2; mkdir -p $O
+O=gpurun_out/r6/${FINAL_TAG:-final2}; mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 2; }
 tail -1 $O/pytest_gpu.log
 timeout -k 10 300 python -u __graft_entry__.py smoke > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 3; }
