@@ -96,3 +96,44 @@ def test_sweep_with_adapter_bank_matches_single_word_models():
         for a, b in zip([p for p in pairs if p.word == word], pw):
             assert a.resp == b.resp
             assert abs(a.nll - b.nll) < 0.05
+
+
+def test_lora_t_plan_tiles_are_built():
+    """ops.lora_t_plan only picks (bm, bn) tiles the RG_LMASK kernel is built with (csrc/gemm_ring.hip
+    RG_LMASK_TILES) that divide the used width, splits at decode row counts and folds at the tails' row counts."""
+    from taboo_brittleness_amd import ops
+
+    built = {(16, 32), (32, 32), (64, 32), (128, 32), (16, 64), (32, 64), (64, 64), (128, 64), (16, 96), (32, 96),
+             (64, 96)}
+    for K in (3584, 4096, 14336, 640):
+        for nt in (32, 64, 96):
+            for M in (1, 16, 64, 100, 256, 512, 1000, 2048, 4096, 8192, 32768, 100000):
+                split, bm, bn = ops.lora_t_plan(M, K, nt)
+                assert (bm, bn) in built and nt % bn == 0, (M, K, nt, bm, bn)
+                if M <= 64:
+                    assert split
+                if M >= 32768:
+                    assert not split
+    assert ops.lora_t_plan(4096, 14336, 32)[0] and not ops.lora_t_plan(8192, 14336, 32)[0]
+
+
+def test_zero_up_bank_is_the_base_model():
+    """``LoRABank.zero_up`` (PEFT's B = 0 init; bench.py's equal-work control): the bank adds nothing."""
+    spec = replace(GEMMA2_TINY, vocab_size=512, layers=2)
+    w = random_gemma2(spec, dtype=torch.float32, seed=3)
+    bank = LoRABank.random(spec, ["a", "b"], r=4, alpha=8.0, seed=1, std=0.2, dtype=torch.float32)
+    bank.zero_up()
+    for l in range(spec.layers):
+        for lin in ("qkv", "o", "gu", "down"):
+            assert torch.count_nonzero(bank.merged_delta(0, l, lin)) == 0
+    ma, mb = Gemma2Model(w, "cpu"), Gemma2Model(w, "cpu")
+    ma.set_lora(bank)
+    ids = torch.randint(0, spec.vocab_size, (2, 5), generator=torch.Generator().manual_seed(0)).int()
+    pos = torch.arange(5, dtype=torch.int32).expand(2, 5).contiguous()
+    outs = []
+    for m in (ma, mb):
+        c = m.new_cache(2, 8)
+        if m is ma:
+            c.adapter.copy_(torch.tensor([0, 1], dtype=torch.int32))
+        outs.append(m.logits(m.forward(ids, pos, c, torch.arange(2, dtype=torch.int32))))
+    torch.testing.assert_close(outs[0], outs[1], rtol=0, atol=1e-6)
