@@ -260,11 +260,15 @@ gemm4_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, voi
     if ((g) < PI)                                                                                                  \
       __builtin_amdgcn_raw_ptr_buffer_load_lds(__builtin_amdgcn_make_buffer_rsrc(wtile, 0, wbytes, 0x00020000),    \
                                                (g4_lds_t*)(d_ + (g) * 4096), 16, vp[(g) < PI ? (g) : 0], (t) * 128, 0, 0); \
-    else if (L2A && (t) >= NT0)           /* the second A source: its own descriptor, row offsets, K offset */    \
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(__builtin_amdgcn_make_buffer_rsrc(atile2, 0, abytes2, 0x00020000),  \
-                                               (g4_lds_t*)(d_ + PIMG + ((g) - PI) * 4096), 16,                      \
-                                               vq2[L2A && (g) >= PI ? (g) - PI : 0], ((t) - NT0) * 128, 0, 0);      \
-    else                                                                                                           \
+    else if constexpr (L2A) {   /* the second A source from K tile NT0 on: descriptor, row offsets and K offset    \
+                                   picked by uniform selects, not a branch in the scheduled K loop */              \
+      const bool s2_ = (t) >= NT0;                                                                                 \
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(                                                                    \
+          __builtin_amdgcn_make_buffer_rsrc(s2_ ? atile2 : atile, 0, s2_ ? abytes2 : abytes, 0x00020000),          \
+          (g4_lds_t*)(d_ + PIMG + ((g) - PI) * 4096), 16,                                                          \
+          s2_ ? vq2[(g) >= PI ? (g) - PI : 0] : vq[(g) >= PI ? (g) - PI : 0], s2_ ? ((t) - NT0) * 128 : (t) * 128,  \
+          0, 0);                                                                                                   \
+    } else                                                                                                         \
       __builtin_amdgcn_raw_ptr_buffer_load_lds(__builtin_amdgcn_make_buffer_rsrc(atile, 0, abytes, 0x00020000),    \
                                                (g4_lds_t*)(d_ + PIMG + ((g) - PI) * 4096), 16,                      \
                                                vq[(g) >= PI ? (g) - PI : 0], (t) * 128, 0, 0);                      \
