@@ -215,8 +215,9 @@ class Gemma2Model:
         if bank is not None and getattr(bank, "fused", None) is not None:
             for l, ent in enumerate(bank.fused):
                 for lin in ent:
-                    setattr(self.w.layers[l], self._BASE_ATTR[lin], None)
-                    self._released.append((l, lin))
+                    if getattr(self.w.layers[l], self._BASE_ATTR[lin]) is not None:
+                        setattr(self.w.layers[l], self._BASE_ATTR[lin], None)
+                        self._released.append((l, lin))
         self._ws.clear()           # workspaces with the bank's T buffer
 
     def base_weight(self, l: int, lin: str) -> torch.Tensor:
