@@ -187,8 +187,9 @@ gemm_ring_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W,
   // all A rows, BN % 8 == 0)
   const int KA = L2A ? ra.k0 : K, K2 = K - KA, NT0 = KA >> 6;
   const uint16_t* src[GMAX];
-  const uint16_t* src2[L2A ? GMAX : 1];
-  bool isa[L2A ? GMAX : 1];
+  // (L2A: per instruction the byte offset from its first-source row to its second-source row at the same K tile,
+  // 0 for W rows -- added under a uniform mask from K tile k0 / 64 on, no per-instruction select)
+  int64_t dlt[L2A ? GMAX : 1];
 #pragma unroll
   for (int q = 0; q < GMAX; ++q) {
     const int j = wid + 4 * q, lr = min(8 * j + (lane >> 3), R - 1);
@@ -197,8 +198,9 @@ gemm_ring_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W,
     const uint16_t* row = lr < BN ? W + (size_t)wrow(lr) * K : A + (size_t)am * KA;
     src[q] = row + lc * 8 + kt0 * 64;
     if constexpr (L2A) {
-      isa[q] = 8 * j >= BN;
-      src2[q] = ra.a2 + (size_t)(isa[q] ? am : 0) * K2 + lc * 8;
+      const bool isa = 8 * j >= BN;
+      const uint16_t* s2 = ra.a2 + (size_t)(isa ? am : 0) * K2 + lc * 8;   // K tile NT0 of the second source
+      dlt[q] = isa ? (int64_t)((uintptr_t)s2 - (uintptr_t)(src[q] + (size_t)NT0 * 64)) : 0;
     }
   }
   const bool gx = wid < GX;   // this wave issues GLO + 1 instructions per K tile
@@ -210,9 +212,7 @@ gemm_ring_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W,
         if (q < GLO || gx) {
           const int kt = t * KU + kk;
           const uint16_t* p = src[q] + kt * 64;
-          if constexpr (L2A) {
-            if (isa[q] && kt >= NT0) p = src2[q] + (kt - NT0) * 64;
-          }
+          if constexpr (L2A) p = (const uint16_t*)((const char*)p + (dlt[q] & -(int64_t)(kt >= NT0)));
           __builtin_amdgcn_global_load_lds((rg_gbl_t*)p,
                                            (rg_lds_t*)(smem + stg * SB + kk * IB + (wid + 4 * q) * 1024), 16, 0, 0);
         }
